@@ -1,0 +1,128 @@
+"""ctypes binding of the CPU oracle (oracle/build/liboracle.so).
+
+Test infrastructure only: used by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg as the checker.  The product library never imports it.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(REPO, 'oracle')
+ORACLE_SO = os.path.join(ORACLE_DIR, 'build', 'liboracle.so')
+
+_lib = None
+
+
+def build_oracle():
+    subprocess.check_call(['make', '-s', '-C', ORACLE_DIR])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.isfile(ORACLE_SO):
+            build_oracle()
+        L = ctypes.CDLL(ORACLE_SO)
+        vp, sz = ctypes.c_void_p, ctypes.c_size_t
+        L.oracle_load.restype = vp
+        L.oracle_load.argtypes = [ctypes.c_char_p]
+        L.oracle_free.argtypes = [vp]
+        L.oracle_info.argtypes = [vp, vp]
+        L.oracle_init_state.argtypes = [vp, vp]
+        L.oracle_eval.argtypes = [vp, vp, sz, vp, vp, vp]
+        L.oracle_eval.restype = ctypes.c_int
+        L.oracle_quantize_file.argtypes = [ctypes.c_char_p] * 3
+        L.oracle_quantize_file.restype = ctypes.c_int
+        L.oracle_set_threads.argtypes = [ctypes.c_int]
+        L.oracle_get_threads.restype = ctypes.c_int
+        L.oracle_block_bytes.argtypes = [ctypes.c_int]
+        L.oracle_block_bytes.restype = sz
+        L.oracle_quantize_row.argtypes = [ctypes.c_int, vp, vp, ctypes.c_int64]
+        L.oracle_quantize_act.argtypes = [ctypes.c_int, vp, vp, ctypes.c_int64]
+        L.oracle_dequantize_row.argtypes = [ctypes.c_int, vp, vp, ctypes.c_int64]
+        L.oracle_matmul.argtypes = [ctypes.c_int, vp, ctypes.c_int64, ctypes.c_int64, vp, ctypes.c_int64, vp]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data
+
+
+class OracleModel:
+    """Mirror of the rwkv.h eval semantics on the CPU restatement."""
+
+    def __init__(self, path):
+        self.ptr = lib().oracle_load(path.encode())
+        if not self.ptr:
+            raise ValueError(f'oracle failed to load {path}')
+        info = np.zeros(8, np.int64)
+        lib().oracle_info(self.ptr, _p(info))
+        (self.n_vocab, self.n_embed, self.n_layer, self.arch_major, self.arch_minor,
+         self.head_count, self.head_size, self.state_len) = [int(v) for v in info]
+
+    def init_state(self):
+        s = np.zeros(self.state_len, np.float32)
+        lib().oracle_init_state(self.ptr, _p(s))
+        return s
+
+    def eval_sequence(self, tokens, state_in=None, want_logits=True):
+        toks = np.ascontiguousarray(np.asarray(tokens, dtype=np.uint32))
+        st = np.zeros(self.state_len, np.float32)
+        lg = np.zeros(self.n_vocab, np.float32) if want_logits else None
+        rc = lib().oracle_eval(self.ptr, _p(toks), len(toks), _p(state_in), _p(st), _p(lg))
+        if rc:
+            raise ValueError(f'oracle_eval failed rc={rc}')
+        return lg, st
+
+    def eval_serial(self, tokens, state_in=None):
+        st = state_in
+        lg = None
+        for t in tokens:
+            lg, st = self.eval_sequence([t], st)
+        return lg, st
+
+    def close(self):
+        if self.ptr:
+            lib().oracle_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def quantize_file(src, dst, fmt):
+    rc = lib().oracle_quantize_file(src.encode(), dst.encode(), fmt.encode())
+    if rc:
+        raise ValueError(f'oracle_quantize_file rc={rc}')
+
+
+TYPE_IDS = {'FP32': 0, 'FP16': 1, 'Q4_0': 2, 'Q4_1': 3, 'Q5_0': 7, 'Q5_1': 8, 'Q8_0': 9, 'Q8_1': 10}
+
+
+def quantize_rows(fmt, x):
+    """File quantizer on a [M, K] float32 matrix -> raw block bytes."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    t = TYPE_IDS[fmt]
+    M, K = x.shape
+    bb = lib().oracle_block_bytes(t)
+    out = np.zeros(M * (K // 32) * bb, np.uint8)
+    for m in range(M):
+        lib().oracle_quantize_row(t, _p(x[m]), out.ctypes.data + m * (K // 32) * bb, K)
+    return out
+
+
+def matmul(fmt, w_bytes, K, M, x):
+    """ggml-numerics matmul: x [T, K] float32 -> y [T, M]."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    T = x.shape[0]
+    y = np.zeros((T, M), np.float32)
+    w_bytes = np.ascontiguousarray(w_bytes)
+    lib().oracle_matmul(TYPE_IDS[fmt], _p(w_bytes), K, M, _p(x), T, _p(y))
+    return y

@@ -1,0 +1,63 @@
+/*
+ * rwkv_mi355x.h -- ADDITIVE extensions of librwkv.so (nothing in rwkv.h changes).
+ *
+ * The reference ABI hands the recurrent state over as host float buffers on every call
+ * (rwkv_eval.inc:2-22).  For RWKV-v6-1B6 that is 13 MB each way per token, more than the
+ * weights' HBM time, so these entry points let a caller keep the state resident in HBM.
+ * They are the path bench.py measures as "device-resident"; ABI-level rates are reported
+ * beside them.
+ */
+#ifndef RWKV_MI355X_H
+#define RWKV_MI355X_H
+
+#include "rwkv.h"
+
+#if defined(__cplusplus)
+extern "C" {
+#endif
+
+/* Copies a host state into the context's device-resident state (NULL => fresh state). */
+RWKV_API bool rwkv_mi355x_state_upload(struct rwkv_context * ctx, const float * state);
+/* Copies the device-resident state out to host memory. */
+RWKV_API bool rwkv_mi355x_state_download(struct rwkv_context * ctx, float * state);
+
+/* rwkv_eval_sequence semantics on the device-resident state: tokens host array, T >= 1.
+ * logits_out (host, may be NULL) receives the last token's logits.  No state crosses PCIe.
+ * sync=false returns after enqueueing (the caller later calls rwkv_mi355x_sync). */
+RWKV_API bool rwkv_mi355x_eval_device(struct rwkv_context * ctx, const uint32_t * tokens, size_t T,
+                                      float * logits_out, bool sync);
+RWKV_API bool rwkv_mi355x_sync(struct rwkv_context * ctx);
+
+/* The context's HIP stream (hipStream_t), so callers can time kernels with events on it. */
+RWKV_API void * rwkv_mi355x_stream(struct rwkv_context * ctx);
+
+/* Device pointer of the current device-resident state (state_len floats). */
+RWKV_API float * rwkv_mi355x_device_state(struct rwkv_context * ctx);
+
+/* Per-token algorithmic HBM bytes of one decode step (weights read + state read/written),
+ * counted from the original block sizes (Q4_0 18 B / 32 weights ...), see DESIGN.md. */
+RWKV_API double rwkv_mi355x_decode_bytes(const struct rwkv_context * ctx, bool with_logits);
+
+/* Algorithmic bytes of the model's weight matrices only (all layers, + head if asked). */
+RWKV_API double rwkv_mi355x_weight_bytes(const struct rwkv_context * ctx, bool with_head);
+
+/* 2*M*K summed over every matmul of one token (head included if asked). */
+RWKV_API double rwkv_mi355x_matmul_flops_per_token(const struct rwkv_context * ctx, bool with_head);
+
+/* Architecture info: out[0..3] = arch_major, arch_minor, head_count, head_size. */
+RWKV_API void rwkv_mi355x_arch(const struct rwkv_context * ctx, int64_t out[4]);
+
+/* Writes a synthetic rwkv.cpp model file with the exact tensor shapes of a real checkpoint,
+ * seeded random weights (N(0, 1/sqrt(fan_in)) for matrices), quantized with this library's
+ * quantizer.  arch: 4, 5 (v5.2), 6, 7.  fmt: "FP32" "FP16" "Q4_0" "Q4_1" "Q5_0" "Q5_1" "Q8_0".
+ * ffn = 0 picks the architecture's default FFN width; head_size 64 for v5+; lora dims of
+ * the real checkpoints.  Used by bench.py (no checkpoints are downloadable). */
+RWKV_API bool rwkv_mi355x_write_synthetic_model(const char * path, int arch, uint32_t n_vocab,
+                                                uint32_t n_embed, uint32_t n_layer, uint32_t ffn,
+                                                const char * fmt, uint64_t seed);
+
+#if defined(__cplusplus)
+}
+#endif
+
+#endif

@@ -1,0 +1,110 @@
+// common.hpp -- shared types for the MI355X (gfx950) RWKV eval engine.
+//
+// Data layout in HBM (see DESIGN.md "Data layout"):
+//   * quantized weights are repacked at load time into structure-of-arrays:
+//       qs  [M][nb][16]   (Q4_0/Q4_1/Q5_0/Q5_1: 16 nibble bytes per 32-block;
+//                          low nibble of byte j = element j, high = element j+16 --
+//                          the ggml block order, rwkv_graph.inc's mul_mat operand)
+//       qs  [M][nb][32]   (Q8_0 int8)
+//       qh  [M][nb] u32   (Q5_*: bit j = 5th bit of element j)
+//       sc  [M][nb] u16   (_0 formats: fp16 d)  /  u32 (_1 formats: fp16 d | fp16 m << 16)
+//     so every lane load is a 16-byte aligned dwordx4 and the algorithmic bytes per block
+//     stay 18/20/22/24/34 (ggml block sizes).
+//   * F16 / F32 matrices stay row-major [M][K].
+//   * activations feeding a matmul are produced directly in the consumer's input format
+//     (ActBuf): fp32, fp16, or Q8 blocks (int8 [T][K] + fp32 d/s + int qsum [T][K/32]),
+//     mirroring ggml's src1 conversion (vec_dot_type) in rwkv_graph.inc's ggml_mul_mat calls.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+#include <stdint.h>
+#include <stddef.h>
+
+namespace rwkvmi {
+
+// rwkv.cpp file type ids (reference rwkv_file_format.inc:5-24)
+enum WType : int { W_F32 = 0, W_F16 = 1, W_Q4_0 = 2, W_Q4_1 = 3, W_Q5_0 = 7, W_Q5_1 = 8, W_Q8_0 = 9 };
+
+// activation formats (ggml vec_dot_type of the consuming weight type)
+enum AFmt : int { A_F32 = 0, A_F16 = 1, A_Q8_0 = 2, A_Q8_1 = 3 };
+
+__host__ __device__ inline int act_fmt_for(int wtype) {
+    switch (wtype) {
+        case W_F32: return A_F32;
+        case W_F16: return A_F16;
+        case W_Q4_1:
+        case W_Q5_1: return A_Q8_1;
+        default: return A_Q8_0;
+    }
+}
+
+inline bool wtype_quantized(int t) { return t == W_Q4_0 || t == W_Q4_1 || t == W_Q5_0 || t == W_Q5_1 || t == W_Q8_0; }
+
+// Activation buffer: T rows of K elements in one format.
+struct ActBuf {
+    int fmt;
+    int K;
+    float * f;       // [T][K]       A_F32
+    __half * h;      // [T][K]       A_F16
+    int8_t * q;      // [T][K]       A_Q8_*
+    float * d;       // [T][K/32]    fp16-rounded block scale, stored as fp32
+    float * s;       // [T][K/32]    A_Q8_1: fp16-rounded d*sum(q)
+    int * qsum;      // [T][K/32]    sum(q) (exact, used for the -8/-16 offset of _0 formats)
+};
+
+// Device weight matrix, ggml ne=[K, M] (M output rows of K elements).
+struct DMat {
+    int type;
+    int M, K;
+    const uint8_t * qs;     // quantized nibbles / int8, or raw F16/F32 rows
+    const uint32_t * qh;    // Q5 high bits
+    const void * sc;        // u16 d  or u32 (d | m<<16)
+};
+
+enum Epi : int {
+    EPI_STORE = 0,       // y = acc
+    EPI_SIGMOID = 1,     // y = sigmoid(acc)
+    EPI_TANH = 2,        // y = tanh(acc)
+    EPI_SILU = 3,        // y = silu(acc)
+    EPI_RELU_SQ = 4,     // y = relu(acc)^2
+    EPI_ADD = 5,         // y = y + acc                    (residual)
+    EPI_SIGMUL_ADD = 6,  // y = y + sigmoid(aux) * acc     (FFN v4-v6: x += r * (Wv k))
+    EPI_DECAY6 = 7,      // y = exp(-exp(acc + bias))      (rwkv_graph.inc:365-367)
+    EPI_DECAY7 = 8,      // y = exp(sigmoid(acc + bias) * -0.606531)  (rwkv_graph.inc:425-430)
+    EPI_SIGMOID_BIAS = 9,// y = sigmoid(acc + bias)        (rwkv_graph.inc:417-423)
+    EPI_VMIX7 = 10,      // y = y + (aux - y) * sigmoid(acc + bias)  (rwkv_graph.inc:443-452)
+};
+
+struct MMEntry {
+    DMat W;
+    ActBuf in;          // input activations [T][K]
+    float * y;          // fp32 output [T][ldy] (may be null when only emitting)
+    int ldy;
+    const float * aux;  // [T][ldy]
+    const float * bias; // [M]
+    ActBuf out;         // optional: emit post-epilogue values as the next matmul's input
+    int emit;
+    int epi;
+    int block0;         // first workgroup of this entry
+};
+
+constexpr int MM_MAX_ENTRIES = 8;
+
+struct MMGroup {
+    MMEntry e[MM_MAX_ENTRIES];
+    int n;
+    int T;
+};
+
+#define HIP_OK(x)                                                                             \
+    do {                                                                                      \
+        hipError_t _e = (x);                                                                  \
+        if (_e != hipSuccess) {                                                               \
+            fprintf(stderr, "HIP error %s at %s:%d: %s\n", hipGetErrorString(_e), __FILE__, \
+                    __LINE__, #x);                                                            \
+            return false;                                                                     \
+        }                                                                                     \
+    } while (0)
+
+}  // namespace rwkvmi

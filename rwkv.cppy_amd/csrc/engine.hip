@@ -1,0 +1,730 @@
+// engine.hip -- device model upload and the per-version forward programs.
+//
+// A token step is a fixed sequence of launches on the context's stream.  The T == 1 step
+// is captured once into a hipGraph per (state parity, logits) and replayed, so decode pays
+// no host launch cost.  Per-layer programs restate rwkv_graph.inc:
+//   v4  :84-197 + FFN :484-511      v5  :199-292 + FFN :484-511
+//   v6  :294-385 + FFN :513-531     v7  :387-482 + FFN :533-543
+#include "engine.hpp"
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <string>
+
+#include "kernels.hpp"
+
+namespace rwkvmi {
+
+// ------------------------------------------------------------------------- upload
+
+template <typename T>
+static T * dalloc(DeviceModel & dm, size_t n) {
+    void * p = nullptr;
+    if (hipMalloc(&p, n * sizeof(T) + 16) != hipSuccess) return nullptr;
+    dm.allocs.push_back(p);
+    return (T *)p;
+}
+
+static float * upload_vec(DeviceModel & dm, const HostTensor * t) {
+    if (!t) return nullptr;
+    const uint64_t n = t->nel();
+    std::vector<float> v(n);
+    if (t->type == W_F32) {
+        memcpy(v.data(), t->data.data(), n * 4);
+    } else if (t->type == W_F16) {
+        for (uint64_t i = 0; i < n; i++) {
+            uint16_t h;
+            memcpy(&h, t->data.data() + 2 * i, 2);
+            v[i] = f16_to_f32(h);
+        }
+    } else {
+        fprintf(stderr, "rwkv: parameter %s must be FP32/FP16\n", t->name.c_str());
+        return nullptr;
+    }
+    float * d = dalloc<float>(dm, n);
+    if (!d || hipMemcpy(d, v.data(), n * 4, hipMemcpyHostToDevice) != hipSuccess) return nullptr;
+    dm.small_param_bytes += (double)n * 4;
+    return d;
+}
+
+static float * upload_host_floats(DeviceModel & dm, const std::vector<float> & v) {
+    float * d = dalloc<float>(dm, v.size());
+    if (!d || hipMemcpy(d, v.data(), v.size() * 4, hipMemcpyHostToDevice) != hipSuccess) return nullptr;
+    dm.small_param_bytes += (double)v.size() * 4;
+    return d;
+}
+
+// Repack one ggml-order matrix ne=[K, M] into the device layout of common.hpp.
+static bool upload_mat(DeviceModel & dm, const HostTensor * t, DMat & out, bool count_bytes = true, bool is_head = false) {
+    if (!t) return true;
+    if (t->ndim != 2) {
+        fprintf(stderr, "rwkv: %s: matrix expected\n", t->name.c_str());
+        return false;
+    }
+    out.type = (int)t->type;
+    out.K = (int)t->ne[0];
+    out.M = (int)t->ne[1];
+    const size_t M = out.M, K = out.K;
+    if (t->type == W_F32 || t->type == W_F16) {
+        const size_t bytes = t->data.size();
+        uint8_t * d = dalloc<uint8_t>(dm, bytes);
+        if (!d || hipMemcpy(d, t->data.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) return false;
+        out.qs = d;
+    } else {
+        if (K % 32) {
+            fprintf(stderr, "rwkv: %s: K=%zu not a multiple of 32\n", t->name.c_str(), K);
+            return false;
+        }
+        const size_t nb = K / 32, nblk = M * nb, bb = type_block_bytes(t->type);
+        const size_t qbytes = (t->type == W_Q8_0) ? 32 : 16;
+        std::vector<uint8_t> qs(nblk * qbytes);
+        std::vector<uint32_t> qh;
+        std::vector<uint16_t> sc16;
+        std::vector<uint32_t> sc32;
+        const bool q5 = t->type == W_Q5_0 || t->type == W_Q5_1;
+        const bool one = t->type == W_Q4_1 || t->type == W_Q5_1;
+        if (q5) qh.resize(nblk);
+        if (one) sc32.resize(nblk); else sc16.resize(nblk);
+        const uint8_t * src = t->data.data();
+        for (size_t i = 0; i < nblk; i++) {
+            const uint8_t * b = src + i * bb;
+            uint16_t d, mm;
+            memcpy(&d, b, 2);
+            switch (t->type) {
+                case W_Q4_0: sc16[i] = d; memcpy(&qs[i * 16], b + 2, 16); break;
+                case W_Q4_1: memcpy(&mm, b + 2, 2); sc32[i] = (uint32_t)d | ((uint32_t)mm << 16); memcpy(&qs[i * 16], b + 4, 16); break;
+                case W_Q5_0: sc16[i] = d; memcpy(&qh[i], b + 2, 4); memcpy(&qs[i * 16], b + 6, 16); break;
+                case W_Q5_1: memcpy(&mm, b + 2, 2); sc32[i] = (uint32_t)d | ((uint32_t)mm << 16); memcpy(&qh[i], b + 4, 4); memcpy(&qs[i * 16], b + 8, 16); break;
+                case W_Q8_0: sc16[i] = d; memcpy(&qs[i * 32], b + 2, 32); break;
+                default: return false;
+            }
+        }
+        uint8_t * dq = dalloc<uint8_t>(dm, qs.size());
+        if (!dq || hipMemcpy(dq, qs.data(), qs.size(), hipMemcpyHostToDevice) != hipSuccess) return false;
+        out.qs = dq;
+        if (q5) {
+            uint32_t * dh = dalloc<uint32_t>(dm, qh.size());
+            if (!dh || hipMemcpy(dh, qh.data(), qh.size() * 4, hipMemcpyHostToDevice) != hipSuccess) return false;
+            out.qh = dh;
+        }
+        if (one) {
+            uint32_t * ds = dalloc<uint32_t>(dm, sc32.size());
+            if (!ds || hipMemcpy(ds, sc32.data(), sc32.size() * 4, hipMemcpyHostToDevice) != hipSuccess) return false;
+            out.sc = ds;
+        } else {
+            uint16_t * ds = dalloc<uint16_t>(dm, sc16.size());
+            if (!ds || hipMemcpy(ds, sc16.data(), sc16.size() * 2, hipMemcpyHostToDevice) != hipSuccess) return false;
+            out.sc = ds;
+        }
+    }
+    if (count_bytes) {
+        const double bytes = (double)type_nbytes(t->type, t->nel());
+        const double flops = 2.0 * (double)M * (double)K;
+        if (is_head) {
+            dm.head_weight_bytes += bytes;
+            dm.head_flops += flops;
+        } else {
+            dm.layer_weight_bytes += bytes;
+            dm.layer_flops += flops;
+        }
+    }
+    if (out.K > dm.kmax) dm.kmax = out.K;
+    return true;
+}
+
+bool upload_model(const ModelFile & mf, DeviceModel & dm) {
+    dm.n_vocab = mf.header.n_vocab;
+    dm.n_embed = mf.header.n_embed;
+    dm.n_layer = mf.header.n_layer;
+    dm.major = mf.arch_major;
+    dm.minor = mf.arch_minor;
+    dm.H = mf.head_count;
+    dm.S = mf.head_size;
+    const size_t C = dm.n_embed;
+    dm.state_len = dm.major >= 5 ? C * (2 + (size_t)dm.S) * dm.n_layer : C * 5 * dm.n_layer;
+    if (C % 64) {
+        fprintf(stderr, "rwkv: n_embed %zu must be a multiple of 64\n", C);
+        return false;
+    }
+    auto T = [&](const std::string & n) { return mf.find(n); };
+    if (!upload_mat(dm, T("emb.weight"), dm.emb, false)) return false;
+    if (!upload_mat(dm, T("head.weight"), dm.head, true, true)) return false;
+    if (!(dm.ln0_w = upload_vec(dm, T("blocks.0.ln0.weight"))) || !(dm.ln0_b = upload_vec(dm, T("blocks.0.ln0.bias"))) ||
+        !(dm.lnout_w = upload_vec(dm, T("ln_out.weight"))) || !(dm.lnout_b = upload_vec(dm, T("ln_out.bias"))))
+        return false;
+    dm.layers.resize(dm.n_layer);
+    for (uint32_t i = 0; i < dm.n_layer; i++) {
+        DLayer & L = dm.layers[i];
+        const std::string p = "blocks." + std::to_string(i) + ".";
+        auto V = [&](const char * n) { return upload_vec(dm, T(p + n)); };
+        auto Mt = [&](const char * n, DMat & d) { return upload_mat(dm, T(p + n), d); };
+        bool ok = (L.ln1_w = V("ln1.weight")) && (L.ln1_b = V("ln1.bias")) && (L.ln2_w = V("ln2.weight")) &&
+                  (L.ln2_b = V("ln2.bias"));
+        ok = ok && Mt("att.key.weight", L.att_k) && Mt("att.value.weight", L.att_v) &&
+             Mt("att.receptance.weight", L.att_r) && Mt("att.output.weight", L.att_o) &&
+             Mt("ffn.key.weight", L.ffn_k) && Mt("ffn.value.weight", L.ffn_v);
+        if (!ok) return false;
+        dm.F = L.ffn_k.M;
+        if (dm.major != 7 && !Mt("ffn.receptance.weight", L.ffn_r)) return false;
+        if (dm.major == 4 || dm.major == 5) {
+            ok = (L.att_mix_k = V("att.time_mix_k")) && (L.att_mix_v = V("att.time_mix_v")) &&
+                 (L.att_mix_r = V("att.time_mix_r")) && (L.ffn_mix_k = V("ffn.time_mix_k")) &&
+                 (L.ffn_mix_r = V("ffn.time_mix_r"));
+            if (!ok) return false;
+        }
+        if (dm.major == 4) {
+            if (!(L.att_first = V("att.time_first")) || !(L.att_decay = V("att.time_decay"))) return false;
+        }
+        if (dm.major >= 5) {
+            if (!(L.att_lnx_w = V("att.ln_x.weight")) || !(L.att_lnx_b = V("att.ln_x.bias"))) return false;
+        }
+        if (dm.major == 5) {
+            // wkv6 operands u and w expanded to [C] (5.1 repeats per head, rwkv_graph.inc:256-273)
+            const HostTensor * dec = T(p + "att.time_decay");
+            const HostTensor * fu = dm.minor >= 2 ? T(p + "att.time_faaaa") : T(p + "att.time_first");
+            std::vector<float> u(C), w(C);
+            const float * dd = (const float *)dec->data.data();
+            const float * ff = (const float *)fu->data.data();
+            if (dec->type != W_F32 || fu->type != W_F32) return false;
+            for (int64_t h = 0; h < dm.H; h++)
+                for (int64_t j = 0; j < dm.S; j++) {
+                    u[h * dm.S + j] = dm.minor >= 2 ? ff[h * dm.S + j] : ff[h];
+                    w[h * dm.S + j] = dm.minor >= 2 ? dd[h * dm.S + j] : dd[h];
+                }
+            if (!(L.att_u = upload_host_floats(dm, u)) || !(L.att_w = upload_host_floats(dm, w))) return false;
+            if (dm.minor >= 2) {
+                if (!(L.att_mix_g = V("att.time_mix_g")) || !Mt("att.gate.weight", L.att_g)) return false;
+            }
+        }
+        if (dm.major == 6) {
+            ok = (L.maa_x = V("att.time_maa_x")) && (L.maa[0] = V("att.time_maa_w")) && (L.maa[1] = V("att.time_maa_k")) &&
+                 (L.maa[2] = V("att.time_maa_v")) && (L.maa[3] = V("att.time_maa_r")) && (L.maa[4] = V("att.time_maa_g")) &&
+                 (L.maa_w2 = V("att.time_maa_w2")) && (L.att_u = V("att.time_faaaa")) && (L.decay6 = V("att.time_decay")) &&
+                 (L.ffn_maa_k = V("ffn.time_maa_k")) && (L.ffn_maa_r = V("ffn.time_maa_r"));
+            ok = ok && Mt("att.time_maa_w1", L.maa_w1) && Mt("att.time_decay_w1", L.decay_w1) &&
+                 Mt("att.time_decay_w2", L.decay_w2) && Mt("att.gate.weight", L.att_g);
+            if (!ok) return false;
+            dm.maa_D = (int)T(p + "att.time_maa_w2")->ne[0];
+            if (L.maa_w1.M != 5 * dm.maa_D) {
+                fprintf(stderr, "rwkv: unexpected time_maa_w1 shape\n");
+                return false;
+            }
+        }
+        if (dm.major == 7) {
+            ok = (L.x_rwkvag = V("att.x_rwkvag")) && (L.w0 = V("att.w0")) && (L.a0 = V("att.a0")) &&
+                 (L.k_k = V("att.k_k")) && (L.k_a = V("att.k_a")) && (L.r_k = V("att.r_k")) && (L.ffn_x_k = V("ffn.x_k"));
+            ok = ok && Mt("att.w1", L.w1) && Mt("att.w2", L.w2) && Mt("att.a1", L.a1) && Mt("att.a2", L.a2) &&
+                 Mt("att.g1", L.g1) && Mt("att.g2", L.g2);
+            if (ok && i != 0) ok = (L.v0 = V("att.v0")) && Mt("att.v1", L.v1) && Mt("att.v2", L.v2);
+            if (!ok) return false;
+        }
+    }
+    if (dm.H && dm.S > 64) {
+        fprintf(stderr, "rwkv: head size %lld > 64 unsupported\n", (long long)dm.S);
+        return false;
+    }
+    return hipDeviceSynchronize() == hipSuccess;
+}
+
+void free_model(DeviceModel & dm) {
+    for (void * p : dm.allocs) (void)hipFree(p);
+    dm.allocs.clear();
+}
+
+// ------------------------------------------------------------------------- engine
+
+__global__ void k_init_state(float * st, size_t n, int C, int v4) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float v = 0.0f;
+    if (v4) {
+        const size_t in_layer = i % (5 * (size_t)C);
+        if (in_layer >= 4 * (size_t)C) v = -1e30f;  // rwkv_eval.inc:224-241
+    }
+    st[i] = v;
+}
+
+Engine::~Engine() {
+    if (stream_) (void)hipStreamSynchronize(stream_);
+    for (auto & row : graphs_)
+        for (auto & g : row)
+            if (g) (void)hipGraphExecDestroy(g);
+    for (void * p : ws_allocs_) (void)hipFree(p);
+    if (htokens_) (void)hipHostFree(htokens_);
+    if (tok_event_) (void)hipEventDestroy(tok_event_);
+    if (stream_) (void)hipStreamDestroy(stream_);
+}
+
+bool Engine::init() {
+    HIP_OK(hipSetDevice(m_->device));
+    HIP_OK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    HIP_OK(hipEventCreateWithFlags(&tok_event_, hipEventDisableTiming));
+    HIP_OK(hipEventRecord(tok_event_, stream_));
+    for (int i = 0; i < 2; i++) {
+        HIP_OK(hipMalloc(&dstate_[i], m_->state_len * sizeof(float) + 16));
+        ws_allocs_.push_back(dstate_[i]);
+    }
+    HIP_OK(hipMalloc(&logits_, (size_t)m_->n_vocab * sizeof(float) + 16));
+    ws_allocs_.push_back(logits_);
+    const char * g = getenv("RWKV_MI355X_NO_GRAPH");
+    use_graphs_ = !(g && g[0] == '1');
+    return ensure_workspace(1) && init_state(dstate_[0]);
+}
+
+bool Engine::ensure_workspace(int T) {
+    if (T <= tcap_) return true;
+    HIP_OK(hipStreamSynchronize(stream_));
+    for (auto & row : graphs_)
+        for (auto & gr : row)
+            if (gr) {
+                (void)hipGraphExecDestroy(gr);
+                gr = nullptr;
+            }
+    // keep state and logits, drop the rest
+    std::vector<void *> keep = {dstate_[0], dstate_[1], logits_};
+    for (void * p : ws_allocs_) {
+        bool k = false;
+        for (void * q : keep) k |= (p == q);
+        if (!k) (void)hipFree(p);
+    }
+    ws_allocs_ = keep;
+    HIP_OK(hipEventSynchronize(tok_event_));
+    if (htokens_) {
+        (void)hipHostFree(htokens_);
+        htokens_ = nullptr;
+    }
+    int cap = 1;
+    while (cap < T) cap *= 2;
+    tcap_ = cap;
+    const size_t C = m_->n_embed, TC = (size_t)cap * C;
+    auto A = [&](size_t bytes) -> void * {
+        void * p = nullptr;
+        if (hipMalloc(&p, bytes + 64) != hipSuccess) return nullptr;
+        ws_allocs_.push_back(p);
+        return p;
+    };
+    float ** fbufs[] = {&x_, &xa_, &sx_, &r_, &k_, &v_, &g_, &w_, &y_, &a_, &nb_, &bb_, &vfirst_, &fr_};
+    for (float ** b : fbufs)
+        if (!(*b = (float *)A(TC * 4))) return false;
+    const size_t kmax = std::max<size_t>((size_t)m_->kmax, C);
+    if (!(lora_ = (float *)A((size_t)cap * kmax * 4))) return false;
+    if (!(bonus_ = (float *)A((size_t)cap * std::max<int64_t>(1, m_->H) * 4))) return false;
+    if (!(dtokens_ = (uint32_t *)A((size_t)cap * 4))) return false;
+    for (auto & s : slots_) {
+        const size_t n = (size_t)cap * kmax, nb = n / 32 + 1;
+        s.q = (int8_t *)A(n);
+        s.d = (float *)A(nb * 4);
+        s.s = (float *)A(nb * 4);
+        s.qsum = (int *)A(nb * 4);
+        s.h = (__half *)A(n * 2);
+        s.f = (float *)A(n * 4);
+        if (!s.q || !s.d || !s.s || !s.qsum || !s.h || !s.f) return false;
+    }
+    HIP_OK(hipHostMalloc((void **)&htokens_, (size_t)cap * 4, hipHostMallocDefault));
+    return true;
+}
+
+bool Engine::init_state(float * st) {
+    const size_t n = m_->state_len;
+    hipLaunchKernelGGL(k_init_state, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream_, st, n,
+                       (int)m_->n_embed, m_->major == 4 ? 1 : 0);
+    HIP_OK(hipGetLastError());
+    return true;
+}
+
+ActBuf Engine::Aview(int slot, int K, int fmt) const {
+    const ActSlot & s = slots_[slot];
+    ActBuf a;
+    a.fmt = fmt;
+    a.K = K;
+    a.f = s.f;
+    a.h = s.h;
+    a.q = s.q;
+    a.d = s.d;
+    a.s = s.s;
+    a.qsum = s.qsum;
+    return a;
+}
+
+ActBuf Engine::A(int slot, const DMat & W) const { return Aview(slot, W.K, act_fmt_for(W.type)); }
+
+// Collects matmul entries and launches them grouped by weight type.
+struct MMBatch {
+    std::vector<MMEntry> e;
+    void add(const DMat & W, const ActBuf & in, float * y, int ldy, int epi, const float * aux = nullptr,
+             const float * bias = nullptr, const ActBuf * out = nullptr) {
+        MMEntry m;
+        memset(&m, 0, sizeof(m));
+        m.W = W;
+        m.in = in;
+        m.y = y;
+        m.ldy = ldy;
+        m.aux = aux;
+        m.bias = bias;
+        m.epi = epi;
+        if (out) {
+            m.out = *out;
+            m.emit = 1;
+        }
+        e.push_back(m);
+    }
+    bool run(hipStream_t st, int T) {
+        std::vector<bool> done(e.size(), false);
+        for (size_t i = 0; i < e.size(); i++) {
+            if (done[i]) continue;
+            MMGroup g;
+            memset(&g, 0, sizeof(g));
+            g.T = T;
+            const int type = e[i].W.type;
+            for (size_t j = i; j < e.size() && g.n < MM_MAX_ENTRIES; j++) {
+                if (!done[j] && e[j].W.type == type) {
+                    g.e[g.n++] = e[j];
+                    done[j] = true;
+                }
+            }
+            if (!launch_mm_group(st, g, type)) return false;
+        }
+        e.clear();
+        return true;
+    }
+};
+
+bool Engine::ffn(int l, int T, const float * si, float * so) {
+    const DLayer & L = m_->layers[l];
+    const int C = (int)m_->n_embed;
+    LnMixArgs a;
+    memset(&a, 0, sizeof(a));
+    a.T = T;
+    a.C = C;
+    a.x = x_;
+    a.carry_in = si;        // ffn_xx at layer offset 0
+    a.carry_out = so;
+    a.lnw = L.ln2_w;
+    a.lnb = L.ln2_b;
+    MMBatch b;
+    if (m_->major == 7) {
+        // rwkv_graph.inc:533-543
+        a.form = 1;
+        a.n_out = 1;
+        a.mu[0] = L.ffn_x_k;
+        a.out[0] = A(0, L.ffn_k);
+        if (!launch_ln_mix(stream_, a)) return false;
+        ActBuf kin = A(1, L.ffn_v);
+        b.add(L.ffn_k, A(0, L.ffn_k), nullptr, 0, EPI_RELU_SQ, nullptr, nullptr, &kin);
+        if (!b.run(stream_, T)) return false;
+        b.add(L.ffn_v, kin, x_, C, EPI_ADD);
+        return b.run(stream_, T);
+    }
+    // v4/v5: rwkv_graph.inc:484-511 (form 0); v6: :513-531 (form 1)
+    a.form = m_->major == 6 ? 1 : 0;
+    a.n_out = 2;
+    a.mu[0] = m_->major == 6 ? L.ffn_maa_k : L.ffn_mix_k;
+    a.mu[1] = m_->major == 6 ? L.ffn_maa_r : L.ffn_mix_r;
+    a.out[0] = A(0, L.ffn_k);
+    a.out[1] = A(1, L.ffn_r);
+    if (!launch_ln_mix(stream_, a)) return false;
+    ActBuf kin = A(2, L.ffn_v);
+    b.add(L.ffn_r, A(1, L.ffn_r), fr_, C, EPI_STORE);
+    b.add(L.ffn_k, A(0, L.ffn_k), nullptr, 0, EPI_RELU_SQ, nullptr, nullptr, &kin);
+    if (!b.run(stream_, T)) return false;
+    b.add(L.ffn_v, kin, x_, C, EPI_SIGMUL_ADD, fr_);
+    return b.run(stream_, T);
+}
+
+bool Engine::layer_v4(int l, int T, const float * si, float * so) {
+    const DLayer & L = m_->layers[l];
+    const int C = (int)m_->n_embed;
+    LnMixArgs a;
+    memset(&a, 0, sizeof(a));
+    a.T = T;
+    a.C = C;
+    a.x = x_;
+    a.carry_in = si + C;
+    a.carry_out = so + C;
+    a.lnw = L.ln1_w;
+    a.lnb = L.ln1_b;
+    a.form = 0;
+    a.n_out = 3;
+    a.mu[0] = L.att_mix_k;
+    a.mu[1] = L.att_mix_v;
+    a.mu[2] = L.att_mix_r;
+    a.out[0] = A(0, L.att_k);
+    a.out[1] = A(1, L.att_v);
+    a.out[2] = A(2, L.att_r);
+    if (!launch_ln_mix(stream_, a)) return false;
+    MMBatch b;
+    b.add(L.att_r, A(2, L.att_r), r_, C, EPI_SIGMOID);
+    b.add(L.att_k, A(0, L.att_k), k_, C, EPI_STORE);
+    b.add(L.att_v, A(1, L.att_v), v_, C, EPI_STORE);
+    if (!b.run(stream_, T)) return false;
+    ActBuf o = A(3, L.att_o);
+    if (!launch_wkv4(stream_, T, C, r_, k_, v_, L.att_first, L.att_decay, si, so, o)) return false;
+    b.add(L.att_o, o, x_, C, EPI_ADD);
+    if (!b.run(stream_, T)) return false;
+    return ffn(l, T, si, so);
+}
+
+bool Engine::layer_v5(int l, int T, const float * si, float * so) {
+    const DLayer & L = m_->layers[l];
+    const int C = (int)m_->n_embed, H = (int)m_->H, S = (int)m_->S;
+    const bool v52 = m_->minor >= 2;
+    LnMixArgs a;
+    memset(&a, 0, sizeof(a));
+    a.T = T;
+    a.C = C;
+    a.x = x_;
+    a.carry_in = si + C;
+    a.carry_out = so + C;
+    a.lnw = L.ln1_w;
+    a.lnb = L.ln1_b;
+    a.form = 0;
+    a.n_out = v52 ? 4 : 3;
+    a.mu[0] = L.att_mix_k;
+    a.mu[1] = L.att_mix_v;
+    a.mu[2] = L.att_mix_r;
+    a.out[0] = A(0, L.att_k);
+    a.out[1] = A(1, L.att_v);
+    a.out[2] = A(2, L.att_r);
+    if (v52) {
+        a.mu[3] = L.att_mix_g;
+        a.out[3] = A(3, L.att_g);
+    }
+    if (!launch_ln_mix(stream_, a)) return false;
+    MMBatch b;
+    b.add(L.att_r, A(2, L.att_r), r_, C, EPI_STORE);
+    b.add(L.att_k, A(0, L.att_k), k_, C, EPI_STORE);
+    b.add(L.att_v, A(1, L.att_v), v_, C, EPI_STORE);
+    if (v52) b.add(L.att_g, A(3, L.att_g), g_, C, EPI_SILU);
+    if (!b.run(stream_, T)) return false;
+    if (!launch_wkv6(stream_, T, H, S, k_, v_, r_, L.att_u, L.att_w, 0, si + 2 * C, so + 2 * C, y_)) return false;
+    ActBuf o = A(4, L.att_o);
+    if (!launch_groupnorm(stream_, T, H, S, 1e-5f, y_, L.att_lnx_w, L.att_lnx_b, v52 ? 1 : 0, g_, nullptr, nullptr, o))
+        return false;
+    b.add(L.att_o, o, x_, C, EPI_ADD);
+    if (!b.run(stream_, T)) return false;
+    return ffn(l, T, si, so);
+}
+
+bool Engine::layer_v6(int l, int T, const float * si, float * so) {
+    const DLayer & L = m_->layers[l];
+    const int C = (int)m_->n_embed, H = (int)m_->H, S = (int)m_->S, D = m_->maa_D;
+    LnMixArgs a;
+    memset(&a, 0, sizeof(a));
+    a.T = T;
+    a.C = C;
+    a.x = x_;
+    a.carry_in = si + C;
+    a.carry_out = so + C;
+    a.lnw = L.ln1_w;
+    a.lnb = L.ln1_b;
+    a.form = 1;
+    a.n_out = 1;
+    a.mu[0] = L.maa_x;
+    a.out[0] = A(0, L.maa_w1);
+    a.out_xa = xa_;
+    a.out_sx = sx_;
+    if (!launch_ln_mix(stream_, a)) return false;
+    MMBatch b;
+    b.add(L.maa_w1, A(0, L.maa_w1), lora_, 5 * D, EPI_TANH);
+    if (!b.run(stream_, T)) return false;
+    // order w, k, v, r, g (rwkv_graph.inc:336-346)
+    ActBuf outs[5] = {A(1, L.decay_w1), A(2, L.att_k), A(3, L.att_v), A(4, L.att_r), A(5, L.att_g)};
+    if (!launch_v6_mix5(stream_, T, C, D, lora_, L.maa_w2, L.maa, xa_, sx_, outs)) return false;
+    ActBuf dl = A(6, L.decay_w2);
+    b.add(L.att_r, outs[3], r_, C, EPI_STORE);
+    b.add(L.att_k, outs[1], k_, C, EPI_STORE);
+    b.add(L.att_v, outs[2], v_, C, EPI_STORE);
+    b.add(L.att_g, outs[4], g_, C, EPI_SILU);
+    b.add(L.decay_w1, outs[0], nullptr, 0, EPI_TANH, nullptr, nullptr, &dl);
+    if (!b.run(stream_, T)) return false;
+    b.add(L.decay_w2, dl, w_, C, EPI_DECAY6, nullptr, L.decay6);
+    if (!b.run(stream_, T)) return false;
+    if (!launch_wkv6(stream_, T, H, S, k_, v_, r_, L.att_u, w_, 1, si + 2 * C, so + 2 * C, y_)) return false;
+    ActBuf o = A(7, L.att_o);
+    if (!launch_groupnorm(stream_, T, H, S, 64e-5f, y_, L.att_lnx_w, L.att_lnx_b, 1, g_, nullptr, nullptr, o)) return false;
+    b.add(L.att_o, o, x_, C, EPI_ADD);
+    if (!b.run(stream_, T)) return false;
+    return ffn(l, T, si, so);
+}
+
+bool Engine::layer_v7(int l, int T, const float * si, float * so) {
+    const DLayer & L = m_->layers[l];
+    const int C = (int)m_->n_embed, H = (int)m_->H, S = (int)m_->S;
+    LnMixArgs a;
+    memset(&a, 0, sizeof(a));
+    a.T = T;
+    a.C = C;
+    a.x = x_;
+    a.carry_in = si + C;
+    a.carry_out = so + C;
+    a.lnw = L.ln1_w;
+    a.lnb = L.ln1_b;
+    a.form = 1;
+    // order r, w, k, v, a, g (rwkv_graph.inc:404-413)
+    const DMat * cons[6] = {&L.att_r, &L.w1, &L.att_k, &L.att_v, &L.a1, &L.g1};
+    a.n_out = 6;
+    for (int n = 0; n < 6; n++) {
+        a.mu[n] = L.x_rwkvag + (size_t)n * C;
+        a.out[n] = A(n, *cons[n]);
+    }
+    const bool vlora = l != 0;
+    ActBuf xv1;
+    if (vlora) {
+        xv1 = A(9, L.v1);
+        if (xv1.fmt == a.out[3].fmt) {
+            xv1 = a.out[3];
+            xv1.K = L.v1.K;
+        } else {
+            // second emission of xv in the LoRA's input format; mix kernels take <= 6 outputs,
+            // so re-run the mix for this one vector
+            LnMixArgs a2 = a;
+            a2.n_out = 1;
+            a2.mu[0] = a.mu[3];
+            a2.out[0] = xv1;
+            a2.carry_out = nullptr;
+            if (!launch_ln_mix(stream_, a2)) return false;
+        }
+    }
+    if (!launch_ln_mix(stream_, a)) return false;
+    MMBatch b;
+    ActBuf lw = A(6, L.w2), la = A(7, L.a2), lg = A(8, L.g2);
+    b.add(L.att_r, a.out[0], r_, C, EPI_STORE);
+    b.add(L.att_k, a.out[2], k_, C, EPI_STORE);
+    b.add(L.att_v, a.out[3], v_, C, EPI_STORE);
+    b.add(L.w1, a.out[1], nullptr, 0, EPI_TANH, nullptr, nullptr, &lw);
+    b.add(L.a1, a.out[4], nullptr, 0, EPI_STORE, nullptr, nullptr, &la);
+    b.add(L.g1, a.out[5], nullptr, 0, EPI_SIGMOID, nullptr, nullptr, &lg);
+    ActBuf lvv;
+    if (vlora) {
+        lvv = A(10, L.v2);
+        b.add(L.v1, xv1, nullptr, 0, EPI_STORE, nullptr, nullptr, &lvv);
+    }
+    if (!b.run(stream_, T)) return false;
+    if (l == 0) {
+        HIP_OK(hipMemcpyAsync(vfirst_, v_, (size_t)T * C * 4, hipMemcpyDeviceToDevice, stream_));
+    }
+    b.add(L.w2, lw, w_, C, EPI_DECAY7, nullptr, L.w0);
+    b.add(L.a2, la, a_, C, EPI_SIGMOID_BIAS, nullptr, L.a0);
+    b.add(L.g2, lg, g_, C, EPI_STORE);
+    if (vlora) b.add(L.v2, lvv, v_, C, EPI_VMIX7, vfirst_, L.v0);
+    if (!b.run(stream_, T)) return false;
+    if (!launch_v7_prep(stream_, T, H, S, k_, a_, r_, L.k_k, L.k_a, L.r_k, nb_, bb_, bonus_)) return false;
+    if (!launch_wkv7(stream_, T, H, S, r_, w_, k_, v_, nb_, bb_, si + 2 * C, so + 2 * C, y_)) return false;
+    ActBuf o = A(0, L.att_o);
+    if (!launch_groupnorm(stream_, T, H, S, 64e-5f, y_, L.att_lnx_w, L.att_lnx_b, 2, g_, v_, bonus_, o)) return false;
+    b.add(L.att_o, o, x_, C, EPI_ADD);
+    if (!b.run(stream_, T)) return false;
+    return ffn(l, T, si, so);
+}
+
+bool Engine::forward(int T, const float * sin, float * sout, bool logits) {
+    const size_t C = m_->n_embed;
+    if (!launch_embed_ln(stream_, dtokens_, T, m_->emb, m_->ln0_w, m_->ln0_b, x_)) return false;
+    const size_t per_layer = m_->major >= 5 ? C * (2 + (size_t)m_->S) : 5 * C;
+    for (uint32_t l = 0; l < m_->n_layer; l++) {
+        const float * si = sin + l * per_layer;
+        float * so = sout + l * per_layer;
+        bool ok = false;
+        switch (m_->major) {
+            case 4: ok = layer_v4((int)l, T, si, so); break;
+            case 5: ok = layer_v5((int)l, T, si, so); break;
+            case 6: ok = layer_v6((int)l, T, si, so); break;
+            case 7: ok = layer_v7((int)l, T, si, so); break;
+            default: break;
+        }
+        if (!ok) return false;
+    }
+    if (logits) {
+        // rwkv_graph.inc:704-708 / :850-854
+        ActBuf hin = A(0, m_->head);
+        if (!launch_ln_emit(stream_, (int)C, x_ + (size_t)(T - 1) * C, m_->lnout_w, m_->lnout_b, hin)) return false;
+        MMBatch b;
+        b.add(m_->head, hin, logits_, (int)m_->n_vocab, EPI_STORE);
+        if (!b.run(stream_, 1)) return false;
+    }
+    return true;
+}
+
+// Runs T tokens from dstate_[cur_] (ping-pong), chunked by the workspace capacity.
+bool Engine::run_tokens(const uint32_t * tokens, size_t T, bool want_logits) {
+    const size_t kChunkMax = 1024;
+    size_t done = 0;
+    while (done < T) {
+        const size_t n = std::min(T - done, kChunkMax);
+        const bool last = done + n == T;
+        if (!ensure_workspace((int)n)) return false;
+        // the pinned token buffer may still feed the previous (async) call's copy
+        HIP_OK(hipEventSynchronize(tok_event_));
+        memcpy(htokens_, tokens + done, n * 4);
+        HIP_OK(hipMemcpyAsync(dtokens_, htokens_, n * 4, hipMemcpyHostToDevice, stream_));
+        HIP_OK(hipEventRecord(tok_event_, stream_));
+        const bool lg = last && want_logits;
+        if (n == 1 && use_graphs_) {
+            hipGraphExec_t & ge = graphs_[cur_][lg ? 1 : 0];
+            if (!ge) {
+                hipGraph_t g = nullptr;
+                HIP_OK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
+                const bool ok = forward(1, dstate_[cur_], dstate_[cur_ ^ 1], lg);
+                HIP_OK(hipStreamEndCapture(stream_, &g));
+                if (!ok) {
+                    (void)hipGraphDestroy(g);
+                    return false;
+                }
+                HIP_OK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+                (void)hipGraphDestroy(g);
+            }
+            HIP_OK(hipGraphLaunch(ge, stream_));
+        } else {
+            if (!forward((int)n, dstate_[cur_], dstate_[cur_ ^ 1], lg)) return false;
+        }
+        // tokens buffer is reused by the next chunk: wait before overwriting the pinned copy
+        if (!last) HIP_OK(hipStreamSynchronize(stream_));
+        cur_ ^= 1;
+        done += n;
+    }
+    return true;
+}
+
+bool Engine::state_upload(const float * state) {
+    if (state) {
+        HIP_OK(hipMemcpyAsync(dstate_[cur_], state, m_->state_len * 4, hipMemcpyHostToDevice, stream_));
+        return true;
+    }
+    return init_state(dstate_[cur_]);
+}
+
+bool Engine::state_download(float * state) {
+    HIP_OK(hipMemcpyAsync(state, dstate_[cur_], m_->state_len * 4, hipMemcpyDeviceToHost, stream_));
+    HIP_OK(hipStreamSynchronize(stream_));
+    return true;
+}
+
+bool Engine::sync() {
+    HIP_OK(hipStreamSynchronize(stream_));
+    return true;
+}
+
+bool Engine::eval(const uint32_t * tokens, size_t T, const float * state_in, float * state_out, float * logits_out) {
+    HIP_OK(hipSetDevice(m_->device));
+    if (!state_upload(state_in)) return false;
+    if (!run_tokens(tokens, T, logits_out != nullptr)) return false;
+    if (logits_out)
+        HIP_OK(hipMemcpyAsync(logits_out, logits_, (size_t)m_->n_vocab * 4, hipMemcpyDeviceToHost, stream_));
+    if (state_out)
+        HIP_OK(hipMemcpyAsync(state_out, dstate_[cur_], m_->state_len * 4, hipMemcpyDeviceToHost, stream_));
+    HIP_OK(hipStreamSynchronize(stream_));
+    return true;
+}
+
+bool Engine::eval_device(const uint32_t * tokens, size_t T, float * logits_out, bool sync_after) {
+    HIP_OK(hipSetDevice(m_->device));
+    if (!run_tokens(tokens, T, logits_out != nullptr)) return false;
+    if (logits_out)
+        HIP_OK(hipMemcpyAsync(logits_out, logits_, (size_t)m_->n_vocab * 4, hipMemcpyDeviceToHost, stream_));
+    if (sync_after || logits_out) HIP_OK(hipStreamSynchronize(stream_));
+    return true;
+}
+
+}  // namespace rwkvmi

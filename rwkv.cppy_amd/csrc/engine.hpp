@@ -1,0 +1,109 @@
+// engine.hpp -- device-resident RWKV model and the per-version forward programs.
+#pragma once
+
+#include <vector>
+
+#include "common.hpp"
+#include "model_file.hpp"
+
+namespace rwkvmi {
+
+struct DLayer {
+    float *ln1_w = nullptr, *ln1_b = nullptr, *ln2_w = nullptr, *ln2_b = nullptr;
+    // v4 / v5
+    float *att_mix_k = nullptr, *att_mix_v = nullptr, *att_mix_r = nullptr, *att_mix_g = nullptr;
+    float *att_first = nullptr, *att_decay = nullptr;  // v4 (per channel)
+    float *att_u = nullptr, *att_w = nullptr;          // v5/v6 wkv6 u (faaaa/first) and v5 w, expanded to [C]
+    float *att_lnx_w = nullptr, *att_lnx_b = nullptr;
+    // v6
+    float *maa_x = nullptr, *maa[5] = {nullptr, nullptr, nullptr, nullptr, nullptr}, *maa_w2 = nullptr;
+    float *decay6 = nullptr;
+    // v7
+    float *x_rwkvag = nullptr, *w0 = nullptr, *a0 = nullptr, *v0 = nullptr, *k_k = nullptr, *k_a = nullptr, *r_k = nullptr;
+    // ffn
+    float *ffn_mix_k = nullptr, *ffn_mix_r = nullptr, *ffn_maa_k = nullptr, *ffn_maa_r = nullptr, *ffn_x_k = nullptr;
+    DMat att_r{}, att_k{}, att_v{}, att_o{}, att_g{}, maa_w1{}, decay_w1{}, decay_w2{};
+    DMat w1{}, w2{}, a1{}, a2{}, g1{}, g2{}, v1{}, v2{};
+    DMat ffn_k{}, ffn_v{}, ffn_r{};
+};
+
+struct DeviceModel {
+    int refcount = 0;
+    int device = 0;
+    uint32_t n_vocab = 0, n_embed = 0, n_layer = 0;
+    int major = 4, minor = 0;
+    int64_t H = 0, S = 0;
+    int F = 0;          // FFN width
+    int maa_D = 0;      // v6 maa LoRA width (per mix)
+    int kmax = 0;       // largest matmul K
+    size_t state_len = 0;
+    DMat emb{}, head{};
+    float *ln0_w = nullptr, *ln0_b = nullptr, *lnout_w = nullptr, *lnout_b = nullptr;
+    std::vector<DLayer> layers;
+    std::vector<void *> allocs;
+    double layer_weight_bytes = 0;   // algorithmic bytes of all layer matrices (original block sizes)
+    double head_weight_bytes = 0;
+    double layer_flops = 0, head_flops = 0;  // 2*M*K per token
+    double small_param_bytes = 0;    // fp32 vectors read per token
+};
+
+bool upload_model(const ModelFile & mf, DeviceModel & dm);
+void free_model(DeviceModel & dm);
+
+struct ActSlot {
+    int8_t * q = nullptr;
+    float * d = nullptr;
+    float * s = nullptr;
+    int * qsum = nullptr;
+    __half * h = nullptr;
+    float * f = nullptr;
+};
+
+class Engine {
+  public:
+    explicit Engine(DeviceModel * m) : m_(m) {}
+    ~Engine();
+
+    bool init();
+    // ABI-level evaluation (host buffers).  tokens host, T >= 1.
+    bool eval(const uint32_t * tokens, size_t T, const float * state_in, float * state_out, float * logits_out);
+    // device-resident evaluation on the context's own state
+    bool eval_device(const uint32_t * tokens, size_t T, float * logits_out, bool sync);
+    bool state_upload(const float * state);
+    bool state_download(float * state);
+    bool sync();
+    hipStream_t stream() const { return stream_; }
+    float * device_state() const { return dstate_[cur_]; }
+
+  private:
+    bool ensure_workspace(int T);
+    bool init_state(float * st);
+    bool forward(int T, const float * sin, float * sout, bool logits);
+    bool run_tokens(const uint32_t * tokens, size_t T, bool want_logits);
+    bool layer_v4(int l, int T, const float * si, float * so);
+    bool layer_v5(int l, int T, const float * si, float * so);
+    bool layer_v6(int l, int T, const float * si, float * so);
+    bool layer_v7(int l, int T, const float * si, float * so);
+    bool ffn(int l, int T, const float * si, float * so);
+    ActBuf A(int slot, const DMat & W) const;
+    ActBuf Aview(int slot, int K, int fmt) const;
+
+    DeviceModel * m_;
+    hipStream_t stream_ = nullptr;
+    int tcap_ = 0;
+    std::vector<void *> ws_allocs_;
+    float *x_ = nullptr, *xa_ = nullptr, *sx_ = nullptr, *r_ = nullptr, *k_ = nullptr, *v_ = nullptr, *g_ = nullptr;
+    float *w_ = nullptr, *y_ = nullptr, *a_ = nullptr, *nb_ = nullptr, *bb_ = nullptr, *vfirst_ = nullptr;
+    float *fr_ = nullptr, *lora_ = nullptr, *bonus_ = nullptr, *logits_ = nullptr;
+    uint32_t * dtokens_ = nullptr;
+    uint32_t * htokens_ = nullptr;  // pinned
+    static constexpr int kSlots = 12;
+    ActSlot slots_[kSlots];
+    float * dstate_[2] = {nullptr, nullptr};
+    int cur_ = 0;
+    hipGraphExec_t graphs_[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // [cur][logits]
+    bool use_graphs_ = true;
+    hipEvent_t tok_event_ = nullptr;
+};
+
+}  // namespace rwkvmi

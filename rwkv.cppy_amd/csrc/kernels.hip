@@ -1,0 +1,758 @@
+// kernels.hip -- gfx950 kernels for the RWKV eval hot path.
+//
+// Numerics mirror the reference's CPU path (rwkv_graph.inc + ggml CPU ops), restated in
+// oracle/oracle.c, and are compiled with -ffp-contract=off so every multiply/add rounds
+// where the reference rounds; fused multiply-adds appear only where ggml's x86 kernels use
+// them (the quantized block accumulation).
+#include "kernels.hpp"
+
+#include <stdio.h>
+
+namespace rwkvmi {
+
+// --------------------------------------------------------------------------- helpers
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// sum over groups of `width` adjacent lanes (width power of two <= 64); all lanes get the sum
+template <typename T>
+__device__ __forceinline__ T group_sum(T v, int width) {
+    for (int o = width >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// deterministic block sum (fixed tree): every thread returns the total
+__device__ double block_sum_d(double v, double * sh) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+    v = wave_sum(v);
+    if (lane == 0) sh[wave] = v;
+    __syncthreads();
+    double r = 0.0;
+    for (int w = 0; w < nw; w++) r += sh[w];
+    __syncthreads();
+    return r;
+}
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+__device__ __forceinline__ float siluf_(float x) { return x / (1.0f + expf(-x)); }
+
+__device__ __forceinline__ float h2f(uint16_t b) { return __half2float(__ushort_as_half(b)); }
+__device__ __forceinline__ float f16_round(float f) { return __half2float(__float2half(f)); }
+
+// Emit one element per lane into an activation buffer.  The 32 lanes of each half-wave must
+// hold the 32 consecutive elements of one block (k & 31 == lane & 31) of the same row t, and
+// all 32 must call (block-uniform control flow).  Mirrors ggml quantize_row_q8_0/q8_1 (x86):
+// d = amax/127 (fp16), q = rint(x * 127/amax), s = fp16(d * sum q).
+__device__ __forceinline__ void emit32(const ActBuf & a, int t, int k, float v) {
+    const size_t idx = (size_t)t * a.K + k;
+    if (a.fmt == A_F32) {
+        a.f[idx] = v;
+        return;
+    }
+    if (a.fmt == A_F16) {
+        a.h[idx] = __float2half(v);
+        return;
+    }
+    float am = fabsf(v);
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) am = fmaxf(am, __shfl_xor(am, o, 32));
+    const float d = am / 127.f;
+    const float id = (am != 0.0f) ? 127.f / am : 0.0f;
+    const int q = (int)rintf(v * id);
+    int sum = q;
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 32);
+    a.q[idx] = (int8_t)q;
+    if ((k & 31) == 0) {
+        const size_t bi = (size_t)t * (a.K >> 5) + (k >> 5);
+        a.d[bi] = f16_round(d);
+        a.qsum[bi] = sum;
+        if (a.fmt == A_Q8_1) a.s[bi] = f16_round(d * (float)sum);
+    }
+}
+
+// --------------------------------------------------------------------------- matmul
+// One workgroup = 4 waves; each wave owns RPW consecutive rows; lanes stride over the K
+// blocks of a row (lane l reads block l, l+64, ...: one 16-byte dwordx4 of nibbles per lane,
+// 1 KiB per wave-instruction, fully coalesced).  Per 32-block: integer v_dot4 of the weight
+// ints with the Q8 activation ints, then acc = fma(d_w * d_x, sumi, acc) (ggml x86 order);
+// the m*s terms of the _1 formats go to a second accumulator added at the end.
+
+__device__ __forceinline__ uint32_t spread4(uint32_t x) {
+    // bit k of x (k<4) -> bit 4 of byte k
+    return ((x & 1u) << 4) | ((x & 2u) << 11) | ((x & 4u) << 18) | ((x & 8u) << 25);
+}
+
+template <int WF>
+__device__ __forceinline__ int block_dot(const DMat & W, int row, int b, int nb, const int4 & alo,
+                                         const int4 & ahi, int qsum, float & dw, float & mw) {
+    const size_t bi = (size_t)row * nb + b;
+    int sumi = 0;
+    if constexpr (WF == W_Q8_0) {
+        const int4 * p = (const int4 *)(W.qs + bi * 32);
+        const int4 w0 = p[0], w1 = p[1];
+        sumi = __builtin_amdgcn_sdot4(w0.x, alo.x, sumi, false);
+        sumi = __builtin_amdgcn_sdot4(w0.y, alo.y, sumi, false);
+        sumi = __builtin_amdgcn_sdot4(w0.z, alo.z, sumi, false);
+        sumi = __builtin_amdgcn_sdot4(w0.w, alo.w, sumi, false);
+        sumi = __builtin_amdgcn_sdot4(w1.x, ahi.x, sumi, false);
+        sumi = __builtin_amdgcn_sdot4(w1.y, ahi.y, sumi, false);
+        sumi = __builtin_amdgcn_sdot4(w1.z, ahi.z, sumi, false);
+        sumi = __builtin_amdgcn_sdot4(w1.w, ahi.w, sumi, false);
+        dw = h2f(((const uint16_t *)W.sc)[bi]);
+        mw = 0.0f;
+        (void)qsum;
+        return sumi;
+    } else {
+        const int4 w = *(const int4 *)(W.qs + bi * 16);
+        uint32_t lo0 = (uint32_t)w.x & 0x0F0F0F0Fu, lo1 = (uint32_t)w.y & 0x0F0F0F0Fu;
+        uint32_t lo2 = (uint32_t)w.z & 0x0F0F0F0Fu, lo3 = (uint32_t)w.w & 0x0F0F0F0Fu;
+        uint32_t hi0 = ((uint32_t)w.x >> 4) & 0x0F0F0F0Fu, hi1 = ((uint32_t)w.y >> 4) & 0x0F0F0F0Fu;
+        uint32_t hi2 = ((uint32_t)w.z >> 4) & 0x0F0F0F0Fu, hi3 = ((uint32_t)w.w >> 4) & 0x0F0F0F0Fu;
+        if constexpr (WF == W_Q5_0 || WF == W_Q5_1) {
+            const uint32_t qh = W.qh[bi];
+            lo0 |= spread4(qh & 0xF);
+            lo1 |= spread4((qh >> 4) & 0xF);
+            lo2 |= spread4((qh >> 8) & 0xF);
+            lo3 |= spread4((qh >> 12) & 0xF);
+            hi0 |= spread4((qh >> 16) & 0xF);
+            hi1 |= spread4((qh >> 20) & 0xF);
+            hi2 |= spread4((qh >> 24) & 0xF);
+            hi3 |= spread4((qh >> 28) & 0xF);
+        }
+        sumi = __builtin_amdgcn_sdot4((int)lo0, alo.x, sumi, false);
+        sumi = __builtin_amdgcn_sdot4((int)lo1, alo.y, sumi, false);
+        sumi = __builtin_amdgcn_sdot4((int)lo2, alo.z, sumi, false);
+        sumi = __builtin_amdgcn_sdot4((int)lo3, alo.w, sumi, false);
+        sumi = __builtin_amdgcn_sdot4((int)hi0, ahi.x, sumi, false);
+        sumi = __builtin_amdgcn_sdot4((int)hi1, ahi.y, sumi, false);
+        sumi = __builtin_amdgcn_sdot4((int)hi2, ahi.z, sumi, false);
+        sumi = __builtin_amdgcn_sdot4((int)hi3, ahi.w, sumi, false);
+        if constexpr (WF == W_Q4_0) {
+            sumi -= 8 * qsum;
+        } else if constexpr (WF == W_Q5_0) {
+            sumi -= 16 * qsum;
+        }
+        if constexpr (WF == W_Q4_1 || WF == W_Q5_1) {
+            const uint32_t dm = ((const uint32_t *)W.sc)[bi];
+            dw = h2f((uint16_t)(dm & 0xFFFF));
+            mw = h2f((uint16_t)(dm >> 16));
+        } else {
+            dw = h2f(((const uint16_t *)W.sc)[bi]);
+            mw = 0.0f;
+        }
+        return sumi;
+    }
+}
+
+typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
+
+template <int WF, int RPW, int NT>
+__device__ __forceinline__ void mm_accumulate(const MMEntry & E, int row0, int t0, int T, int lane,
+                                              float (&acc)[RPW][NT], float (&acc2)[RPW][NT]) {
+    const DMat & W = E.W;
+    const int K = W.K, M = W.M;
+    if constexpr (WF == W_F32) {
+        for (int k = lane * 4; k < K; k += 256) {
+            float4 x[NT];
+#pragma unroll
+            for (int n = 0; n < NT; n++)
+                x[n] = (t0 + n < T) ? *(const float4 *)(E.in.f + (size_t)(t0 + n) * K + k) : make_float4(0, 0, 0, 0);
+#pragma unroll
+            for (int r = 0; r < RPW; r++) {
+                const int row = row0 + r;
+                if (row < M) {
+                    const float4 w = *(const float4 *)((const float *)W.qs + (size_t)row * K + k);
+#pragma unroll
+                    for (int n = 0; n < NT; n++) {
+                        float a = acc[r][n];
+                        a = fmaf(w.x, x[n].x, a);
+                        a = fmaf(w.y, x[n].y, a);
+                        a = fmaf(w.z, x[n].z, a);
+                        a = fmaf(w.w, x[n].w, a);
+                        acc[r][n] = a;
+                    }
+                }
+            }
+        }
+    } else if constexpr (WF == W_F16) {
+        for (int k = lane * 8; k < K; k += 512) {
+            int4 x[NT];
+#pragma unroll
+            for (int n = 0; n < NT; n++)
+                x[n] = (t0 + n < T) ? *(const int4 *)(E.in.h + (size_t)(t0 + n) * K + k) : make_int4(0, 0, 0, 0);
+#pragma unroll
+            for (int r = 0; r < RPW; r++) {
+                const int row = row0 + r;
+                if (row < M) {
+                    const int4 w = *(const int4 *)((const __half *)W.qs + (size_t)row * K + k);
+#pragma unroll
+                    for (int n = 0; n < NT; n++) {
+                        float a = acc[r][n];
+                        a = __builtin_amdgcn_fdot2(__builtin_bit_cast(half2_t, w.x), __builtin_bit_cast(half2_t, x[n].x), a, false);
+                        a = __builtin_amdgcn_fdot2(__builtin_bit_cast(half2_t, w.y), __builtin_bit_cast(half2_t, x[n].y), a, false);
+                        a = __builtin_amdgcn_fdot2(__builtin_bit_cast(half2_t, w.z), __builtin_bit_cast(half2_t, x[n].z), a, false);
+                        a = __builtin_amdgcn_fdot2(__builtin_bit_cast(half2_t, w.w), __builtin_bit_cast(half2_t, x[n].w), a, false);
+                        acc[r][n] = a;
+                    }
+                }
+            }
+        }
+    } else {
+        const int nb = K >> 5;
+        for (int b = lane; b < nb; b += 64) {
+            int4 alo[NT], ahi[NT];
+            float dx[NT], sx[NT];
+            int qs[NT];
+#pragma unroll
+            for (int n = 0; n < NT; n++) {
+                if (t0 + n < T) {
+                    const int4 * ap = (const int4 *)(E.in.q + (size_t)(t0 + n) * K + (size_t)b * 32);
+                    alo[n] = ap[0];
+                    ahi[n] = ap[1];
+                    const size_t bi = (size_t)(t0 + n) * nb + b;
+                    dx[n] = E.in.d[bi];
+                    qs[n] = E.in.qsum[bi];
+                    sx[n] = (WF == W_Q4_1 || WF == W_Q5_1) ? E.in.s[bi] : 0.0f;
+                } else {
+                    alo[n] = make_int4(0, 0, 0, 0);
+                    ahi[n] = alo[n];
+                    dx[n] = 0.0f;
+                    qs[n] = 0;
+                    sx[n] = 0.0f;
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < RPW; r++) {
+                const int row = row0 + r;
+                if (row < M) {
+#pragma unroll
+                    for (int n = 0; n < NT; n++) {
+                        float dw, mw;
+                        const int sumi = block_dot<WF>(W, row, b, nb, alo[n], ahi[n], qs[n], dw, mw);
+                        acc[r][n] = fmaf(dw * dx[n], (float)sumi, acc[r][n]);
+                        if constexpr (WF == W_Q4_1 || WF == W_Q5_1) acc2[r][n] += mw * sx[n];
+                    }
+                }
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ float apply_epi(const MMEntry & E, int t, int row, float acc) {
+    const size_t yi = (size_t)t * E.ldy + row;
+    switch (E.epi) {
+        case EPI_SIGMOID: return sigmoidf_(acc);
+        case EPI_TANH: return tanhf(acc);
+        case EPI_SILU: return siluf_(acc);
+        case EPI_RELU_SQ: {
+            const float r = acc > 0.0f ? acc : 0.0f;
+            return r * r;
+        }
+        case EPI_ADD: return E.y[yi] + acc;
+        case EPI_SIGMUL_ADD: return E.y[yi] + sigmoidf_(E.aux[yi]) * acc;
+        case EPI_DECAY6: return expf(-expf(acc + E.bias[row]));
+        case EPI_DECAY7: return expf(sigmoidf_(acc + E.bias[row]) * -0.606531f);
+        case EPI_SIGMOID_BIAS: return sigmoidf_(acc + E.bias[row]);
+        case EPI_VMIX7: {
+            const float v = E.y[yi];
+            return v + (E.aux[yi] - v) * sigmoidf_(acc + E.bias[row]);
+        }
+        default: return acc;
+    }
+}
+
+template <int WF, int RPW, int NT>
+__global__ __launch_bounds__(256) void k_mm(MMGroup g) {
+    constexpr int RW = 4 * RPW;  // rows per workgroup
+    __shared__ float red[NT][RW];
+    __shared__ float red2[NT][RW];
+    int e = 0;
+#pragma unroll 1
+    while (e + 1 < g.n && (int)blockIdx.x >= g.e[e + 1].block0) e++;
+    const MMEntry & E = g.e[e];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int rowwg = ((int)blockIdx.x - E.block0) * RW;
+    const int row0 = rowwg + wave * RPW;
+    const int T = g.T;
+    for (int t0 = 0; t0 < T; t0 += NT) {
+        float acc[RPW][NT], acc2[RPW][NT];
+#pragma unroll
+        for (int r = 0; r < RPW; r++)
+#pragma unroll
+            for (int n = 0; n < NT; n++) acc[r][n] = acc2[r][n] = 0.0f;
+        mm_accumulate<WF, RPW, NT>(E, row0, t0, T, lane, acc, acc2);
+#pragma unroll
+        for (int r = 0; r < RPW; r++)
+#pragma unroll
+            for (int n = 0; n < NT; n++) {
+                const float s = wave_sum(acc[r][n]);
+                float s2 = 0.0f;
+                if constexpr (WF == W_Q4_1 || WF == W_Q5_1) s2 = wave_sum(acc2[r][n]);
+                if (lane == 0) {
+                    red[n][wave * RPW + r] = s;
+                    red2[n][wave * RPW + r] = s2;
+                }
+            }
+        __syncthreads();
+        const int tid = threadIdx.x;
+        if (tid < RW * NT) {
+            const int n = tid / RW, r = tid % RW;
+            const int t = t0 + n, row = rowwg + r;
+            // (t < T) is uniform across each 32-lane half-wave since RW is a multiple of 32
+            // whenever emission is used (RPW == 8).
+            if (t < T) {
+                const float acc_v = red[n][r] + red2[n][r];
+                float v = 0.0f;
+                if (row < E.W.M) {
+                    v = apply_epi(E, t, row, acc_v);
+                    if (E.y) E.y[(size_t)t * E.ldy + row] = v;
+                }
+                if (E.emit) emit32(E.out, t, row, v);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+template <int WF>
+static bool launch_mm_wf(hipStream_t st, MMGroup & g) {
+    bool emit = false;
+    for (int i = 0; i < g.n; i++) emit |= g.e[i].emit != 0;
+    const int T = g.T;
+    // Emission needs 32 rows per workgroup (one quantization block per half-wave).
+    const int rpw = emit ? 8 : 2;
+    const int rw = 4 * rpw;
+    int blocks = 0;
+    for (int i = 0; i < g.n; i++) {
+        if (g.e[i].emit && (g.e[i].W.M % 32 != 0)) {
+            fprintf(stderr, "rwkv: emitting matmul needs M %% 32 == 0 (M=%d)\n", g.e[i].W.M);
+            return false;
+        }
+        if (g.e[i].W.K % 32 != 0) {
+            fprintf(stderr, "rwkv: matmul needs K %% 32 == 0 (K=%d)\n", g.e[i].W.K);
+            return false;
+        }
+        g.e[i].block0 = blocks;
+        blocks += (g.e[i].W.M + rw - 1) / rw;
+    }
+    if (blocks == 0) return true;
+    dim3 grid(blocks), block(256);
+    if (T == 1) {
+        if (emit) hipLaunchKernelGGL((k_mm<WF, 8, 1>), grid, block, 0, st, g);
+        else hipLaunchKernelGGL((k_mm<WF, 2, 1>), grid, block, 0, st, g);
+    } else {
+        if (emit) hipLaunchKernelGGL((k_mm<WF, 8, 4>), grid, block, 0, st, g);
+        else hipLaunchKernelGGL((k_mm<WF, 2, 4>), grid, block, 0, st, g);
+    }
+    HIP_OK(hipGetLastError());
+    return true;
+}
+
+bool launch_mm_group(hipStream_t st, MMGroup & g, int wtype) {
+    switch (wtype) {
+        case W_F32: return launch_mm_wf<W_F32>(st, g);
+        case W_F16: return launch_mm_wf<W_F16>(st, g);
+        case W_Q4_0: return launch_mm_wf<W_Q4_0>(st, g);
+        case W_Q4_1: return launch_mm_wf<W_Q4_1>(st, g);
+        case W_Q5_0: return launch_mm_wf<W_Q5_0>(st, g);
+        case W_Q5_1: return launch_mm_wf<W_Q5_1>(st, g);
+        case W_Q8_0: return launch_mm_wf<W_Q8_0>(st, g);
+        default:
+            fprintf(stderr, "rwkv: unsupported weight type %d\n", wtype);
+            return false;
+    }
+}
+
+// --------------------------------------------------------------------------- LayerNorm family
+
+// ggml_norm statistics with double accumulation (mean, 1/sqrt(var + eps))
+__device__ void ln_stats(const float * x, int C, float eps, float & mean, float & scale, double * sh) {
+    double s = 0.0;
+    for (int c = threadIdx.x; c < C; c += blockDim.x) s += (double)x[c];
+    s = block_sum_d(s, sh);
+    mean = (float)(s / (double)C);
+    double s2 = 0.0;
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+        const float v = x[c] - mean;
+        s2 += (double)(v * v);
+    }
+    s2 = block_sum_d(s2, sh);
+    const float var = (float)(s2 / (double)C);
+    scale = 1.0f / sqrtf(var + eps);
+}
+
+__device__ __forceinline__ float ln_apply(float x, float mean, float scale, float w, float b) {
+    float y = (x - mean) * scale;
+    y = y * w;
+    return y + b;
+}
+
+__global__ __launch_bounds__(256) void k_embed_ln(const uint32_t * tokens, DMat emb, const float * w,
+                                                  const float * b, float * x) {
+    __shared__ double sh[8];
+    const int t = blockIdx.x, C = emb.K;
+    const size_t tok = tokens[t];
+    float * xr = x + (size_t)t * C;
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+        xr[c] = emb.type == W_F16 ? __half2float(((const __half *)emb.qs)[tok * C + c])
+                                  : ((const float *)emb.qs)[tok * C + c];
+    }
+    __syncthreads();
+    float mean, scale;
+    ln_stats(xr, C, 1e-5f, mean, scale, sh);
+    for (int c = threadIdx.x; c < C; c += blockDim.x) xr[c] = ln_apply(xr[c], mean, scale, w[c], b[c]);
+}
+
+bool launch_embed_ln(hipStream_t st, const uint32_t * tokens, int T, const DMat & emb, const float * w,
+                     const float * b, float * x) {
+    hipLaunchKernelGGL(k_embed_ln, dim3(T), dim3(256), 0, st, tokens, emb, w, b, x);
+    HIP_OK(hipGetLastError());
+    return true;
+}
+
+// rwkv_carry_x (rwkv_graph.inc:56-82) + the token-shift mixes of each version.
+__global__ __launch_bounds__(256) void k_ln_mix(LnMixArgs a) {
+    __shared__ double sh[8];
+    const int t = blockIdx.x, C = a.C;
+    const float * xt = a.x + (size_t)t * C;
+    float mean, scale, pmean = 0.0f, pscale = 0.0f;
+    ln_stats(xt, C, 1e-5f, mean, scale, sh);
+    if (t > 0) ln_stats(xt - C, C, 1e-5f, pmean, pscale, sh);
+    for (int c0 = 0; c0 < C; c0 += blockDim.x) {
+        const int c = c0 + threadIdx.x;
+        if (c0 + (int)(threadIdx.x & ~63) >= C) continue;  // whole wave out of range (C % 64 == 0)
+        const float xa = ln_apply(xt[c], mean, scale, a.lnw[c], a.lnb[c]);
+        const float xp = (t > 0) ? ln_apply(xt[c - C], pmean, pscale, a.lnw[c], a.lnb[c]) : a.carry_in[c];
+        if (t == a.T - 1 && a.carry_out) a.carry_out[c] = xa;
+        if (a.out_xa) a.out_xa[(size_t)t * C + c] = xa;
+        if (a.out_sx) a.out_sx[(size_t)t * C + c] = xp - xa;
+        for (int n = 0; n < a.n_out; n++) {
+            const float mu = a.mu[n][c];
+            float v;
+            if (a.form == 0) {
+                v = xa * mu + (xp - xp * mu);
+            } else {
+                v = (xp - xa) * mu + xa;
+            }
+            emit32(a.out[n], t, c, v);
+        }
+    }
+}
+
+bool launch_ln_mix(hipStream_t st, const LnMixArgs & a) {
+    hipLaunchKernelGGL(k_ln_mix, dim3(a.T), dim3(256), 0, st, a);
+    HIP_OK(hipGetLastError());
+    return true;
+}
+
+__global__ __launch_bounds__(256) void k_ln_emit(int C, const float * x, const float * w, const float * b, ActBuf out) {
+    __shared__ double sh[8];
+    float mean, scale;
+    ln_stats(x, C, 1e-5f, mean, scale, sh);
+    for (int c0 = 0; c0 < C; c0 += blockDim.x) {
+        const int c = c0 + threadIdx.x;
+        if (c0 + (int)(threadIdx.x & ~63) >= C) continue;
+        emit32(out, 0, c, ln_apply(x[c], mean, scale, w[c], b[c]));
+    }
+}
+
+bool launch_ln_emit(hipStream_t st, int C, const float * x, const float * w, const float * b, const ActBuf & out) {
+    hipLaunchKernelGGL(k_ln_emit, dim3(1), dim3(256), 0, st, C, x, w, b, out);
+    HIP_OK(hipGetLastError());
+    return true;
+}
+
+// --------------------------------------------------------------------------- v6 mix5
+struct Mix5Args {
+    int T, C, D;
+    const float * lora;
+    const float * w2;
+    const float * maa[5];
+    const float * xa;
+    const float * sx;
+    ActBuf out[5];
+};
+
+__global__ __launch_bounds__(256) void k_v6_mix5(Mix5Args a) {
+    const int t = blockIdx.y;
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if ((int)(blockIdx.x * blockDim.x + (threadIdx.x & ~63)) >= a.C) return;  // wave-uniform
+    const int C = a.C, D = a.D;
+    const size_t ti = (size_t)t * C + c;
+    const float xa = a.xa[ti], sx = a.sx[ti];
+    for (int n = 0; n < 5; n++) {
+        const float * w2 = a.w2 + ((size_t)n * C + c) * D;
+        const float * lv = a.lora + (size_t)t * 5 * D + n * D;
+        double acc = 0.0;
+        for (int i = 0; i < D; i++) acc += (double)(w2[i] * lv[i]);
+        const float m = (float)acc;
+        emit32(a.out[n], t, c, (m + a.maa[n][c]) * sx + xa);
+    }
+}
+
+bool launch_v6_mix5(hipStream_t st, int T, int C, int D, const float * lora, const float * w2,
+                    const float * const * maa, const float * xa, const float * sx, const ActBuf * outs) {
+    Mix5Args a;
+    a.T = T;
+    a.C = C;
+    a.D = D;
+    a.lora = lora;
+    a.w2 = w2;
+    for (int n = 0; n < 5; n++) {
+        a.maa[n] = maa[n];
+        a.out[n] = outs[n];
+    }
+    a.xa = xa;
+    a.sx = sx;
+    hipLaunchKernelGGL(k_v6_mix5, dim3((C + 255) / 256, T), dim3(256), 0, st, a);
+    HIP_OK(hipGetLastError());
+    return true;
+}
+
+// --------------------------------------------------------------------------- v4 wkv
+__global__ __launch_bounds__(256) void k_wkv4(int T, int C, const float * r, const float * k, const float * v,
+                                              const float * first, const float * decay, const float * sin,
+                                              float * sout, ActBuf out) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if ((int)(blockIdx.x * blockDim.x + (threadIdx.x & ~63)) >= C) return;
+    float aa = sin[2 * C + c], bb = sin[3 * C + c], pp = sin[4 * C + c];
+    const float fi = first[c], de = decay[c];
+    for (int t = 0; t < T; t++) {
+        const size_t i = (size_t)t * C + c;
+        const float kt = k[i], vt = v[i];
+        float ww = fi + kt;
+        float qq = fmaxf(pp, ww);
+        float e1 = expf(pp - qq), e2 = expf(ww - qq);
+        const float an = e1 * aa + e2 * vt;
+        const float bn = e1 * bb + e2;
+        ww = pp + de;
+        qq = fmaxf(ww, kt);
+        e1 = expf(ww - qq);
+        e2 = expf(kt - qq);
+        aa = e1 * aa + e2 * vt;
+        bb = e1 * bb + e2;
+        pp = qq;
+        emit32(out, t, c, r[i] * (an / bn));
+    }
+    sout[2 * C + c] = aa;
+    sout[3 * C + c] = bb;
+    sout[4 * C + c] = pp;
+}
+
+bool launch_wkv4(hipStream_t st, int T, int C, const float * r, const float * k, const float * v,
+                 const float * first, const float * decay, const float * state_in, float * state_out,
+                 const ActBuf & out) {
+    hipLaunchKernelGGL(k_wkv4, dim3((C + 255) / 256), dim3(256), 0, st, T, C, r, k, v, first, decay, state_in,
+                       state_out, out);
+    HIP_OK(hipGetLastError());
+    return true;
+}
+
+// --------------------------------------------------------------------------- wkv6 (v5/v6)
+// One workgroup per head; lane group (j, g): j = value index, g splits the key index i.
+// The state column S[i][j] for the lane's IPG keys lives in registers across all T tokens.
+template <int IPG>
+__global__ void k_wkv6(int T, int H, int S, int G, const float * k, const float * v, const float * r,
+                       const float * u, const float * w, int w_per_token, const float * sin, float * sout,
+                       float * y) {
+    const int h = blockIdx.x;
+    const int j = threadIdx.x / G, g = threadIdx.x % G;
+    const int C = H * S;
+    float st[IPG];
+    const size_t hb = (size_t)h * S * S;
+#pragma unroll
+    for (int ii = 0; ii < IPG; ii++) st[ii] = sin[hb + (size_t)(g * IPG + ii) * S + j];
+    float uu[IPG];
+#pragma unroll
+    for (int ii = 0; ii < IPG; ii++) uu[ii] = u[h * S + g * IPG + ii];
+    for (int t = 0; t < T; t++) {
+        const size_t th = (size_t)t * C + (size_t)h * S;
+        const float * wt = w + (w_per_token ? (size_t)t * C : 0) + (size_t)h * S;
+        const float vj = v[th + j];
+        float acc = 0.0f;
+#pragma unroll
+        for (int ii = 0; ii < IPG; ii++) {
+            const int i = g * IPG + ii;
+            const float kv = vj * k[th + i];
+            const float prev = st[ii];
+            const float temp = kv * uu[ii] + prev;
+            acc += temp * r[th + i];
+            st[ii] = prev * wt[i] + kv;
+        }
+        acc = group_sum(acc, G);
+        if (g == 0) y[th + j] = acc;
+    }
+#pragma unroll
+    for (int ii = 0; ii < IPG; ii++) sout[hb + (size_t)(g * IPG + ii) * S + j] = st[ii];
+}
+
+static int pick_groups(int S) {
+    int G = 256 / S;
+    if (G > S) G = S;
+    if (G < 1) G = 1;
+    return G;
+}
+
+bool launch_wkv6(hipStream_t st, int T, int H, int S, const float * k, const float * v, const float * r,
+                 const float * u, const float * w, int w_per_token, const float * state_in, float * state_out,
+                 float * y) {
+    const int G = pick_groups(S), IPG = S / G;
+    dim3 grid(H), block(S * G);
+    switch (IPG) {
+        case 1: hipLaunchKernelGGL(k_wkv6<1>, grid, block, 0, st, T, H, S, G, k, v, r, u, w, w_per_token, state_in, state_out, y); break;
+        case 2: hipLaunchKernelGGL(k_wkv6<2>, grid, block, 0, st, T, H, S, G, k, v, r, u, w, w_per_token, state_in, state_out, y); break;
+        case 4: hipLaunchKernelGGL(k_wkv6<4>, grid, block, 0, st, T, H, S, G, k, v, r, u, w, w_per_token, state_in, state_out, y); break;
+        case 8: hipLaunchKernelGGL(k_wkv6<8>, grid, block, 0, st, T, H, S, G, k, v, r, u, w, w_per_token, state_in, state_out, y); break;
+        case 16: hipLaunchKernelGGL(k_wkv6<16>, grid, block, 0, st, T, H, S, G, k, v, r, u, w, w_per_token, state_in, state_out, y); break;
+        case 32: hipLaunchKernelGGL(k_wkv6<32>, grid, block, 0, st, T, H, S, G, k, v, r, u, w, w_per_token, state_in, state_out, y); break;
+        default: fprintf(stderr, "rwkv: unsupported head size %d\n", S); return false;
+    }
+    HIP_OK(hipGetLastError());
+    return true;
+}
+
+// --------------------------------------------------------------------------- v7
+// Per token: thread per channel, heads are S consecutive channels (S <= 64, power of two).
+__global__ __launch_bounds__(256) void k_v7_prep(int T, int H, int S, float * k, const float * a, const float * r,
+                                                 const float * k_k, const float * k_a, const float * r_k, float * nb,
+                                                 float * bb, float * bonus) {
+    const int t = blockIdx.x, C = H * S;
+    for (int c0 = 0; c0 < C; c0 += blockDim.x) {
+        const int c = c0 + threadIdx.x;
+        if (c0 + (int)(threadIdx.x & ~63) >= C) continue;
+        const size_t i = (size_t)t * C + c;
+        const float kv = k[i];
+        const float kkr = kv * k_k[c];
+        const float sum = group_sum(kkr * kkr, S);
+        const float scale = 1.0f / fmaxf(sqrtf(sum), 1e-12f);
+        const float kk = kkr * scale;
+        const float av = a[i];
+        const float ka = kv * k_a[c];
+        const float kadj = kv + (av * ka - ka);
+        k[i] = kadj;
+        nb[i] = -kk;
+        bb[i] = kk * av;
+        const float bsum = group_sum((kadj * r[i]) * r_k[c], S);
+        if ((c % S) == 0) bonus[(size_t)t * H + c / S] = bsum;
+    }
+}
+
+bool launch_v7_prep(hipStream_t st, int T, int H, int S, float * k, const float * a, const float * r,
+                    const float * k_k, const float * k_a, const float * r_k, float * nb, float * bb, float * bonus) {
+    if (S > 64 || (S & (S - 1))) {
+        fprintf(stderr, "rwkv: v7 head size %d unsupported\n", S);
+        return false;
+    }
+    hipLaunchKernelGGL(k_v7_prep, dim3(T), dim3(256), 0, st, T, H, S, k, a, r, k_k, k_a, r_k, nb, bb, bonus);
+    HIP_OK(hipGetLastError());
+    return true;
+}
+
+// state [h][i(value)][j(key)]; lane group (i, g): g splits j.
+template <int JPG>
+__global__ void k_wkv7(int T, int H, int S, int G, const float * r, const float * w, const float * k,
+                       const float * v, const float * a, const float * b, const float * sin, float * sout,
+                       float * y) {
+    const int h = blockIdx.x;
+    const int i = threadIdx.x / G, g = threadIdx.x % G;
+    const int C = H * S;
+    const size_t hb = (size_t)h * S * S + (size_t)i * S + g * JPG;
+    float st[JPG];
+#pragma unroll
+    for (int jj = 0; jj < JPG; jj++) st[jj] = sin[hb + jj];
+    for (int t = 0; t < T; t++) {
+        const size_t th = (size_t)t * C + (size_t)h * S + g * JPG;
+        float sa = 0.0f;
+#pragma unroll
+        for (int jj = 0; jj < JPG; jj++) sa += a[th + jj] * st[jj];
+        sa = group_sum(sa, G);
+        const float vi = v[(size_t)t * C + (size_t)h * S + i];
+        float acc = 0.0f;
+#pragma unroll
+        for (int jj = 0; jj < JPG; jj++) {
+            const float kv = vi * k[th + jj];
+            const float ns = st[jj] * w[th + jj] + kv + sa * b[th + jj];
+            st[jj] = ns;
+            acc += ns * r[th + jj];
+        }
+        acc = group_sum(acc, G);
+        if (g == 0) y[(size_t)t * C + (size_t)h * S + i] = acc;
+    }
+#pragma unroll
+    for (int jj = 0; jj < JPG; jj++) sout[hb + jj] = st[jj];
+}
+
+bool launch_wkv7(hipStream_t st, int T, int H, int S, const float * r, const float * w, const float * k,
+                 const float * v, const float * a, const float * b, const float * state_in, float * state_out,
+                 float * y) {
+    const int G = pick_groups(S), JPG = S / G;
+    dim3 grid(H), block(S * G);
+    switch (JPG) {
+        case 1: hipLaunchKernelGGL(k_wkv7<1>, grid, block, 0, st, T, H, S, G, r, w, k, v, a, b, state_in, state_out, y); break;
+        case 2: hipLaunchKernelGGL(k_wkv7<2>, grid, block, 0, st, T, H, S, G, r, w, k, v, a, b, state_in, state_out, y); break;
+        case 4: hipLaunchKernelGGL(k_wkv7<4>, grid, block, 0, st, T, H, S, G, r, w, k, v, a, b, state_in, state_out, y); break;
+        case 8: hipLaunchKernelGGL(k_wkv7<8>, grid, block, 0, st, T, H, S, G, r, w, k, v, a, b, state_in, state_out, y); break;
+        case 16: hipLaunchKernelGGL(k_wkv7<16>, grid, block, 0, st, T, H, S, G, r, w, k, v, a, b, state_in, state_out, y); break;
+        case 32: hipLaunchKernelGGL(k_wkv7<32>, grid, block, 0, st, T, H, S, G, r, w, k, v, a, b, state_in, state_out, y); break;
+        default: fprintf(stderr, "rwkv: unsupported head size %d\n", S); return false;
+    }
+    HIP_OK(hipGetLastError());
+    return true;
+}
+
+// --------------------------------------------------------------------------- GroupNorm
+__global__ __launch_bounds__(256) void k_groupnorm(int T, int H, int S, float eps, const float * y, const float * w,
+                                                   const float * b, int mode, const float * g, const float * v,
+                                                   const float * bonus, ActBuf out) {
+    const int t = blockIdx.x, C = H * S;
+    for (int c0 = 0; c0 < C; c0 += blockDim.x) {
+        const int c = c0 + threadIdx.x;
+        if (c0 + (int)(threadIdx.x & ~63) >= C) continue;
+        const size_t i = (size_t)t * C + c;
+        const float x = y[i];
+        const double s = group_sum((double)x, S);
+        const float mean = (float)(s / (double)S);
+        const float d = x - mean;
+        const double s2 = group_sum((double)(d * d), S);
+        const float var = (float)(s2 / (double)S);
+        const float scale = 1.0f / sqrtf(var + eps);
+        float o = d * scale;
+        o = o * w[c];
+        o = o + b[c];
+        if (mode == 2) o = o + v[i] * bonus[(size_t)t * H + c / S];
+        if (mode >= 1) o = o * g[i];
+        emit32(out, t, c, o);
+    }
+}
+
+bool launch_groupnorm(hipStream_t st, int T, int H, int S, float eps, const float * y, const float * w,
+                      const float * b, int mode, const float * g, const float * v, const float * bonus,
+                      const ActBuf & out) {
+    if (S > 64 || (S & (S - 1))) {
+        fprintf(stderr, "rwkv: head size %d unsupported by groupnorm\n", S);
+        return false;
+    }
+    hipLaunchKernelGGL(k_groupnorm, dim3(T), dim3(256), 0, st, T, H, S, eps, y, w, b, mode, g, v, bonus, out);
+    HIP_OK(hipGetLastError());
+    return true;
+}
+
+__global__ void k_fill(float * p, size_t n, float value) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = value;
+}
+
+bool launch_fill(hipStream_t st, float * p, size_t n, float value) {
+    if (!n) return true;
+    hipLaunchKernelGGL(k_fill, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, p, n, value);
+    HIP_OK(hipGetLastError());
+    return true;
+}
+
+}  // namespace rwkvmi

@@ -1,0 +1,68 @@
+// kernels.hpp -- host launchers for the gfx950 kernels (kernels.hip).
+#pragma once
+
+#include "common.hpp"
+
+namespace rwkvmi {
+
+// ---- matmul (dequant-matvec / batched) --------------------------------------------------
+// Launches one grouped matmul: every entry shares the weight type `wtype`.
+bool launch_mm_group(hipStream_t st, MMGroup & g, int wtype);
+
+// ---- elementwise / recurrence kernels -----------------------------------------------------
+// x[t] = LN(emb[tokens[t]]; w, b)   (rwkv_graph.inc:654-658)
+bool launch_embed_ln(hipStream_t st, const uint32_t * tokens, int T, const DMat & emb,
+                     const float * w, const float * b, float * x);
+
+struct LnMixArgs {
+    int T, C;
+    const float * x;            // [T][C] residual stream
+    const float * carry_in;     // [C] previous token's LN output (state *_xx)
+    float * carry_out;          // [C] <- LN(x[T-1])
+    const float * lnw, * lnb;
+    int form;                   // 0: xa*mu + (xp - xp*mu)  (v4/v5)   1: (xp - xa)*mu + xa (v6/v7)
+    int n_out;
+    const float * mu[6];
+    ActBuf out[6];
+    float * out_xa;             // optional fp32 [T][C]
+    float * out_sx;             // optional fp32 [T][C] (xp - xa)
+};
+bool launch_ln_mix(hipStream_t st, const LnMixArgs & a);
+
+// v6: xs[n] = (W2[n] . lora_n + maa[n]) * sx + xa, n = w,k,v,r,g   (rwkv_graph.inc:313-346)
+bool launch_v6_mix5(hipStream_t st, int T, int C, int D, const float * lora, const float * w2,
+                    const float * const * maa, const float * xa, const float * sx, const ActBuf * outs);
+
+// v4 wkv with aa/bb/pp state (rwkv_graph.inc:119-161); emits r*wkv into `out`.
+bool launch_wkv4(hipStream_t st, int T, int C, const float * r, const float * k, const float * v,
+                 const float * first, const float * decay, const float * state_in, float * state_out,
+                 const ActBuf & out);
+
+// ggml_rwkv_wkv6 semantics (v5/v6): y[T][C]; w_per_token selects v6 (w [T][C]) vs v5 (w [C]).
+bool launch_wkv6(hipStream_t st, int T, int H, int S, const float * k, const float * v, const float * r,
+                 const float * u, const float * w, int w_per_token, const float * state_in,
+                 float * state_out, float * y);
+
+// v7 per-head prep: kk = l2norm(k*k_k); k += a*ka - ka; nb = -kk; bb = kk*a; bonus = sum(k*r*r_k)
+bool launch_v7_prep(hipStream_t st, int T, int H, int S, float * k, const float * a, const float * r,
+                    const float * k_k, const float * k_a, const float * r_k, float * nb, float * bb,
+                    float * bonus);
+
+// rwkv_operators_wkv_v7.inc:37-107
+bool launch_wkv7(hipStream_t st, int T, int H, int S, const float * r, const float * w, const float * k,
+                 const float * v, const float * a, const float * b, const float * state_in,
+                 float * state_out, float * y);
+
+// GroupNorm over heads + ln_x (+ v7 bonus) (+ gate), emitted as the output projection's input.
+// mode 0: none, 1: *g, 2: + v*bonus then *g
+bool launch_groupnorm(hipStream_t st, int T, int H, int S, float eps, const float * y, const float * w,
+                      const float * b, int mode, const float * g, const float * v, const float * bonus,
+                      const ActBuf & out);
+
+// LN of one row (x[row]) emitted into a 1-row ActBuf (head input).
+bool launch_ln_emit(hipStream_t st, int C, const float * x, const float * w, const float * b, const ActBuf & out);
+
+// v4 state init value helper: fills n floats with value
+bool launch_fill(hipStream_t st, float * p, size_t n, float value);
+
+}  // namespace rwkvmi

@@ -1,0 +1,252 @@
+// rwkv_abi.cpp -- the rwkv.h C ABI (reference rwkv.h:70-224, rwkv.cpp:70-258, rwkv_eval.inc:37-241)
+// on top of the MI355X engine.  Error, ownership and NULL-argument semantics follow the
+// reference; evaluation always runs on the GPU (see include/rwkv.h notes).
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <atomic>
+#include <inttypes.h>
+#include <mutex>
+#include <string>
+
+#include "../../include/rwkv.h"
+#include "../../include/rwkv_mi355x.h"
+#include "engine.hpp"
+#include "model_file.hpp"
+
+using namespace rwkvmi;
+
+struct SharedModel {
+    DeviceModel dm;
+    std::atomic<int> refcount{0};
+};
+
+struct rwkv_context {
+    SharedModel * model = nullptr;
+    Engine * engine = nullptr;
+    uint32_t n_threads = 1;
+    enum rwkv_error_flags last_error = RWKV_ERROR_NONE;
+    bool print_errors = true;
+};
+
+static std::mutex g_model_mutex;
+
+#define CTX_CHECK(ctx, FLAGS, RET, cond, ...)                                        \
+    do {                                                                             \
+        if (!(cond)) {                                                               \
+            (ctx)->last_error = (ctx)->last_error | (FLAGS);                         \
+            if ((ctx)->print_errors) {                                               \
+                fprintf(stderr, __VA_ARGS__);                                        \
+                fprintf(stderr, "\n%s:%d: %s\n", __FILE__, __LINE__, #cond);         \
+            }                                                                        \
+            return RET;                                                              \
+        }                                                                            \
+    } while (0)
+
+static int pick_device() {
+    const char * e = getenv("RWKV_MI355X_DEVICE");
+    if (e && *e) return atoi(e);
+    const char * lr = getenv("LOCAL_RANK");
+    int n = 0;
+    if (lr && *lr && hipGetDeviceCount(&n) == hipSuccess && n > 0) return atoi(lr) % n;
+    return 0;
+}
+
+extern "C" {
+
+RWKV_API void rwkv_set_print_errors(struct rwkv_context * ctx, const bool print_errors) {
+    if (ctx) ctx->print_errors = print_errors; else g_print_errors = print_errors;
+}
+
+RWKV_API bool rwkv_get_print_errors(const struct rwkv_context * ctx) { return ctx ? ctx->print_errors : g_print_errors; }
+
+RWKV_API enum rwkv_error_flags rwkv_get_last_error(struct rwkv_context * ctx) {
+    enum rwkv_error_flags * p = ctx ? &ctx->last_error : &g_last_error;
+    const enum rwkv_error_flags v = *p;
+    *p = RWKV_ERROR_NONE;
+    return v;
+}
+
+static struct rwkv_context * new_context(SharedModel * sm, uint32_t n_threads) {
+    rwkv_context * ctx = new (std::nothrow) rwkv_context();
+    RWKV_CHECK(RWKV_ERROR_CTX | RWKV_ERROR_ALLOC, nullptr, ctx != nullptr, "Failed to allocate rwkv_context");
+    ctx->model = sm;
+    ctx->n_threads = n_threads;
+    ctx->print_errors = g_print_errors;
+    ctx->engine = new (std::nothrow) Engine(&sm->dm);
+    if (!ctx->engine || !ctx->engine->init()) {
+        delete ctx->engine;
+        delete ctx;
+        RWKV_CHECK(RWKV_ERROR_CTX | RWKV_ERROR_ALLOC, nullptr, false, "Failed to allocate device workspace");
+    }
+    sm->refcount++;
+    return ctx;
+}
+
+RWKV_API struct rwkv_context * rwkv_init_from_file(const char * path, const uint32_t n_threads, const uint32_t n_gpu_layers) {
+    (void)n_gpu_layers;
+    g_last_error = RWKV_ERROR_NONE;
+    int ndev = 0;
+    const hipError_t de = hipGetDeviceCount(&ndev);
+    RWKV_CHECK(RWKV_ERROR_CTX | RWKV_ERROR_UNSUPPORTED, nullptr, de == hipSuccess && ndev > 0,
+               "No HIP device available: this library evaluates RWKV on an AMD Instinct MI355X (gfx950) only");
+    ModelFile mf;
+    if (!load_model_file(path, mf)) return nullptr;
+    SharedModel * sm = new (std::nothrow) SharedModel();
+    RWKV_CHECK(RWKV_ERROR_CTX | RWKV_ERROR_ALLOC, nullptr, sm != nullptr, "Failed to allocate model");
+    sm->dm.device = pick_device();
+    if (sm->dm.device >= ndev) sm->dm.device = 0;
+    if (hipSetDevice(sm->dm.device) != hipSuccess || !upload_model(mf, sm->dm)) {
+        free_model(sm->dm);
+        delete sm;
+        RWKV_CHECK(RWKV_ERROR_MODEL | RWKV_ERROR_ALLOC, nullptr, false, "Failed to upload the model to the GPU");
+    }
+    mf.tensors.clear();
+    rwkv_context * ctx = new_context(sm, n_threads);
+    if (!ctx) {
+        free_model(sm->dm);
+        delete sm;
+    }
+    return ctx;
+}
+
+RWKV_API struct rwkv_context * rwkv_clone_context(struct rwkv_context * ctx, const uint32_t n_threads) {
+    if (!ctx) return nullptr;
+    rwkv_context * c = new_context(ctx->model, n_threads);
+    if (c) c->print_errors = ctx->print_errors;
+    return c;
+}
+
+RWKV_API bool rwkv_eval(struct rwkv_context * ctx, const uint32_t token, const float * state_in, float * state_out,
+                        float * logits_out) {
+    ctx->last_error = RWKV_ERROR_NONE;
+    const size_t n_vocab = ctx->model->dm.n_vocab;
+    CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, token < n_vocab, "Token (%" PRIu32 ") is out of range (0 .. %zu)", token, n_vocab - 1);
+    CTX_CHECK(ctx, RWKV_ERROR_CTX, false, ctx->engine->eval(&token, 1, state_in, state_out, logits_out), "GPU evaluation failed");
+    return true;
+}
+
+RWKV_API bool rwkv_eval_sequence(struct rwkv_context * ctx, const uint32_t * tokens, const size_t T, const float * state_in,
+                                 float * state_out, float * logits_out) {
+    ctx->last_error = RWKV_ERROR_NONE;
+    CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, T > 0, "Sequence length is 0");
+    if (!tokens) return true;  // build/cache only (rwkv_eval_inc:102,122): workspace is allocated lazily
+    if (T == 1) return rwkv_eval(ctx, tokens[0], state_in, state_out, logits_out);
+    const size_t n_vocab = ctx->model->dm.n_vocab;
+    for (size_t i = 0; i < T; i++) {
+        CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, tokens[i] < n_vocab, "Token at index %zu (%" PRIu32 ") is out of range (0 .. %zu)",
+                  i, tokens[i], n_vocab - 1);
+    }
+    CTX_CHECK(ctx, RWKV_ERROR_CTX, false, ctx->engine->eval(tokens, T, state_in, state_out, logits_out), "GPU evaluation failed");
+    return true;
+}
+
+RWKV_API bool rwkv_eval_sequence_in_chunks(struct rwkv_context * ctx, const uint32_t * tokens, const size_t T,
+                                           const size_t chunk_size, const float * state_in, float * state_out,
+                                           float * logits_out) {
+    CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, T > 0, "Sequence length is 0");
+    CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, chunk_size > 0, "Chunk size is 0");
+    // The per-token arithmetic of this engine does not depend on how a sequence is cut, so the
+    // chunked call is one device-resident pass (state never returns to the host in between);
+    // results are bit-identical to the reference's chunk loop (rwkv_eval.inc:158-221).
+    return rwkv_eval_sequence(ctx, tokens, T, state_in, state_out, logits_out);
+}
+
+RWKV_API size_t rwkv_get_n_vocab(const struct rwkv_context * ctx) { return ctx->model->dm.n_vocab; }
+RWKV_API size_t rwkv_get_n_embed(const struct rwkv_context * ctx) { return ctx->model->dm.n_embed; }
+RWKV_API size_t rwkv_get_n_layer(const struct rwkv_context * ctx) { return ctx->model->dm.n_layer; }
+RWKV_API size_t rwkv_get_state_len(const struct rwkv_context * ctx) { return ctx->model->dm.state_len; }
+RWKV_API size_t rwkv_get_logits_len(const struct rwkv_context * ctx) { return ctx->model->dm.n_vocab; }
+
+RWKV_API uint32_t rwkv_get_state_buffer_element_count(const struct rwkv_context * ctx) { return (uint32_t)rwkv_get_state_len(ctx); }
+RWKV_API uint32_t rwkv_get_logits_buffer_element_count(const struct rwkv_context * ctx) { return (uint32_t)rwkv_get_logits_len(ctx); }
+
+RWKV_API void rwkv_init_state(const struct rwkv_context * ctx, float * state) {
+    const DeviceModel & dm = ctx->model->dm;
+    memset(state, 0, dm.state_len * sizeof(float));
+    if (dm.major >= 5) return;
+    const size_t C = dm.n_embed;
+    for (size_t l = 0; l < dm.n_layer; l++)
+        for (size_t i = 4 * C; i < 5 * C; i++) state[l * 5 * C + i] = -1e30f;
+}
+
+RWKV_API void rwkv_free(struct rwkv_context * ctx) {
+    if (!ctx) return;
+    delete ctx->engine;
+    SharedModel * sm = ctx->model;
+    delete ctx;
+    std::lock_guard<std::mutex> lk(g_model_mutex);
+    if (--sm->refcount == 0) {
+        (void)hipSetDevice(sm->dm.device);
+        free_model(sm->dm);
+        delete sm;
+    }
+}
+
+RWKV_API const char * rwkv_get_system_info_string(void) {
+    static std::string s;
+    static std::once_flag once;
+    std::call_once(once, []() {
+        int n = 0, rt = 0;
+        (void)hipGetDeviceCount(&n);
+        (void)hipRuntimeGetVersion(&rt);
+        s = "HIP=1 HIP_RUNTIME=" + std::to_string(rt) + " DEVICES=" + std::to_string(n);
+        if (n > 0) {
+            hipDeviceProp_t p;
+            if (hipGetDeviceProperties(&p, 0) == hipSuccess) {
+                s += std::string(" GFX=") + p.gcnArchName + " CUS=" + std::to_string(p.multiProcessorCount) +
+                     " HBM_GB=" + std::to_string((unsigned long long)(p.totalGlobalMem >> 30));
+            }
+        }
+        s += " CPU_PATH=0";
+    });
+    return s.c_str();
+}
+
+// ------------------------------------------------------------------ additive extensions
+
+RWKV_API bool rwkv_mi355x_state_upload(struct rwkv_context * ctx, const float * state) { return ctx->engine->state_upload(state); }
+RWKV_API bool rwkv_mi355x_state_download(struct rwkv_context * ctx, float * state) { return ctx->engine->state_download(state); }
+
+RWKV_API bool rwkv_mi355x_eval_device(struct rwkv_context * ctx, const uint32_t * tokens, size_t T, float * logits_out, bool sync) {
+    ctx->last_error = RWKV_ERROR_NONE;
+    CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, T > 0 && tokens != nullptr, "Sequence length is 0");
+    for (size_t i = 0; i < T; i++)
+        CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, tokens[i] < ctx->model->dm.n_vocab, "Token out of range");
+    CTX_CHECK(ctx, RWKV_ERROR_CTX, false, ctx->engine->eval_device(tokens, T, logits_out, sync), "GPU evaluation failed");
+    return true;
+}
+
+RWKV_API bool rwkv_mi355x_sync(struct rwkv_context * ctx) { return ctx->engine->sync(); }
+RWKV_API void * rwkv_mi355x_stream(struct rwkv_context * ctx) { return (void *)ctx->engine->stream(); }
+RWKV_API float * rwkv_mi355x_device_state(struct rwkv_context * ctx) { return ctx->engine->device_state(); }
+
+RWKV_API double rwkv_mi355x_weight_bytes(const struct rwkv_context * ctx, bool with_head) {
+    const DeviceModel & dm = ctx->model->dm;
+    return dm.layer_weight_bytes + (with_head ? dm.head_weight_bytes : 0.0);
+}
+
+RWKV_API double rwkv_mi355x_decode_bytes(const struct rwkv_context * ctx, bool with_logits) {
+    const DeviceModel & dm = ctx->model->dm;
+    // weights + per-token small parameters + state read and written + embedding row
+    double b = dm.layer_weight_bytes + dm.small_param_bytes + 2.0 * (double)dm.state_len * 4.0;
+    b += (double)dm.n_embed * (dm.emb.type == W_F16 ? 2.0 : 4.0);
+    if (with_logits) b += dm.head_weight_bytes + (double)dm.n_vocab * 4.0;
+    return b;
+}
+
+RWKV_API double rwkv_mi355x_matmul_flops_per_token(const struct rwkv_context * ctx, bool with_head) {
+    const DeviceModel & dm = ctx->model->dm;
+    return dm.layer_flops + (with_head ? dm.head_flops : 0.0);
+}
+
+RWKV_API void rwkv_mi355x_arch(const struct rwkv_context * ctx, int64_t out[4]) {
+    const DeviceModel & dm = ctx->model->dm;
+    out[0] = dm.major;
+    out[1] = dm.minor;
+    out[2] = dm.H;
+    out[3] = dm.S;
+}
+
+}  // extern "C"

@@ -56,6 +56,16 @@ RWKV_API bool rwkv_mi355x_write_synthetic_model(const char * path, int arch, uin
                                                 uint32_t n_embed, uint32_t n_layer, uint32_t ffn,
                                                 const char * fmt, uint64_t seed);
 
+/* ---- kernel self-tests (used by tests/ for per-kernel parity; not on the eval path) ----
+ * Runs the library's activation quantizer (the emit stage every producer kernel uses) on
+ * x [T][K] (host) for the activation format of weight type `wtype` (rwkv file type id) and
+ * returns the int8 codes, fp16-rounded scales d and (Q8_1) s, as fp32.  q/d/s may be NULL. */
+RWKV_API bool rwkv_mi355x_selftest_quantize_act(int wtype, const float * x, int T, int K, int8_t * q, float * d,
+                                                float * s);
+/* Runs the decode/sequence matmul kernel on W (ggml block bytes of type wtype, ne=[K, M],
+ * host) and x [T][K] (host): y [T][M] = W x with the library's activation quantization. */
+RWKV_API bool rwkv_mi355x_selftest_matmul(int wtype, const void * W, int K, int M, const float * x, int T, float * y);
+
 #if defined(__cplusplus)
 }
 #endif

@@ -438,6 +438,14 @@ static inline void block_ints(int type, const uint8_t * b, int * w, float * d, f
 /* ------------------------------------------------------------------ matmul */
 
 static int g_threads = 0;
+/* Variant bits re-associate the reductions -- equally valid restatements used only to
+ * measure how strongly a model amplifies last-bit differences (the "noise floor" the GPU
+ * comparison is judged against).  Variant 0 is the ggml-x86 mirror.
+ *   1: reverse summation order   2: ggml's scalar quantized dot (no fma, m*s inline)
+ *   4: fp32 instead of fp64 accumulators in the F32/F16 dots and norms */
+static int g_variant = 0;
+
+void oracle_set_variant(int v) { g_variant = v; }
 
 void oracle_set_threads(int n) { g_threads = n; }
 
@@ -462,7 +470,12 @@ void oracle_matmul(int wtype, const void * Wv, int64_t K, int64_t M,
             for (int64_t t = 0; t < T; t++) {
                 const float * xt = x + t * K;
                 double acc = 0.0;
-                for (int64_t k = 0; k < K; k++) acc += (double)(w[k] * xt[k]);
+                float fa = 0.0f;
+                for (int64_t kk = 0; kk < K; kk++) {
+                    const int64_t k = (g_variant & 1) ? K - 1 - kk : kk;
+                    if (g_variant & 4) fa += w[k] * xt[k]; else acc += (double)(w[k] * xt[k]);
+                }
+                if (g_variant & 4) acc = fa;
                 y[t * M + m] = (float)acc;
             }
         }
@@ -478,7 +491,12 @@ void oracle_matmul(int wtype, const void * Wv, int64_t K, int64_t M,
             for (int64_t t = 0; t < T; t++) {
                 const float * xt = xh + t * K;
                 double acc = 0.0;
-                for (int64_t k = 0; k < K; k++) acc += (double)(h2f(w + 2 * k) * xt[k]);
+                float fa = 0.0f;
+                for (int64_t kk = 0; kk < K; kk++) {
+                    const int64_t k = (g_variant & 1) ? K - 1 - kk : kk;
+                    if (g_variant & 4) fa += h2f(w + 2 * k) * xt[k]; else acc += (double)(h2f(w + 2 * k) * xt[k]);
+                }
+                if (g_variant & 4) acc = fa;
                 y[t * M + m] = (float)acc;
             }
         }
@@ -502,13 +520,20 @@ void oracle_matmul(int wtype, const void * Wv, int64_t K, int64_t M,
             /* ggml x86 vec_dot_q*_q8_*: acc = fma(d_w*d_x, sumi, acc) in fp32; the
              * m_w*s_x terms of the _1 formats are summed separately and added last. */
             float acc = 0.0f, summs = 0.0f;
-            for (int64_t b = 0; b < nb; b++) {
+            for (int64_t bi = 0; bi < nb; bi++) {
+                const int64_t b = (g_variant & 1) ? nb - 1 - bi : bi;
                 float dw, mw;
                 block_ints(wtype, wrow + b * wbb, wi, &dw, &mw);
                 const uint8_t * xb = xr + b * abb;
                 int sumi = 0;
                 for (int j = 0; j < 32; j++) sumi += wi[j] * (int8_t)xb[aqo + j];
                 const float dx = h2f(xb);
+                if (g_variant & 2) {
+                    /* ggml scalar form: sumf += sumi*dx*dy (+ m*s inline) */
+                    acc += (float)sumi * dw * dx;
+                    if (atype == OT_Q8_1) acc += mw * h2f(xb + 2);
+                    continue;
+                }
                 acc = fmaf(dw * dx, (float)sumi, acc);
                 if (atype == OT_Q8_1) summs += mw * h2f(xb + 2);
             }
@@ -819,14 +844,22 @@ void oracle_init_state(const oracle_model * m, float * state) {
 /* ggml_norm (double accumulation) then *w +b, rwkv_operators.inc:93-97 */
 static void norm_row(const float * x, float * y, int64_t n, float eps, const float * w, const float * b) {
     double sum = 0.0;
-    for (int64_t i = 0; i < n; i++) sum += (double)x[i];
+    float fs = 0.0f;
+    for (int64_t ii = 0; ii < n; ii++) {
+        const int64_t i = (g_variant & 1) ? n - 1 - ii : ii;
+        if (g_variant & 4) fs += x[i]; else sum += (double)x[i];
+    }
+    if (g_variant & 4) sum = fs;
     const float mean = (float)(sum / (double)n);
     double sum2 = 0.0;
+    float fs2 = 0.0f;
     for (int64_t i = 0; i < n; i++) {
         float v = x[i] - mean;
         y[i] = v;
         sum2 += (double)(v * v);
+        fs2 += v * v;
     }
+    if (g_variant & 4) sum2 = fs2;
     const float variance = (float)(sum2 / (double)n);
     const float scale = 1.0f / sqrtf(variance + eps);
     for (int64_t i = 0; i < n; i++) y[i] = y[i] * scale;

@@ -44,6 +44,9 @@ int oracle_eval(const oracle_model * m, const uint32_t * tokens, size_t T,
 /* rwkv_quantize_model_file semantics (rwkv_quantize.inc:16-171).  0 on success. */
 int oracle_quantize_file(const char * in_path, const char * out_path, const char * format);
 
+/* 0: ggml-mirror numerics (default).  1, 2: re-associated reductions (noise-floor probes). */
+void oracle_set_variant(int v);
+
 /* Number of OpenMP threads used by the matmuls (<=0: library default). */
 void oracle_set_threads(int n);
 int  oracle_get_threads(void);

@@ -57,7 +57,7 @@ static float * upload_host_floats(DeviceModel & dm, const std::vector<float> & v
 }
 
 // Repack one ggml-order matrix ne=[K, M] into the device layout of common.hpp.
-static bool upload_mat(DeviceModel & dm, const HostTensor * t, DMat & out, bool count_bytes = true, bool is_head = false) {
+bool upload_mat(DeviceModel & dm, const HostTensor * t, DMat & out, bool count_bytes, bool is_head) {
     if (!t) return true;
     if (t->ndim != 2) {
         fprintf(stderr, "rwkv: %s: matrix expected\n", t->name.c_str());
@@ -149,7 +149,7 @@ bool upload_model(const ModelFile & mf, DeviceModel & dm) {
         return false;
     }
     auto T = [&](const std::string & n) { return mf.find(n); };
-    if (!upload_mat(dm, T("emb.weight"), dm.emb, false)) return false;
+    if (!upload_mat(dm, T("emb.weight"), dm.emb, false, false)) return false;
     if (!upload_mat(dm, T("head.weight"), dm.head, true, true)) return false;
     if (!(dm.ln0_w = upload_vec(dm, T("blocks.0.ln0.weight"))) || !(dm.ln0_b = upload_vec(dm, T("blocks.0.ln0.bias"))) ||
         !(dm.lnout_w = upload_vec(dm, T("ln_out.weight"))) || !(dm.lnout_b = upload_vec(dm, T("ln_out.bias"))))
@@ -159,7 +159,7 @@ bool upload_model(const ModelFile & mf, DeviceModel & dm) {
         DLayer & L = dm.layers[i];
         const std::string p = "blocks." + std::to_string(i) + ".";
         auto V = [&](const char * n) { return upload_vec(dm, T(p + n)); };
-        auto Mt = [&](const char * n, DMat & d) { return upload_mat(dm, T(p + n), d); };
+        auto Mt = [&](const char * n, DMat & d) { return upload_mat(dm, T(p + n), d, true, false); };
         bool ok = (L.ln1_w = V("ln1.weight")) && (L.ln1_b = V("ln1.bias")) && (L.ln2_w = V("ln2.weight")) &&
                   (L.ln2_b = V("ln2.bias"));
         ok = ok && Mt("att.key.weight", L.att_k) && Mt("att.value.weight", L.att_v) &&

@@ -48,6 +48,8 @@ struct DeviceModel {
 };
 
 bool upload_model(const ModelFile & mf, DeviceModel & dm);
+// repacks one ggml-order matrix into the device layout (allocations recorded in dm.allocs)
+bool upload_mat(DeviceModel & dm, const HostTensor * t, DMat & out, bool count_bytes, bool is_head);
 void free_model(DeviceModel & dm);
 
 struct ActSlot {

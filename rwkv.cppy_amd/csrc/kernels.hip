@@ -756,3 +756,23 @@ bool launch_fill(hipStream_t st, float * p, size_t n, float value) {
 }
 
 }  // namespace rwkvmi
+
+namespace rwkvmi {
+
+__global__ __launch_bounds__(256) void k_act_from_f32(const float * x, int K, ActBuf out) {
+    const int t = blockIdx.x;
+    for (int k0 = 0; k0 < K; k0 += blockDim.x) {
+        const int k = k0 + threadIdx.x;
+        if (k0 + (int)(threadIdx.x & ~31) >= K) continue;  // half-wave uniform (K % 32 == 0)
+        emit32(out, t, k, x[(size_t)t * K + k]);
+    }
+}
+
+bool launch_act_from_f32(hipStream_t st, const float * x, int T, int K, const ActBuf & out) {
+    if (K % 32) return false;
+    hipLaunchKernelGGL(k_act_from_f32, dim3(T), dim3(256), 0, st, x, K, out);
+    HIP_OK(hipGetLastError());
+    return true;
+}
+
+}  // namespace rwkvmi

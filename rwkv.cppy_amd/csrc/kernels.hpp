@@ -66,3 +66,8 @@ bool launch_ln_emit(hipStream_t st, int C, const float * x, const float * w, con
 bool launch_fill(hipStream_t st, float * p, size_t n, float value);
 
 }  // namespace rwkvmi
+
+namespace rwkvmi {
+// x [T][K] fp32 -> activation buffer (emit32 path); used by the self-test entry points.
+bool launch_act_from_f32(hipStream_t st, const float * x, int T, int K, const ActBuf & out);
+}  // namespace rwkvmi

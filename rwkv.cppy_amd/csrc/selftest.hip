@@ -1,0 +1,102 @@
+// selftest.hip -- kernel self-test entry points (include/rwkv_mi355x.h): run one kernel on
+// host-provided operands so tests can check it against the oracle's primitive of the same
+// name (oracle_quantize_act, oracle_matmul) without whole-model noise.
+#include <string.h>
+
+#include <vector>
+
+#include "../../include/rwkv_mi355x.h"
+#include "engine.hpp"
+#include "kernels.hpp"
+
+using namespace rwkvmi;
+
+namespace {
+
+struct DevBufs {
+    std::vector<void *> p;
+    void * alloc(size_t n) {
+        void * q = nullptr;
+        if (hipMalloc(&q, n + 64) != hipSuccess) return nullptr;
+        (void)hipMemset(q, 0, n + 64);
+        p.push_back(q);
+        return q;
+    }
+    ~DevBufs() {
+        for (void * q : p) (void)hipFree(q);
+    }
+};
+
+bool make_act(DevBufs & b, int fmt, int T, int K, ActBuf & a) {
+    memset(&a, 0, sizeof(a));
+    a.fmt = fmt;
+    a.K = K;
+    const size_t n = (size_t)T * K, nb = n / 32 + 1;
+    a.f = (float *)b.alloc(n * 4);
+    a.h = (__half *)b.alloc(n * 2);
+    a.q = (int8_t *)b.alloc(n);
+    a.d = (float *)b.alloc(nb * 4);
+    a.s = (float *)b.alloc(nb * 4);
+    a.qsum = (int *)b.alloc(nb * 4);
+    return a.f && a.h && a.q && a.d && a.s && a.qsum;
+}
+
+}  // namespace
+
+extern "C" RWKV_API bool rwkv_mi355x_selftest_quantize_act(int wtype, const float * x, int T, int K, int8_t * q,
+                                                           float * d, float * s) {
+    if (K % 32 || T <= 0) return false;
+    DevBufs b;
+    ActBuf a;
+    const int fmt = act_fmt_for(wtype);
+    float * dx = (float *)b.alloc((size_t)T * K * 4);
+    if (!dx || !make_act(b, fmt, T, K, a)) return false;
+    if (hipMemcpy(dx, x, (size_t)T * K * 4, hipMemcpyHostToDevice) != hipSuccess) return false;
+    if (!launch_act_from_f32(nullptr, dx, T, K, a)) return false;
+    if (hipDeviceSynchronize() != hipSuccess) return false;
+    const size_t nb = (size_t)T * K / 32;
+    if (q && hipMemcpy(q, a.q, (size_t)T * K, hipMemcpyDeviceToHost) != hipSuccess) return false;
+    if (d && hipMemcpy(d, a.d, nb * 4, hipMemcpyDeviceToHost) != hipSuccess) return false;
+    if (s && hipMemcpy(s, a.s, nb * 4, hipMemcpyDeviceToHost) != hipSuccess) return false;
+    return true;
+}
+
+extern "C" RWKV_API bool rwkv_mi355x_selftest_matmul(int wtype, const void * W, int K, int M, const float * x, int T,
+                                                     float * y) {
+    if (K % 32 || T <= 0 || M <= 0) return false;
+    HostTensor ht;
+    ht.name = "selftest";
+    ht.type = (uint32_t)wtype;
+    ht.ndim = 2;
+    ht.ne[0] = (uint32_t)K;
+    ht.ne[1] = (uint32_t)M;
+    const size_t nbytes = type_nbytes(ht.type, ht.nel());
+    if (!nbytes) return false;
+    ht.data.assign((const uint8_t *)W, (const uint8_t *)W + nbytes);
+    DeviceModel dm;
+    DMat dmat{};
+    bool ok = upload_mat(dm, &ht, dmat, false, false);
+    DevBufs b;
+    ActBuf a;
+    float * dx = (float *)b.alloc((size_t)T * K * 4);
+    float * dy = (float *)b.alloc((size_t)T * M * 4);
+    ok = ok && dx && dy && make_act(b, act_fmt_for(wtype), T, K, a);
+    ok = ok && hipMemcpy(dx, x, (size_t)T * K * 4, hipMemcpyHostToDevice) == hipSuccess;
+    ok = ok && launch_act_from_f32(nullptr, dx, T, K, a);
+    if (ok) {
+        MMGroup g;
+        memset(&g, 0, sizeof(g));
+        g.n = 1;
+        g.T = T;
+        g.e[0].W = dmat;
+        g.e[0].in = a;
+        g.e[0].y = dy;
+        g.e[0].ldy = M;
+        g.e[0].epi = EPI_STORE;
+        ok = launch_mm_group(nullptr, g, wtype);
+    }
+    ok = ok && hipDeviceSynchronize() == hipSuccess;
+    ok = ok && hipMemcpy(y, dy, (size_t)T * M * 4, hipMemcpyDeviceToHost) == hipSuccess;
+    free_model(dm);
+    return ok;
+}

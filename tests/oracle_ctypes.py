@@ -126,3 +126,55 @@ def matmul(fmt, w_bytes, K, M, x):
     w_bytes = np.ascontiguousarray(w_bytes)
     lib().oracle_matmul(TYPE_IDS[fmt], _p(w_bytes), K, M, _p(x), T, _p(y))
     return y
+
+
+def set_variant(v):
+    L = lib()
+    L.oracle_set_variant.argtypes = [ctypes.c_int]
+    L.oracle_set_variant(v)
+
+
+def noise_band(path, tokens, sequence=False):
+    """Oracle logits/state (variant 0) plus the largest deviation any re-associated variant
+    (1..7: reversed order / scalar ggml dot / fp32 accumulators) produces: how strongly this
+    model amplifies last-bit differences.  Returns (logits, state, noise_logits, variants)."""
+    outs = []
+    try:
+        for v in range(8):
+            set_variant(v)
+            m = OracleModel(path)
+            outs.append(m.eval_sequence(tokens) if sequence else m.eval_serial(tokens))
+            m.close()
+    finally:
+        set_variant(0)
+    lg0, st0 = outs[0]
+    noise = max(float(np.abs(o[0] - lg0).max()) for o in outs[1:])
+    return lg0, st0, noise, [o[0] for o in outs]
+
+
+def dequantize(fmt, w_bytes, K, M):
+    L = lib()
+    t = TYPE_IDS[fmt]
+    out = np.zeros((M, K), np.float32)
+    bpr = (K // 32) * L.oracle_block_bytes(t) if t not in (0, 1) else K * (4 if t == 0 else 2)
+    w_bytes = np.ascontiguousarray(w_bytes)
+    for m in range(M):
+        L.oracle_dequantize_row(t, w_bytes.ctypes.data + m * bpr, out[m].ctypes.data, K)
+    return out
+
+
+def quantize_act(fmt, x):
+    """ggml activation quantizer (Q8_0 / Q8_1) on one row: returns (q int8 [K], d [K/32], s [K/32])."""
+    L = lib()
+    t = TYPE_IDS[fmt]
+    K = x.shape[0]
+    bb = 36 if fmt == 'Q8_1' else 34
+    buf = np.zeros((K // 32) * bb, np.uint8)
+    x = np.ascontiguousarray(x, np.float32)
+    L.oracle_quantize_act(t, x.ctypes.data, buf.ctypes.data, K)
+    blk = buf.reshape(-1, bb)
+    d = blk[:, 0:2].copy().view(np.float16).astype(np.float32).ravel()
+    off = 4 if fmt == 'Q8_1' else 2
+    s = blk[:, 2:4].copy().view(np.float16).astype(np.float32).ravel() if fmt == 'Q8_1' else None
+    q = blk[:, off:off + 32].copy().view(np.int8).ravel()
+    return q, d, s

@@ -1,11 +1,15 @@
 """GPU parity: librwkv.so on the MI355X vs the CPU oracle and the reference's fixtures.
 
 Tolerances (written here, see DESIGN.md "Parity"):
-  * FP32 / FP16 weights: |logit_gpu - logit_oracle| <= 1e-3 (north-star bound), state max
-    abs diff <= 1e-3; FP32 logits vs the reference's expected-logits <= 1e-3.
-  * Quantized weights: activations are re-quantized to Q8 blocks at every matmul
-    (ggml numerics), so a last-bit difference can flip one int8 step; logits must agree to
-    2e-2 absolute and the reference's own signed-sum rule (|sum| <= 1.05*|bound|) must hold.
+  * FP32 weights: |logit_gpu - logit_oracle| <= 1e-3 (north-star bound), state <= 1e-3,
+    and FP32 logits vs the reference's expected-logits <= 1e-3.
+  * FP16 / quantized weights: activations are rounded to fp16 / re-quantized to Q8 blocks at
+    every matmul (ggml numerics), so a last-bit difference anywhere can flip one rounding
+    step and some tiny checkpoints (5v1/5v2) amplify that.  The oracle measures this itself
+    (noise_band: the largest deviation among 7 re-associated restatements).  The GPU must
+    agree with the oracle to max(1e-3, 1.5 * noise) -- i.e. at the north-star bound unless
+    the oracle's own restatements disagree by more -- and satisfy the reference's signed-sum
+    rule |sum(logits - expected)| <= 1.05*|bound| (logit_difference_validator.inc:68,83).
   * Layout/bookkeeping properties are bit-exact: serial == sequence == chunked state,
     NULL-logits state, cloned contexts (reference tests/test_eval_sequence_in_chunks.c,
     test_logit_calculation_skipping.c, test_context_cloning.c).
@@ -16,7 +20,7 @@ import os
 import numpy as np
 import pytest
 
-from oracle_ctypes import OracleModel, quantize_file as oracle_quantize
+from oracle_ctypes import OracleModel, noise_band, quantize_file as oracle_quantize
 from rwkv_lib import RWKVModel, library
 
 pytestmark = pytest.mark.gpu
@@ -59,12 +63,12 @@ def model_path(v, fmt, qdir):
 @pytest.mark.parametrize('fmt', ['FP32', 'FP16'])
 def test_float_models_match_oracle(v, fmt, quantized_dir):
     path = model_path(v, fmt, quantized_dir)
-    ref = OracleModel(path)
     m = RWKVModel(library(), path, gpu_layer_count=99)
     lg, st = gpu_serial(m, PROMPT)
-    olg, ost = ref.eval_serial(PROMPT)
-    assert np.abs(lg - olg).max() <= 1e-3
-    assert np.abs(st - ost).max() <= 1e-3
+    olg, ost, noise, _ = noise_band(path, PROMPT)
+    tol = 1e-3 if fmt == 'FP32' else max(1e-3, 1.5 * noise)
+    assert np.abs(lg - olg).max() <= tol, (np.abs(lg - olg).max(), noise)
+    assert np.abs(st - ost).max() <= max(tol, 1e-3)
     if fmt == 'FP32':
         assert np.abs(lg - expected(v)).max() <= 1e-3
     s = float((lg - expected(v)).sum())
@@ -78,11 +82,10 @@ def test_float_models_match_oracle(v, fmt, quantized_dir):
 def test_quantized_models_match_oracle(v, q, src, quantized_dir):
     fmt = f'{src}-to-{q}'
     path = model_path(v, fmt, quantized_dir)
-    ref = OracleModel(path)
     m = RWKVModel(library(), path)
     lg, st = gpu_serial(m, PROMPT)
-    olg, _ = ref.eval_serial(PROMPT)
-    assert np.abs(lg - olg).max() <= 2e-2, np.abs(lg - olg).max()
+    olg, _, noise, _ = noise_band(path, PROMPT)
+    assert np.abs(lg - olg).max() <= max(1e-3, 1.5 * noise), (np.abs(lg - olg).max(), noise)
     s = float((lg - expected(v)).sum())
     assert abs(s) <= abs(CONST[f'quantized_{src}'][v][q]) * 1.05, s
     m.free()
@@ -91,11 +94,10 @@ def test_quantized_models_match_oracle(v, q, src, quantized_dir):
 @pytest.mark.parametrize('q', ['Q5_0', 'Q5_1'])
 def test_v6_compat_models(q):
     path = os.path.join(GOLD, f'tiny-rwkv-6v0-3m-{q}.bin')
-    ref = OracleModel(path)
     m = RWKVModel(library(), path)
     lg, st = gpu_serial(m, PROMPT)
-    olg, ost = ref.eval_serial(PROMPT)
-    assert np.abs(lg - olg).max() <= 2e-2
+    olg, _, noise, _ = noise_band(path, PROMPT)
+    assert np.abs(lg - olg).max() <= max(1e-3, 1.5 * noise), (np.abs(lg - olg).max(), noise)
     s = float((lg - expected('6v0-3m')).sum())
     assert abs(s) <= abs(CONST['compat']['6v0-3m'][q]) * 1.05
     m.free()
@@ -103,11 +105,10 @@ def test_v6_compat_models(q):
 
 def test_v6_fp16_to_q4_0():
     path = os.path.join(GOLD, 'tiny-rwkv-6v0-3m-FP16-to-Q4_0.bin')
-    ref = OracleModel(path)
     m = RWKVModel(library(), path)
     lg, _ = gpu_serial(m, LONG[:16])
-    olg, _ = ref.eval_serial(LONG[:16])
-    assert np.abs(lg - olg).max() <= 2e-2
+    olg, _, noise, _ = noise_band(path, LONG[:16])
+    assert np.abs(lg - olg).max() <= max(1e-3, 1.5 * noise), (np.abs(lg - olg).max(), noise)
     m.free()
 
 
@@ -252,13 +253,11 @@ def test_synthetic_real_width_matches_oracle(tmp_path, arch, fmt):
     L = library()
     p = str(tmp_path / f'syn{arch}.bin')
     assert L.library.rwkv_mi355x_write_synthetic_model(p.encode(), arch, 4096, 2048, 2, 0, fmt.encode(), 7)
-    ref = OracleModel(p)
     m = RWKVModel(L, p)
     toks = [5, 77, 1023, 4000, 9, 2048]
     lg, st = m.eval_sequence(toks, None, use_numpy=True)
-    olg, ost = ref.eval_sequence(toks)
-    scale = max(1.0, float(np.abs(olg).max()))
-    assert np.abs(lg - olg).max() <= 2e-2 * scale, np.abs(lg - olg).max()
+    olg, ost, noise, _ = noise_band(p, toks, sequence=True)
+    assert np.abs(lg - olg).max() <= max(1e-3, 1.5 * noise), (np.abs(lg - olg).max(), noise)
     lg2, st2 = gpu_serial(m, toks)
     assert np.array_equal(st, st2) and np.array_equal(lg, lg2)
     m.free()

@@ -1,0 +1,248 @@
+#!/usr/bin/env python3
+"""Benchmark of the RWKV eval hot path on MI355X (BASELINE.json metric).
+
+A "step" is one single-token decode (rwkv_eval semantics: the whole model incl. the head,
+logits produced) of RWKV-v6-World-1B6 Q4_0 with the recurrent state resident in HBM
+(rwkv_mi355x_eval_device).  Steps are enqueued back to back on the context's stream.
+value = tokens decoded by all ranks / max-over-ranks wall time of the K timed steps.
+Multi-GPU: decode does not shard -- each rank runs an independent replica
+("scaling": "weak").
+
+Also reported (same run): 1024-token rwkv_eval_sequence throughput, ABI-level decode
+(13 MB of host state in and out per token, the reference's contract), the dominant kernel's
+roofline (HIP events on the context stream, algorithmic bytes), and the CPU restatement of
+the reference arithmetic (oracle/) timed on this host's cores.
+
+Synthetic weights (no checkpoint can be downloaded): rwkv_mi355x_write_synthetic_model
+writes an rwkv.cpp file with the exact tensor shapes of the real checkpoint.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, 'rwkv.cppy_amd', 'python'))
+sys.path.insert(0, os.path.join(REPO, 'tests'))
+
+METRIC = 'tokens/sec RWKV-v6-World-1B6 Q4_0 decode + seq-eval @1/2/4/8 GPU; HBM GB/s vs peak'
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+
+CONFIGS = {
+    # name: arch, n_vocab, n_embed, n_layer, ffn (0 = arch default), format, label
+    'v6-1b6-q4_0': (6, 65536, 2048, 24, 0, 'Q4_0', 'RWKV-v6-World-1B6 Q4_0'),
+    'v4-169m-q8_0': (4, 50277, 768, 12, 0, 'Q8_0', 'RWKV-v4-Pile-169M Q8_0'),
+    'v7-2b9-q5_1': (7, 65536, 2560, 32, 0, 'Q5_1', 'RWKV-v7-World-2.9B Q5_1'),
+    'v5-7b-q4_1': (5, 65536, 4096, 32, 14336, 'Q4_1', 'RWKV-v5-World-7B Q4_1'),
+}
+
+
+def log(*a):
+    print('[bench]', *a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=256)
+    ap.add_argument('--warmup', type=int, default=16)
+    ap.add_argument('--config', default='v6-1b6-q4_0', choices=sorted(CONFIGS))
+    ap.add_argument('--seq-len', type=int, default=1024)
+    ap.add_argument('--seq-reps', type=int, default=3)
+    ap.add_argument('--abi-steps', type=int, default=16)
+    ap.add_argument('--timing-steps', type=int, default=8)
+    ap.add_argument('--cpu-seconds', type=float, default=12.0)
+    ap.add_argument('--skip-cpu', action='store_true')
+    ap.add_argument('--model-dir', default=os.environ.get('RWKV_BENCH_DIR', '/tmp/rwkv_bench'))
+    args = ap.parse_args()
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local_rank = int(os.environ.get('LOCAL_RANK', '0'))
+    os.environ.setdefault('RWKV_MI355X_DEVICE', str(local_rank))
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local_rank))
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    import rwkv_cpp
+    lib = rwkv_cpp.RWKVSharedLibrary(os.path.join(REPO, 'rwkv.cppy_amd', 'build', 'librwkv.so'))
+    L = lib.library
+    arch, V, C, NL, F, fmt, label = CONFIGS[args.config]
+    os.makedirs(args.model_dir, exist_ok=True)
+    path = os.path.join(args.model_dir, f'{args.config}-seed1.bin')
+    if rank == 0 and not os.path.isfile(path):
+        t = time.time()
+        tmp = path + '.tmp'
+        assert L.rwkv_mi355x_write_synthetic_model(tmp.encode(), arch, V, C, NL, F, fmt.encode(), 1)
+        os.replace(tmp, path)
+        log(f'wrote synthetic {label} ({os.path.getsize(path) / 1e9:.2f} GB) in {time.time() - t:.1f}s')
+    barrier()
+
+    t = time.time()
+    ctx = lib.rwkv_init_from_file(path, 1, NL + 1)
+    log(f'rank {rank}: loaded {label} in {time.time() - t:.1f}s  [{lib.rwkv_get_system_info_string()}]')
+    n_vocab = L.rwkv_get_n_vocab(ctx.ptr)
+    state_len = L.rwkv_get_state_len(ctx.ptr)
+    rng = np.random.default_rng(1234 + rank)
+    P_INT = ctypes.POINTER(ctypes.c_int32)
+    P_F = ctypes.POINTER(ctypes.c_float)
+
+    def tok_arr(toks):
+        a = np.ascontiguousarray(np.asarray(toks, dtype=np.int32))
+        return a, a.ctypes.data_as(P_INT)
+
+    assert L.rwkv_mi355x_state_upload(ctx.ptr, None)
+
+    # ---------------- decode (device-resident state) ----------------
+    dec_tokens = rng.integers(0, n_vocab, size=args.warmup + args.steps)
+    arrs = [tok_arr([int(t)]) for t in dec_tokens]
+
+    def step(i):
+        if not L.rwkv_mi355x_eval_device(ctx.ptr, arrs[i][1], 1, True, None, False):
+            raise RuntimeError('eval_device failed')
+
+    for i in range(args.warmup):
+        step(i)
+    L.rwkv_mi355x_sync(ctx.ptr)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.warmup, args.warmup + args.steps):
+        step(i)
+    L.rwkv_mi355x_sync(ctx.ptr)
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], device='cuda')
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    ms_per_step = elapsed * 1e3 / args.steps
+    value = world * args.steps / elapsed
+    log(f'decode: {ms_per_step * 1e3:.1f} us/token, {value:.1f} tok/s aggregate over {world} GPU(s)')
+
+    # ---------------- sequence eval ----------------
+    seq = rng.integers(0, n_vocab, size=args.seq_len)
+    sa, sp = tok_arr(seq)
+    assert L.rwkv_mi355x_state_upload(ctx.ptr, None)
+    assert L.rwkv_mi355x_eval_device(ctx.ptr, sp, len(seq), True, None, True)  # warm-up / workspace
+    ts = []
+    for _ in range(args.seq_reps):
+        assert L.rwkv_mi355x_state_upload(ctx.ptr, None)
+        L.rwkv_mi355x_sync(ctx.ptr)
+        t1 = time.perf_counter()
+        assert L.rwkv_mi355x_eval_device(ctx.ptr, sp, len(seq), True, None, True)
+        ts.append(time.perf_counter() - t1)
+    seq_s = min(ts)
+    seq_tps = args.seq_len / seq_s
+    log(f'seq-eval T={args.seq_len}: {seq_s * 1e3:.1f} ms, {seq_tps:.0f} tok/s')
+
+    # ---------------- ABI-level decode (host state, reference contract) ----------------
+    state = np.zeros(state_len, np.float32)
+    logits = np.zeros(n_vocab, np.float32)
+    L.rwkv_init_state(ctx.ptr, state.ctypes.data_as(P_F))
+    L.rwkv_eval(ctx.ptr, int(dec_tokens[0]), state.ctypes.data_as(P_F), state.ctypes.data_as(P_F),
+                logits.ctypes.data_as(P_F))
+    t2 = time.perf_counter()
+    for i in range(args.abi_steps):
+        assert L.rwkv_eval(ctx.ptr, int(dec_tokens[i]), state.ctypes.data_as(P_F), state.ctypes.data_as(P_F),
+                           logits.ctypes.data_as(P_F))
+    abi_tps = args.abi_steps / (time.perf_counter() - t2)
+    log(f'ABI decode (host state {state_len * 4 / 1e6:.1f} MB each way): {abi_tps:.1f} tok/s')
+
+    # ---------------- dominant-kernel roofline (HIP events on the context stream) ----------------
+    assert L.rwkv_mi355x_state_upload(ctx.ptr, None)
+    L.rwkv_mi355x_set_kernel_timing(ctx.ptr, True)
+    for i in range(args.timing_steps):
+        step(i)
+    L.rwkv_mi355x_sync(ctx.ptr)
+    n = L.rwkv_mi355x_kernel_stats(ctx.ptr, -1, None, 0, None, None, None, None)
+    kstats = []
+    for i in range(n):
+        name = ctypes.create_string_buffer(128)
+        la, ms, by, fl = ctypes.c_longlong(), ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        L.rwkv_mi355x_kernel_stats(ctx.ptr, i, name, 128, ctypes.byref(la), ctypes.byref(ms), ctypes.byref(by),
+                                   ctypes.byref(fl))
+        kstats.append(dict(name=name.value.decode(), launches=la.value, ms=ms.value, bytes=by.value, flops=fl.value))
+    L.rwkv_mi355x_set_kernel_timing(ctx.ptr, False)
+    kstats.sort(key=lambda k: -k['ms'])
+    for k in kstats:
+        log(f"  {k['name']:<18} launches {k['launches']:5d} avg {k['ms'] / k['launches'] * 1e3:8.2f} us "
+            f"{k['bytes'] / k['launches'] / 1e6:8.3f} MB/launch -> {k['bytes'] / k['ms'] / 1e6:8.1f} GB/s")
+    dom = kstats[0]
+    avg_us = dom['ms'] / dom['launches'] * 1e3
+    bytes_per_launch = dom['bytes'] / dom['launches']
+    achieved = bytes_per_launch / (avg_us * 1e-6) / 1e9
+    mm_ms = sum(k['ms'] for k in kstats) / args.timing_steps
+    mm_bytes = sum(k['bytes'] for k in kstats) / args.timing_steps
+    roofline = {
+        'kernel': dom['name'], 'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+        'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': None,
+        'avg_launch_us': round(avg_us, 3), 'algorithmic_bytes_per_launch': round(bytes_per_launch),
+        'all_matmuls_GBps': round(mm_bytes / (mm_ms * 1e-3) / 1e9, 1),
+        'decode_bytes_per_token': round(L.rwkv_mi355x_decode_bytes(ctx.ptr, True)),
+        'decode_GBps_end_to_end': round(L.rwkv_mi355x_decode_bytes(ctx.ptr, True) / (ms_per_step * 1e-3) / 1e9, 1),
+    }
+
+    # ---------------- CPU baseline: oracle (CPU restatement of the reference arithmetic) ----------------
+    cpu = None
+    if rank == 0 and world == 1 and not args.skip_cpu:
+        try:
+            from oracle_ctypes import OracleModel, lib as olib
+            threads = int(os.environ.get('OMP_NUM_THREADS', '0') or 0) or min(16, os.cpu_count() or 1)
+            olib().oracle_set_threads(threads)
+            t3 = time.time()
+            om = OracleModel(path)
+            load_s = time.time() - t3
+            st = None
+            ntok = 0
+            t4 = time.perf_counter()
+            while True:
+                lg, st = om.eval_sequence([int(dec_tokens[ntok])], st)
+                ntok += 1
+                if time.perf_counter() - t4 >= args.cpu_seconds or ntok >= 256:
+                    break
+            cpu_s = time.perf_counter() - t4
+            cpu = {'value': round(ntok / cpu_s, 3), 'unit': 'tokens/s', 'cores': olib().oracle_get_threads(),
+                   'kind': 'port',
+                   'sample': f'{label} single-token decode (logits on), {ntok} tokens from a fresh state, '
+                             f'{cpu_s:.1f}s; oracle/ C restatement of the reference CPU arithmetic '
+                             f'(ggml Q8 activation quantization + int8 block dots), OpenMP over rows'}
+            log(f'cpu baseline: {cpu["value"]} tok/s on {cpu["cores"]} threads (load {load_s:.1f}s)')
+            om.close()
+        except Exception as e:  # the baseline is reported, never required
+            log(f'cpu baseline failed: {e}')
+
+    L.rwkv_free(ctx.ptr)
+    if rank == 0:
+        out = {
+            'metric': METRIC, 'value': round(value, 2), 'unit': 'tokens/s', 'n_gpus': world, 'steps': args.steps,
+            'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 5), 'higher_is_better': True,
+            'scaling': 'weak', 'vs_baseline': None, 'dtype': 'i8 (q4 x q8 int8 dot) + f32', 'data': 'synthetic',
+            'config': {'workload': f'{label} single-token decode (rwkv_eval semantics, logits on), '
+                                   f'state resident in HBM', 'n_embed': C, 'n_layer': NL, 'n_vocab': V,
+                       'weights': fmt, 'parallelism': f'replicas x{world}'},
+            'seq_eval': {'tokens_per_s': round(seq_tps * world, 1), 'T': args.seq_len,
+                         'ms_per_sequence': round(seq_s * 1e3, 3)},
+            'abi_decode_tokens_per_s': round(abi_tps * world, 2),
+            'roofline': roofline,
+            'cpu_baseline': cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -22,10 +22,11 @@ RWKV_API bool rwkv_mi355x_state_upload(struct rwkv_context * ctx, const float * 
 RWKV_API bool rwkv_mi355x_state_download(struct rwkv_context * ctx, float * state);
 
 /* rwkv_eval_sequence semantics on the device-resident state: tokens host array, T >= 1.
- * logits_out (host, may be NULL) receives the last token's logits.  No state crosses PCIe.
- * sync=false returns after enqueueing (the caller later calls rwkv_mi355x_sync). */
+ * compute_logits: run the head on the last token (logits stay in HBM); logits_out (host, may be
+ * NULL) additionally receives them.  No state crosses PCIe.  sync=false returns after
+ * enqueueing (the caller later calls rwkv_mi355x_sync). */
 RWKV_API bool rwkv_mi355x_eval_device(struct rwkv_context * ctx, const uint32_t * tokens, size_t T,
-                                      float * logits_out, bool sync);
+                                      bool compute_logits, float * logits_out, bool sync);
 RWKV_API bool rwkv_mi355x_sync(struct rwkv_context * ctx);
 
 /* The context's HIP stream (hipStream_t), so callers can time kernels with events on it. */
@@ -55,6 +56,17 @@ RWKV_API void rwkv_mi355x_arch(const struct rwkv_context * ctx, int64_t out[4]);
 RWKV_API bool rwkv_mi355x_write_synthetic_model(const char * path, int arch, uint32_t n_vocab,
                                                 uint32_t n_embed, uint32_t n_layer, uint32_t ffn,
                                                 const char * fmt, uint64_t seed);
+
+/* Kernel timing: while on, every matmul launch on the context stream is bracketed by hipEvents
+ * (decode runs eagerly, not from the captured graph) and accumulated per kernel class -- the
+ * template instantiation name rocprofv3 reports, e.g. "k_mm<2, 2, 1>" (weight type, rows per
+ * wave, columns per pass).  Turning it on clears the counters. */
+RWKV_API void rwkv_mi355x_set_kernel_timing(struct rwkv_context * ctx, bool on);
+/* Reads counter `index`; returns the number of kernel classes (call with index -1 to count).
+ * total_bytes: algorithmic bytes (weights at original block sizes + activations in/out). */
+RWKV_API int rwkv_mi355x_kernel_stats(struct rwkv_context * ctx, int index, char * name, size_t name_len,
+                                      long long * launches, double * total_ms, double * total_bytes,
+                                      double * total_flops);
 
 /* ---- kernel self-tests (used by tests/ for per-kernel parity; not on the eval path) ----
  * Runs the library's activation quantizer (the emit stage every producer kernel uses) on

@@ -253,6 +253,8 @@ Engine::~Engine() {
             if (g) (void)hipGraphExecDestroy(g);
     for (void * p : ws_allocs_) (void)hipFree(p);
     if (htokens_) (void)hipHostFree(htokens_);
+    collect_timing();
+    for (hipEvent_t e : event_pool_) (void)hipEventDestroy(e);
     if (tok_event_) (void)hipEventDestroy(tok_event_);
     if (stream_) (void)hipStreamDestroy(stream_);
 }
@@ -370,7 +372,7 @@ struct MMBatch {
         }
         e.push_back(m);
     }
-    bool run(hipStream_t st, int T) {
+    bool run(Engine & eng, int T) {
         std::vector<bool> done(e.size(), false);
         for (size_t i = 0; i < e.size(); i++) {
             if (done[i]) continue;
@@ -384,12 +386,87 @@ struct MMBatch {
                     done[j] = true;
                 }
             }
-            if (!launch_mm_group(st, g, type)) return false;
+            if (!eng.mm_launch(g, type)) return false;
         }
         e.clear();
         return true;
     }
 };
+
+static double act_bytes(const ActBuf & a, double T) {
+    const double K = a.K;
+    switch (a.fmt) {
+        case A_F32: return T * K * 4;
+        case A_F16: return T * K * 2;
+        case A_Q8_1: return T * K + T * K / 32 * 12;
+        default: return T * K + T * K / 32 * 8;
+    }
+}
+
+void Engine::set_timing(bool on) {
+    (void)hipStreamSynchronize(stream_);
+    collect_timing();
+    timing_ = on;
+    if (on) stats_.clear();
+}
+
+bool Engine::mm_launch(MMGroup & g, int wtype) {
+    if (!timing_) return launch_mm_group(stream_, g, wtype);
+    bool emit = false;
+    double bytes = 0, flops = 0;
+    for (int i = 0; i < g.n; i++) {
+        const MMEntry & e = g.e[i];
+        emit |= e.emit != 0;
+        bytes += (double)type_nbytes((uint32_t)e.W.type, (uint64_t)e.W.M * e.W.K) + act_bytes(e.in, g.T);
+        if (e.y) bytes += (double)g.T * e.W.M * 4 * ((e.epi == EPI_ADD || e.epi == EPI_SIGMUL_ADD || e.epi == EPI_VMIX7) ? 2 : 1);
+        if (e.emit) bytes += act_bytes(e.out, g.T);
+        flops += 2.0 * e.W.M * e.W.K * g.T;
+    }
+    // kernel class = the template instantiation rocprofv3 reports: k_mm<WF, RPW, NT>
+    const std::string name = "k_mm<" + std::to_string(wtype) + ", " + (emit ? "8" : "2") + ", " + (g.T == 1 ? "1" : "4") + ">";
+    int si = -1;
+    for (size_t i = 0; i < stats_.size(); i++)
+        if (stats_[i].name == name) si = (int)i;
+    if (si < 0) {
+        stats_.push_back(KernelStat{name});
+        si = (int)stats_.size() - 1;
+    }
+    stats_[si].total_bytes += bytes;
+    stats_[si].total_flops += flops;
+    stats_[si].launches++;
+    hipEvent_t a, b;
+    if (event_pool_.size() >= 2) {
+        a = event_pool_.back();
+        event_pool_.pop_back();
+        b = event_pool_.back();
+        event_pool_.pop_back();
+    } else {
+        HIP_OK(hipEventCreate(&a));
+        HIP_OK(hipEventCreate(&b));
+    }
+    HIP_OK(hipEventRecord(a, stream_));
+    const bool ok = launch_mm_group(stream_, g, wtype);
+    HIP_OK(hipEventRecord(b, stream_));
+    pending_.push_back(Pending{si, a, b});
+    return ok;
+}
+
+void Engine::collect_timing() {
+    for (auto & p : pending_) {
+        float ms = 0;
+        if (hipEventSynchronize(p.b) == hipSuccess && hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess)
+            stats_[p.stat].total_ms += ms;
+        event_pool_.push_back(p.a);
+        event_pool_.push_back(p.b);
+    }
+    pending_.clear();
+}
+
+const std::vector<KernelStat> & Engine::stats() {
+    (void)hipStreamSynchronize(stream_);
+    collect_timing();
+    return stats_;
+}
 
 bool Engine::ffn(int l, int T, const float * si, float * so) {
     const DLayer & L = m_->layers[l];
@@ -413,9 +490,9 @@ bool Engine::ffn(int l, int T, const float * si, float * so) {
         if (!launch_ln_mix(stream_, a)) return false;
         ActBuf kin = A(1, L.ffn_v);
         b.add(L.ffn_k, A(0, L.ffn_k), nullptr, 0, EPI_RELU_SQ, nullptr, nullptr, &kin);
-        if (!b.run(stream_, T)) return false;
+        if (!b.run(*this, T)) return false;
         b.add(L.ffn_v, kin, x_, C, EPI_ADD);
-        return b.run(stream_, T);
+        return b.run(*this, T);
     }
     // v4/v5: rwkv_graph.inc:484-511 (form 0); v6: :513-531 (form 1)
     a.form = m_->major == 6 ? 1 : 0;
@@ -428,9 +505,9 @@ bool Engine::ffn(int l, int T, const float * si, float * so) {
     ActBuf kin = A(2, L.ffn_v);
     b.add(L.ffn_r, A(1, L.ffn_r), fr_, C, EPI_STORE);
     b.add(L.ffn_k, A(0, L.ffn_k), nullptr, 0, EPI_RELU_SQ, nullptr, nullptr, &kin);
-    if (!b.run(stream_, T)) return false;
+    if (!b.run(*this, T)) return false;
     b.add(L.ffn_v, kin, x_, C, EPI_SIGMUL_ADD, fr_);
-    return b.run(stream_, T);
+    return b.run(*this, T);
 }
 
 bool Engine::layer_v4(int l, int T, const float * si, float * so) {
@@ -458,11 +535,11 @@ bool Engine::layer_v4(int l, int T, const float * si, float * so) {
     b.add(L.att_r, A(2, L.att_r), r_, C, EPI_SIGMOID);
     b.add(L.att_k, A(0, L.att_k), k_, C, EPI_STORE);
     b.add(L.att_v, A(1, L.att_v), v_, C, EPI_STORE);
-    if (!b.run(stream_, T)) return false;
+    if (!b.run(*this, T)) return false;
     ActBuf o = A(3, L.att_o);
     if (!launch_wkv4(stream_, T, C, r_, k_, v_, L.att_first, L.att_decay, si, so, o)) return false;
     b.add(L.att_o, o, x_, C, EPI_ADD);
-    if (!b.run(stream_, T)) return false;
+    if (!b.run(*this, T)) return false;
     return ffn(l, T, si, so);
 }
 
@@ -497,13 +574,13 @@ bool Engine::layer_v5(int l, int T, const float * si, float * so) {
     b.add(L.att_k, A(0, L.att_k), k_, C, EPI_STORE);
     b.add(L.att_v, A(1, L.att_v), v_, C, EPI_STORE);
     if (v52) b.add(L.att_g, A(3, L.att_g), g_, C, EPI_SILU);
-    if (!b.run(stream_, T)) return false;
+    if (!b.run(*this, T)) return false;
     if (!launch_wkv6(stream_, T, H, S, k_, v_, r_, L.att_u, L.att_w, 0, si + 2 * C, so + 2 * C, y_)) return false;
     ActBuf o = A(4, L.att_o);
     if (!launch_groupnorm(stream_, T, H, S, 1e-5f, y_, L.att_lnx_w, L.att_lnx_b, v52 ? 1 : 0, g_, nullptr, nullptr, o))
         return false;
     b.add(L.att_o, o, x_, C, EPI_ADD);
-    if (!b.run(stream_, T)) return false;
+    if (!b.run(*this, T)) return false;
     return ffn(l, T, si, so);
 }
 
@@ -528,7 +605,7 @@ bool Engine::layer_v6(int l, int T, const float * si, float * so) {
     if (!launch_ln_mix(stream_, a)) return false;
     MMBatch b;
     b.add(L.maa_w1, A(0, L.maa_w1), lora_, 5 * D, EPI_TANH);
-    if (!b.run(stream_, T)) return false;
+    if (!b.run(*this, T)) return false;
     // order w, k, v, r, g (rwkv_graph.inc:336-346)
     ActBuf outs[5] = {A(1, L.decay_w1), A(2, L.att_k), A(3, L.att_v), A(4, L.att_r), A(5, L.att_g)};
     if (!launch_v6_mix5(stream_, T, C, D, lora_, L.maa_w2, L.maa, xa_, sx_, outs)) return false;
@@ -538,14 +615,14 @@ bool Engine::layer_v6(int l, int T, const float * si, float * so) {
     b.add(L.att_v, outs[2], v_, C, EPI_STORE);
     b.add(L.att_g, outs[4], g_, C, EPI_SILU);
     b.add(L.decay_w1, outs[0], nullptr, 0, EPI_TANH, nullptr, nullptr, &dl);
-    if (!b.run(stream_, T)) return false;
+    if (!b.run(*this, T)) return false;
     b.add(L.decay_w2, dl, w_, C, EPI_DECAY6, nullptr, L.decay6);
-    if (!b.run(stream_, T)) return false;
+    if (!b.run(*this, T)) return false;
     if (!launch_wkv6(stream_, T, H, S, k_, v_, r_, L.att_u, w_, 1, si + 2 * C, so + 2 * C, y_)) return false;
     ActBuf o = A(7, L.att_o);
     if (!launch_groupnorm(stream_, T, H, S, 64e-5f, y_, L.att_lnx_w, L.att_lnx_b, 1, g_, nullptr, nullptr, o)) return false;
     b.add(L.att_o, o, x_, C, EPI_ADD);
-    if (!b.run(stream_, T)) return false;
+    if (!b.run(*this, T)) return false;
     return ffn(l, T, si, so);
 }
 
@@ -601,7 +678,7 @@ bool Engine::layer_v7(int l, int T, const float * si, float * so) {
         lvv = A(10, L.v2);
         b.add(L.v1, xv1, nullptr, 0, EPI_STORE, nullptr, nullptr, &lvv);
     }
-    if (!b.run(stream_, T)) return false;
+    if (!b.run(*this, T)) return false;
     if (l == 0) {
         HIP_OK(hipMemcpyAsync(vfirst_, v_, (size_t)T * C * 4, hipMemcpyDeviceToDevice, stream_));
     }
@@ -609,13 +686,13 @@ bool Engine::layer_v7(int l, int T, const float * si, float * so) {
     b.add(L.a2, la, a_, C, EPI_SIGMOID_BIAS, nullptr, L.a0);
     b.add(L.g2, lg, g_, C, EPI_STORE);
     if (vlora) b.add(L.v2, lvv, v_, C, EPI_VMIX7, vfirst_, L.v0);
-    if (!b.run(stream_, T)) return false;
+    if (!b.run(*this, T)) return false;
     if (!launch_v7_prep(stream_, T, H, S, k_, a_, r_, L.k_k, L.k_a, L.r_k, nb_, bb_, bonus_)) return false;
     if (!launch_wkv7(stream_, T, H, S, r_, w_, k_, v_, nb_, bb_, si + 2 * C, so + 2 * C, y_)) return false;
     ActBuf o = A(0, L.att_o);
     if (!launch_groupnorm(stream_, T, H, S, 64e-5f, y_, L.att_lnx_w, L.att_lnx_b, 2, g_, v_, bonus_, o)) return false;
     b.add(L.att_o, o, x_, C, EPI_ADD);
-    if (!b.run(stream_, T)) return false;
+    if (!b.run(*this, T)) return false;
     return ffn(l, T, si, so);
 }
 
@@ -642,7 +719,7 @@ bool Engine::forward(int T, const float * sin, float * sout, bool logits) {
         if (!launch_ln_emit(stream_, (int)C, x_ + (size_t)(T - 1) * C, m_->lnout_w, m_->lnout_b, hin)) return false;
         MMBatch b;
         b.add(m_->head, hin, logits_, (int)m_->n_vocab, EPI_STORE);
-        if (!b.run(stream_, 1)) return false;
+        if (!b.run(*this, 1)) return false;
     }
     return true;
 }
@@ -661,7 +738,7 @@ bool Engine::run_tokens(const uint32_t * tokens, size_t T, bool want_logits) {
         HIP_OK(hipMemcpyAsync(dtokens_, htokens_, n * 4, hipMemcpyHostToDevice, stream_));
         HIP_OK(hipEventRecord(tok_event_, stream_));
         const bool lg = last && want_logits;
-        if (n == 1 && use_graphs_) {
+        if (n == 1 && use_graphs_ && !timing_) {
             hipGraphExec_t & ge = graphs_[cur_][lg ? 1 : 0];
             if (!ge) {
                 hipGraph_t g = nullptr;
@@ -718,9 +795,9 @@ bool Engine::eval(const uint32_t * tokens, size_t T, const float * state_in, flo
     return true;
 }
 
-bool Engine::eval_device(const uint32_t * tokens, size_t T, float * logits_out, bool sync_after) {
+bool Engine::eval_device(const uint32_t * tokens, size_t T, bool want_logits, float * logits_out, bool sync_after) {
     HIP_OK(hipSetDevice(m_->device));
-    if (!run_tokens(tokens, T, logits_out != nullptr)) return false;
+    if (!run_tokens(tokens, T, want_logits || logits_out != nullptr)) return false;
     if (logits_out)
         HIP_OK(hipMemcpyAsync(logits_out, logits_, (size_t)m_->n_vocab * 4, hipMemcpyDeviceToHost, stream_));
     if (sync_after || logits_out) HIP_OK(hipStreamSynchronize(stream_));

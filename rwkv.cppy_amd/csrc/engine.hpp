@@ -1,6 +1,7 @@
 // engine.hpp -- device-resident RWKV model and the per-version forward programs.
 #pragma once
 
+#include <string>
 #include <vector>
 
 #include "common.hpp"
@@ -61,6 +62,15 @@ struct ActSlot {
     float * f = nullptr;
 };
 
+// Per-kernel-class timing collected with hipEvents on the context stream (bench roofline).
+struct KernelStat {
+    std::string name;
+    long long launches = 0;
+    double total_ms = 0;
+    double total_bytes = 0;   // algorithmic bytes (weights at original block size + activations)
+    double total_flops = 0;
+};
+
 class Engine {
   public:
     explicit Engine(DeviceModel * m) : m_(m) {}
@@ -70,11 +80,14 @@ class Engine {
     // ABI-level evaluation (host buffers).  tokens host, T >= 1.
     bool eval(const uint32_t * tokens, size_t T, const float * state_in, float * state_out, float * logits_out);
     // device-resident evaluation on the context's own state
-    bool eval_device(const uint32_t * tokens, size_t T, float * logits_out, bool sync);
+    bool eval_device(const uint32_t * tokens, size_t T, bool want_logits, float * logits_out, bool sync);
     bool state_upload(const float * state);
     bool state_download(float * state);
     bool sync();
     hipStream_t stream() const { return stream_; }
+    void set_timing(bool on);
+    bool mm_launch(MMGroup & g, int wtype);
+    const std::vector<KernelStat> & stats();
     float * device_state() const { return dstate_[cur_]; }
 
   private:
@@ -106,6 +119,15 @@ class Engine {
     hipGraphExec_t graphs_[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // [cur][logits]
     bool use_graphs_ = true;
     hipEvent_t tok_event_ = nullptr;
+    bool timing_ = false;
+    struct Pending {
+        int stat;
+        hipEvent_t a, b;
+    };
+    std::vector<Pending> pending_;
+    std::vector<hipEvent_t> event_pool_;
+    std::vector<KernelStat> stats_;
+    void collect_timing();
 };
 
 }  // namespace rwkvmi

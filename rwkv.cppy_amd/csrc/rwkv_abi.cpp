@@ -209,12 +209,13 @@ RWKV_API const char * rwkv_get_system_info_string(void) {
 RWKV_API bool rwkv_mi355x_state_upload(struct rwkv_context * ctx, const float * state) { return ctx->engine->state_upload(state); }
 RWKV_API bool rwkv_mi355x_state_download(struct rwkv_context * ctx, float * state) { return ctx->engine->state_download(state); }
 
-RWKV_API bool rwkv_mi355x_eval_device(struct rwkv_context * ctx, const uint32_t * tokens, size_t T, float * logits_out, bool sync) {
+RWKV_API bool rwkv_mi355x_eval_device(struct rwkv_context * ctx, const uint32_t * tokens, size_t T, bool compute_logits,
+                                      float * logits_out, bool sync) {
     ctx->last_error = RWKV_ERROR_NONE;
     CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, T > 0 && tokens != nullptr, "Sequence length is 0");
     for (size_t i = 0; i < T; i++)
         CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, tokens[i] < ctx->model->dm.n_vocab, "Token out of range");
-    CTX_CHECK(ctx, RWKV_ERROR_CTX, false, ctx->engine->eval_device(tokens, T, logits_out, sync), "GPU evaluation failed");
+    CTX_CHECK(ctx, RWKV_ERROR_CTX, false, ctx->engine->eval_device(tokens, T, compute_logits || logits_out, logits_out, sync), "GPU evaluation failed");
     return true;
 }
 
@@ -247,6 +248,25 @@ RWKV_API void rwkv_mi355x_arch(const struct rwkv_context * ctx, int64_t out[4]) 
     out[1] = dm.minor;
     out[2] = dm.H;
     out[3] = dm.S;
+}
+
+RWKV_API void rwkv_mi355x_set_kernel_timing(struct rwkv_context * ctx, bool on) { ctx->engine->set_timing(on); }
+
+RWKV_API int rwkv_mi355x_kernel_stats(struct rwkv_context * ctx, int index, char * name, size_t name_len,
+                                      long long * launches, double * total_ms, double * total_bytes,
+                                      double * total_flops) {
+    const auto & st = ctx->engine->stats();
+    if (index < 0 || index >= (int)st.size()) return (int)st.size();
+    const KernelStat & k = st[index];
+    if (name && name_len) {
+        strncpy(name, k.name.c_str(), name_len - 1);
+        name[name_len - 1] = 0;
+    }
+    if (launches) *launches = k.launches;
+    if (total_ms) *total_ms = k.total_ms;
+    if (total_bytes) *total_bytes = k.total_bytes;
+    if (total_flops) *total_flops = k.total_flops;
+    return (int)st.size();
 }
 
 }  // extern "C"

@@ -70,7 +70,7 @@ class RWKVSharedLibrary:
         L.rwkv_mi355x_state_upload.restype = ctypes.c_bool
         L.rwkv_mi355x_state_download.argtypes = [vp, P_FLOAT]
         L.rwkv_mi355x_state_download.restype = ctypes.c_bool
-        L.rwkv_mi355x_eval_device.argtypes = [vp, P_INT, sz, P_FLOAT, ctypes.c_bool]
+        L.rwkv_mi355x_eval_device.argtypes = [vp, P_INT, sz, ctypes.c_bool, P_FLOAT, ctypes.c_bool]
         L.rwkv_mi355x_eval_device.restype = ctypes.c_bool
         L.rwkv_mi355x_sync.argtypes = [vp]
         L.rwkv_mi355x_sync.restype = ctypes.c_bool
@@ -89,6 +89,12 @@ class RWKVSharedLibrary:
         L.rwkv_mi355x_write_synthetic_model.argtypes = [ctypes.c_char_p, ctypes.c_int, u32, u32, u32, u32,
                                                         ctypes.c_char_p, ctypes.c_uint64]
         L.rwkv_mi355x_write_synthetic_model.restype = ctypes.c_bool
+        L.rwkv_mi355x_set_kernel_timing.argtypes = [vp, ctypes.c_bool]
+        L.rwkv_mi355x_set_kernel_timing.restype = None
+        L.rwkv_mi355x_kernel_stats.argtypes = [vp, ctypes.c_int, ctypes.c_char_p, sz, ctypes.POINTER(ctypes.c_longlong),
+                                               ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                               ctypes.POINTER(ctypes.c_double)]
+        L.rwkv_mi355x_kernel_stats.restype = ctypes.c_int
 
         self.nullptr = ctypes.cast(0, ctypes.c_void_p)
 

@@ -236,9 +236,9 @@ def test_device_resident_matches_abi():
     lg = np.zeros(m._logits_buffer_element_count, np.float32)
     for t in LONG[:19]:
         arr = (ctypes.c_int32 * 1)(t)
-        assert lib.rwkv_mi355x_eval_device(m._ctx.ptr, ctypes.cast(arr, ctypes.POINTER(ctypes.c_int32)), 1, None, False)
+        assert lib.rwkv_mi355x_eval_device(m._ctx.ptr, ctypes.cast(arr, ctypes.POINTER(ctypes.c_int32)), 1, False, None, False)
     arr = (ctypes.c_int32 * 1)(LONG[19])
-    assert lib.rwkv_mi355x_eval_device(m._ctx.ptr, ctypes.cast(arr, ctypes.POINTER(ctypes.c_int32)), 1,
+    assert lib.rwkv_mi355x_eval_device(m._ctx.ptr, ctypes.cast(arr, ctypes.POINTER(ctypes.c_int32)), 1, True,
                                        lg.ctypes.data_as(P), True)
     st = np.zeros(m._state_buffer_element_count, np.float32)
     assert lib.rwkv_mi355x_state_download(m._ctx.ptr, st.ctypes.data_as(P))

@@ -207,6 +207,18 @@ bool upload_model(const ModelFile & mf, DeviceModel & dm) {
                  Mt("att.time_decay_w2", L.decay_w2) && Mt("att.gate.weight", L.att_g);
             if (!ok) return false;
             dm.maa_D = (int)T(p + "att.time_maa_w2")->ne[0];
+            {
+                const HostTensor * w2 = T(p + "att.time_maa_w2");
+                if (w2->type != W_F32) return false;
+                const size_t D = w2->ne[0], Cc = w2->ne[1];
+                const float * src = (const float *)w2->data.data();
+                std::vector<float> t(5 * D * Cc);
+                for (size_t n = 0; n < 5; n++)
+                    for (size_t c = 0; c < Cc; c++)
+                        for (size_t i = 0; i < D; i++) t[(n * D + i) * Cc + c] = src[(n * Cc + c) * D + i];
+                if (!(L.maa_w2t = upload_host_floats(dm, t))) return false;
+                dm.small_param_bytes -= (double)t.size() * 4;  // same bytes as maa_w2, counted once
+            }
             if (L.maa_w1.M != 5 * dm.maa_D) {
                 fprintf(stderr, "rwkv: unexpected time_maa_w1 shape\n");
                 return false;
@@ -272,6 +284,8 @@ bool Engine::init() {
     ws_allocs_.push_back(logits_);
     const char * g = getenv("RWKV_MI355X_NO_GRAPH");
     use_graphs_ = !(g && g[0] == '1');
+    const char * gd = getenv("RWKV_MI355X_GENERIC_DECODE");
+    generic_decode_ = gd && gd[0] == '1';
     return ensure_workspace(1) && init_state(dstate_[0]);
 }
 
@@ -313,6 +327,8 @@ bool Engine::ensure_workspace(int T) {
     const size_t kmax = std::max<size_t>((size_t)m_->kmax, C);
     if (!(lora_ = (float *)A((size_t)cap * kmax * 4))) return false;
     if (!(bonus_ = (float *)A((size_t)cap * std::max<int64_t>(1, m_->H) * 4))) return false;
+    for (auto & p : dsmall_)
+        if (!(p = (float *)A(kmax * 4))) return false;
     if (!(dtokens_ = (uint32_t *)A((size_t)cap * 4))) return false;
     for (auto & s : slots_) {
         const size_t n = (size_t)cap * kmax, nb = n / 32 + 1;
@@ -608,7 +624,7 @@ bool Engine::layer_v6(int l, int T, const float * si, float * so) {
     if (!b.run(*this, T)) return false;
     // order w, k, v, r, g (rwkv_graph.inc:336-346)
     ActBuf outs[5] = {A(1, L.decay_w1), A(2, L.att_k), A(3, L.att_v), A(4, L.att_r), A(5, L.att_g)};
-    if (!launch_v6_mix5(stream_, T, C, D, lora_, L.maa_w2, L.maa, xa_, sx_, outs)) return false;
+    if (!launch_v6_mix5(stream_, T, C, D, lora_, L.maa_w2t, L.maa, xa_, sx_, outs)) return false;
     ActBuf dl = A(6, L.decay_w2);
     b.add(L.att_r, outs[3], r_, C, EPI_STORE);
     b.add(L.att_k, outs[1], k_, C, EPI_STORE);
@@ -697,6 +713,7 @@ bool Engine::layer_v7(int l, int T, const float * si, float * so) {
 }
 
 bool Engine::forward(int T, const float * sin, float * sout, bool logits) {
+    if (T == 1 && !generic_decode_) return forward_decode(sin, sout, logits);
     const size_t C = m_->n_embed;
     if (!launch_embed_ln(stream_, dtokens_, T, m_->emb, m_->ln0_w, m_->ln0_b, x_)) return false;
     const size_t per_layer = m_->major >= 5 ? C * (2 + (size_t)m_->S) : 5 * C;
@@ -720,6 +737,244 @@ bool Engine::forward(int T, const float * sin, float * sout, bool logits) {
         MMBatch b;
         b.add(m_->head, hin, logits_, (int)m_->n_vocab, EPI_STORE);
         if (!b.run(*this, 1)) return false;
+    }
+    return true;
+}
+
+bool Engine::mv(MVGroup & g) {
+    if (!timing_) return launch_mv_group(stream_, g);
+    // timing: account the group like mm_launch does, under the kernel name "k_mv<2>"
+    double bytes = 0, flops = 0;
+    for (int i = 0; i < g.n; i++) {
+        const MVEntry & e = g.e[i];
+        bytes += (double)type_nbytes((uint32_t)e.W.type, (uint64_t)e.W.M * e.W.K);
+        bytes += e.src == SRC_ACT ? act_bytes(e.act, 1) : (double)e.W.K * 4 * (e.src == SRC_LNMIX ? 5 : 1);
+        bytes += (double)e.W.M * 4 * ((e.epi == EPI_ADD || e.epi == EPI_SIGMUL_ADD || e.epi == EPI_VMIX7) ? 2 : 1);
+        flops += 2.0 * e.W.M * e.W.K;
+    }
+    const std::string name = "k_mv<2>";
+    int si = -1;
+    for (size_t i = 0; i < stats_.size(); i++)
+        if (stats_[i].name == name) si = (int)i;
+    if (si < 0) {
+        stats_.push_back(KernelStat{name});
+        si = (int)stats_.size() - 1;
+    }
+    stats_[si].total_bytes += bytes;
+    stats_[si].total_flops += flops;
+    stats_[si].launches++;
+    hipEvent_t a, b;
+    if (event_pool_.size() >= 2) {
+        a = event_pool_.back();
+        event_pool_.pop_back();
+        b = event_pool_.back();
+        event_pool_.pop_back();
+    } else {
+        HIP_OK(hipEventCreate(&a));
+        HIP_OK(hipEventCreate(&b));
+    }
+    HIP_OK(hipEventRecord(a, stream_));
+    const bool ok = launch_mv_group(stream_, g);
+    HIP_OK(hipEventRecord(b, stream_));
+    pending_.push_back(Pending{si, a, b});
+    return ok;
+}
+
+// Builder for decode matvec groups.
+struct MV {
+    MVGroup g;
+    MV() { memset(&g, 0, sizeof(g)); }
+    MVEntry & add(const DMat & W, float * y, int epi, const float * aux = nullptr, const float * bias = nullptr) {
+        MVEntry & e = g.e[g.n++];
+        e.W = W;
+        e.y = y;
+        e.epi = epi;
+        e.aux = aux;
+        e.bias = bias;
+        return e;
+    }
+};
+
+static void src_lnmix(MVEntry & e, const float * x, const float * carry, const float * lnw, const float * lnb,
+                      const float * mu, int form, float * carry_out = nullptr) {
+    e.src = SRC_LNMIX;
+    e.x = x;
+    e.carry = carry;
+    e.lnw = lnw;
+    e.lnb = lnb;
+    e.mu = mu;
+    e.form = form;
+    e.carry_out = carry_out;
+}
+
+static void src_f32(MVEntry & e, const float * f) {
+    e.src = SRC_F32;
+    e.f = f;
+}
+
+// Single-token forward: the fused decode program (kernels_decode.hip).  Per layer:
+//   v6: W1+LN (1) -> mix5 (1) -> r,k,v,g,Wd1 (1) -> decay tail+wkv+GN (1) -> Wo (1) -> FFN k,r+LN (1) -> FFN v (1)
+//   v5: r,k,v,g+LN (1) -> wkv+GN (1) -> Wo (1) -> FFN (2)      v4: r,k,v+LN (1) -> wkv4 (1) -> Wo (1) -> FFN (2)
+//   v7: r,k,v,LoRA-in+LN (1) -> LoRA-out (1) -> prep+wkv7+GN (1) -> Wo (1) -> FFN (2)
+bool Engine::forward_decode(const float * sin, float * sout, bool logits) {
+    const int C = (int)m_->n_embed, H = (int)m_->H, S = (int)m_->S;
+    if (!launch_embed_ln(stream_, dtokens_, 1, m_->emb, m_->ln0_w, m_->ln0_b, x_)) return false;
+    const size_t per_layer = m_->major >= 5 ? (size_t)C * (2 + (size_t)S) : 5 * (size_t)C;
+    for (uint32_t l = 0; l < m_->n_layer; l++) {
+        const DLayer & L = m_->layers[l];
+        const float * si = sin + l * per_layer;
+        float * so = sout + l * per_layer;
+        // ---------------- time mixing ----------------
+        if (m_->major == 4) {
+            MV b;
+            src_lnmix(b.add(L.att_r, r_, EPI_SIGMOID), x_, si + C, L.ln1_w, L.ln1_b, L.att_mix_r, 0, so + C);
+            src_lnmix(b.add(L.att_k, k_, EPI_STORE), x_, si + C, L.ln1_w, L.ln1_b, L.att_mix_k, 0);
+            src_lnmix(b.add(L.att_v, v_, EPI_STORE), x_, si + C, L.ln1_w, L.ln1_b, L.att_mix_v, 0);
+            if (!mv(b.g)) return false;
+            ActBuf o = A(0, L.att_o);
+            if (!launch_wkv4(stream_, 1, C, r_, k_, v_, L.att_first, L.att_decay, si, so, o)) return false;
+            MV c;
+            MVEntry & e = c.add(L.att_o, x_, EPI_ADD);
+            e.src = SRC_ACT;
+            e.act = o;
+            if (!mv(c.g)) return false;
+        } else if (m_->major == 5) {
+            const bool v52 = m_->minor >= 2;
+            MV b;
+            src_lnmix(b.add(L.att_r, r_, EPI_STORE), x_, si + C, L.ln1_w, L.ln1_b, L.att_mix_r, 0, so + C);
+            src_lnmix(b.add(L.att_k, k_, EPI_STORE), x_, si + C, L.ln1_w, L.ln1_b, L.att_mix_k, 0);
+            src_lnmix(b.add(L.att_v, v_, EPI_STORE), x_, si + C, L.ln1_w, L.ln1_b, L.att_mix_v, 0);
+            if (v52) src_lnmix(b.add(L.att_g, g_, EPI_SILU), x_, si + C, L.ln1_w, L.ln1_b, L.att_mix_g, 0);
+            if (!mv(b.g)) return false;
+            Att6Dec a;
+            memset(&a, 0, sizeof(a));
+            a.H = H;
+            a.S = S;
+            a.r = r_;
+            a.k = k_;
+            a.v = v_;
+            a.g = v52 ? g_ : nullptr;
+            a.u = L.att_u;
+            a.w = L.att_w;
+            a.sin = si + 2 * C;
+            a.sout = so + 2 * C;
+            a.lnx_w = L.att_lnx_w;
+            a.lnx_b = L.att_lnx_b;
+            a.eps = 1e-5f;
+            a.y = y_;
+            if (!launch_att6_dec(stream_, a)) return false;
+            MV c;
+            src_f32(c.add(L.att_o, x_, EPI_ADD), y_);
+            if (!mv(c.g)) return false;
+        } else if (m_->major == 6) {
+            const int D = m_->maa_D;
+            MV b;
+            src_lnmix(b.add(L.maa_w1, lora_, EPI_TANH), x_, si + C, L.ln1_w, L.ln1_b, L.maa_x, 1, so + C);
+            if (!mv(b.g)) return false;
+            ActBuf outs[5] = {A(1, L.decay_w1), A(2, L.att_k), A(3, L.att_v), A(4, L.att_r), A(5, L.att_g)};
+            if (!launch_v6_mix5_dec(stream_, C, D, x_, si + C, L.ln1_w, L.ln1_b, lora_, L.maa_w2t, L.maa, outs))
+                return false;
+            MV c;
+            const int mats[5] = {3, 1, 2, 4, 0};  // r, k, v, g, w
+            float * ys[5] = {r_, k_, v_, g_, dsmall_[0]};
+            const DMat * Ws[5] = {&L.att_r, &L.att_k, &L.att_v, &L.att_g, &L.decay_w1};
+            const int epis[5] = {EPI_STORE, EPI_STORE, EPI_STORE, EPI_SILU, EPI_TANH};
+            for (int i = 0; i < 5; i++) {
+                MVEntry & e = c.add(*Ws[i], ys[i], epis[i]);
+                e.src = SRC_ACT;
+                e.act = outs[mats[i]];
+            }
+            if (!mv(c.g)) return false;
+            Att6Dec a;
+            memset(&a, 0, sizeof(a));
+            a.H = H;
+            a.S = S;
+            a.r = r_;
+            a.k = k_;
+            a.v = v_;
+            a.g = g_;
+            a.u = L.att_u;
+            a.w = nullptr;
+            a.wd2 = L.decay_w2;
+            a.dl = dsmall_[0];
+            a.decay = L.decay6;
+            a.sin = si + 2 * C;
+            a.sout = so + 2 * C;
+            a.lnx_w = L.att_lnx_w;
+            a.lnx_b = L.att_lnx_b;
+            a.eps = 64e-5f;
+            a.y = y_;
+            if (!launch_att6_dec(stream_, a)) return false;
+            MV d;
+            src_f32(d.add(L.att_o, x_, EPI_ADD), y_);
+            if (!mv(d.g)) return false;
+        } else {
+            // v7, order r, w, k, v, a, g of x_rwkvag (rwkv_graph.inc:404-413)
+            MV b;
+            const float * mu = L.x_rwkvag;
+            src_lnmix(b.add(L.att_r, r_, EPI_STORE), x_, si + C, L.ln1_w, L.ln1_b, mu, 1, so + C);
+            src_lnmix(b.add(L.att_k, k_, EPI_STORE), x_, si + C, L.ln1_w, L.ln1_b, mu + 2 * (size_t)C, 1);
+            src_lnmix(b.add(L.att_v, v_, EPI_STORE), x_, si + C, L.ln1_w, L.ln1_b, mu + 3 * (size_t)C, 1);
+            src_lnmix(b.add(L.w1, dsmall_[0], EPI_TANH), x_, si + C, L.ln1_w, L.ln1_b, mu + 1 * (size_t)C, 1);
+            src_lnmix(b.add(L.a1, dsmall_[1], EPI_STORE), x_, si + C, L.ln1_w, L.ln1_b, mu + 4 * (size_t)C, 1);
+            src_lnmix(b.add(L.g1, dsmall_[2], EPI_SIGMOID), x_, si + C, L.ln1_w, L.ln1_b, mu + 5 * (size_t)C, 1);
+            if (l != 0) src_lnmix(b.add(L.v1, dsmall_[3], EPI_STORE), x_, si + C, L.ln1_w, L.ln1_b, mu + 3 * (size_t)C, 1);
+            if (!mv(b.g)) return false;
+            if (l == 0) HIP_OK(hipMemcpyAsync(vfirst_, v_, (size_t)C * 4, hipMemcpyDeviceToDevice, stream_));
+            MV c;
+            src_f32(c.add(L.w2, w_, EPI_DECAY7, nullptr, L.w0), dsmall_[0]);
+            src_f32(c.add(L.a2, a_, EPI_SIGMOID_BIAS, nullptr, L.a0), dsmall_[1]);
+            src_f32(c.add(L.g2, g_, EPI_STORE), dsmall_[2]);
+            if (l != 0) src_f32(c.add(L.v2, v_, EPI_VMIX7, vfirst_, L.v0), dsmall_[3]);
+            if (!mv(c.g)) return false;
+            Att7Dec a;
+            memset(&a, 0, sizeof(a));
+            a.H = H;
+            a.S = S;
+            a.r = r_;
+            a.w = w_;
+            a.k = k_;
+            a.v = v_;
+            a.a = a_;
+            a.g = g_;
+            a.k_k = L.k_k;
+            a.k_a = L.k_a;
+            a.r_k = L.r_k;
+            a.sin = si + 2 * C;
+            a.sout = so + 2 * C;
+            a.lnx_w = L.att_lnx_w;
+            a.lnx_b = L.att_lnx_b;
+            a.y = y_;
+            if (!launch_att7_dec(stream_, a)) return false;
+            MV d;
+            src_f32(d.add(L.att_o, x_, EPI_ADD), y_);
+            if (!mv(d.g)) return false;
+        }
+        // ---------------- channel mixing ----------------
+        if (m_->major == 7) {
+            MV b;
+            src_lnmix(b.add(L.ffn_k, lora_, EPI_RELU_SQ), x_, si, L.ln2_w, L.ln2_b, L.ffn_x_k, 1, so);
+            if (!mv(b.g)) return false;
+            MV c;
+            src_f32(c.add(L.ffn_v, x_, EPI_ADD), lora_);
+            if (!mv(c.g)) return false;
+        } else {
+            const int form = m_->major == 6 ? 1 : 0;
+            const float * muk = m_->major == 6 ? L.ffn_maa_k : L.ffn_mix_k;
+            const float * mur = m_->major == 6 ? L.ffn_maa_r : L.ffn_mix_r;
+            MV b;
+            src_lnmix(b.add(L.ffn_k, lora_, EPI_RELU_SQ), x_, si, L.ln2_w, L.ln2_b, muk, form, so);
+            src_lnmix(b.add(L.ffn_r, fr_, EPI_STORE), x_, si, L.ln2_w, L.ln2_b, mur, form);
+            if (!mv(b.g)) return false;
+            MV c;
+            src_f32(c.add(L.ffn_v, x_, EPI_SIGMUL_ADD, fr_), lora_);
+            if (!mv(c.g)) return false;
+        }
+    }
+    if (logits) {
+        MV h;
+        src_lnmix(h.add(m_->head, logits_, EPI_STORE), x_, nullptr, m_->lnout_w, m_->lnout_b, nullptr, 2);
+        if (!mv(h.g)) return false;
     }
     return true;
 }

@@ -5,6 +5,7 @@
 #include <vector>
 
 #include "common.hpp"
+#include "kernels.hpp"
 #include "model_file.hpp"
 
 namespace rwkvmi {
@@ -18,6 +19,7 @@ struct DLayer {
     float *att_lnx_w = nullptr, *att_lnx_b = nullptr;
     // v6
     float *maa_x = nullptr, *maa[5] = {nullptr, nullptr, nullptr, nullptr, nullptr}, *maa_w2 = nullptr;
+    float *maa_w2t = nullptr;  // time_maa_w2 transposed to [5][D][C] (coalesced per-channel dots)
     float *decay6 = nullptr;
     // v7
     float *x_rwkvag = nullptr, *w0 = nullptr, *a0 = nullptr, *v0 = nullptr, *k_k = nullptr, *k_a = nullptr, *r_k = nullptr;
@@ -94,6 +96,8 @@ class Engine {
     bool ensure_workspace(int T);
     bool init_state(float * st);
     bool forward(int T, const float * sin, float * sout, bool logits);
+    bool forward_decode(const float * sin, float * sout, bool logits);
+    bool mv(MVGroup & g);
     bool run_tokens(const uint32_t * tokens, size_t T, bool want_logits);
     bool layer_v4(int l, int T, const float * si, float * so);
     bool layer_v5(int l, int T, const float * si, float * so);
@@ -110,6 +114,7 @@ class Engine {
     float *x_ = nullptr, *xa_ = nullptr, *sx_ = nullptr, *r_ = nullptr, *k_ = nullptr, *v_ = nullptr, *g_ = nullptr;
     float *w_ = nullptr, *y_ = nullptr, *a_ = nullptr, *nb_ = nullptr, *bb_ = nullptr, *vfirst_ = nullptr;
     float *fr_ = nullptr, *lora_ = nullptr, *bonus_ = nullptr, *logits_ = nullptr;
+    float *dsmall_[4] = {nullptr, nullptr, nullptr, nullptr};  // decode LoRA intermediates [kmax]
     uint32_t * dtokens_ = nullptr;
     uint32_t * htokens_ = nullptr;  // pinned
     static constexpr int kSlots = 12;
@@ -118,6 +123,7 @@ class Engine {
     int cur_ = 0;
     hipGraphExec_t graphs_[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // [cur][logits]
     bool use_graphs_ = true;
+    bool generic_decode_ = false;  // RWKV_MI355X_GENERIC_DECODE=1: decode through the T>1 kernels
     hipEvent_t tok_event_ = nullptr;
     bool timing_ = false;
     struct Pending {

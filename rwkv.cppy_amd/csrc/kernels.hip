@@ -5,152 +5,13 @@
 // where the reference rounds; fused multiply-adds appear only where ggml's x86 kernels use
 // them (the quantized block accumulation).
 #include "kernels.hpp"
+#include "device_common.hpp"
 
 #include <stdio.h>
 
 namespace rwkvmi {
 
-// --------------------------------------------------------------------------- helpers
 
-template <typename T>
-__device__ __forceinline__ T wave_sum(T v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
-
-// sum over groups of `width` adjacent lanes (width power of two <= 64); all lanes get the sum
-template <typename T>
-__device__ __forceinline__ T group_sum(T v, int width) {
-    for (int o = width >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
-
-// deterministic block sum (fixed tree): every thread returns the total
-__device__ double block_sum_d(double v, double * sh) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
-    v = wave_sum(v);
-    if (lane == 0) sh[wave] = v;
-    __syncthreads();
-    double r = 0.0;
-    for (int w = 0; w < nw; w++) r += sh[w];
-    __syncthreads();
-    return r;
-}
-
-__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
-__device__ __forceinline__ float siluf_(float x) { return x / (1.0f + expf(-x)); }
-
-__device__ __forceinline__ float h2f(uint16_t b) { return __half2float(__ushort_as_half(b)); }
-__device__ __forceinline__ float f16_round(float f) { return __half2float(__float2half(f)); }
-
-// Emit one element per lane into an activation buffer.  The 32 lanes of each half-wave must
-// hold the 32 consecutive elements of one block (k & 31 == lane & 31) of the same row t, and
-// all 32 must call (block-uniform control flow).  Mirrors ggml quantize_row_q8_0/q8_1 (x86):
-// d = amax/127 (fp16), q = rint(x * 127/amax), s = fp16(d * sum q).
-__device__ __forceinline__ void emit32(const ActBuf & a, int t, int k, float v) {
-    const size_t idx = (size_t)t * a.K + k;
-    if (a.fmt == A_F32) {
-        a.f[idx] = v;
-        return;
-    }
-    if (a.fmt == A_F16) {
-        a.h[idx] = __float2half(v);
-        return;
-    }
-    float am = fabsf(v);
-#pragma unroll
-    for (int o = 16; o > 0; o >>= 1) am = fmaxf(am, __shfl_xor(am, o, 32));
-    const float d = am / 127.f;
-    const float id = (am != 0.0f) ? 127.f / am : 0.0f;
-    const int q = (int)rintf(v * id);
-    int sum = q;
-#pragma unroll
-    for (int o = 16; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 32);
-    a.q[idx] = (int8_t)q;
-    if ((k & 31) == 0) {
-        const size_t bi = (size_t)t * (a.K >> 5) + (k >> 5);
-        a.d[bi] = f16_round(d);
-        a.qsum[bi] = sum;
-        if (a.fmt == A_Q8_1) a.s[bi] = f16_round(d * (float)sum);
-    }
-}
-
-// --------------------------------------------------------------------------- matmul
-// One workgroup = 4 waves; each wave owns RPW consecutive rows; lanes stride over the K
-// blocks of a row (lane l reads block l, l+64, ...: one 16-byte dwordx4 of nibbles per lane,
-// 1 KiB per wave-instruction, fully coalesced).  Per 32-block: integer v_dot4 of the weight
-// ints with the Q8 activation ints, then acc = fma(d_w * d_x, sumi, acc) (ggml x86 order);
-// the m*s terms of the _1 formats go to a second accumulator added at the end.
-
-__device__ __forceinline__ uint32_t spread4(uint32_t x) {
-    // bit k of x (k<4) -> bit 4 of byte k
-    return ((x & 1u) << 4) | ((x & 2u) << 11) | ((x & 4u) << 18) | ((x & 8u) << 25);
-}
-
-template <int WF>
-__device__ __forceinline__ int block_dot(const DMat & W, int row, int b, int nb, const int4 & alo,
-                                         const int4 & ahi, int qsum, float & dw, float & mw) {
-    const size_t bi = (size_t)row * nb + b;
-    int sumi = 0;
-    if constexpr (WF == W_Q8_0) {
-        const int4 * p = (const int4 *)(W.qs + bi * 32);
-        const int4 w0 = p[0], w1 = p[1];
-        sumi = __builtin_amdgcn_sdot4(w0.x, alo.x, sumi, false);
-        sumi = __builtin_amdgcn_sdot4(w0.y, alo.y, sumi, false);
-        sumi = __builtin_amdgcn_sdot4(w0.z, alo.z, sumi, false);
-        sumi = __builtin_amdgcn_sdot4(w0.w, alo.w, sumi, false);
-        sumi = __builtin_amdgcn_sdot4(w1.x, ahi.x, sumi, false);
-        sumi = __builtin_amdgcn_sdot4(w1.y, ahi.y, sumi, false);
-        sumi = __builtin_amdgcn_sdot4(w1.z, ahi.z, sumi, false);
-        sumi = __builtin_amdgcn_sdot4(w1.w, ahi.w, sumi, false);
-        dw = h2f(((const uint16_t *)W.sc)[bi]);
-        mw = 0.0f;
-        (void)qsum;
-        return sumi;
-    } else {
-        const int4 w = *(const int4 *)(W.qs + bi * 16);
-        uint32_t lo0 = (uint32_t)w.x & 0x0F0F0F0Fu, lo1 = (uint32_t)w.y & 0x0F0F0F0Fu;
-        uint32_t lo2 = (uint32_t)w.z & 0x0F0F0F0Fu, lo3 = (uint32_t)w.w & 0x0F0F0F0Fu;
-        uint32_t hi0 = ((uint32_t)w.x >> 4) & 0x0F0F0F0Fu, hi1 = ((uint32_t)w.y >> 4) & 0x0F0F0F0Fu;
-        uint32_t hi2 = ((uint32_t)w.z >> 4) & 0x0F0F0F0Fu, hi3 = ((uint32_t)w.w >> 4) & 0x0F0F0F0Fu;
-        if constexpr (WF == W_Q5_0 || WF == W_Q5_1) {
-            const uint32_t qh = W.qh[bi];
-            lo0 |= spread4(qh & 0xF);
-            lo1 |= spread4((qh >> 4) & 0xF);
-            lo2 |= spread4((qh >> 8) & 0xF);
-            lo3 |= spread4((qh >> 12) & 0xF);
-            hi0 |= spread4((qh >> 16) & 0xF);
-            hi1 |= spread4((qh >> 20) & 0xF);
-            hi2 |= spread4((qh >> 24) & 0xF);
-            hi3 |= spread4((qh >> 28) & 0xF);
-        }
-        sumi = __builtin_amdgcn_sdot4((int)lo0, alo.x, sumi, false);
-        sumi = __builtin_amdgcn_sdot4((int)lo1, alo.y, sumi, false);
-        sumi = __builtin_amdgcn_sdot4((int)lo2, alo.z, sumi, false);
-        sumi = __builtin_amdgcn_sdot4((int)lo3, alo.w, sumi, false);
-        sumi = __builtin_amdgcn_sdot4((int)hi0, ahi.x, sumi, false);
-        sumi = __builtin_amdgcn_sdot4((int)hi1, ahi.y, sumi, false);
-        sumi = __builtin_amdgcn_sdot4((int)hi2, ahi.z, sumi, false);
-        sumi = __builtin_amdgcn_sdot4((int)hi3, ahi.w, sumi, false);
-        if constexpr (WF == W_Q4_0) {
-            sumi -= 8 * qsum;
-        } else if constexpr (WF == W_Q5_0) {
-            sumi -= 16 * qsum;
-        }
-        if constexpr (WF == W_Q4_1 || WF == W_Q5_1) {
-            const uint32_t dm = ((const uint32_t *)W.sc)[bi];
-            dw = h2f((uint16_t)(dm & 0xFFFF));
-            mw = h2f((uint16_t)(dm >> 16));
-        } else {
-            dw = h2f(((const uint16_t *)W.sc)[bi]);
-            mw = 0.0f;
-        }
-        return sumi;
-    }
-}
-
-typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
 
 template <int WF, int RPW, int NT>
 __device__ __forceinline__ void mm_accumulate(const MMEntry & E, int row0, int t0, int T, int lane,
@@ -241,29 +102,6 @@ __device__ __forceinline__ void mm_accumulate(const MMEntry & E, int row0, int t
                 }
             }
         }
-    }
-}
-
-__device__ __forceinline__ float apply_epi(const MMEntry & E, int t, int row, float acc) {
-    const size_t yi = (size_t)t * E.ldy + row;
-    switch (E.epi) {
-        case EPI_SIGMOID: return sigmoidf_(acc);
-        case EPI_TANH: return tanhf(acc);
-        case EPI_SILU: return siluf_(acc);
-        case EPI_RELU_SQ: {
-            const float r = acc > 0.0f ? acc : 0.0f;
-            return r * r;
-        }
-        case EPI_ADD: return E.y[yi] + acc;
-        case EPI_SIGMUL_ADD: return E.y[yi] + sigmoidf_(E.aux[yi]) * acc;
-        case EPI_DECAY6: return expf(-expf(acc + E.bias[row]));
-        case EPI_DECAY7: return expf(sigmoidf_(acc + E.bias[row]) * -0.606531f);
-        case EPI_SIGMOID_BIAS: return sigmoidf_(acc + E.bias[row]);
-        case EPI_VMIX7: {
-            const float v = E.y[yi];
-            return v + (E.aux[yi] - v) * sigmoidf_(acc + E.bias[row]);
-        }
-        default: return acc;
     }
 }
 
@@ -371,28 +209,6 @@ bool launch_mm_group(hipStream_t st, MMGroup & g, int wtype) {
 
 // --------------------------------------------------------------------------- LayerNorm family
 
-// ggml_norm statistics with double accumulation (mean, 1/sqrt(var + eps))
-__device__ void ln_stats(const float * x, int C, float eps, float & mean, float & scale, double * sh) {
-    double s = 0.0;
-    for (int c = threadIdx.x; c < C; c += blockDim.x) s += (double)x[c];
-    s = block_sum_d(s, sh);
-    mean = (float)(s / (double)C);
-    double s2 = 0.0;
-    for (int c = threadIdx.x; c < C; c += blockDim.x) {
-        const float v = x[c] - mean;
-        s2 += (double)(v * v);
-    }
-    s2 = block_sum_d(s2, sh);
-    const float var = (float)(s2 / (double)C);
-    scale = 1.0f / sqrtf(var + eps);
-}
-
-__device__ __forceinline__ float ln_apply(float x, float mean, float scale, float w, float b) {
-    float y = (x - mean) * scale;
-    y = y * w;
-    return y + b;
-}
-
 __global__ __launch_bounds__(256) void k_embed_ln(const uint32_t * tokens, DMat emb, const float * w,
                                                   const float * b, float * x) {
     __shared__ double sh[8];
@@ -487,10 +303,10 @@ __global__ __launch_bounds__(256) void k_v6_mix5(Mix5Args a) {
     const size_t ti = (size_t)t * C + c;
     const float xa = a.xa[ti], sx = a.sx[ti];
     for (int n = 0; n < 5; n++) {
-        const float * w2 = a.w2 + ((size_t)n * C + c) * D;
+        const float * w2 = a.w2 + (size_t)n * D * C + c;   // transposed [5][D][C]
         const float * lv = a.lora + (size_t)t * 5 * D + n * D;
         double acc = 0.0;
-        for (int i = 0; i < D; i++) acc += (double)(w2[i] * lv[i]);
+        for (int i = 0; i < D; i++) acc += (double)(w2[(size_t)i * C] * lv[i]);
         const float m = (float)acc;
         emit32(a.out[n], t, c, (m + a.maa[n][c]) * sx + xa);
     }

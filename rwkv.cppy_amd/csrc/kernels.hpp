@@ -71,3 +71,76 @@ namespace rwkvmi {
 // x [T][K] fp32 -> activation buffer (emit32 path); used by the self-test entry points.
 bool launch_act_from_f32(hipStream_t st, const float * x, int T, int K, const ActBuf & out);
 }  // namespace rwkvmi
+
+// ---------------------------------------------------------------------------------------
+// Decode (T == 1) kernels: kernels_decode.hip
+namespace rwkvmi {
+
+enum MVSrc : int {
+    SRC_ACT = 0,    // pre-quantized activation row in global memory (ActBuf, row 0)
+    SRC_F32 = 1,    // fp32 vector in global memory; each workgroup quantizes it into LDS
+    SRC_LNMIX = 2,  // LN(x) + token shift + mix, computed and quantized into LDS per workgroup
+};
+
+struct MVEntry {
+    DMat W;
+    int src;
+    ActBuf act;              // SRC_ACT
+    const float * f;         // SRC_F32 [K]
+    const float * x;         // SRC_LNMIX residual stream [K]
+    const float * carry;     // previous token's LN output (state *_xx)
+    const float * lnw, * lnb, * mu;
+    int form;                // 0: xa*mu + (xp - xp*mu)   1: (xp - xa)*mu + xa   2: xa (plain LN)
+    float * carry_out;       // entry's first workgroup writes xa here (new *_xx state)
+    float * y;               // fp32 [M]
+    const float * aux;
+    const float * bias;
+    int epi;
+    int block0;
+};
+
+struct MVGroup {
+    MVEntry e[MM_MAX_ENTRIES];
+    int n;
+    int lds_bytes;
+};
+
+bool launch_mv_group(hipStream_t st, MVGroup & g);
+
+// v6 token-shift mixes with the maa LoRA (rwkv_graph.inc:308-346), LN recomputed per block;
+// w2t is time_maa_w2 transposed to [5][D][C]; emits the five mixed vectors w,k,v,r,g.
+bool launch_v6_mix5_dec(hipStream_t st, int C, int D, const float * x, const float * carry, const float * lnw,
+                        const float * lnb, const float * lora, const float * w2t, const float * const * maa,
+                        const ActBuf * outs);
+
+// v5/v6 attention core for one token, one workgroup per head: (v6: decay LoRA second stage
+// w = exp(-exp(Wd2 . dl + decay))) + wkv6 + GroupNorm*ln_x (+ *g).  Writes fp32 y [C].
+struct Att6Dec {
+    int H, S;
+    const float * r, * k, * v, * g, * u;
+    const float * w;         // v5: w [C]
+    DMat wd2;                // v6: time_decay_w2 (M = C, K = D)
+    const float * dl;        // v6: tanh(Wd1 . xw) [D]
+    const float * decay;     // v6: time_decay [C]
+    const float * sin;
+    float * sout;
+    const float * lnx_w, * lnx_b;
+    float eps;
+    float * y;
+};
+bool launch_att6_dec(hipStream_t st, const Att6Dec & a);
+
+// v7 attention core for one token, one workgroup per head: kk/k/a prep, wkv7, GroupNorm,
+// + v*sum(k*r*r_k), *g.  Writes fp32 y [C].
+struct Att7Dec {
+    int H, S;
+    const float * r, * w, * k, * v, * a, * g;
+    const float * k_k, * k_a, * r_k;
+    const float * sin;
+    float * sout;
+    const float * lnx_w, * lnx_b;
+    float * y;
+};
+bool launch_att7_dec(hipStream_t st, const Att7Dec & a);
+
+}  // namespace rwkvmi

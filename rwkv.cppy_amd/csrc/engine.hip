@@ -953,21 +953,33 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits) {
         // ---------------- channel mixing ----------------
         if (m_->major == 7) {
             MV b;
-            src_lnmix(b.add(L.ffn_k, lora_, EPI_RELU_SQ), x_, si, L.ln2_w, L.ln2_b, L.ffn_x_k, 1, so);
+            ActBuf kin = A(0, L.ffn_v);
+            MVEntry & ek = b.add(L.ffn_k, nullptr, EPI_RELU_SQ);
+            src_lnmix(ek, x_, si, L.ln2_w, L.ln2_b, L.ffn_x_k, 1, so);
+            ek.emit = 1;
+            ek.act_out = kin;
             if (!mv(b.g)) return false;
             MV c;
-            src_f32(c.add(L.ffn_v, x_, EPI_ADD), lora_);
+            MVEntry & ev = c.add(L.ffn_v, x_, EPI_ADD);
+            ev.src = SRC_ACT;
+            ev.act = kin;
             if (!mv(c.g)) return false;
         } else {
             const int form = m_->major == 6 ? 1 : 0;
             const float * muk = m_->major == 6 ? L.ffn_maa_k : L.ffn_mix_k;
             const float * mur = m_->major == 6 ? L.ffn_maa_r : L.ffn_mix_r;
             MV b;
-            src_lnmix(b.add(L.ffn_k, lora_, EPI_RELU_SQ), x_, si, L.ln2_w, L.ln2_b, muk, form, so);
+            ActBuf kin = A(0, L.ffn_v);
+            MVEntry & ek = b.add(L.ffn_k, nullptr, EPI_RELU_SQ);
+            src_lnmix(ek, x_, si, L.ln2_w, L.ln2_b, muk, form, so);
+            ek.emit = 1;
+            ek.act_out = kin;
             src_lnmix(b.add(L.ffn_r, fr_, EPI_STORE), x_, si, L.ln2_w, L.ln2_b, mur, form);
             if (!mv(b.g)) return false;
             MV c;
-            src_f32(c.add(L.ffn_v, x_, EPI_SIGMUL_ADD, fr_), lora_);
+            MVEntry & ev = c.add(L.ffn_v, x_, EPI_SIGMUL_ADD, fr_);
+            ev.src = SRC_ACT;
+            ev.act = kin;
             if (!mv(c.g)) return false;
         }
     }

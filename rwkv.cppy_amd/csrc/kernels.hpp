@@ -92,10 +92,12 @@ struct MVEntry {
     const float * lnw, * lnb, * mu;
     int form;                // 0: xa*mu + (xp - xp*mu)   1: (xp - xa)*mu + xa   2: xa (plain LN)
     float * carry_out;       // entry's first workgroup writes xa here (new *_xx state)
-    float * y;               // fp32 [M]
+    float * y;               // fp32 [M] (may be null when emitting)
     const float * aux;
     const float * bias;
     int epi;
+    int emit;                // emit the post-epilogue values into act_out (needs M % 32 == 0)
+    ActBuf act_out;
     int block0;
 };
 

@@ -127,82 +127,170 @@ __device__ __forceinline__ void mv_accumulate(const DMat & W, const ActBuf & a, 
     }
 }
 
-template <int R>
+// Per-thread register image of a K-vector: thread t owns k = i*256 + t (i < E).  All loads of
+// a phase are issued before any is used (one dependent L2 round trip per phase).
+template <int E>
+__device__ __forceinline__ void load_vec(float (&v)[E], const float * p, int K) {
+#pragma unroll
+    for (int i = 0; i < E; i++) {
+        const int k = i * 256 + (int)threadIdx.x;
+        v[i] = (k < K) ? p[k] : 0.0f;
+    }
+}
+
+// LayerNorm statistics of the register image (ggml_norm: fp64 sums, two passes).
+template <int E>
+__device__ __forceinline__ void ln_stats_reg(const float (&xv)[E], int K, float & mean, float & scale, double * sh) {
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < E; i++)
+        if (i * 256 + (int)threadIdx.x < K) s += (double)xv[i];
+    s = block_sum_d(s, sh);
+    mean = (float)(s / (double)K);
+    double s2 = 0.0;
+#pragma unroll
+    for (int i = 0; i < E; i++)
+        if (i * 256 + (int)threadIdx.x < K) {
+            const float d = xv[i] - mean;
+            s2 += (double)(d * d);
+        }
+    s2 = block_sum_d(s2, sh);
+    scale = 1.0f / sqrtf((float)(s2 / (double)K) + 1e-5f);
+}
+
+template <int R, int E, bool EMIT>
 __global__ __launch_bounds__(256) void k_mv(MVGroup g) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ double sh[8];
+    __shared__ float red[4 * R];
     int e = 0;
 #pragma unroll 1
     while (e + 1 < g.n && (int)blockIdx.x >= g.e[e + 1].block0) e++;
-    const MVEntry & E = g.e[e];
-    const int K = E.W.K, fmt = act_fmt_for(E.W.type);
+    const MVEntry & Ent = g.e[e];
+    const int K = Ent.W.K, fmt = act_fmt_for(Ent.W.type);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     ActBuf a;
-    if (E.src == SRC_ACT) {
-        a = E.act;
+    if (Ent.src == SRC_ACT) {
+        a = Ent.act;
     } else {
         a = lds_act(smem, fmt, K);
-        float mean = 0.0f, scale = 0.0f;
-        if (E.src == SRC_LNMIX) ln_stats(E.x, K, 1e-5f, mean, scale, sh);
-        const bool write_carry = E.carry_out && (int)blockIdx.x == E.block0;
-        for (int k0 = 0; k0 < K; k0 += 256) {
-            const int k = k0 + tid;
-            if (k0 + (tid & ~31) >= K) continue;  // half-wave uniform (K % 32 == 0)
-            float v;
-            if (E.src == SRC_F32) {
-                v = E.f[k];
-            } else {
-                const float xa = ln_apply(E.x[k], mean, scale, E.lnw[k], E.lnb[k]);
-                if (write_carry) E.carry_out[k] = xa;
-                if (E.form == 2) {
-                    v = xa;
-                } else {
-                    const float xp = E.carry[k], mu = E.mu[k];
-                    v = (E.form == 0) ? xa * mu + (xp - xp * mu) : (xp - xa) * mu + xa;
-                }
+        float v[E];
+        if (Ent.src == SRC_F32) {
+            load_vec<E>(v, Ent.f, K);
+        } else {
+            float xv[E], lw[E], lb[E];
+            load_vec<E>(xv, Ent.x, K);
+            load_vec<E>(lw, Ent.lnw, K);
+            load_vec<E>(lb, Ent.lnb, K);
+            float cv[E], mv[E];
+            if (Ent.form != 2) {
+                load_vec<E>(cv, Ent.carry, K);
+                load_vec<E>(mv, Ent.mu, K);
             }
-            emit32(a, 0, k, v);
+            float mean, scale;
+            ln_stats_reg<E>(xv, K, mean, scale, sh);
+            const bool write_carry = Ent.carry_out && (int)blockIdx.x == Ent.block0;
+#pragma unroll
+            for (int i = 0; i < E; i++) {
+                const float xa = ln_apply(xv[i], mean, scale, lw[i], lb[i]);
+                const int k = i * 256 + tid;
+                if (write_carry && k < K) Ent.carry_out[k] = xa;
+                if (Ent.form == 2) v[i] = xa;
+                else if (Ent.form == 0) v[i] = xa * mv[i] + (cv[i] - cv[i] * mv[i]);
+                else v[i] = (cv[i] - xa) * mv[i] + xa;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < E; i++) {
+            const int k0 = i * 256;
+            if (k0 + (tid & ~31) < K) emit32(a, 0, k0 + tid, v[i]);  // half-wave uniform
         }
         __syncthreads();
     }
-    const int row0 = ((int)blockIdx.x - E.block0) * 4 * R + wave * R;
+    const int rowwg = ((int)blockIdx.x - Ent.block0) * 4 * R;
+    const int row0 = rowwg + wave * R;
     float acc[R], acc2[R];
 #pragma unroll
     for (int r = 0; r < R; r++) acc[r] = acc2[r] = 0.0f;
-    switch (E.W.type) {
-        case W_F32: mv_accumulate<W_F32, R>(E.W, a, row0, lane, acc, acc2); break;
-        case W_F16: mv_accumulate<W_F16, R>(E.W, a, row0, lane, acc, acc2); break;
-        case W_Q4_0: mv_accumulate<W_Q4_0, R>(E.W, a, row0, lane, acc, acc2); break;
-        case W_Q4_1: mv_accumulate<W_Q4_1, R>(E.W, a, row0, lane, acc, acc2); break;
-        case W_Q5_0: mv_accumulate<W_Q5_0, R>(E.W, a, row0, lane, acc, acc2); break;
-        case W_Q5_1: mv_accumulate<W_Q5_1, R>(E.W, a, row0, lane, acc, acc2); break;
-        case W_Q8_0: mv_accumulate<W_Q8_0, R>(E.W, a, row0, lane, acc, acc2); break;
+    switch (Ent.W.type) {
+        case W_F32: mv_accumulate<W_F32, R>(Ent.W, a, row0, lane, acc, acc2); break;
+        case W_F16: mv_accumulate<W_F16, R>(Ent.W, a, row0, lane, acc, acc2); break;
+        case W_Q4_0: mv_accumulate<W_Q4_0, R>(Ent.W, a, row0, lane, acc, acc2); break;
+        case W_Q4_1: mv_accumulate<W_Q4_1, R>(Ent.W, a, row0, lane, acc, acc2); break;
+        case W_Q5_0: mv_accumulate<W_Q5_0, R>(Ent.W, a, row0, lane, acc, acc2); break;
+        case W_Q5_1: mv_accumulate<W_Q5_1, R>(Ent.W, a, row0, lane, acc, acc2); break;
+        case W_Q8_0: mv_accumulate<W_Q8_0, R>(Ent.W, a, row0, lane, acc, acc2); break;
         default: break;
     }
+    if constexpr (!EMIT) {
 #pragma unroll
-    for (int r = 0; r < R; r++) {
-        const float s = wave_sum(acc[r]) + wave_sum(acc2[r]);
-        const int row = row0 + r;
-        if (lane == 0 && row < E.W.M) E.y[row] = apply_epi_mv(E, row, s);
+        for (int r = 0; r < R; r++) {
+            const float s = wave_sum(acc[r]) + wave_sum(acc2[r]);
+            const int row = row0 + r;
+            if (lane == 0 && row < Ent.W.M) Ent.y[row] = apply_epi_mv(Ent, row, s);
+        }
+    } else {
+        // 4*R == 32 rows per workgroup: apply the epilogue and emit the 32 values as one
+        // quantization block of the next matmul's input (ggml Q8 / fp16 / fp32)
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            const float s = wave_sum(acc[r]) + wave_sum(acc2[r]);
+            if (lane == 0) red[wave * R + r] = s;
+        }
+        __syncthreads();
+        if (tid < 32) {
+            const int row = rowwg + tid;
+            float vv = 0.0f;
+            if (row < Ent.W.M) {
+                vv = apply_epi_mv(Ent, row, red[tid]);
+                if (Ent.y) Ent.y[row] = vv;
+            }
+            if (Ent.act_out.fmt >= 0 && Ent.emit) emit32(Ent.act_out, 0, row, vv);
+        }
+    }
+}
+
+template <int R, bool EMIT>
+static void launch_mv_e(hipStream_t st, MVGroup & g, int E, int blocks) {
+    dim3 grid(blocks), block(256);
+    switch (E) {
+        case 4: hipLaunchKernelGGL((k_mv<R, 4, EMIT>), grid, block, g.lds_bytes, st, g); break;
+        case 16: hipLaunchKernelGGL((k_mv<R, 16, EMIT>), grid, block, g.lds_bytes, st, g); break;
+        default: hipLaunchKernelGGL((k_mv<R, 32, EMIT>), grid, block, g.lds_bytes, st, g); break;
     }
 }
 
 bool launch_mv_group(hipStream_t st, MVGroup & g) {
-    constexpr int R = 2, RW = 4 * R;
-    int blocks = 0, lds = 0;
+    bool emit = false;
+    for (int i = 0; i < g.n; i++) emit |= g.e[i].emit != 0;
+    const int R = emit ? 8 : 2, RW = 4 * R;
+    int blocks = 0, lds = 0, kmax = 0;
     for (int i = 0; i < g.n; i++) {
         MVEntry & e = g.e[i];
         if (e.W.K % 32) {
             fprintf(stderr, "rwkv: matvec needs K %% 32 == 0 (K=%d)\n", e.W.K);
             return false;
         }
+        if (e.emit && e.W.M % 32) {
+            fprintf(stderr, "rwkv: emitting matvec needs M %% 32 == 0 (M=%d)\n", e.W.M);
+            return false;
+        }
         e.block0 = blocks;
         blocks += (e.W.M + RW - 1) / RW;
-        if (e.src != SRC_ACT) lds = std::max(lds, lds_bytes_for(act_fmt_for(e.W.type), e.W.K));
+        if (e.src != SRC_ACT) {
+            lds = std::max(lds, lds_bytes_for(act_fmt_for(e.W.type), e.W.K));
+            kmax = std::max(kmax, e.W.K);
+        }
+    }
+    if (kmax > 32 * 256) {
+        fprintf(stderr, "rwkv: matvec prologue K=%d > 8192 unsupported\n", kmax);
+        return false;
     }
     g.lds_bytes = lds;
     if (!blocks) return true;
-    hipLaunchKernelGGL(k_mv<R>, dim3(blocks), dim3(256), lds, st, g);
+    const int E = kmax <= 1024 ? 4 : kmax <= 4096 ? 16 : 32;
+    if (emit) launch_mv_e<8, true>(st, g, E, blocks);
+    else launch_mv_e<2, false>(st, g, E, blocks);
     HIP_OK(hipGetLastError());
     return true;
 }
@@ -218,21 +306,32 @@ struct Mix5Dec {
 // grid (C/256, 5): block (cx, n) computes mixed vector n for 256 channels.  w2t [5][D][C]
 // makes the per-channel D-long dots coalesced across lanes; accumulation order matches the
 // oracle (sequential over i, fp64).
+template <int E>
 __global__ __launch_bounds__(256) void k_v6_mix5_dec(Mix5Dec a) {
     __shared__ double sh[8];
     const int n = blockIdx.y, C = a.C, D = a.D;
-    float mean, scale;
-    ln_stats(a.x, C, 1e-5f, mean, scale, sh);
+    float xv[E];
+    load_vec<E>(xv, a.x, C);
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if ((int)(blockIdx.x * blockDim.x + (threadIdx.x & ~63)) >= C) return;  // wave-uniform
-    const float xa = ln_apply(a.x[c], mean, scale, a.lnw[c], a.lnb[c]);
-    const float sx = a.carry[c] - xa;
-    const float * w2 = a.w2t + (size_t)n * D * C + c;
+    const bool active = (int)(blockIdx.x * blockDim.x + (threadIdx.x & ~63)) < C;  // wave-uniform
+    float w2v[64];
+    const float * w2 = a.w2t + (size_t)n * D * C + (active ? c : 0);
+#pragma unroll
+    for (int i = 0; i < 64; i++) w2v[i] = (i < D) ? w2[(size_t)i * C] : 0.0f;
+    const float xc = active ? a.x[c] : 0.0f, cc = active ? a.carry[c] : 0.0f;
+    const float lw = active ? a.lnw[c] : 0.0f, lb = active ? a.lnb[c] : 0.0f, mu = active ? a.maa[n][c] : 0.0f;
+    float mean, scale;
+    ln_stats_reg<E>(xv, C, mean, scale, sh);
+    if (!active) return;
+    const float xa = ln_apply(xc, mean, scale, lw, lb);
+    const float sx = cc - xa;
     const float * lv = a.lora + n * D;
     double acc = 0.0;
-    for (int i = 0; i < D; i++) acc += (double)(w2[(size_t)i * C] * lv[i]);
+#pragma unroll
+    for (int i = 0; i < 64; i++)
+        if (i < D) acc += (double)(w2v[i] * lv[i]);
     const float m = (float)acc;
-    emit32(a.out[n], 0, c, (m + a.maa[n][c]) * sx + xa);
+    emit32(a.out[n], 0, c, (m + mu) * sx + xa);
 }
 
 bool launch_v6_mix5_dec(hipStream_t st, int C, int D, const float * x, const float * carry, const float * lnw,
@@ -251,7 +350,14 @@ bool launch_v6_mix5_dec(hipStream_t st, int C, int D, const float * x, const flo
         a.maa[n] = maa[n];
         a.out[n] = outs[n];
     }
-    hipLaunchKernelGGL(k_v6_mix5_dec, dim3((C + 255) / 256, 5), dim3(256), 0, st, a);
+    if (D > 64 || C > 32 * 256) {
+        fprintf(stderr, "rwkv: v6 maa LoRA width %d / n_embed %d unsupported\n", D, C);
+        return false;
+    }
+    dim3 grid((C + 255) / 256, 5);
+    if (C <= 1024) hipLaunchKernelGGL(k_v6_mix5_dec<4>, grid, dim3(256), 0, st, a);
+    else if (C <= 4096) hipLaunchKernelGGL(k_v6_mix5_dec<16>, grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(k_v6_mix5_dec<32>, grid, dim3(256), 0, st, a);
     HIP_OK(hipGetLastError());
     return true;
 }
@@ -281,24 +387,50 @@ __global__ __launch_bounds__(256) void k_att6_dec(Att6Dec a) {
             emit32(act, 0, k, a.dl[k]);
         }
         __syncthreads();
-        // one wave per row, lanes over K blocks: the same arithmetic as the batched matmul
-        // kernel (k_mm, T > 1), so serial and sequence evaluation stay bit-identical
-        const int lane = tid & 63, nw = blockDim.x >> 6;
-        for (int j = tid >> 6; j < S; j += nw) {
-            float acc[1] = {0.0f}, acc2[1] = {0.0f};
-            const int row = c0 + j;
-            switch (a.wd2.type) {
-                case W_F32: mv_accumulate<W_F32, 1>(a.wd2, act, row, lane, acc, acc2); break;
-                case W_F16: mv_accumulate<W_F16, 1>(a.wd2, act, row, lane, acc, acc2); break;
-                case W_Q4_0: mv_accumulate<W_Q4_0, 1>(a.wd2, act, row, lane, acc, acc2); break;
-                case W_Q4_1: mv_accumulate<W_Q4_1, 1>(a.wd2, act, row, lane, acc, acc2); break;
-                case W_Q5_0: mv_accumulate<W_Q5_0, 1>(a.wd2, act, row, lane, acc, acc2); break;
-                case W_Q5_1: mv_accumulate<W_Q5_1, 1>(a.wd2, act, row, lane, acc, acc2); break;
-                case W_Q8_0: mv_accumulate<W_Q8_0, 1>(a.wd2, act, row, lane, acc, acc2); break;
-                default: break;
+        // rows of Wd2 for this head: LPR = pow2(#blocks) lanes per row.  Each lane computes one
+        // block partial like k_mm's lane b, and the LPR-lane butterfly adds them in the same
+        // order as k_mm's full-wave butterfly (the other lanes there hold exact zeros), so
+        // serial and sequence evaluation stay bit-identical.
+        const int nbk = a.wd2.type <= W_F16 ? 0 : D / 32;
+        if (nbk > 0 && nbk <= 64) {
+            int LPR = 1;
+            while (LPR < nbk) LPR <<= 1;
+            const int rows_per_pass = (int)blockDim.x / LPR;
+            const int sub = tid % LPR, rsel = tid / LPR;
+            for (int j0 = 0; j0 < S; j0 += rows_per_pass) {
+                const int j = j0 + rsel;
+                float p = 0.0f, p2 = 0.0f;
+                if (j < S && sub < nbk) {
+                    const int4 * ap = (const int4 *)(act.q + (size_t)sub * 32);
+                    float dw = 0.0f, mw = 0.0f;
+                    int sumi = 0;
+                    const int row = c0 + j;
+                    switch (a.wd2.type) {
+                        case W_Q4_0: sumi = block_dot<W_Q4_0>(a.wd2, row, sub, nbk, ap[0], ap[1], act.qsum[sub], dw, mw); break;
+                        case W_Q4_1: sumi = block_dot<W_Q4_1>(a.wd2, row, sub, nbk, ap[0], ap[1], act.qsum[sub], dw, mw); break;
+                        case W_Q5_0: sumi = block_dot<W_Q5_0>(a.wd2, row, sub, nbk, ap[0], ap[1], act.qsum[sub], dw, mw); break;
+                        case W_Q5_1: sumi = block_dot<W_Q5_1>(a.wd2, row, sub, nbk, ap[0], ap[1], act.qsum[sub], dw, mw); break;
+                        case W_Q8_0: sumi = block_dot<W_Q8_0>(a.wd2, row, sub, nbk, ap[0], ap[1], act.qsum[sub], dw, mw); break;
+                        default: break;
+                    }
+                    p = fmaf(dw * act.d[sub], (float)sumi, 0.0f);
+                    if (act.fmt == A_Q8_1) p2 = mw * act.s[sub];
+                }
+                p = group_sum(p, LPR);
+                p2 = group_sum(p2, LPR);
+                if (sub == 0 && j < S) sw[j] = expf(-expf((p + p2) + a.decay[c0 + j]));
             }
-            const float sum = wave_sum(acc[0]) + wave_sum(acc2[0]);
-            if (lane == 0) sw[j] = expf(-expf(sum + a.decay[row]));
+        } else {
+            // F32 / F16 decay LoRA (FP16 checkpoints keep time_decay_w2 in FP32): one wave per row
+            const int lane = tid & 63, nw = blockDim.x >> 6;
+            for (int j = tid >> 6; j < S; j += nw) {
+                float acc[1] = {0.0f}, acc2[1] = {0.0f};
+                const int row = c0 + j;
+                if (a.wd2.type == W_F32) mv_accumulate<W_F32, 1>(a.wd2, act, row, lane, acc, acc2);
+                else mv_accumulate<W_F16, 1>(a.wd2, act, row, lane, acc, acc2);
+                const float sum = wave_sum(acc[0]) + wave_sum(acc2[0]);
+                if (lane == 0) sw[j] = expf(-expf(sum + a.decay[row]));
+            }
         }
     }
     __syncthreads();

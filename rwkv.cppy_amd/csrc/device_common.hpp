@@ -14,6 +14,26 @@ __device__ __forceinline__ T wave_sum(T v) {
     return v;
 }
 
+// Full-wave float sum with DPP (no LDS traffic): quad butterflies, row half-mirror and mirror
+// give every lane its 16-lane row sum, then row_bcast15 / row_bcast31 fold the rows upward.
+// The total is valid in lane 63 only.  Every matmul kernel (decode and sequence) reduces with
+// this one function, so both paths round identically.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ float dpp_add(float v) {
+    const int o = __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROW_MASK, 0xF, false);
+    return v + __builtin_bit_cast(float, o);
+}
+
+__device__ __forceinline__ float wave_sum63(float v) {
+    v = dpp_add<0xB1, 0xF>(v);   // quad_perm [1,0,3,2]
+    v = dpp_add<0x4E, 0xF>(v);   // quad_perm [2,3,0,1]
+    v = dpp_add<0x141, 0xF>(v);  // row_half_mirror
+    v = dpp_add<0x140, 0xF>(v);  // row_mirror
+    v = dpp_add<0x142, 0xA>(v);  // row_bcast:15 into rows 1 and 3
+    v = dpp_add<0x143, 0xC>(v);  // row_bcast:31 into rows 2 and 3
+    return v;
+}
+
 // sum over groups of `width` adjacent lanes (width power of two <= 64); all lanes get the sum
 template <typename T>
 __device__ __forceinline__ T group_sum(T v, int width) {
@@ -83,34 +103,55 @@ __device__ __forceinline__ uint32_t spread4(uint32_t x) {
     return ((x & 1u) << 4) | ((x & 2u) << 11) | ((x & 4u) << 18) | ((x & 8u) << 25);
 }
 
+// One quantized weight block, loaded (phase 1) separately from its use (phase 2) so a lane can
+// keep several 16-byte HBM loads in flight.
+struct WBlk {
+    int4 q0, q1;     // nibbles (Q4/Q5: q0 only) or int8 (Q8_0: q0, q1)
+    uint32_t qh;     // Q5 high bits
+    uint32_t sc;     // fp16 d (low half) | fp16 m << 16 (_1 formats)
+};
+
 template <int WF>
-__device__ __forceinline__ int block_dot(const DMat & W, int row, int b, int nb, const int4 & alo,
-                                         const int4 & ahi, int qsum, float & dw, float & mw) {
-    const size_t bi = (size_t)row * nb + b;
-    int sumi = 0;
+__device__ __forceinline__ WBlk load_wblk(const DMat & W, size_t bi) {
+    WBlk w;
     if constexpr (WF == W_Q8_0) {
         const int4 * p = (const int4 *)(W.qs + bi * 32);
-        const int4 w0 = p[0], w1 = p[1];
-        sumi = __builtin_amdgcn_sdot4(w0.x, alo.x, sumi, false);
-        sumi = __builtin_amdgcn_sdot4(w0.y, alo.y, sumi, false);
-        sumi = __builtin_amdgcn_sdot4(w0.z, alo.z, sumi, false);
-        sumi = __builtin_amdgcn_sdot4(w0.w, alo.w, sumi, false);
-        sumi = __builtin_amdgcn_sdot4(w1.x, ahi.x, sumi, false);
-        sumi = __builtin_amdgcn_sdot4(w1.y, ahi.y, sumi, false);
-        sumi = __builtin_amdgcn_sdot4(w1.z, ahi.z, sumi, false);
-        sumi = __builtin_amdgcn_sdot4(w1.w, ahi.w, sumi, false);
-        dw = h2f(((const uint16_t *)W.sc)[bi]);
+        w.q0 = p[0];
+        w.q1 = p[1];
+    } else {
+        w.q0 = *(const int4 *)(W.qs + bi * 16);
+        w.q1 = make_int4(0, 0, 0, 0);
+    }
+    w.qh = (WF == W_Q5_0 || WF == W_Q5_1) ? W.qh[bi] : 0u;
+    if constexpr (WF == W_Q4_1 || WF == W_Q5_1) w.sc = ((const uint32_t *)W.sc)[bi];
+    else w.sc = ((const uint16_t *)W.sc)[bi];
+    return w;
+}
+
+template <int WF>
+__device__ __forceinline__ int dot_wblk(const WBlk & w, const int4 & alo, const int4 & ahi, int qsum, float & dw,
+                                        float & mw) {
+    int sumi = 0;
+    if constexpr (WF == W_Q8_0) {
+        sumi = __builtin_amdgcn_sdot4(w.q0.x, alo.x, sumi, false);
+        sumi = __builtin_amdgcn_sdot4(w.q0.y, alo.y, sumi, false);
+        sumi = __builtin_amdgcn_sdot4(w.q0.z, alo.z, sumi, false);
+        sumi = __builtin_amdgcn_sdot4(w.q0.w, alo.w, sumi, false);
+        sumi = __builtin_amdgcn_sdot4(w.q1.x, ahi.x, sumi, false);
+        sumi = __builtin_amdgcn_sdot4(w.q1.y, ahi.y, sumi, false);
+        sumi = __builtin_amdgcn_sdot4(w.q1.z, ahi.z, sumi, false);
+        sumi = __builtin_amdgcn_sdot4(w.q1.w, ahi.w, sumi, false);
+        dw = h2f((uint16_t)(w.sc & 0xFFFF));
         mw = 0.0f;
         (void)qsum;
         return sumi;
     } else {
-        const int4 w = *(const int4 *)(W.qs + bi * 16);
-        uint32_t lo0 = (uint32_t)w.x & 0x0F0F0F0Fu, lo1 = (uint32_t)w.y & 0x0F0F0F0Fu;
-        uint32_t lo2 = (uint32_t)w.z & 0x0F0F0F0Fu, lo3 = (uint32_t)w.w & 0x0F0F0F0Fu;
-        uint32_t hi0 = ((uint32_t)w.x >> 4) & 0x0F0F0F0Fu, hi1 = ((uint32_t)w.y >> 4) & 0x0F0F0F0Fu;
-        uint32_t hi2 = ((uint32_t)w.z >> 4) & 0x0F0F0F0Fu, hi3 = ((uint32_t)w.w >> 4) & 0x0F0F0F0Fu;
+        uint32_t lo0 = (uint32_t)w.q0.x & 0x0F0F0F0Fu, lo1 = (uint32_t)w.q0.y & 0x0F0F0F0Fu;
+        uint32_t lo2 = (uint32_t)w.q0.z & 0x0F0F0F0Fu, lo3 = (uint32_t)w.q0.w & 0x0F0F0F0Fu;
+        uint32_t hi0 = ((uint32_t)w.q0.x >> 4) & 0x0F0F0F0Fu, hi1 = ((uint32_t)w.q0.y >> 4) & 0x0F0F0F0Fu;
+        uint32_t hi2 = ((uint32_t)w.q0.z >> 4) & 0x0F0F0F0Fu, hi3 = ((uint32_t)w.q0.w >> 4) & 0x0F0F0F0Fu;
         if constexpr (WF == W_Q5_0 || WF == W_Q5_1) {
-            const uint32_t qh = W.qh[bi];
+            const uint32_t qh = w.qh;
             lo0 |= spread4(qh & 0xF);
             lo1 |= spread4((qh >> 4) & 0xF);
             lo2 |= spread4((qh >> 8) & 0xF);
@@ -133,16 +174,17 @@ __device__ __forceinline__ int block_dot(const DMat & W, int row, int b, int nb,
         } else if constexpr (WF == W_Q5_0) {
             sumi -= 16 * qsum;
         }
-        if constexpr (WF == W_Q4_1 || WF == W_Q5_1) {
-            const uint32_t dm = ((const uint32_t *)W.sc)[bi];
-            dw = h2f((uint16_t)(dm & 0xFFFF));
-            mw = h2f((uint16_t)(dm >> 16));
-        } else {
-            dw = h2f(((const uint16_t *)W.sc)[bi]);
-            mw = 0.0f;
-        }
+        dw = h2f((uint16_t)(w.sc & 0xFFFF));
+        mw = (WF == W_Q4_1 || WF == W_Q5_1) ? h2f((uint16_t)(w.sc >> 16)) : 0.0f;
         return sumi;
     }
+}
+
+template <int WF>
+__device__ __forceinline__ int block_dot(const DMat & W, int row, int b, int nb, const int4 & alo,
+                                         const int4 & ahi, int qsum, float & dw, float & mw) {
+    const WBlk w = load_wblk<WF>(W, (size_t)row * nb + b);
+    return dot_wblk<WF>(w, alo, ahi, qsum, dw, mw);
 }
 
 typedef _Float16 half2_t __attribute__((ext_vector_type(2)));

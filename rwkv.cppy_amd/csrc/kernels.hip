@@ -129,10 +129,10 @@ __global__ __launch_bounds__(256) void k_mm(MMGroup g) {
         for (int r = 0; r < RPW; r++)
 #pragma unroll
             for (int n = 0; n < NT; n++) {
-                const float s = wave_sum(acc[r][n]);
+                const float s = wave_sum63(acc[r][n]);
                 float s2 = 0.0f;
-                if constexpr (WF == W_Q4_1 || WF == W_Q5_1) s2 = wave_sum(acc2[r][n]);
-                if (lane == 0) {
+                if constexpr (WF == W_Q4_1 || WF == W_Q5_1) s2 = wave_sum63(acc2[r][n]);
+                if (lane == 63) {
                     red[n][wave * RPW + r] = s;
                     red2[n][wave * RPW + r] = s2;
                 }

@@ -66,19 +66,23 @@ static int lds_bytes_for(int fmt, int K) {
     return ((K + 15) & ~15) + 3 * ((nb + 3) & ~3) * 4;
 }
 
-// One row-block of a matvec for a lane: weights for R rows of block b loaded first (R
-// independent 16-byte loads in flight), then the int8 dots.
-template <int WF, int R>
+// One row-block of a matvec for a lane: the weight blocks of all R rows (and the activation
+// block) are loaded unconditionally first -- rows past M are clamped to M-1 and discarded --
+// so R 16-byte HBM loads are in flight together; then the int8 dots.  LDS=true reads the
+// activation through a __shared__ pointer (ds_read), LDS=false from global memory.
+template <int WF, int R, bool LDS>
 __device__ __forceinline__ void mv_accumulate(const DMat & W, const ActBuf & a, int row0, int lane, float (&acc)[R],
                                               float (&acc2)[R]) {
     const int K = W.K, M = W.M;
+    int rows[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) rows[r] = min(row0 + r, M - 1);
     if constexpr (WF == W_F32) {
         for (int k = lane * 4; k < K; k += 256) {
-            const float4 x = *(const float4 *)(a.f + k);
             float4 w[R];
 #pragma unroll
-            for (int r = 0; r < R; r++)
-                w[r] = (row0 + r < M) ? *(const float4 *)((const float *)W.qs + (size_t)(row0 + r) * K + k) : make_float4(0, 0, 0, 0);
+            for (int r = 0; r < R; r++) w[r] = *(const float4 *)((const float *)W.qs + (size_t)rows[r] * K + k);
+            const float4 x = *(const float4 *)(a.f + k);
 #pragma unroll
             for (int r = 0; r < R; r++) {
                 float s = acc[r];
@@ -91,11 +95,10 @@ __device__ __forceinline__ void mv_accumulate(const DMat & W, const ActBuf & a, 
         }
     } else if constexpr (WF == W_F16) {
         for (int k = lane * 8; k < K; k += 512) {
-            const int4 x = *(const int4 *)(a.h + k);
             int4 w[R];
 #pragma unroll
-            for (int r = 0; r < R; r++)
-                w[r] = (row0 + r < M) ? *(const int4 *)((const __half *)W.qs + (size_t)(row0 + r) * K + k) : make_int4(0, 0, 0, 0);
+            for (int r = 0; r < R; r++) w[r] = *(const int4 *)((const __half *)W.qs + (size_t)rows[r] * K + k);
+            const int4 x = *(const int4 *)(a.h + k);
 #pragma unroll
             for (int r = 0; r < R; r++) {
                 float s = acc[r];
@@ -109,21 +112,55 @@ __device__ __forceinline__ void mv_accumulate(const DMat & W, const ActBuf & a, 
     } else {
         const int nb = K >> 5;
         for (int b = lane; b < nb; b += 64) {
-            const int4 * ap = (const int4 *)(a.q + (size_t)b * 32);
-            const int4 alo = ap[0], ahi = ap[1];
-            const float dx = a.d[b];
-            const int qs = a.qsum[b];
-            const float sx = (WF == W_Q4_1 || WF == W_Q5_1) ? a.s[b] : 0.0f;
+            WBlk w[R];
+#pragma unroll
+            for (int r = 0; r < R; r++) w[r] = load_wblk<WF>(W, (size_t)rows[r] * nb + b);
+            int4 alo, ahi;
+            float dx, sx;
+            int qs;
+            if constexpr (LDS) {
+                typedef int i32x4 __attribute__((ext_vector_type(4)));
+                typedef __attribute__((address_space(3))) const i32x4 lds_i32x4;
+                typedef __attribute__((address_space(3))) const float lds_float;
+                typedef __attribute__((address_space(3))) const int lds_int;
+                const lds_i32x4 * ap = (const lds_i32x4 *)(uintptr_t)(a.q + (size_t)b * 32);
+                const i32x4 t0 = ap[0], t1 = ap[1];
+                alo = make_int4(t0.x, t0.y, t0.z, t0.w);
+                ahi = make_int4(t1.x, t1.y, t1.z, t1.w);
+                dx = *(const lds_float *)(uintptr_t)(a.d + b);
+                qs = *(const lds_int *)(uintptr_t)(a.qsum + b);
+                sx = (WF == W_Q4_1 || WF == W_Q5_1) ? *(const lds_float *)(uintptr_t)(a.s + b) : 0.0f;
+            } else {
+                const int4 * ap = (const int4 *)(a.q + (size_t)b * 32);
+                alo = ap[0];
+                ahi = ap[1];
+                dx = a.d[b];
+                qs = a.qsum[b];
+                sx = (WF == W_Q4_1 || WF == W_Q5_1) ? a.s[b] : 0.0f;
+            }
 #pragma unroll
             for (int r = 0; r < R; r++) {
-                if (row0 + r < M) {
-                    float dw, mw;
-                    const int sumi = block_dot<WF>(W, row0 + r, b, nb, alo, ahi, qs, dw, mw);
-                    acc[r] = fmaf(dw * dx, (float)sumi, acc[r]);
-                    if constexpr (WF == W_Q4_1 || WF == W_Q5_1) acc2[r] += mw * sx;
-                }
+                float dw, mw;
+                const int sumi = dot_wblk<WF>(w[r], alo, ahi, qs, dw, mw);
+                acc[r] = fmaf(dw * dx, (float)sumi, acc[r]);
+                if constexpr (WF == W_Q4_1 || WF == W_Q5_1) acc2[r] += mw * sx;
             }
         }
+    }
+}
+
+template <int R, bool LDS>
+__device__ __forceinline__ void mv_dispatch(const DMat & W, const ActBuf & a, int row0, int lane, float (&acc)[R],
+                                            float (&acc2)[R]) {
+    switch (W.type) {
+        case W_F32: mv_accumulate<W_F32, R, LDS>(W, a, row0, lane, acc, acc2); break;
+        case W_F16: mv_accumulate<W_F16, R, LDS>(W, a, row0, lane, acc, acc2); break;
+        case W_Q4_0: mv_accumulate<W_Q4_0, R, LDS>(W, a, row0, lane, acc, acc2); break;
+        case W_Q4_1: mv_accumulate<W_Q4_1, R, LDS>(W, a, row0, lane, acc, acc2); break;
+        case W_Q5_0: mv_accumulate<W_Q5_0, R, LDS>(W, a, row0, lane, acc, acc2); break;
+        case W_Q5_1: mv_accumulate<W_Q5_1, R, LDS>(W, a, row0, lane, acc, acc2); break;
+        case W_Q8_0: mv_accumulate<W_Q8_0, R, LDS>(W, a, row0, lane, acc, acc2); break;
+        default: break;
     }
 }
 
@@ -212,30 +249,23 @@ __global__ __launch_bounds__(256) void k_mv(MVGroup g) {
     float acc[R], acc2[R];
 #pragma unroll
     for (int r = 0; r < R; r++) acc[r] = acc2[r] = 0.0f;
-    switch (Ent.W.type) {
-        case W_F32: mv_accumulate<W_F32, R>(Ent.W, a, row0, lane, acc, acc2); break;
-        case W_F16: mv_accumulate<W_F16, R>(Ent.W, a, row0, lane, acc, acc2); break;
-        case W_Q4_0: mv_accumulate<W_Q4_0, R>(Ent.W, a, row0, lane, acc, acc2); break;
-        case W_Q4_1: mv_accumulate<W_Q4_1, R>(Ent.W, a, row0, lane, acc, acc2); break;
-        case W_Q5_0: mv_accumulate<W_Q5_0, R>(Ent.W, a, row0, lane, acc, acc2); break;
-        case W_Q5_1: mv_accumulate<W_Q5_1, R>(Ent.W, a, row0, lane, acc, acc2); break;
-        case W_Q8_0: mv_accumulate<W_Q8_0, R>(Ent.W, a, row0, lane, acc, acc2); break;
-        default: break;
-    }
+    if (Ent.src == SRC_ACT) mv_dispatch<R, false>(Ent.W, a, row0, lane, acc, acc2);
+    else mv_dispatch<R, true>(Ent.W, a, row0, lane, acc, acc2);
+    const bool one = Ent.W.type == W_Q4_1 || Ent.W.type == W_Q5_1;
     if constexpr (!EMIT) {
 #pragma unroll
         for (int r = 0; r < R; r++) {
-            const float s = wave_sum(acc[r]) + wave_sum(acc2[r]);
+            const float s = one ? wave_sum63(acc[r]) + wave_sum63(acc2[r]) : wave_sum63(acc[r]) + 0.0f;
             const int row = row0 + r;
-            if (lane == 0 && row < Ent.W.M) Ent.y[row] = apply_epi_mv(Ent, row, s);
+            if (lane == 63 && row < Ent.W.M) Ent.y[row] = apply_epi_mv(Ent, row, s);
         }
     } else {
         // 4*R == 32 rows per workgroup: apply the epilogue and emit the 32 values as one
         // quantization block of the next matmul's input (ggml Q8 / fp16 / fp32)
 #pragma unroll
         for (int r = 0; r < R; r++) {
-            const float s = wave_sum(acc[r]) + wave_sum(acc2[r]);
-            if (lane == 0) red[wave * R + r] = s;
+            const float s = one ? wave_sum63(acc[r]) + wave_sum63(acc2[r]) : wave_sum63(acc[r]) + 0.0f;
+            if (lane == 63) red[wave * R + r] = s;
         }
         __syncthreads();
         if (tid < 32) {
@@ -387,38 +417,49 @@ __global__ __launch_bounds__(256) void k_att6_dec(Att6Dec a) {
             emit32(act, 0, k, a.dl[k]);
         }
         __syncthreads();
-        // rows of Wd2 for this head: LPR = pow2(#blocks) lanes per row.  Each lane computes one
-        // block partial like k_mm's lane b, and the LPR-lane butterfly adds them in the same
-        // order as k_mm's full-wave butterfly (the other lanes there hold exact zeros), so
-        // serial and sequence evaluation stay bit-identical.
+        // rows of Wd2 for this head, one wave per group of rows, lanes over the K blocks with
+        // all rows' weight blocks loaded first; reduced with wave_sum63 exactly like the
+        // batched matmul kernel (k_mm, T > 1) so serial and sequence stay bit-identical.
         const int nbk = a.wd2.type <= W_F16 ? 0 : D / 32;
         if (nbk > 0 && nbk <= 64) {
-            int LPR = 1;
-            while (LPR < nbk) LPR <<= 1;
-            const int rows_per_pass = (int)blockDim.x / LPR;
-            const int sub = tid % LPR, rsel = tid / LPR;
-            for (int j0 = 0; j0 < S; j0 += rows_per_pass) {
-                const int j = j0 + rsel;
-                float p = 0.0f, p2 = 0.0f;
-                if (j < S && sub < nbk) {
-                    const int4 * ap = (const int4 *)(act.q + (size_t)sub * 32);
-                    float dw = 0.0f, mw = 0.0f;
-                    int sumi = 0;
-                    const int row = c0 + j;
-                    switch (a.wd2.type) {
-                        case W_Q4_0: sumi = block_dot<W_Q4_0>(a.wd2, row, sub, nbk, ap[0], ap[1], act.qsum[sub], dw, mw); break;
-                        case W_Q4_1: sumi = block_dot<W_Q4_1>(a.wd2, row, sub, nbk, ap[0], ap[1], act.qsum[sub], dw, mw); break;
-                        case W_Q5_0: sumi = block_dot<W_Q5_0>(a.wd2, row, sub, nbk, ap[0], ap[1], act.qsum[sub], dw, mw); break;
-                        case W_Q5_1: sumi = block_dot<W_Q5_1>(a.wd2, row, sub, nbk, ap[0], ap[1], act.qsum[sub], dw, mw); break;
-                        case W_Q8_0: sumi = block_dot<W_Q8_0>(a.wd2, row, sub, nbk, ap[0], ap[1], act.qsum[sub], dw, mw); break;
-                        default: break;
+            const int lane = tid & 63, nw = blockDim.x >> 6;
+            const int rpw = (S + nw - 1) / nw;  // rows per wave (<= 64)
+            const int jbase = (tid >> 6) * rpw;
+            for (int jj = 0; jj < rpw; jj += 16) {
+                float p[16], p2[16];
+#pragma unroll
+                for (int q = 0; q < 16; q++) p[q] = p2[q] = 0.0f;
+                if (lane < nbk) {
+                    const int4 * ap = (const int4 *)(act.q + (size_t)lane * 32);
+                    const int4 alo = ap[0], ahi = ap[1];
+                    const float dx = act.d[lane];
+                    const int qs = act.qsum[lane];
+                    const float sx = act.fmt == A_Q8_1 ? act.s[lane] : 0.0f;
+#pragma unroll
+                    for (int q = 0; q < 16; q++) {
+                        const int j = min(jbase + jj + q, S - 1);
+                        float dw = 0.0f, mw = 0.0f;
+                        int sumi = 0;
+                        const int row = c0 + j;
+                        switch (a.wd2.type) {
+                            case W_Q4_0: sumi = block_dot<W_Q4_0>(a.wd2, row, lane, nbk, alo, ahi, qs, dw, mw); break;
+                            case W_Q4_1: sumi = block_dot<W_Q4_1>(a.wd2, row, lane, nbk, alo, ahi, qs, dw, mw); break;
+                            case W_Q5_0: sumi = block_dot<W_Q5_0>(a.wd2, row, lane, nbk, alo, ahi, qs, dw, mw); break;
+                            case W_Q5_1: sumi = block_dot<W_Q5_1>(a.wd2, row, lane, nbk, alo, ahi, qs, dw, mw); break;
+                            case W_Q8_0: sumi = block_dot<W_Q8_0>(a.wd2, row, lane, nbk, alo, ahi, qs, dw, mw); break;
+                            default: break;
+                        }
+                        p[q] = fmaf(dw * dx, (float)sumi, 0.0f);
+                        p2[q] = 0.0f + mw * sx;
                     }
-                    p = fmaf(dw * act.d[sub], (float)sumi, 0.0f);
-                    if (act.fmt == A_Q8_1) p2 = mw * act.s[sub];
                 }
-                p = group_sum(p, LPR);
-                p2 = group_sum(p2, LPR);
-                if (sub == 0 && j < S) sw[j] = expf(-expf((p + p2) + a.decay[c0 + j]));
+                const bool one = act.fmt == A_Q8_1;
+#pragma unroll
+                for (int q = 0; q < 16; q++) {
+                    const float sum = one ? wave_sum63(p[q]) + wave_sum63(p2[q]) : wave_sum63(p[q]) + 0.0f;
+                    const int j = jbase + jj + q;
+                    if (lane == 63 && j < S && jj + q < rpw) sw[j] = expf(-expf(sum + a.decay[c0 + j]));
+                }
             }
         } else {
             // F32 / F16 decay LoRA (FP16 checkpoints keep time_decay_w2 in FP32): one wave per row
@@ -426,10 +467,10 @@ __global__ __launch_bounds__(256) void k_att6_dec(Att6Dec a) {
             for (int j = tid >> 6; j < S; j += nw) {
                 float acc[1] = {0.0f}, acc2[1] = {0.0f};
                 const int row = c0 + j;
-                if (a.wd2.type == W_F32) mv_accumulate<W_F32, 1>(a.wd2, act, row, lane, acc, acc2);
-                else mv_accumulate<W_F16, 1>(a.wd2, act, row, lane, acc, acc2);
-                const float sum = wave_sum(acc[0]) + wave_sum(acc2[0]);
-                if (lane == 0) sw[j] = expf(-expf(sum + a.decay[row]));
+                if (a.wd2.type == W_F32) mv_accumulate<W_F32, 1, false>(a.wd2, act, row, lane, acc, acc2);
+                else mv_accumulate<W_F16, 1, false>(a.wd2, act, row, lane, acc, acc2);
+                const float sum = wave_sum63(acc[0]) + 0.0f;
+                if (lane == 63) sw[j] = expf(-expf(sum + a.decay[row]));
             }
         }
     }

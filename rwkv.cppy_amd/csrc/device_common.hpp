@@ -41,11 +41,32 @@ __device__ __forceinline__ T group_sum(T v, int width) {
     return v;
 }
 
-// deterministic block sum (fixed tree): every thread returns the total
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ double dpp_add_d(double v) {
+    const long long b = __builtin_bit_cast(long long, v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffll), CTRL, ROW_MASK, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, ROW_MASK, 0xF, false);
+    const long long o = ((long long)hi << 32) | (long long)(unsigned)lo;
+    return v + __builtin_bit_cast(double, o);
+}
+
+// wave_sum63 for doubles (same tree); valid in lane 63
+__device__ __forceinline__ double wave_sum63_d(double v) {
+    v = dpp_add_d<0xB1, 0xF>(v);
+    v = dpp_add_d<0x4E, 0xF>(v);
+    v = dpp_add_d<0x141, 0xF>(v);
+    v = dpp_add_d<0x140, 0xF>(v);
+    v = dpp_add_d<0x142, 0xA>(v);
+    v = dpp_add_d<0x143, 0xC>(v);
+    return v;
+}
+
+// deterministic block sum (fixed tree): every thread returns the total.  Every LayerNorm on
+// the device (decode prologues and the sequence kernels) reduces through this one function.
 __device__ inline double block_sum_d(double v, double * sh) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
-    v = wave_sum(v);
-    if (lane == 0) sh[wave] = v;
+    v = wave_sum63_d(v);
+    if (lane == 63) sh[wave] = v;
     __syncthreads();
     double r = 0.0;
     for (int w = 0; w < nw; w++) r += sh[w];

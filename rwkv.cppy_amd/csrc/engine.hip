@@ -872,7 +872,7 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits) {
             src_lnmix(b.add(L.maa_w1, lora_, EPI_TANH), x_, si + C, L.ln1_w, L.ln1_b, L.maa_x, 1, so + C);
             if (!mv(b.g)) return false;
             ActBuf outs[5] = {A(1, L.decay_w1), A(2, L.att_k), A(3, L.att_v), A(4, L.att_r), A(5, L.att_g)};
-            if (!launch_v6_mix5_dec(stream_, C, D, x_, si + C, L.ln1_w, L.ln1_b, lora_, L.maa_w2t, L.maa, outs))
+            if (!launch_v6_mix5_dec(stream_, C, D, so + C, si + C, lora_, L.maa_w2t, L.maa, outs))
                 return false;
             MV c;
             const int mats[5] = {3, 1, 2, 4, 0};  // r, k, v, g, w

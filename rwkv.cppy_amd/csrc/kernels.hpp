@@ -109,11 +109,11 @@ struct MVGroup {
 
 bool launch_mv_group(hipStream_t st, MVGroup & g);
 
-// v6 token-shift mixes with the maa LoRA (rwkv_graph.inc:308-346), LN recomputed per block;
-// w2t is time_maa_w2 transposed to [5][D][C]; emits the five mixed vectors w,k,v,r,g.
-bool launch_v6_mix5_dec(hipStream_t st, int C, int D, const float * x, const float * carry, const float * lnw,
-                        const float * lnb, const float * lora, const float * w2t, const float * const * maa,
-                        const ActBuf * outs);
+// v6 token-shift mixes with the maa LoRA (rwkv_graph.inc:308-346); xa = LN(x) is the new
+// att_xx carry already written by the W1 matvec prologue; w2t is time_maa_w2 transposed to
+// [5][D][C]; emits the five mixed vectors w,k,v,r,g.
+bool launch_v6_mix5_dec(hipStream_t st, int C, int D, const float * xa, const float * carry, const float * lora,
+                        const float * w2t, const float * const * maa, const ActBuf * outs);
 
 // v5/v6 attention core for one token, one workgroup per head: (v6: decay LoRA second stage
 // w = exp(-exp(Wd2 . dl + decay))) + wkv6 + GroupNorm*ln_x (+ *g).  Writes fp32 y [C].

@@ -66,106 +66,122 @@ static int lds_bytes_for(int fmt, int K) {
     return ((K + 15) & ~15) + 3 * ((nb + 3) & ~3) * 4;
 }
 
-// One row-block of a matvec for a lane: the weight blocks of all R rows (and the activation
-// block) are loaded unconditionally first -- rows past M are clamped to M-1 and discarded --
-// so R 16-byte HBM loads are in flight together; then the int8 dots.  LDS=true reads the
-// activation through a __shared__ pointer (ds_read), LDS=false from global memory.
-template <int WF, int R, bool LDS>
-__device__ __forceinline__ void mv_accumulate(const DMat & W, const ActBuf & a, int row0, int lane, float (&acc)[R],
-                                              float (&acc2)[R]) {
-    const int K = W.K, M = W.M;
-    int rows[R];
-#pragma unroll
-    for (int r = 0; r < R; r++) rows[r] = min(row0 + r, M - 1);
+// --------------------------------------------------------------------------- decode matvec
+// A lane owns 16-byte "units" of a row: quantized weights one 32-block (lane + 64u), F16 eight
+// halves (k = 8*lane + 512u), F32 four floats (k = 4*lane + 256u) -- the same lane/unit
+// assignment and accumulation order as the batched kernel k_mm, so decode and sequence
+// results are bit-identical.  All R*U weight units of a wave are loaded before anything else
+// waits (rows past M clamp to M-1, units past K clamp to the last unit and are skipped in the
+// dot), so the whole row-block is one HBM round trip, overlapped with the prologue.
+
+__host__ __device__ inline int mv_units(int type, int K) {
+    if (type == W_F32) return (K + 255) / 256;
+    if (type == W_F16) return (K + 511) / 512;
+    return (K / 32 + 63) / 64;
+}
+
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) const i32x4_t lds_i32x4_t;
+typedef __attribute__((address_space(3))) const float lds_float_t;
+typedef __attribute__((address_space(3))) const int lds_int_t;
+
+template <bool LDS>
+__device__ __forceinline__ int4 load16(const void * p) {
+    if constexpr (LDS) {
+        const i32x4_t t = *(const lds_i32x4_t *)(uintptr_t)p;
+        return make_int4(t.x, t.y, t.z, t.w);
+    } else {
+        return *(const int4 *)p;
+    }
+}
+template <bool LDS>
+__device__ __forceinline__ float loadf(const float * p) {
+    if constexpr (LDS) return *(const lds_float_t *)(uintptr_t)p;
+    else return *p;
+}
+template <bool LDS>
+__device__ __forceinline__ int loadi(const int * p) {
+    if constexpr (LDS) return *(const lds_int_t *)(uintptr_t)p;
+    else return *p;
+}
+
+template <int WF>
+__device__ __forceinline__ WBlk load_unit(const DMat & W, int row, int u, int lane) {
+    const int K = W.K;
     if constexpr (WF == W_F32) {
-        for (int k = lane * 4; k < K; k += 256) {
-            float4 w[R];
-#pragma unroll
-            for (int r = 0; r < R; r++) w[r] = *(const float4 *)((const float *)W.qs + (size_t)rows[r] * K + k);
-            const float4 x = *(const float4 *)(a.f + k);
-#pragma unroll
-            for (int r = 0; r < R; r++) {
-                float s = acc[r];
-                s = fmaf(w[r].x, x.x, s);
-                s = fmaf(w[r].y, x.y, s);
-                s = fmaf(w[r].z, x.z, s);
-                s = fmaf(w[r].w, x.w, s);
-                acc[r] = s;
-            }
-        }
+        WBlk w;
+        const int k = min(lane * 4 + u * 256, K - 4);
+        w.q0 = *(const int4 *)((const float *)W.qs + (size_t)row * K + k);
+        return w;
     } else if constexpr (WF == W_F16) {
-        for (int k = lane * 8; k < K; k += 512) {
-            int4 w[R];
-#pragma unroll
-            for (int r = 0; r < R; r++) w[r] = *(const int4 *)((const __half *)W.qs + (size_t)rows[r] * K + k);
-            const int4 x = *(const int4 *)(a.h + k);
-#pragma unroll
-            for (int r = 0; r < R; r++) {
-                float s = acc[r];
-                s = __builtin_amdgcn_fdot2(__builtin_bit_cast(half2_t, w[r].x), __builtin_bit_cast(half2_t, x.x), s, false);
-                s = __builtin_amdgcn_fdot2(__builtin_bit_cast(half2_t, w[r].y), __builtin_bit_cast(half2_t, x.y), s, false);
-                s = __builtin_amdgcn_fdot2(__builtin_bit_cast(half2_t, w[r].z), __builtin_bit_cast(half2_t, x.z), s, false);
-                s = __builtin_amdgcn_fdot2(__builtin_bit_cast(half2_t, w[r].w), __builtin_bit_cast(half2_t, x.w), s, false);
-                acc[r] = s;
-            }
-        }
+        WBlk w;
+        const int k = min(lane * 8 + u * 512, K - 8);
+        w.q0 = *(const int4 *)((const __half *)W.qs + (size_t)row * K + k);
+        return w;
     } else {
         const int nb = K >> 5;
-        for (int b = lane; b < nb; b += 64) {
-            WBlk w[R];
-#pragma unroll
-            for (int r = 0; r < R; r++) w[r] = load_wblk<WF>(W, (size_t)rows[r] * nb + b);
-            int4 alo, ahi;
-            float dx, sx;
-            int qs;
-            if constexpr (LDS) {
-                typedef int i32x4 __attribute__((ext_vector_type(4)));
-                typedef __attribute__((address_space(3))) const i32x4 lds_i32x4;
-                typedef __attribute__((address_space(3))) const float lds_float;
-                typedef __attribute__((address_space(3))) const int lds_int;
-                const lds_i32x4 * ap = (const lds_i32x4 *)(uintptr_t)(a.q + (size_t)b * 32);
-                const i32x4 t0 = ap[0], t1 = ap[1];
-                alo = make_int4(t0.x, t0.y, t0.z, t0.w);
-                ahi = make_int4(t1.x, t1.y, t1.z, t1.w);
-                dx = *(const lds_float *)(uintptr_t)(a.d + b);
-                qs = *(const lds_int *)(uintptr_t)(a.qsum + b);
-                sx = (WF == W_Q4_1 || WF == W_Q5_1) ? *(const lds_float *)(uintptr_t)(a.s + b) : 0.0f;
-            } else {
-                const int4 * ap = (const int4 *)(a.q + (size_t)b * 32);
-                alo = ap[0];
-                ahi = ap[1];
-                dx = a.d[b];
-                qs = a.qsum[b];
-                sx = (WF == W_Q4_1 || WF == W_Q5_1) ? a.s[b] : 0.0f;
-            }
-#pragma unroll
-            for (int r = 0; r < R; r++) {
-                float dw, mw;
-                const int sumi = dot_wblk<WF>(w[r], alo, ahi, qs, dw, mw);
-                acc[r] = fmaf(dw * dx, (float)sumi, acc[r]);
-                if constexpr (WF == W_Q4_1 || WF == W_Q5_1) acc2[r] += mw * sx;
-            }
-        }
+        const int b = min(lane + u * 64, nb - 1);
+        return load_wblk<WF>(W, (size_t)row * nb + b);
     }
 }
 
-template <int R, bool LDS>
-__device__ __forceinline__ void mv_dispatch(const DMat & W, const ActBuf & a, int row0, int lane, float (&acc)[R],
-                                            float (&acc2)[R]) {
-    switch (W.type) {
-        case W_F32: mv_accumulate<W_F32, R, LDS>(W, a, row0, lane, acc, acc2); break;
-        case W_F16: mv_accumulate<W_F16, R, LDS>(W, a, row0, lane, acc, acc2); break;
-        case W_Q4_0: mv_accumulate<W_Q4_0, R, LDS>(W, a, row0, lane, acc, acc2); break;
-        case W_Q4_1: mv_accumulate<W_Q4_1, R, LDS>(W, a, row0, lane, acc, acc2); break;
-        case W_Q5_0: mv_accumulate<W_Q5_0, R, LDS>(W, a, row0, lane, acc, acc2); break;
-        case W_Q5_1: mv_accumulate<W_Q5_1, R, LDS>(W, a, row0, lane, acc, acc2); break;
-        case W_Q8_0: mv_accumulate<W_Q8_0, R, LDS>(W, a, row0, lane, acc, acc2); break;
-        default: break;
+struct AUnit {
+    int4 lo, hi;
+    float d, s;
+    int qs;
+};
+
+template <int WF, bool LDS>
+__device__ __forceinline__ AUnit load_act_unit(const ActBuf & a, int u, int lane) {
+    AUnit x;
+    const int K = a.K;
+    if constexpr (WF == W_F32) {
+        x.lo = load16<LDS>(a.f + min(lane * 4 + u * 256, K - 4));
+    } else if constexpr (WF == W_F16) {
+        x.lo = load16<LDS>(a.h + min(lane * 8 + u * 512, K - 8));
+    } else {
+        const int b = min(lane + u * 64, (K >> 5) - 1);
+        x.lo = load16<LDS>(a.q + (size_t)b * 32);
+        x.hi = load16<LDS>(a.q + (size_t)b * 32 + 16);
+        x.d = loadf<LDS>(a.d + b);
+        x.qs = loadi<LDS>(a.qsum + b);
+        x.s = (WF == W_Q4_1 || WF == W_Q5_1) ? loadf<LDS>(a.s + b) : 0.0f;
+    }
+    return x;
+}
+
+template <int WF>
+__device__ __forceinline__ bool unit_valid(int K, int u, int lane) {
+    if constexpr (WF == W_F32) return lane * 4 + u * 256 < K;
+    else if constexpr (WF == W_F16) return lane * 8 + u * 512 < K;
+    else return lane + u * 64 < (K >> 5);
+}
+
+template <int WF>
+__device__ __forceinline__ void dot_unit(const WBlk & w, const AUnit & x, float & acc, float & acc2) {
+    if constexpr (WF == W_F32) {
+        float s = acc;
+        s = fmaf(__int_as_float(w.q0.x), __int_as_float(x.lo.x), s);
+        s = fmaf(__int_as_float(w.q0.y), __int_as_float(x.lo.y), s);
+        s = fmaf(__int_as_float(w.q0.z), __int_as_float(x.lo.z), s);
+        s = fmaf(__int_as_float(w.q0.w), __int_as_float(x.lo.w), s);
+        acc = s;
+    } else if constexpr (WF == W_F16) {
+        float s = acc;
+        s = __builtin_amdgcn_fdot2(__builtin_bit_cast(half2_t, w.q0.x), __builtin_bit_cast(half2_t, x.lo.x), s, false);
+        s = __builtin_amdgcn_fdot2(__builtin_bit_cast(half2_t, w.q0.y), __builtin_bit_cast(half2_t, x.lo.y), s, false);
+        s = __builtin_amdgcn_fdot2(__builtin_bit_cast(half2_t, w.q0.z), __builtin_bit_cast(half2_t, x.lo.z), s, false);
+        s = __builtin_amdgcn_fdot2(__builtin_bit_cast(half2_t, w.q0.w), __builtin_bit_cast(half2_t, x.lo.w), s, false);
+        acc = s;
+    } else {
+        float dw, mw;
+        const int sumi = dot_wblk<WF>(w, x.lo, x.hi, x.qs, dw, mw);
+        acc = fmaf(dw * x.d, (float)sumi, acc);
+        if constexpr (WF == W_Q4_1 || WF == W_Q5_1) acc2 += mw * x.s;
     }
 }
 
-// Per-thread register image of a K-vector: thread t owns k = i*256 + t (i < E).  All loads of
-// a phase are issued before any is used (one dependent L2 round trip per phase).
+// Per-thread register image of a K-vector: thread t owns k = i*256 + t (i < E).
 template <int E>
 __device__ __forceinline__ void load_vec(float (&v)[E], const float * p, int K) {
 #pragma unroll
@@ -195,69 +211,101 @@ __device__ __forceinline__ void ln_stats_reg(const float (&xv)[E], int K, float 
     scale = 1.0f / sqrtf((float)(s2 / (double)K) + 1e-5f);
 }
 
-template <int R, int E, bool EMIT>
-__global__ __launch_bounds__(256) void k_mv(MVGroup g) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    __shared__ double sh[8];
-    __shared__ float red[4 * R];
-    int e = 0;
-#pragma unroll 1
-    while (e + 1 < g.n && (int)blockIdx.x >= g.e[e + 1].block0) e++;
-    const MVEntry & Ent = g.e[e];
-    const int K = Ent.W.K, fmt = act_fmt_for(Ent.W.type);
+// One workgroup = 4 waves x R rows.  E == 0: the input is an activation buffer in global
+// memory (SRC_ACT); E > 0: the prologue builds it in LDS (SRC_F32 / SRC_LNMIX, K <= 256*E).
+template <int WF, int R, int U, int E, bool EMIT>
+__device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, char * smem, double * sh, float * red) {
+    constexpr int EE = E > 0 ? E : 1;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    ActBuf a;
-    if (Ent.src == SRC_ACT) {
-        a = Ent.act;
-    } else {
-        a = lds_act(smem, fmt, K);
-        float v[E];
-        if (Ent.src == SRC_F32) {
-            load_vec<E>(v, Ent.f, K);
-        } else {
-            float xv[E], lw[E], lb[E];
-            load_vec<E>(xv, Ent.x, K);
-            load_vec<E>(lw, Ent.lnw, K);
-            load_vec<E>(lb, Ent.lnb, K);
-            float cv[E], mv[E];
-            if (Ent.form != 2) {
-                load_vec<E>(cv, Ent.carry, K);
-                load_vec<E>(mv, Ent.mu, K);
-            }
-            float mean, scale;
-            ln_stats_reg<E>(xv, K, mean, scale, sh);
-            const bool write_carry = Ent.carry_out && (int)blockIdx.x == Ent.block0;
+    const DMat & W = Ent.W;
+    const int M = W.M, K = W.K;
+    const int rowwg = wgi * 4 * R, row0 = rowwg + wave * R;
+    int rows[R];
 #pragma unroll
-            for (int i = 0; i < E; i++) {
+    for (int r = 0; r < R; r++) rows[r] = min(row0 + r, M - 1);
+    const int units = mv_units(WF, K);
+
+    // (1) prologue inputs: small fp32 vectors, L2-resident
+    float xv[EE], lw[EE], lb[EE], cv[EE], mv[EE];
+    if constexpr (E > 0) {
+        if (Ent.src == SRC_F32) {
+            load_vec<EE>(xv, Ent.f, K);
+        } else {
+            load_vec<EE>(xv, Ent.x, K);
+            load_vec<EE>(lw, Ent.lnw, K);
+            load_vec<EE>(lb, Ent.lnb, K);
+            if (Ent.form != 2) {
+                load_vec<EE>(cv, Ent.carry, K);
+                load_vec<EE>(mv, Ent.mu, K);
+            }
+        }
+    }
+    // (2) this wave's weight units (HBM), in flight during the prologue
+    WBlk w[R][U];
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+        for (int r = 0; r < R; r++) w[r][u] = load_unit<WF>(W, rows[r], u, lane);
+
+    // (3) prologue: LayerNorm + token-shift mix + ggml activation quantization into LDS
+    ActBuf a;
+    if constexpr (E > 0) {
+        a = lds_act(smem, act_fmt_for(WF), K);
+        if (Ent.src != SRC_F32) {
+            float mean, scale;
+            ln_stats_reg<EE>(xv, K, mean, scale, sh);
+            const bool write_carry = Ent.carry_out && wgi == 0;
+#pragma unroll
+            for (int i = 0; i < EE; i++) {
                 const float xa = ln_apply(xv[i], mean, scale, lw[i], lb[i]);
                 const int k = i * 256 + tid;
                 if (write_carry && k < K) Ent.carry_out[k] = xa;
-                if (Ent.form == 2) v[i] = xa;
-                else if (Ent.form == 0) v[i] = xa * mv[i] + (cv[i] - cv[i] * mv[i]);
-                else v[i] = (cv[i] - xa) * mv[i] + xa;
+                if (Ent.form == 2) xv[i] = xa;
+                else if (Ent.form == 0) xv[i] = xa * mv[i] + (cv[i] - cv[i] * mv[i]);
+                else xv[i] = (cv[i] - xa) * mv[i] + xa;
             }
         }
 #pragma unroll
-        for (int i = 0; i < E; i++) {
+        for (int i = 0; i < EE; i++) {
             const int k0 = i * 256;
-            if (k0 + (tid & ~31) < K) emit32(a, 0, k0 + tid, v[i]);  // half-wave uniform
+            if (k0 + (tid & ~31) < K) emit32(a, 0, k0 + tid, xv[i]);  // half-wave uniform
         }
         __syncthreads();
+    } else {
+        a = Ent.act;
     }
-    const int rowwg = ((int)blockIdx.x - Ent.block0) * 4 * R;
-    const int row0 = rowwg + wave * R;
+
+    // (4) dots
     float acc[R], acc2[R];
 #pragma unroll
     for (int r = 0; r < R; r++) acc[r] = acc2[r] = 0.0f;
-    if (Ent.src == SRC_ACT) mv_dispatch<R, false>(Ent.W, a, row0, lane, acc, acc2);
-    else mv_dispatch<R, true>(Ent.W, a, row0, lane, acc, acc2);
-    const bool one = Ent.W.type == W_Q4_1 || Ent.W.type == W_Q5_1;
+    for (int u0 = 0; u0 < units; u0 += U) {
+        if (u0 > 0) {
+#pragma unroll
+            for (int u = 0; u < U; u++)
+#pragma unroll
+                for (int r = 0; r < R; r++) w[r][u] = load_unit<WF>(W, rows[r], u0 + u, lane);
+        }
+        AUnit x[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) x[u] = load_act_unit<WF, (E > 0)>(a, u0 + u, lane);
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            if (unit_valid<WF>(K, u0 + u, lane)) {
+#pragma unroll
+                for (int r = 0; r < R; r++) dot_unit<WF>(w[r][u], x[u], acc[r], acc2[r]);
+            }
+        }
+    }
+
+    // (5) reduce + epilogue
+    constexpr bool one = WF == W_Q4_1 || WF == W_Q5_1;
     if constexpr (!EMIT) {
 #pragma unroll
         for (int r = 0; r < R; r++) {
             const float s = one ? wave_sum63(acc[r]) + wave_sum63(acc2[r]) : wave_sum63(acc[r]) + 0.0f;
             const int row = row0 + r;
-            if (lane == 63 && row < Ent.W.M) Ent.y[row] = apply_epi_mv(Ent, row, s);
+            if (lane == 63 && row < M) Ent.y[row] = apply_epi_mv(Ent, row, s);
         }
     } else {
         // 4*R == 32 rows per workgroup: apply the epilogue and emit the 32 values as one
@@ -271,7 +319,7 @@ __global__ __launch_bounds__(256) void k_mv(MVGroup g) {
         if (tid < 32) {
             const int row = rowwg + tid;
             float vv = 0.0f;
-            if (row < Ent.W.M) {
+            if (row < M) {
                 vv = apply_epi_mv(Ent, row, red[tid]);
                 if (Ent.y) Ent.y[row] = vv;
             }
@@ -280,21 +328,59 @@ __global__ __launch_bounds__(256) void k_mv(MVGroup g) {
     }
 }
 
-template <int R, bool EMIT>
-static void launch_mv_e(hipStream_t st, MVGroup & g, int E, int blocks) {
-    dim3 grid(blocks), block(256);
+template <int R, int U, int E, bool EMIT>
+__global__ __launch_bounds__(256) void k_mv(MVGroup g) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    __shared__ double sh[8];
+    __shared__ float red[4 * R];
+    int e = 0;
+#pragma unroll 1
+    while (e + 1 < g.n && (int)blockIdx.x >= g.e[e + 1].block0) e++;
+    const MVEntry & Ent = g.e[e];
+    const int wgi = (int)blockIdx.x - Ent.block0;
+    switch (Ent.W.type) {
+        case W_F32: mv_body<W_F32, R, U, E, EMIT>(Ent, wgi, smem, sh, red); break;
+        case W_F16: mv_body<W_F16, R, U, E, EMIT>(Ent, wgi, smem, sh, red); break;
+        case W_Q4_0: mv_body<W_Q4_0, R, U, E, EMIT>(Ent, wgi, smem, sh, red); break;
+        case W_Q4_1: mv_body<W_Q4_1, R, U, E, EMIT>(Ent, wgi, smem, sh, red); break;
+        case W_Q5_0: mv_body<W_Q5_0, R, U, E, EMIT>(Ent, wgi, smem, sh, red); break;
+        case W_Q5_1: mv_body<W_Q5_1, R, U, E, EMIT>(Ent, wgi, smem, sh, red); break;
+        case W_Q8_0: mv_body<W_Q8_0, R, U, E, EMIT>(Ent, wgi, smem, sh, red); break;
+        default: break;
+    }
+}
+
+template <int R, int U, bool EMIT>
+static void launch_mv_u(hipStream_t st, MVGroup & g, int E, dim3 grid) {
+    dim3 block(256);
     switch (E) {
-        case 4: hipLaunchKernelGGL((k_mv<R, 4, EMIT>), grid, block, g.lds_bytes, st, g); break;
-        case 16: hipLaunchKernelGGL((k_mv<R, 16, EMIT>), grid, block, g.lds_bytes, st, g); break;
-        default: hipLaunchKernelGGL((k_mv<R, 32, EMIT>), grid, block, g.lds_bytes, st, g); break;
+        case 0: hipLaunchKernelGGL((k_mv<R, U, 0, EMIT>), grid, block, g.lds_bytes, st, g); break;
+        case 8: hipLaunchKernelGGL((k_mv<R, U, 8, EMIT>), grid, block, g.lds_bytes, st, g); break;
+        default: hipLaunchKernelGGL((k_mv<R, U, 32, EMIT>), grid, block, g.lds_bytes, st, g); break;
+    }
+}
+
+template <int R, bool EMIT>
+static void launch_mv_r(hipStream_t st, MVGroup & g, int U, int E, dim3 grid) {
+    switch (U) {
+        case 1: launch_mv_u<R, 1, EMIT>(st, g, E, grid); break;
+        case 2: launch_mv_u<R, 2, EMIT>(st, g, E, grid); break;
+        default: launch_mv_u<R, 4, EMIT>(st, g, E, grid); break;
     }
 }
 
 bool launch_mv_group(hipStream_t st, MVGroup & g) {
-    bool emit = false;
-    for (int i = 0; i < g.n; i++) emit |= g.e[i].emit != 0;
+    bool emit = false, prologue = false, plain = false;
+    for (int i = 0; i < g.n; i++) {
+        emit |= g.e[i].emit != 0;
+        (g.e[i].src == SRC_ACT ? plain : prologue) = true;
+    }
+    if (prologue && plain) {
+        fprintf(stderr, "rwkv: matvec group mixes activation and prologue sources\n");
+        return false;
+    }
     const int R = emit ? 8 : 2, RW = 4 * R;
-    int blocks = 0, lds = 0, kmax = 0;
+    int blocks = 0, lds = 0, kmax = 0, umax = 1;
     for (int i = 0; i < g.n; i++) {
         MVEntry & e = g.e[i];
         if (e.W.K % 32) {
@@ -305,8 +391,13 @@ bool launch_mv_group(hipStream_t st, MVGroup & g) {
             fprintf(stderr, "rwkv: emitting matvec needs M %% 32 == 0 (M=%d)\n", e.W.M);
             return false;
         }
+        if (e.src == SRC_ACT && (e.act.K != e.W.K || e.act.fmt != act_fmt_for(e.W.type))) {
+            fprintf(stderr, "rwkv: matvec input format/size mismatch (K=%d vs %d)\n", e.act.K, e.W.K);
+            return false;
+        }
         e.block0 = blocks;
         blocks += (e.W.M + RW - 1) / RW;
+        umax = std::max(umax, mv_units(e.W.type, e.W.K));
         if (e.src != SRC_ACT) {
             lds = std::max(lds, lds_bytes_for(act_fmt_for(e.W.type), e.W.K));
             kmax = std::max(kmax, e.W.K);
@@ -318,9 +409,17 @@ bool launch_mv_group(hipStream_t st, MVGroup & g) {
     }
     g.lds_bytes = lds;
     if (!blocks) return true;
-    const int E = kmax <= 1024 ? 4 : kmax <= 4096 ? 16 : 32;
-    if (emit) launch_mv_e<8, true>(st, g, E, blocks);
-    else launch_mv_e<2, false>(st, g, E, blocks);
+    const int E = !prologue ? 0 : kmax <= 8 * 256 ? 8 : 32;
+    const int U = umax <= 1 ? 1 : umax <= 2 ? 2 : 4;
+    if (emit) {
+        if (!prologue) {
+            fprintf(stderr, "rwkv: emitting matvec needs a prologue source\n");
+            return false;
+        }
+        launch_mv_r<8, true>(st, g, U, E, dim3(blocks));
+    } else {
+        launch_mv_r<2, false>(st, g, U, E, dim3(blocks));
+    }
     HIP_OK(hipGetLastError());
     return true;
 }
@@ -328,32 +427,24 @@ bool launch_mv_group(hipStream_t st, MVGroup & g) {
 // --------------------------------------------------------------------------- v6 mix5 (decode)
 struct Mix5Dec {
     int C, D;
-    const float * x, * carry, * lnw, * lnb, * lora, * w2t;
+    const float * xa, * carry, * lora, * w2t;
     const float * maa[5];
     ActBuf out[5];
 };
 
-// grid (C/256, 5): block (cx, n) computes mixed vector n for 256 channels.  w2t [5][D][C]
-// makes the per-channel D-long dots coalesced across lanes; accumulation order matches the
-// oracle (sequential over i, fp64).
-template <int E>
+// grid (C/256, 5): block (cx, n) computes mixed vector n for 256 channels from xa = LN(x),
+// which the preceding W1 matvec already wrote as the new att_xx carry.  w2t [5][D][C] makes
+// the per-channel D-long dots coalesced across lanes; accumulation order matches the oracle
+// (sequential over i, fp64).
 __global__ __launch_bounds__(256) void k_v6_mix5_dec(Mix5Dec a) {
-    __shared__ double sh[8];
     const int n = blockIdx.y, C = a.C, D = a.D;
-    float xv[E];
-    load_vec<E>(xv, a.x, C);
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool active = (int)(blockIdx.x * blockDim.x + (threadIdx.x & ~63)) < C;  // wave-uniform
+    if ((int)(blockIdx.x * blockDim.x + (threadIdx.x & ~31)) >= C) return;  // half-wave uniform
     float w2v[64];
-    const float * w2 = a.w2t + (size_t)n * D * C + (active ? c : 0);
+    const float * w2 = a.w2t + (size_t)n * D * C + c;
 #pragma unroll
     for (int i = 0; i < 64; i++) w2v[i] = (i < D) ? w2[(size_t)i * C] : 0.0f;
-    const float xc = active ? a.x[c] : 0.0f, cc = active ? a.carry[c] : 0.0f;
-    const float lw = active ? a.lnw[c] : 0.0f, lb = active ? a.lnb[c] : 0.0f, mu = active ? a.maa[n][c] : 0.0f;
-    float mean, scale;
-    ln_stats_reg<E>(xv, C, mean, scale, sh);
-    if (!active) return;
-    const float xa = ln_apply(xc, mean, scale, lw, lb);
+    const float xa = a.xa[c], cc = a.carry[c], mu = a.maa[n][c];
     const float sx = cc - xa;
     const float * lv = a.lora + n * D;
     double acc = 0.0;
@@ -364,42 +455,128 @@ __global__ __launch_bounds__(256) void k_v6_mix5_dec(Mix5Dec a) {
     emit32(a.out[n], 0, c, (m + mu) * sx + xa);
 }
 
-bool launch_v6_mix5_dec(hipStream_t st, int C, int D, const float * x, const float * carry, const float * lnw,
-                        const float * lnb, const float * lora, const float * w2t, const float * const * maa,
-                        const ActBuf * outs) {
+bool launch_v6_mix5_dec(hipStream_t st, int C, int D, const float * xa, const float * carry, const float * lora,
+                        const float * w2t, const float * const * maa, const ActBuf * outs) {
     Mix5Dec a;
     a.C = C;
     a.D = D;
-    a.x = x;
+    a.xa = xa;
     a.carry = carry;
-    a.lnw = lnw;
-    a.lnb = lnb;
     a.lora = lora;
     a.w2t = w2t;
     for (int n = 0; n < 5; n++) {
         a.maa[n] = maa[n];
         a.out[n] = outs[n];
     }
-    if (D > 64 || C > 32 * 256) {
+    if (D > 64 || C % 32) {
         fprintf(stderr, "rwkv: v6 maa LoRA width %d / n_embed %d unsupported\n", D, C);
         return false;
     }
     dim3 grid((C + 255) / 256, 5);
-    if (C <= 1024) hipLaunchKernelGGL(k_v6_mix5_dec<4>, grid, dim3(256), 0, st, a);
-    else if (C <= 4096) hipLaunchKernelGGL(k_v6_mix5_dec<16>, grid, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL(k_v6_mix5_dec<32>, grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_v6_mix5_dec, grid, dim3(256), 0, st, a);
     HIP_OK(hipGetLastError());
     return true;
 }
 
 // --------------------------------------------------------------------------- v5/v6 attention (decode)
-template <int IPG>
+// wave_sum63's fixed tree applied to partials held by one thread: p[l] is what lane l of the
+// batched kernel (k_mm) accumulates for a row whose units fit in lanes 0..31 (one unit each).
+__device__ __forceinline__ float tree16(const float * p) {
+    const float q0 = (p[0] + p[1]) + (p[2] + p[3]);
+    const float q1 = (p[4] + p[5]) + (p[6] + p[7]);
+    const float q2 = (p[8] + p[9]) + (p[10] + p[11]);
+    const float q3 = (p[12] + p[13]) + (p[14] + p[15]);
+    return (q0 + q1) + (q2 + q3);
+}
+__device__ __forceinline__ float tree_wave32(const float (&p)[32]) {
+    const float r0 = tree16(p), r1 = tree16(p + 16);
+    return (0.0f + 0.0f) + (r1 + r0);
+}
+
+// One row of the v6 decay LoRA tail by one thread (units <= 32, one per lane of k_mm);
+// PF units were prefetched into wp[].
+template <int WF, int PF>
+__device__ __forceinline__ float decay_row_thread(const DMat & W, int row, const ActBuf & act, int nl,
+                                                  const WBlk (&wp)[PF > 0 ? PF : 1]) {
+    float p[32], p2[32];
+#pragma unroll
+    for (int l = 0; l < 32; l++) {
+        p[l] = p2[l] = 0.0f;
+        if (l < nl) {
+            const WBlk w = (l < PF) ? wp[l < PF ? l : 0] : load_unit<WF>(W, row, 0, l);
+            const AUnit x = load_act_unit<WF, true>(act, 0, l);
+            dot_unit<WF>(w, x, p[l], p2[l]);
+        }
+    }
+    constexpr bool one = WF == W_Q4_1 || WF == W_Q5_1;
+    return one ? tree_wave32(p) + tree_wave32(p2) : tree_wave32(p) + 0.0f;
+}
+
+// One row by one wave, exactly k_mm's loop (any K).
+template <int WF>
+__device__ __forceinline__ float decay_row_wave(const DMat & W, int row, const ActBuf & act, int lane) {
+    float acc = 0.0f, acc2 = 0.0f;
+    const int units = mv_units(WF, W.K);
+    for (int u = 0; u < units; u++) {
+        const WBlk w = load_unit<WF>(W, row, u, lane);
+        const AUnit x = load_act_unit<WF, true>(act, u, lane);
+        if (unit_valid<WF>(W.K, u, lane)) dot_unit<WF>(w, x, acc, acc2);
+    }
+    constexpr bool one = WF == W_Q4_1 || WF == W_Q5_1;
+    return one ? wave_sum63(acc) + wave_sum63(acc2) : wave_sum63(acc) + 0.0f;
+}
+
+// lanes of k_mm that hold a unit of a K-long row, when each holds at most one; else 0
+__host__ __device__ inline int one_unit_lanes(int type, int K) {
+    const int per = type == W_F32 ? 4 : type == W_F16 ? 8 : 32;
+    const int n = K / per;
+    return n <= 64 ? n : 0;
+}
+
+template <int WF>
+__device__ __forceinline__ void decay_rows(const Att6Dec & a, const ActBuf & act, float * sw, int c0, int S) {
+    const int tid = threadIdx.x;
+    const int nl = one_unit_lanes(WF, a.wd2.K);
+    if (nl > 0 && nl <= 32) {
+        const WBlk none[1] = {};
+        if (tid < S) {
+            const float s = decay_row_thread<WF, 0>(a.wd2, c0 + tid, act, nl, none);
+            sw[tid] = expf(-expf(s + a.decay[c0 + tid]));
+        }
+    } else {
+        const int lane = tid & 63, nw = blockDim.x >> 6;
+        for (int j = tid >> 6; j < S; j += nw) {
+            const float s = decay_row_wave<WF>(a.wd2, c0 + j, act, lane);
+            if (lane == 63) sw[j] = expf(-expf(s + a.decay[c0 + j]));
+        }
+    }
+}
+
+// One workgroup per head, S*G threads (G = min(256/S, S), as the sequence kernel k_wkv6):
+// thread (j = tid % S, g = tid / S) owns state column j for keys i in [g*IPG, (g+1)*IPG) --
+// each state load/store instruction covers S consecutive floats.  The per-thread partial y
+// sums meet in LDS and are folded with group_sum's butterfly tree, so decode and sequence
+// agree bit for bit.  PF > 0: quantized decay LoRA with <= PF units per row, prefetched.
+template <int WF, int PF>
 __global__ __launch_bounds__(256) void k_att6_dec(Att6Dec a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    __shared__ float sr[64], sk[64], sv[64], sw[64], su[64], sy[64];
-    const int h = blockIdx.x, S = a.S, G = S / IPG, C = a.H * S;
-    const int tid = threadIdx.x;
-    const int c0 = h * S;
+    __shared__ float sr[64], sk[64], sv[64], sw[64], su[64];
+    __shared__ float part[16][64];
+    const int h = blockIdx.x, S = a.S, G = min(256 / S, S), IPG = S / G;
+    const int tid = threadIdx.x, j = tid % S, g = min(tid / S, G - 1), c0 = h * S;
+    const bool active = tid < S * G;
+    const size_t hb = (size_t)h * S * S;
+    float st[16];
+#pragma unroll
+    for (int ii = 0; ii < 16; ii++)
+        st[ii] = ii < IPG && active ? a.sin[hb + (size_t)(g * IPG + ii) * S + j] : 0.0f;
+    WBlk wp[PF > 0 ? PF : 1];
+    if constexpr (PF > 0) {
+        const int nb = a.wd2.K >> 5;
+        const int row = c0 + min(tid, S - 1);
+#pragma unroll
+        for (int l = 0; l < PF; l++) wp[l] = load_wblk<WF>(a.wd2, (size_t)row * nb + min(l, nb - 1));
+    }
     if (tid < S) {
         sr[tid] = a.r[c0 + tid];
         sk[tid] = a.k[c0 + tid];
@@ -407,96 +584,66 @@ __global__ __launch_bounds__(256) void k_att6_dec(Att6Dec a) {
         su[tid] = a.u[c0 + tid];
         if (a.w) sw[tid] = a.w[c0 + tid];
     }
+    ActBuf act;
     if (!a.w) {
         // v6 decay LoRA tail: w = exp(-exp(Wd2 . dl + decay)), rwkv_graph.inc:357-367
         const int D = a.wd2.K;
-        ActBuf act = lds_act(smem, act_fmt_for(a.wd2.type), D);
+        act = lds_act(smem, act_fmt_for(a.wd2.type), D);
         for (int k0 = 0; k0 < D; k0 += blockDim.x) {
-            const int k = k0 + tid;
             if (k0 + (tid & ~31) >= D) continue;
-            emit32(act, 0, k, a.dl[k]);
-        }
-        __syncthreads();
-        // rows of Wd2 for this head, one wave per group of rows, lanes over the K blocks with
-        // all rows' weight blocks loaded first; reduced with wave_sum63 exactly like the
-        // batched matmul kernel (k_mm, T > 1) so serial and sequence stay bit-identical.
-        const int nbk = a.wd2.type <= W_F16 ? 0 : D / 32;
-        if (nbk > 0 && nbk <= 64) {
-            const int lane = tid & 63, nw = blockDim.x >> 6;
-            const int rpw = (S + nw - 1) / nw;  // rows per wave (<= 64)
-            const int jbase = (tid >> 6) * rpw;
-            for (int jj = 0; jj < rpw; jj += 16) {
-                float p[16], p2[16];
-#pragma unroll
-                for (int q = 0; q < 16; q++) p[q] = p2[q] = 0.0f;
-                if (lane < nbk) {
-                    const int4 * ap = (const int4 *)(act.q + (size_t)lane * 32);
-                    const int4 alo = ap[0], ahi = ap[1];
-                    const float dx = act.d[lane];
-                    const int qs = act.qsum[lane];
-                    const float sx = act.fmt == A_Q8_1 ? act.s[lane] : 0.0f;
-#pragma unroll
-                    for (int q = 0; q < 16; q++) {
-                        const int j = min(jbase + jj + q, S - 1);
-                        float dw = 0.0f, mw = 0.0f;
-                        int sumi = 0;
-                        const int row = c0 + j;
-                        switch (a.wd2.type) {
-                            case W_Q4_0: sumi = block_dot<W_Q4_0>(a.wd2, row, lane, nbk, alo, ahi, qs, dw, mw); break;
-                            case W_Q4_1: sumi = block_dot<W_Q4_1>(a.wd2, row, lane, nbk, alo, ahi, qs, dw, mw); break;
-                            case W_Q5_0: sumi = block_dot<W_Q5_0>(a.wd2, row, lane, nbk, alo, ahi, qs, dw, mw); break;
-                            case W_Q5_1: sumi = block_dot<W_Q5_1>(a.wd2, row, lane, nbk, alo, ahi, qs, dw, mw); break;
-                            case W_Q8_0: sumi = block_dot<W_Q8_0>(a.wd2, row, lane, nbk, alo, ahi, qs, dw, mw); break;
-                            default: break;
-                        }
-                        p[q] = fmaf(dw * dx, (float)sumi, 0.0f);
-                        p2[q] = 0.0f + mw * sx;
-                    }
-                }
-                const bool one = act.fmt == A_Q8_1;
-#pragma unroll
-                for (int q = 0; q < 16; q++) {
-                    const float sum = one ? wave_sum63(p[q]) + wave_sum63(p2[q]) : wave_sum63(p[q]) + 0.0f;
-                    const int j = jbase + jj + q;
-                    if (lane == 63 && j < S && jj + q < rpw) sw[j] = expf(-expf(sum + a.decay[c0 + j]));
-                }
-            }
-        } else {
-            // F32 / F16 decay LoRA (FP16 checkpoints keep time_decay_w2 in FP32): one wave per row
-            const int lane = tid & 63, nw = blockDim.x >> 6;
-            for (int j = tid >> 6; j < S; j += nw) {
-                float acc[1] = {0.0f}, acc2[1] = {0.0f};
-                const int row = c0 + j;
-                if (a.wd2.type == W_F32) mv_accumulate<W_F32, 1, false>(a.wd2, act, row, lane, acc, acc2);
-                else mv_accumulate<W_F16, 1, false>(a.wd2, act, row, lane, acc, acc2);
-                const float sum = wave_sum63(acc[0]) + 0.0f;
-                if (lane == 63) sw[j] = expf(-expf(sum + a.decay[row]));
-            }
+            emit32(act, 0, k0 + tid, a.dl[k0 + tid]);
         }
     }
     __syncthreads();
-    // wkv6 for one token (ggml_rwkv_wkv6 semantics): lane group (j, g), g splits the keys i
-    if (tid < S * G) {
-        const int j = tid / G, g = tid % G;
-        const size_t hb = (size_t)h * S * S;
+    if (!a.w) {
+        if constexpr (PF > 0) {
+            if (tid < S) {
+                const float s = decay_row_thread<WF, PF>(a.wd2, c0 + tid, act, a.wd2.K >> 5, wp);
+                sw[tid] = expf(-expf(s + a.decay[c0 + tid]));
+            }
+        } else {
+            switch (a.wd2.type) {
+                case W_F32: decay_rows<W_F32>(a, act, sw, c0, S); break;
+                case W_F16: decay_rows<W_F16>(a, act, sw, c0, S); break;
+                case W_Q4_0: decay_rows<W_Q4_0>(a, act, sw, c0, S); break;
+                case W_Q4_1: decay_rows<W_Q4_1>(a, act, sw, c0, S); break;
+                case W_Q5_0: decay_rows<W_Q5_0>(a, act, sw, c0, S); break;
+                case W_Q5_1: decay_rows<W_Q5_1>(a, act, sw, c0, S); break;
+                case W_Q8_0: decay_rows<W_Q8_0>(a, act, sw, c0, S); break;
+                default: break;
+            }
+        }
+        __syncthreads();
+    }
+    // wkv6 for one token (ggml_rwkv_wkv6 semantics, same arithmetic as k_wkv6)
+    if (active) {
         const float vj = sv[j];
         float acc = 0.0f;
 #pragma unroll
-        for (int ii = 0; ii < IPG; ii++) {
-            const int i = g * IPG + ii;
-            const float prev = a.sin[hb + (size_t)i * S + j];
-            const float kv = vj * sk[i];
-            const float temp = kv * su[i] + prev;
-            acc += temp * sr[i];
-            a.sout[hb + (size_t)i * S + j] = prev * sw[i] + kv;
+        for (int ii = 0; ii < 16; ii++) {
+            if (ii < IPG) {
+                const int i = g * IPG + ii;
+                const float prev = st[ii];
+                const float kv = vj * sk[i];
+                const float temp = kv * su[i] + prev;
+                acc += temp * sr[i];
+                a.sout[hb + (size_t)i * S + j] = prev * sw[i] + kv;
+            }
         }
-        acc = group_sum(acc, G);
-        if (g == 0) sy[j] = acc;
+        part[g][j] = acc;
     }
     __syncthreads();
     // GroupNorm over the head (ggml_norm, fp64 sums) * ln_x (+ b) (* g)
     if (tid < S) {
-        const float x = sy[tid];
+        float p[16];
+#pragma unroll
+        for (int q = 0; q < 16; q++) p[q] = q < G ? part[q][tid] : 0.0f;
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1)
+            if (o < G)
+#pragma unroll
+                for (int q = 0; q < o; q++) p[q] = p[q] + p[q + o];
+        const float x = p[0];
         const double s = group_sum((double)x, S);
         const float mean = (float)(s / (double)S);
         const float d = x - mean;
@@ -509,7 +656,6 @@ __global__ __launch_bounds__(256) void k_att6_dec(Att6Dec a) {
         if (a.g) o = o * a.g[c0 + tid];
         a.y[c0 + tid] = o;
     }
-    (void)C;
 }
 
 bool launch_att6_dec(hipStream_t st, const Att6Dec & a) {
@@ -519,23 +665,28 @@ bool launch_att6_dec(hipStream_t st, const Att6Dec & a) {
     }
     int G = 256 / a.S;
     if (G > a.S) G = a.S;
-    const int IPG = a.S / G;
-    int threads = a.S * G;
+    const int threads = a.S * G;
     int lds = 0;
     if (!a.w) {
         const int D = a.wd2.K;
-        threads = std::max(threads, (D + 63) / 64 * 64);
+        if (D % 32) {
+            fprintf(stderr, "rwkv: v6 decay LoRA width %d unsupported\n", D);
+            return false;
+        }
         lds = lds_bytes_for(act_fmt_for(a.wd2.type), D);
     }
-    threads = std::min(std::max(threads, 64), 256);
-    dim3 grid(a.H), block(threads);
-    switch (IPG) {
-        case 1: hipLaunchKernelGGL(k_att6_dec<1>, grid, block, lds, st, a); break;
-        case 2: hipLaunchKernelGGL(k_att6_dec<2>, grid, block, lds, st, a); break;
-        case 4: hipLaunchKernelGGL(k_att6_dec<4>, grid, block, lds, st, a); break;
-        case 8: hipLaunchKernelGGL(k_att6_dec<8>, grid, block, lds, st, a); break;
-        case 16: hipLaunchKernelGGL(k_att6_dec<16>, grid, block, lds, st, a); break;
-        default: return false;
+    dim3 grid(a.H), block(std::max(threads, 64));
+    const bool pf = !a.w && a.wd2.type >= W_Q4_0 && (a.wd2.K >> 5) <= 4;
+    if (!pf) {
+        hipLaunchKernelGGL((k_att6_dec<-1, 0>), grid, block, lds, st, a);
+    } else {
+        switch (a.wd2.type) {
+            case W_Q4_0: hipLaunchKernelGGL((k_att6_dec<W_Q4_0, 4>), grid, block, lds, st, a); break;
+            case W_Q4_1: hipLaunchKernelGGL((k_att6_dec<W_Q4_1, 4>), grid, block, lds, st, a); break;
+            case W_Q5_0: hipLaunchKernelGGL((k_att6_dec<W_Q5_0, 4>), grid, block, lds, st, a); break;
+            case W_Q5_1: hipLaunchKernelGGL((k_att6_dec<W_Q5_1, 4>), grid, block, lds, st, a); break;
+            default: hipLaunchKernelGGL((k_att6_dec<W_Q8_0, 4>), grid, block, lds, st, a); break;
+        }
     }
     HIP_OK(hipGetLastError());
     return true;

@@ -16,6 +16,9 @@ if len(idx) > 40:
     busy = sum(int(r['End_Timestamp']) - int(r['Start_Timestamp']) for r in tr[a:b]) / 1e3
     print(f'one decode token: {b - a} kernels, span {span:.1f} us, kernel-busy {busy:.1f} us')
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 12
-    for r in tr[a:a + n]:
+    for r in tr[a:a + n] + [None] + tr[b - 3:b]:
+        if r is None:
+            print('  ...')
+            continue
         s, e = int(r['Start_Timestamp']), int(r['End_Timestamp'])
         print(f"  {r['Kernel_Name'][:56]:56s} {(e - s) / 1e3:8.2f}us grid {r['Grid_Size_X']:>7} vgpr {r['VGPR_Count']}")

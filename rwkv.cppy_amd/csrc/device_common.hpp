@@ -80,10 +80,63 @@ __device__ __forceinline__ float siluf_(float x) { return x / (1.0f + expf(-x));
 __device__ __forceinline__ float h2f(uint16_t b) { return __half2float(__ushort_as_half(b)); }
 __device__ __forceinline__ float f16_round(float f) { return __half2float(__float2half(f)); }
 
+// Reductions across each 32-lane half-wave (all lanes get the result): DPP inside the 16-lane
+// rows, then v_permlane16_swap between the two rows of the half.  Max and integer sums are
+// order-independent, so these are exact.
+template <int CTRL>
+__device__ __forceinline__ int dpp_mov(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+__device__ __forceinline__ float half_max(float v) {
+    v = fmaxf(v, __int_as_float(dpp_mov<0xB1>(__float_as_int(v))));
+    v = fmaxf(v, __int_as_float(dpp_mov<0x4E>(__float_as_int(v))));
+    v = fmaxf(v, __int_as_float(dpp_mov<0x141>(__float_as_int(v))));
+    v = fmaxf(v, __int_as_float(dpp_mov<0x140>(__float_as_int(v))));
+    const auto p = __builtin_amdgcn_permlane16_swap(__float_as_int(v), __float_as_int(v), false, false);
+    return fmaxf(__int_as_float(p[0]), __int_as_float(p[1]));
+}
+__device__ __forceinline__ int half_sum_i(int v) {
+    v += dpp_mov<0xB1>(v);
+    v += dpp_mov<0x4E>(v);
+    v += dpp_mov<0x141>(v);
+    v += dpp_mov<0x140>(v);
+    const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return p[0] + p[1];
+}
+
+// ggml quantize_row_q8_0 / q8_1 (x86) of one 32-block held one element per lane of a
+// half-wave: d = amax/127 (fp16), q = rint(x * 127/amax), sum = sum q.  Pure (no stores), so
+// several blocks can be quantized in flight before any is written.
+struct Q32 {
+    int q;
+    float d;
+    int sum;
+};
+__device__ __forceinline__ Q32 quant32(float v) {
+    const float am = half_max(fabsf(v));
+    const float id = (am != 0.0f) ? 127.f / am : 0.0f;
+    Q32 r;
+    r.q = (int)rintf(v * id);
+    r.d = am / 127.f;
+    r.sum = half_sum_i(r.q);
+    return r;
+}
+
+// Store element k of row t (and, from the block's first lane, its scales).
+__device__ __forceinline__ void store32(const ActBuf & a, int t, int k, const Q32 & r) {
+    const size_t idx = (size_t)t * a.K + k;
+    a.q[idx] = (int8_t)r.q;
+    if ((k & 31) == 0) {
+        const size_t bi = (size_t)t * (a.K >> 5) + (k >> 5);
+        a.d[bi] = f16_round(r.d);
+        a.qsum[bi] = r.sum;
+        if (a.fmt == A_Q8_1) a.s[bi] = f16_round(r.d * (float)r.sum);
+    }
+}
+
 // Emit one element per lane into an activation buffer.  The 32 lanes of each half-wave must
 // hold the 32 consecutive elements of one block (k & 31 == lane & 31) of the same row t, and
-// all 32 must call (block-uniform control flow).  Mirrors ggml quantize_row_q8_0/q8_1 (x86):
-// d = amax/127 (fp16), q = rint(x * 127/amax), s = fp16(d * sum q).
+// all 32 must call (block-uniform control flow).
 __device__ __forceinline__ void emit32(const ActBuf & a, int t, int k, float v) {
     const size_t idx = (size_t)t * a.K + k;
     if (a.fmt == A_F32) {
@@ -94,22 +147,7 @@ __device__ __forceinline__ void emit32(const ActBuf & a, int t, int k, float v) 
         a.h[idx] = __float2half(v);
         return;
     }
-    float am = fabsf(v);
-#pragma unroll
-    for (int o = 16; o > 0; o >>= 1) am = fmaxf(am, __shfl_xor(am, o, 32));
-    const float d = am / 127.f;
-    const float id = (am != 0.0f) ? 127.f / am : 0.0f;
-    const int q = (int)rintf(v * id);
-    int sum = q;
-#pragma unroll
-    for (int o = 16; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 32);
-    a.q[idx] = (int8_t)q;
-    if ((k & 31) == 0) {
-        const size_t bi = (size_t)t * (a.K >> 5) + (k >> 5);
-        a.d[bi] = f16_round(d);
-        a.qsum[bi] = sum;
-        if (a.fmt == A_Q8_1) a.s[bi] = f16_round(d * (float)sum);
-    }
+    store32(a, t, k, quant32(v));
 }
 
 // --------------------------------------------------------------------------- matmul
@@ -235,19 +273,81 @@ __device__ __forceinline__ float apply_epi(const MMEntry & E, int t, int row, fl
 
 
 // ggml_norm statistics with double accumulation (mean, 1/sqrt(var + eps))
-__device__ inline void ln_stats(const float * x, int C, float eps, float & mean, float & scale, double * sh) {
-    double s = 0.0;
-    for (int c = threadIdx.x; c < C; c += blockDim.x) s += (double)x[c];
-    s = block_sum_d(s, sh);
-    mean = (float)(s / (double)C);
-    double s2 = 0.0;
-    for (int c = threadIdx.x; c < C; c += blockDim.x) {
-        const float v = x[c] - mean;
-        s2 += (double)(v * v);
+// Sum across the wave, result broadcast to every lane.
+__device__ __forceinline__ double wave_allsum_d(double v) {
+    v = wave_sum63_d(v);
+    const long long b = __builtin_bit_cast(long long, v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), 63);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
+// LayerNorm statistics of x[0..K) by ONE wave, no LDS and no barrier (ggml_norm semantics:
+// fp64 sums, two passes, population variance).  Lane l owns x[l + 64 j] (coalesced loads),
+// summed into four fp64 partials (j % 4) combined as (p0+p1)+(p2+p3), then wave_sum63_d.
+// Every LayerNorm on the device (decode prologues, sequence kernels) uses this one
+// association, so decode and sequence agree bit for bit.  Requires K % 64 == 0,
+// K <= 64*PMAX, all lanes active.
+template <int PC>
+__device__ __forceinline__ void ln_stats_wave(const float * x, int K, float eps, float & mean, float & scale) {
+    const int lane = threadIdx.x & 63, P = K >> 6;
+    double p[4] = {0.0, 0.0, 0.0, 0.0}, q[4] = {0.0, 0.0, 0.0, 0.0};
+    if (P <= PC) {
+        // one chunk: the second pass reuses the registers
+        float v[PC];
+#pragma unroll
+        for (int j = 0; j < PC; j++) v[j] = x[lane + 64 * min(j, P - 1)];
+#pragma unroll
+        for (int j = 0; j < PC; j++)
+            if (j < P) p[j & 3] += (double)v[j];
+        const double s = wave_allsum_d((p[0] + p[1]) + (p[2] + p[3]));
+        mean = (float)(s / (double)K);
+#pragma unroll
+        for (int j = 0; j < PC; j++)
+            if (j < P) {
+                const float d = v[j] - mean;
+                q[j & 3] += (double)(d * d);
+            }
+    } else {
+        // chunks of PC elements per lane, reloaded for the second pass (same association)
+        for (int j0 = 0; j0 < P; j0 += PC) {
+            float v[PC];
+#pragma unroll
+            for (int j = 0; j < PC; j++) v[j] = x[lane + 64 * min(j0 + j, P - 1)];
+#pragma unroll
+            for (int j = 0; j < PC; j++)
+                if (j0 + j < P) p[j & 3] += (double)v[j];
+        }
+        const double s = wave_allsum_d((p[0] + p[1]) + (p[2] + p[3]));
+        mean = (float)(s / (double)K);
+        for (int j0 = 0; j0 < P; j0 += PC) {
+            float v[PC];
+#pragma unroll
+            for (int j = 0; j < PC; j++) v[j] = x[lane + 64 * min(j0 + j, P - 1)];
+#pragma unroll
+            for (int j = 0; j < PC; j++)
+                if (j0 + j < P) {
+                    const float d = v[j] - mean;
+                    q[j & 3] += (double)(d * d);
+                }
+        }
     }
-    s2 = block_sum_d(s2, sh);
-    const float var = (float)(s2 / (double)C);
+    const double s2 = wave_allsum_d((q[0] + q[1]) + (q[2] + q[3]));
+    const float var = (float)(s2 / (double)K);
     scale = 1.0f / sqrtf(var + eps);
+}
+
+// PC (elements per lane held at once) is a multiple of 4, so chunking keeps the j % 4
+// association of the partials.
+__device__ __forceinline__ void ln_stats_any(const float * x, int K, float eps, float & mean, float & scale) {
+    ln_stats_wave<32>(x, K, eps, mean, scale);
+}
+
+// Block-level entry point kept for the sequence kernels: every wave computes the same
+// statistics itself (sh unused).
+__device__ inline void ln_stats(const float * x, int C, float eps, float & mean, float & scale, double * sh) {
+    (void)sh;
+    ln_stats_any(x, C, eps, mean, scale);
 }
 
 __device__ __forceinline__ float ln_apply(float x, float mean, float scale, float w, float b) {

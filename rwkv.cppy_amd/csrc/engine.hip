@@ -273,6 +273,11 @@ Engine::~Engine() {
 
 bool Engine::init() {
     HIP_OK(hipSetDevice(m_->device));
+    {
+        int cus = 0;
+        HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, m_->device));
+        set_mv_device_cus(cus);
+    }
     HIP_OK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     HIP_OK(hipEventCreateWithFlags(&tok_event_, hipEventDisableTiming));
     HIP_OK(hipEventRecord(tok_event_, stream_));
@@ -824,6 +829,22 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits) {
         const DLayer & L = m_->layers[l];
         const float * si = sin + l * per_layer;
         float * so = sout + l * per_layer;
+        // Wo matvec: input emitted by the attention kernel in Wo's format when heads are
+        // whole 32-blocks, else read as fp32 by its own prologue
+        MV c_wo;
+        auto att_out = [&](auto & a, MV & wo, const DMat & Wo) {
+            MVEntry & e = wo.add(Wo, x_, EPI_ADD);
+            a.yq.fmt = -1;
+            a.y = y_;
+            if (S >= 32) {
+                a.yq = A(6, Wo);
+                e.src = SRC_ACT;
+                e.act = a.yq;
+            } else {
+                src_f32(e, y_);
+            }
+            return true;
+        };
         // ---------------- time mixing ----------------
         if (m_->major == 4) {
             MV b;
@@ -861,11 +882,9 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits) {
             a.lnx_w = L.att_lnx_w;
             a.lnx_b = L.att_lnx_b;
             a.eps = 1e-5f;
-            a.y = y_;
+            if (!att_out(a, c_wo, L.att_o)) return false;
             if (!launch_att6_dec(stream_, a)) return false;
-            MV c;
-            src_f32(c.add(L.att_o, x_, EPI_ADD), y_);
-            if (!mv(c.g)) return false;
+            if (!mv(c_wo.g)) return false;
         } else if (m_->major == 6) {
             const int D = m_->maa_D;
             MV b;
@@ -903,11 +922,9 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits) {
             a.lnx_w = L.att_lnx_w;
             a.lnx_b = L.att_lnx_b;
             a.eps = 64e-5f;
-            a.y = y_;
+            if (!att_out(a, c_wo, L.att_o)) return false;
             if (!launch_att6_dec(stream_, a)) return false;
-            MV d;
-            src_f32(d.add(L.att_o, x_, EPI_ADD), y_);
-            if (!mv(d.g)) return false;
+            if (!mv(c_wo.g)) return false;
         } else {
             // v7, order r, w, k, v, a, g of x_rwkvag (rwkv_graph.inc:404-413)
             MV b;
@@ -944,11 +961,9 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits) {
             a.sout = so + 2 * C;
             a.lnx_w = L.att_lnx_w;
             a.lnx_b = L.att_lnx_b;
-            a.y = y_;
+            if (!att_out(a, c_wo, L.att_o)) return false;
             if (!launch_att7_dec(stream_, a)) return false;
-            MV d;
-            src_f32(d.add(L.att_o, x_, EPI_ADD), y_);
-            if (!mv(d.g)) return false;
+            if (!mv(c_wo.g)) return false;
         }
         // ---------------- channel mixing ----------------
         if (m_->major == 7) {

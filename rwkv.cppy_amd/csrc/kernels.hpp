@@ -105,7 +105,10 @@ struct MVGroup {
     MVEntry e[MM_MAX_ENTRIES];
     int n;
     int lds_bytes;
+    int stride;              // set by launch_mv_group: >0 = workgroups walk row blocks
 };
+
+void set_mv_device_cus(int n);
 
 bool launch_mv_group(hipStream_t st, MVGroup & g);
 
@@ -129,6 +132,7 @@ struct Att6Dec {
     const float * lnx_w, * lnx_b;
     float eps;
     float * y;
+    ActBuf yq;               // fmt >= 0 (needs S >= 32): emit y in the Wo input format instead
 };
 bool launch_att6_dec(hipStream_t st, const Att6Dec & a);
 
@@ -142,6 +146,7 @@ struct Att7Dec {
     float * sout;
     const float * lnx_w, * lnx_b;
     float * y;
+    ActBuf yq;               // fmt >= 0 (needs S >= 32): emit y in the Wo input format instead
 };
 bool launch_att7_dec(hipStream_t st, const Att7Dec & a);
 

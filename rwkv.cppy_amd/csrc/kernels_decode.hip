@@ -13,27 +13,18 @@
 
 namespace rwkvmi {
 
-__device__ __forceinline__ float apply_epi_mv(const MVEntry & E, int row, float acc) {
-    switch (E.epi) {
-        case EPI_SIGMOID: return sigmoidf_(acc);
-        case EPI_TANH: return tanhf(acc);
-        case EPI_SILU: return siluf_(acc);
-        case EPI_RELU_SQ: {
-            const float r = acc > 0.0f ? acc : 0.0f;
-            return r * r;
-        }
-        case EPI_ADD: return E.y[row] + acc;
-        case EPI_SIGMUL_ADD: return E.y[row] + sigmoidf_(E.aux[row]) * acc;
-        case EPI_DECAY6: return expf(-expf(acc + E.bias[row]));
-        case EPI_DECAY7: return expf(sigmoidf_(acc + E.bias[row]) * -0.606531f);
-        case EPI_SIGMOID_BIAS: return sigmoidf_(acc + E.bias[row]);
-        case EPI_VMIX7: {
-            const float v = E.y[row];
-            return v + (E.aux[row] - v) * sigmoidf_(acc + E.bias[row]);
-        }
-        default: return acc;
-    }
-}
+// Phase timestamps for tools/mv_probe.hip (never defined in the library build).
+#ifdef MV_PROBE
+__device__ unsigned long long * g_probe;
+#define PROBE(k)                                                                               \
+    do {                                                                                       \
+        if (threadIdx.x == 0 && g_probe) g_probe[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define PROBE(k) \
+    do {         \
+    } while (0)
+#endif
 
 // LDS image of one activation row in the consumer's format.
 __device__ __forceinline__ ActBuf lds_act(char * smem, int fmt, int K) {
@@ -181,191 +172,317 @@ __device__ __forceinline__ void dot_unit(const WBlk & w, const AUnit & x, float 
     }
 }
 
-// Per-thread register image of a K-vector: thread t owns k = i*256 + t (i < E).
-template <int E>
+// Per-thread register image of a K-vector: thread t owns k = i*NT + t (i < E).
+template <int E, int NT = 256>
 __device__ __forceinline__ void load_vec(float (&v)[E], const float * p, int K) {
 #pragma unroll
     for (int i = 0; i < E; i++) {
-        const int k = i * 256 + (int)threadIdx.x;
-        v[i] = (k < K) ? p[k] : 0.0f;
+        // unconditional (clamped) loads: no per-load branches, so the waitcnt pass keeps
+        // them all in flight
+        const int k = i * NT + (int)threadIdx.x;
+        const float t = p[min(k, K - 1)];
+        v[i] = (k < K) ? t : 0.0f;
     }
 }
 
-// LayerNorm statistics of the register image (ggml_norm: fp64 sums, two passes).
-template <int E>
-__device__ __forceinline__ void ln_stats_reg(const float (&xv)[E], int K, float & mean, float & scale, double * sh) {
-    double s = 0.0;
-#pragma unroll
-    for (int i = 0; i < E; i++)
-        if (i * 256 + (int)threadIdx.x < K) s += (double)xv[i];
-    s = block_sum_d(s, sh);
-    mean = (float)(s / (double)K);
-    double s2 = 0.0;
-#pragma unroll
-    for (int i = 0; i < E; i++)
-        if (i * 256 + (int)threadIdx.x < K) {
-            const float d = xv[i] - mean;
-            s2 += (double)(d * d);
-        }
-    s2 = block_sum_d(s2, sh);
-    scale = 1.0f / sqrtf((float)(s2 / (double)K) + 1e-5f);
-}
-
-// One workgroup = 4 waves x R rows.  E == 0: the input is an activation buffer in global
-// memory (SRC_ACT); E > 0: the prologue builds it in LDS (SRC_F32 / SRC_LNMIX, K <= 256*E).
-template <int WF, int R, int U, int E, bool EMIT>
-__device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, char * smem, double * sh, float * red) {
-    constexpr int EE = E > 0 ? E : 1;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const DMat & W = Ent.W;
-    const int M = W.M, K = W.K;
-    const int rowwg = wgi * 4 * R, row0 = rowwg + wave * R;
-    int rows[R];
-#pragma unroll
-    for (int r = 0; r < R; r++) rows[r] = min(row0 + r, M - 1);
-    const int units = mv_units(WF, K);
-
-    // (1) prologue inputs: small fp32 vectors, L2-resident
-    float xv[EE], lw[EE], lb[EE], cv[EE], mv[EE];
-    if constexpr (E > 0) {
-        if (Ent.src == SRC_F32) {
-            load_vec<EE>(xv, Ent.f, K);
+// Matvec prologue (SRC_F32 / SRC_LNMIX): the waves of a workgroup build the activation image
+// in LDS chunk by chunk (512 elements per wave-chunk, 8 consecutive elements per lane, so a
+// quantization block is one lane quad): token-shift mix of the LayerNorm output, then ggml's
+// Q8 quantization with quad DPP reductions (F16: packed halves, F32: as is).
+template <int WF>
+__device__ __forceinline__ void prologue_chunks(const MVEntry & E, const ActBuf & a, float mean, float scale,
+                                                bool write_carry, int wave, int nw, int lane) {
+    const int K = E.W.K;
+    for (int c = wave; c * 512 < K; c += nw) {
+        const int k0 = c * 512 + lane * 8;
+        const bool valid = k0 < K;  // quad-uniform (K % 32 == 0)
+        const int kc = min(k0, K - 8);
+        float v[8];
+        if (E.src == SRC_F32) {
+            const float4 t0 = *(const float4 *)(E.f + kc), t1 = *(const float4 *)(E.f + kc + 4);
+            v[0] = t0.x, v[1] = t0.y, v[2] = t0.z, v[3] = t0.w, v[4] = t1.x, v[5] = t1.y, v[6] = t1.z, v[7] = t1.w;
         } else {
-            load_vec<EE>(xv, Ent.x, K);
-            load_vec<EE>(lw, Ent.lnw, K);
-            load_vec<EE>(lb, Ent.lnb, K);
-            if (Ent.form != 2) {
-                load_vec<EE>(cv, Ent.carry, K);
-                load_vec<EE>(mv, Ent.mu, K);
+            float xs[8], ws[8], bs[8], cs[8], ms[8];
+#pragma unroll
+            for (int h = 0; h < 8; h += 4) {
+                const float4 px = *(const float4 *)(E.x + kc + h);
+                const float4 pw = *(const float4 *)(E.lnw + kc + h);
+                const float4 pb = *(const float4 *)(E.lnb + kc + h);
+                xs[h] = px.x, xs[h + 1] = px.y, xs[h + 2] = px.z, xs[h + 3] = px.w;
+                ws[h] = pw.x, ws[h + 1] = pw.y, ws[h + 2] = pw.z, ws[h + 3] = pw.w;
+                bs[h] = pb.x, bs[h + 1] = pb.y, bs[h + 2] = pb.z, bs[h + 3] = pb.w;
+                if (E.form != 2) {
+                    const float4 pc = *(const float4 *)(E.carry + kc + h);
+                    const float4 pm = *(const float4 *)(E.mu + kc + h);
+                    cs[h] = pc.x, cs[h + 1] = pc.y, cs[h + 2] = pc.z, cs[h + 3] = pc.w;
+                    ms[h] = pm.x, ms[h + 1] = pm.y, ms[h + 2] = pm.z, ms[h + 3] = pm.w;
+                }
+            }
+            float xa[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                xa[j] = ln_apply(xs[j], mean, scale, ws[j], bs[j]);
+                if (E.form == 2) v[j] = xa[j];
+                else if (E.form == 0) v[j] = xa[j] * ms[j] + (cs[j] - cs[j] * ms[j]);
+                else v[j] = (cs[j] - xa[j]) * ms[j] + xa[j];
+            }
+            if (write_carry && valid) {
+                *(float4 *)(E.carry_out + k0) = make_float4(xa[0], xa[1], xa[2], xa[3]);
+                *(float4 *)(E.carry_out + k0 + 4) = make_float4(xa[4], xa[5], xa[6], xa[7]);
+            }
+        }
+        if constexpr (WF == W_F32) {
+            if (valid) {
+                *(float4 *)(a.f + k0) = make_float4(v[0], v[1], v[2], v[3]);
+                *(float4 *)(a.f + k0 + 4) = make_float4(v[4], v[5], v[6], v[7]);
+            }
+        } else if constexpr (WF == W_F16) {
+            int p[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                p[j] = __builtin_bit_cast(int, __halves2half2(__float2half(v[2 * j]), __float2half(v[2 * j + 1])));
+            if (valid) *(int4 *)(a.h + k0) = make_int4(p[0], p[1], p[2], p[3]);
+        } else {
+            // ggml quantize_row_q8_0 / q8_1 (x86): d = amax/127, q = rint(x*127/amax)
+            float am = 0.0f;
+#pragma unroll
+            for (int j = 0; j < 8; j++) am = fmaxf(am, fabsf(v[j]));
+            am = fmaxf(am, __int_as_float(dpp_mov<0xB1>(__float_as_int(am))));
+            am = fmaxf(am, __int_as_float(dpp_mov<0x4E>(__float_as_int(am))));
+            const float d = am / 127.f;
+            const float id = (am != 0.0f) ? 127.f / am : 0.0f;
+            int lo = 0, hi = 0, sum = 0;
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const int q = (int)rintf(v[j] * id);
+                sum += q;
+                if (j < 4) lo |= (q & 0xff) << (8 * j);
+                else hi |= (q & 0xff) << (8 * (j - 4));
+            }
+            sum += dpp_mov<0xB1>(sum);
+            sum += dpp_mov<0x4E>(sum);
+            if (valid) {
+                *(int2 *)(a.q + k0) = make_int2(lo, hi);
+                if ((lane & 3) == 0) {
+                    const int bi = k0 >> 5;
+                    a.d[bi] = f16_round(d);
+                    a.qsum[bi] = sum;
+                    if (a.fmt == A_Q8_1) a.s[bi] = f16_round(d * (float)sum);
+                }
             }
         }
     }
-    // (2) this wave's weight units (HBM), in flight during the prologue
+}
+
+// Epilogue operands of one output row, loaded at kernel start (not after the dots).
+struct EpiIn {
+    float y, aux, bias;
+};
+__device__ __forceinline__ EpiIn epi_load(const MVEntry & E, int row) {
+    EpiIn p;
+    const bool yin = E.epi == EPI_ADD || E.epi == EPI_SIGMUL_ADD || E.epi == EPI_VMIX7;
+    const bool ain = E.epi == EPI_SIGMUL_ADD || E.epi == EPI_VMIX7;
+    const bool bin = E.epi == EPI_DECAY6 || E.epi == EPI_DECAY7 || E.epi == EPI_SIGMOID_BIAS || E.epi == EPI_VMIX7;
+    p.y = yin ? E.y[row] : 0.0f;
+    p.aux = ain ? E.aux[row] : 0.0f;
+    p.bias = bin ? E.bias[row] : 0.0f;
+    return p;
+}
+__device__ __forceinline__ float epi_apply(int epi, float acc, const EpiIn & p) {
+    switch (epi) {
+        case EPI_SIGMOID: return sigmoidf_(acc);
+        case EPI_TANH: return tanhf(acc);
+        case EPI_SILU: return siluf_(acc);
+        case EPI_RELU_SQ: {
+            const float r = acc > 0.0f ? acc : 0.0f;
+            return r * r;
+        }
+        case EPI_ADD: return p.y + acc;
+        case EPI_SIGMUL_ADD: return p.y + sigmoidf_(p.aux) * acc;
+        case EPI_DECAY6: return expf(-expf(acc + p.bias));
+        case EPI_DECAY7: return expf(sigmoidf_(acc + p.bias) * -0.606531f);
+        case EPI_SIGMOID_BIAS: return sigmoidf_(acc + p.bias);
+        case EPI_VMIX7: return p.y + (p.aux - p.y) * sigmoidf_(acc + p.bias);
+        default: return acc;
+    }
+}
+
+// One workgroup = NW waves x R rows (RW = NW*R rows per row block).  E == 0: the input is an
+// activation buffer in global memory (SRC_ACT, NW = 4); E > 0: the prologue builds it in LDS
+// (SRC_F32 / SRC_LNMIX, K <= 64*NW*E; NW = 16 so the per-wave prologue work is short).
+// stride > 0: the workgroup walks row blocks wgi, wgi+stride, ... with one prologue.
+template <int WF, int R, int U, bool PRO, bool EMIT, int NW>
+__device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, int stride, char * smem, float * red) {
+    constexpr int RW = NW * R;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const DMat & W = Ent.W;
+    const int M = W.M, K = W.K;
+    const int nblk = (M + RW - 1) / RW;
+    const int units = mv_units(WF, K);
+    PROBE(0);
+
+    // (1) this wave's weight units (HBM) and the epilogue operands, in flight during the
+    // prologue
+    int row0 = wgi * RW + wave * R;
+    int rows[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) rows[r] = min(row0 + r, M - 1);
     WBlk w[R][U];
 #pragma unroll
     for (int u = 0; u < U; u++)
 #pragma unroll
         for (int r = 0; r < R; r++) w[r][u] = load_unit<WF>(W, rows[r], u, lane);
-
-    // (3) prologue: LayerNorm + token-shift mix + ggml activation quantization into LDS
+    EpiIn ep[R];
+    if constexpr (!EMIT) {
+#pragma unroll
+        for (int r = 0; r < R; r++) ep[r] = epi_load(Ent, rows[r]);
+    } else {
+        ep[0] = epi_load(Ent, min(wgi * RW + (tid < RW ? tid : 0), M - 1));
+    }
+    // (2) prologue: LayerNorm statistics (every wave for itself), then the activation image
     ActBuf a;
-    if constexpr (E > 0) {
+    if constexpr (PRO) {
         a = lds_act(smem, act_fmt_for(WF), K);
-        if (Ent.src != SRC_F32) {
-            float mean, scale;
-            ln_stats_reg<EE>(xv, K, mean, scale, sh);
-            const bool write_carry = Ent.carry_out && wgi == 0;
-#pragma unroll
-            for (int i = 0; i < EE; i++) {
-                const float xa = ln_apply(xv[i], mean, scale, lw[i], lb[i]);
-                const int k = i * 256 + tid;
-                if (write_carry && k < K) Ent.carry_out[k] = xa;
-                if (Ent.form == 2) xv[i] = xa;
-                else if (Ent.form == 0) xv[i] = xa * mv[i] + (cv[i] - cv[i] * mv[i]);
-                else xv[i] = (cv[i] - xa) * mv[i] + xa;
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < EE; i++) {
-            const int k0 = i * 256;
-            if (k0 + (tid & ~31) < K) emit32(a, 0, k0 + tid, xv[i]);  // half-wave uniform
-        }
+        float mean = 0.0f, scale = 0.0f;
+        if (Ent.src == SRC_LNMIX) ln_stats_any(Ent.x, K, 1e-5f, mean, scale);
+#ifdef MV_PROBE
+        if (mean == 1.2345f) g_probe[1] = 0;
+#endif
+        PROBE(4);
+        const bool write_carry = Ent.carry_out && wgi == (int)blockIdx.x - Ent.block0;
+        prologue_chunks<WF>(Ent, a, mean, scale, write_carry, wave, NW, lane);
+        PROBE(6);
         __syncthreads();
     } else {
         a = Ent.act;
     }
+    PROBE(1);
 
-    // (4) dots
-    float acc[R], acc2[R];
+    for (;;) {
+        // (4) dots
+        float acc[R], acc2[R];
 #pragma unroll
-    for (int r = 0; r < R; r++) acc[r] = acc2[r] = 0.0f;
-    for (int u0 = 0; u0 < units; u0 += U) {
-        if (u0 > 0) {
+        for (int r = 0; r < R; r++) acc[r] = acc2[r] = 0.0f;
+        for (int u0 = 0; u0 < units; u0 += U) {
+            if (u0 > 0) {
 #pragma unroll
-            for (int u = 0; u < U; u++)
+                for (int u = 0; u < U; u++)
 #pragma unroll
-                for (int r = 0; r < R; r++) w[r][u] = load_unit<WF>(W, rows[r], u0 + u, lane);
-        }
-        AUnit x[U];
+                    for (int r = 0; r < R; r++) w[r][u] = load_unit<WF>(W, rows[r], u0 + u, lane);
+            }
+            AUnit x[U];
 #pragma unroll
-        for (int u = 0; u < U; u++) x[u] = load_act_unit<WF, (E > 0)>(a, u0 + u, lane);
+            for (int u = 0; u < U; u++) x[u] = load_act_unit<WF, PRO>(a, u0 + u, lane);
 #pragma unroll
-        for (int u = 0; u < U; u++) {
-            if (unit_valid<WF>(K, u0 + u, lane)) {
+            for (int u = 0; u < U; u++) {
+                if (unit_valid<WF>(K, u0 + u, lane)) {
 #pragma unroll
-                for (int r = 0; r < R; r++) dot_unit<WF>(w[r][u], x[u], acc[r], acc2[r]);
+                    for (int r = 0; r < R; r++) dot_unit<WF>(w[r][u], x[u], acc[r], acc2[r]);
+                }
             }
         }
-    }
 
-    // (5) reduce + epilogue
-    constexpr bool one = WF == W_Q4_1 || WF == W_Q5_1;
-    if constexpr (!EMIT) {
+        // (5) reduce + epilogue
+        constexpr bool one = WF == W_Q4_1 || WF == W_Q5_1;
+        float s[R];
 #pragma unroll
-        for (int r = 0; r < R; r++) {
-            const float s = one ? wave_sum63(acc[r]) + wave_sum63(acc2[r]) : wave_sum63(acc[r]) + 0.0f;
-            const int row = row0 + r;
-            if (lane == 63 && row < M) Ent.y[row] = apply_epi_mv(Ent, row, s);
-        }
-    } else {
-        // 4*R == 32 rows per workgroup: apply the epilogue and emit the 32 values as one
-        // quantization block of the next matmul's input (ggml Q8 / fp16 / fp32)
+        for (int r = 0; r < R; r++) s[r] = one ? wave_sum63(acc[r]) + wave_sum63(acc2[r]) : wave_sum63(acc[r]) + 0.0f;
+        if constexpr (!EMIT) {
+#ifdef MV_PROBE
+            if (s[0] == 1.2345f) g_probe[0] = 0;  // orders the stamp after the dots
+#endif
+            PROBE(2);
 #pragma unroll
-        for (int r = 0; r < R; r++) {
-            const float s = one ? wave_sum63(acc[r]) + wave_sum63(acc2[r]) : wave_sum63(acc[r]) + 0.0f;
-            if (lane == 63) red[wave * R + r] = s;
-        }
-        __syncthreads();
-        if (tid < 32) {
-            const int row = rowwg + tid;
-            float vv = 0.0f;
-            if (row < M) {
-                vv = apply_epi_mv(Ent, row, red[tid]);
-                if (Ent.y) Ent.y[row] = vv;
+            for (int r = 0; r < R; r++) {
+                const int row = row0 + r;
+                if (lane == 63 && row < M) Ent.y[row] = epi_apply(Ent.epi, s[r], ep[r]);
             }
-            if (Ent.act_out.fmt >= 0 && Ent.emit) emit32(Ent.act_out, 0, row, vv);
+        } else {
+            // RW rows per block (a multiple of 32): apply the epilogue and emit each 32 rows as
+            // one quantization block of the next matmul's input (ggml Q8 / fp16 / fp32)
+#pragma unroll
+            for (int r = 0; r < R; r++)
+                if (lane == 63) red[wave * R + r] = s[r];
+            __syncthreads();
+            PROBE(2);
+            if (tid < RW) {
+                const int row = wgi * RW + tid;
+                float vv = 0.0f;
+                if (row < M) {
+                    vv = epi_apply(Ent.epi, red[tid], ep[0]);
+                    if (Ent.y) Ent.y[row] = vv;
+                }
+                if (Ent.act_out.fmt >= 0 && Ent.emit) emit32(Ent.act_out, 0, row, vv);
+            }
+        }
+        PROBE(3);
+        wgi += stride;
+        if (stride <= 0 || wgi >= nblk) break;
+        if constexpr (EMIT) __syncthreads();  // red[] reuse
+        row0 = wgi * RW + wave * R;
+#pragma unroll
+        for (int r = 0; r < R; r++) rows[r] = min(row0 + r, M - 1);
+#pragma unroll
+        for (int u = 0; u < U; u++)
+#pragma unroll
+            for (int r = 0; r < R; r++) w[r][u] = load_unit<WF>(W, rows[r], u, lane);
+        if constexpr (!EMIT) {
+#pragma unroll
+            for (int r = 0; r < R; r++) ep[r] = epi_load(Ent, rows[r]);
+        } else {
+            ep[0] = epi_load(Ent, min(wgi * RW + (tid < RW ? tid : 0), M - 1));
         }
     }
 }
 
-template <int R, int U, int E, bool EMIT>
+// WFIX >= 0: every entry of the group has weight type WFIX (one body, fewer registers);
+// WFIX < 0: per-entry switch.
+template <int R, int U, bool PRO, bool EMIT, int WFIX>
 __global__ __launch_bounds__(256) void k_mv(MVGroup g) {
+    constexpr int NW = 4;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    __shared__ double sh[8];
-    __shared__ float red[4 * R];
+    __shared__ float red[NW * R];
     int e = 0;
 #pragma unroll 1
     while (e + 1 < g.n && (int)blockIdx.x >= g.e[e + 1].block0) e++;
     const MVEntry & Ent = g.e[e];
     const int wgi = (int)blockIdx.x - Ent.block0;
-    switch (Ent.W.type) {
-        case W_F32: mv_body<W_F32, R, U, E, EMIT>(Ent, wgi, smem, sh, red); break;
-        case W_F16: mv_body<W_F16, R, U, E, EMIT>(Ent, wgi, smem, sh, red); break;
-        case W_Q4_0: mv_body<W_Q4_0, R, U, E, EMIT>(Ent, wgi, smem, sh, red); break;
-        case W_Q4_1: mv_body<W_Q4_1, R, U, E, EMIT>(Ent, wgi, smem, sh, red); break;
-        case W_Q5_0: mv_body<W_Q5_0, R, U, E, EMIT>(Ent, wgi, smem, sh, red); break;
-        case W_Q5_1: mv_body<W_Q5_1, R, U, E, EMIT>(Ent, wgi, smem, sh, red); break;
-        case W_Q8_0: mv_body<W_Q8_0, R, U, E, EMIT>(Ent, wgi, smem, sh, red); break;
-        default: break;
+    if constexpr (WFIX >= 0) {
+        mv_body<WFIX, R, U, PRO, EMIT, NW>(Ent, wgi, g.stride, smem, red);
+    } else {
+        switch (Ent.W.type) {
+            case W_F32: mv_body<W_F32, R, U, PRO, EMIT, NW>(Ent, wgi, g.stride, smem, red); break;
+            case W_F16: mv_body<W_F16, R, U, PRO, EMIT, NW>(Ent, wgi, g.stride, smem, red); break;
+            case W_Q4_0: mv_body<W_Q4_0, R, U, PRO, EMIT, NW>(Ent, wgi, g.stride, smem, red); break;
+            case W_Q4_1: mv_body<W_Q4_1, R, U, PRO, EMIT, NW>(Ent, wgi, g.stride, smem, red); break;
+            case W_Q5_0: mv_body<W_Q5_0, R, U, PRO, EMIT, NW>(Ent, wgi, g.stride, smem, red); break;
+            case W_Q5_1: mv_body<W_Q5_1, R, U, PRO, EMIT, NW>(Ent, wgi, g.stride, smem, red); break;
+            case W_Q8_0: mv_body<W_Q8_0, R, U, PRO, EMIT, NW>(Ent, wgi, g.stride, smem, red); break;
+            default: break;
+        }
     }
 }
 
-template <int R, int U, bool EMIT>
-static void launch_mv_u(hipStream_t st, MVGroup & g, int E, dim3 grid) {
-    dim3 block(256);
-    switch (E) {
-        case 0: hipLaunchKernelGGL((k_mv<R, U, 0, EMIT>), grid, block, g.lds_bytes, st, g); break;
-        case 8: hipLaunchKernelGGL((k_mv<R, U, 8, EMIT>), grid, block, g.lds_bytes, st, g); break;
-        default: hipLaunchKernelGGL((k_mv<R, U, 32, EMIT>), grid, block, g.lds_bytes, st, g); break;
-    }
+static int g_mv_cus = 256;
+void set_mv_device_cus(int n) { g_mv_cus = n > 0 ? n : 256; }
+
+template <int U, int WFIX>
+static void launch_mv_w(hipStream_t st, MVGroup & g, bool pro, bool emit, dim3 grid) {
+    if (emit) hipLaunchKernelGGL((k_mv<8, U, true, true, WFIX>), grid, dim3(256), g.lds_bytes, st, g);
+    else if (pro) hipLaunchKernelGGL((k_mv<2, U, true, false, WFIX>), grid, dim3(256), g.lds_bytes, st, g);
+    else hipLaunchKernelGGL((k_mv<2, U, false, false, WFIX>), grid, dim3(256), 0, st, g);
 }
 
-template <int R, bool EMIT>
-static void launch_mv_r(hipStream_t st, MVGroup & g, int U, int E, dim3 grid) {
-    switch (U) {
-        case 1: launch_mv_u<R, 1, EMIT>(st, g, E, grid); break;
-        case 2: launch_mv_u<R, 2, EMIT>(st, g, E, grid); break;
-        default: launch_mv_u<R, 4, EMIT>(st, g, E, grid); break;
+template <int U>
+static void launch_mv_u(hipStream_t st, MVGroup & g, bool pro, bool emit, int wfix, dim3 grid) {
+    switch (wfix) {
+        case W_F16: launch_mv_w<U, W_F16>(st, g, pro, emit, grid); break;
+        case W_Q4_0: launch_mv_w<U, W_Q4_0>(st, g, pro, emit, grid); break;
+        case W_Q4_1: launch_mv_w<U, W_Q4_1>(st, g, pro, emit, grid); break;
+        case W_Q5_0: launch_mv_w<U, W_Q5_0>(st, g, pro, emit, grid); break;
+        case W_Q5_1: launch_mv_w<U, W_Q5_1>(st, g, pro, emit, grid); break;
+        case W_Q8_0: launch_mv_w<U, W_Q8_0>(st, g, pro, emit, grid); break;
+        default: launch_mv_w<U, -1>(st, g, pro, emit, grid); break;
     }
 }
 
@@ -379,12 +496,20 @@ bool launch_mv_group(hipStream_t st, MVGroup & g) {
         fprintf(stderr, "rwkv: matvec group mixes activation and prologue sources\n");
         return false;
     }
+    if (emit && !prologue) {
+        fprintf(stderr, "rwkv: emitting matvec needs a prologue source\n");
+        return false;
+    }
     const int R = emit ? 8 : 2, RW = 4 * R;
-    int blocks = 0, lds = 0, kmax = 0, umax = 1;
+    int blocks = 0, umax = 1, lds = 0;
     for (int i = 0; i < g.n; i++) {
         MVEntry & e = g.e[i];
         if (e.W.K % 32) {
             fprintf(stderr, "rwkv: matvec needs K %% 32 == 0 (K=%d)\n", e.W.K);
+            return false;
+        }
+        if (e.src == SRC_LNMIX && (e.W.K % 64 || e.W.K > 64 * 128)) {
+            fprintf(stderr, "rwkv: LayerNorm prologue needs K %% 64 == 0 and K <= 8192 (K=%d)\n", e.W.K);
             return false;
         }
         if (e.emit && e.W.M % 32) {
@@ -398,27 +523,26 @@ bool launch_mv_group(hipStream_t st, MVGroup & g) {
         e.block0 = blocks;
         blocks += (e.W.M + RW - 1) / RW;
         umax = std::max(umax, mv_units(e.W.type, e.W.K));
-        if (e.src != SRC_ACT) {
-            lds = std::max(lds, lds_bytes_for(act_fmt_for(e.W.type), e.W.K));
-            kmax = std::max(kmax, e.W.K);
-        }
-    }
-    if (kmax > 32 * 256) {
-        fprintf(stderr, "rwkv: matvec prologue K=%d > 8192 unsupported\n", kmax);
-        return false;
+        if (e.src != SRC_ACT) lds = std::max(lds, lds_bytes_for(act_fmt_for(e.W.type), e.W.K));
     }
     g.lds_bytes = lds;
     if (!blocks) return true;
-    const int E = !prologue ? 0 : kmax <= 8 * 256 ? 8 : 32;
+    // a single large prologue entry (the head): persistent walk over its row blocks, one
+    // LayerNorm per workgroup
+    g.stride = 0;
+    int grid = blocks;
+    if (prologue && g.n == 1 && !emit && blocks > 8 * g_mv_cus) {
+        grid = 2 * g_mv_cus;
+        g.stride = grid;
+    }
     const int U = umax <= 1 ? 1 : umax <= 2 ? 2 : 4;
-    if (emit) {
-        if (!prologue) {
-            fprintf(stderr, "rwkv: emitting matvec needs a prologue source\n");
-            return false;
-        }
-        launch_mv_r<8, true>(st, g, U, E, dim3(blocks));
-    } else {
-        launch_mv_r<2, false>(st, g, U, E, dim3(blocks));
+    int wfix = g.e[0].W.type;
+    for (int i = 1; i < g.n; i++)
+        if (g.e[i].W.type != wfix) wfix = -1;
+    switch (U) {
+        case 1: launch_mv_u<1>(st, g, prologue, emit, wfix, dim3(grid)); break;
+        case 2: launch_mv_u<2>(st, g, prologue, emit, wfix, dim3(grid)); break;
+        default: launch_mv_u<4>(st, g, prologue, emit, wfix, dim3(grid)); break;
     }
     HIP_OK(hipGetLastError());
     return true;
@@ -443,7 +567,10 @@ __global__ __launch_bounds__(256) void k_v6_mix5_dec(Mix5Dec a) {
     float w2v[64];
     const float * w2 = a.w2t + (size_t)n * D * C + c;
 #pragma unroll
-    for (int i = 0; i < 64; i++) w2v[i] = (i < D) ? w2[(size_t)i * C] : 0.0f;
+    for (int i = 0; i < 64; i++) {
+        const float t = w2[(size_t)min(i, D - 1) * C];
+        w2v[i] = (i < D) ? t : 0.0f;
+    }
     const float xa = a.xa[c], cc = a.carry[c], mu = a.maa[n][c];
     const float sx = cc - xa;
     const float * lv = a.lora + n * D;
@@ -654,7 +781,8 @@ __global__ __launch_bounds__(256) void k_att6_dec(Att6Dec a) {
         o = o * a.lnx_w[c0 + tid];
         o = o + a.lnx_b[c0 + tid];
         if (a.g) o = o * a.g[c0 + tid];
-        a.y[c0 + tid] = o;
+        if (a.yq.fmt >= 0) emit32(a.yq, 0, c0 + tid, o);  // S >= 32: whole half-wave blocks
+        else a.y[c0 + tid] = o;
     }
 }
 
@@ -674,6 +802,10 @@ bool launch_att6_dec(hipStream_t st, const Att6Dec & a) {
             return false;
         }
         lds = lds_bytes_for(act_fmt_for(a.wd2.type), D);
+    }
+    if (a.yq.fmt >= 0 && a.S < 32) {
+        fprintf(stderr, "rwkv: quantized attention output needs head size >= 32\n");
+        return false;
     }
     dim3 grid(a.H), block(std::max(threads, 64));
     const bool pf = !a.w && a.wd2.type >= W_Q4_0 && (a.wd2.K >> 5) <= 4;
@@ -760,7 +892,8 @@ __global__ __launch_bounds__(256) void k_att7_dec(Att7Dec a) {
         o = o + a.lnx_b[c];
         o = o + sv[tid] * sbonus;
         o = o * a.g[c];
-        a.y[c] = o;
+        if (a.yq.fmt >= 0) emit32(a.yq, 0, c, o);  // S >= 32: whole half-wave blocks
+        else a.y[c] = o;
     }
 }
 
@@ -773,6 +906,10 @@ bool launch_att7_dec(hipStream_t st, const Att7Dec & a) {
     if (G > a.S) G = a.S;
     const int JPG = a.S / G;
     const int threads = std::max(64, a.S * G);
+    if (a.yq.fmt >= 0 && a.S < 32) {
+        fprintf(stderr, "rwkv: quantized attention output needs head size >= 32\n");
+        return false;
+    }
     dim3 grid(a.H), block(threads);
     switch (JPG) {
         case 1: hipLaunchKernelGGL(k_att7_dec<1>, grid, block, 0, st, a); break;

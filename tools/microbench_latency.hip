@@ -43,6 +43,38 @@ __global__ void k_stream(const int4 * w, int4 * out, size_t n) {
     if (acc.x == 0x12345678) out[0] = acc;
 }
 
+struct BigArg {
+    int v[512];
+};
+
+// N dependent scalar loads from the kernel-argument segment
+template <int N>
+__global__ void k_karg_chain(BigArg a, int * out) {
+    int i = a.v[0];
+#pragma unroll
+    for (int k = 1; k < N; k++) i = a.v[i & 511];
+    if (threadIdx.x == 0 && i == -7) out[0] = i;
+}
+
+// N dependent scalar loads from a device buffer
+template <int N>
+__global__ void k_dev_chain(const int * __restrict__ p, int * out) {
+    int i = p[0];
+#pragma unroll
+    for (int k = 1; k < N; k++) i = p[i & 511];
+    if (threadIdx.x == 0 && i == -7) out[0] = i;
+}
+
+// N dependent per-lane vector loads from a buffer the previous kernel wrote
+template <int N>
+__global__ void k_vec_chain(int * p, int * out) {
+    int i = p[threadIdx.x & 63];
+#pragma unroll
+    for (int k = 1; k < N; k++) i = p[(i + threadIdx.x) & 511];
+    if (blockIdx.x == 0 && threadIdx.x < 64) p[threadIdx.x] = i & 7;  // write for the next launch
+    if (i == -7) out[0] = i;
+}
+
 int main() {
     hipStream_t st;
     CK(hipStreamCreate(&st));
@@ -76,6 +108,36 @@ int main() {
         printf("%-40s %8.2f us/launch (graph of %d)\n", name, ms * 1000 / reps, reps);
         hipGraphExecDestroy(ge); hipGraphDestroy(g);
     };
+    {
+        BigArg ba;
+        for (int i = 0; i < 512; i++) ba.v[i] = (i * 7 + 3) & 511;
+        int * dv;
+        CK(hipMalloc(&dv, 4096));
+        CK(hipMemcpy(dv, ba.v, 2048, hipMemcpyHostToDevice));
+        int * ob;
+        CK(hipMalloc(&ob, 4096));
+        for (int grid : {1, 256, 1024}) {
+            char nm[64];
+            snprintf(nm, sizeof nm, "kernarg chain 1 grid %d", grid);
+            timeit(nm, [&]() { hipLaunchKernelGGL(k_karg_chain<1>, dim3(grid), dim3(256), 0, st, ba, ob); }, 500);
+            snprintf(nm, sizeof nm, "kernarg chain 4 grid %d", grid);
+            timeit(nm, [&]() { hipLaunchKernelGGL(k_karg_chain<4>, dim3(grid), dim3(256), 0, st, ba, ob); }, 500);
+            snprintf(nm, sizeof nm, "kernarg chain 8 grid %d", grid);
+            timeit(nm, [&]() { hipLaunchKernelGGL(k_karg_chain<8>, dim3(grid), dim3(256), 0, st, ba, ob); }, 500);
+            snprintf(nm, sizeof nm, "devbuf chain 1 grid %d", grid);
+            timeit(nm, [&]() { hipLaunchKernelGGL(k_dev_chain<1>, dim3(grid), dim3(256), 0, st, dv, ob); }, 500);
+            snprintf(nm, sizeof nm, "devbuf chain 4 grid %d", grid);
+            timeit(nm, [&]() { hipLaunchKernelGGL(k_dev_chain<4>, dim3(grid), dim3(256), 0, st, dv, ob); }, 500);
+            snprintf(nm, sizeof nm, "devbuf chain 8 grid %d", grid);
+            timeit(nm, [&]() { hipLaunchKernelGGL(k_dev_chain<8>, dim3(grid), dim3(256), 0, st, dv, ob); }, 500);
+            snprintf(nm, sizeof nm, "vector chain 1 grid %d", grid);
+            timeit(nm, [&]() { hipLaunchKernelGGL(k_vec_chain<1>, dim3(grid), dim3(256), 0, st, dv, ob); }, 500);
+            snprintf(nm, sizeof nm, "vector chain 4 grid %d", grid);
+            timeit(nm, [&]() { hipLaunchKernelGGL(k_vec_chain<4>, dim3(grid), dim3(256), 0, st, dv, ob); }, 500);
+            snprintf(nm, sizeof nm, "vector chain 8 grid %d", grid);
+            timeit(nm, [&]() { hipLaunchKernelGGL(k_vec_chain<8>, dim3(grid), dim3(256), 0, st, dv, ob); }, 500);
+        }
+    }
     timeit("empty 1 WG", [&]() { hipLaunchKernelGGL(k_empty, dim3(1), dim3(64), 0, st, y); }, 1000);
     timeit("empty 256 WG", [&]() { hipLaunchKernelGGL(k_empty, dim3(256), dim3(256), 0, st, y); }, 1000);
     timeit("empty 2048 WG", [&]() { hipLaunchKernelGGL(k_empty, dim3(2048), dim3(256), 0, st, y); }, 1000);

@@ -288,6 +288,34 @@ __device__ __forceinline__ double wave_allsum_d(double v) {
 // Every LayerNorm on the device (decode prologues, sequence kernels) uses this one
 // association, so decode and sequence agree bit for bit.  Requires K % 64 == 0,
 // K <= 64*PMAX, all lanes active.
+// Register form of ln_stats_wave for K <= 64*PC: load phase and compute phase separate, so a
+// caller can put other loads in flight between them.
+template <int PC>
+__device__ __forceinline__ void ln_load_regs(const float * x, int K, float (&v)[PC]) {
+    const int lane = threadIdx.x & 63, P = K >> 6;
+#pragma unroll
+    for (int j = 0; j < PC; j++) v[j] = x[lane + 64 * min(j, P - 1)];
+}
+template <int PC>
+__device__ __forceinline__ void ln_stats_regs(const float (&v)[PC], int K, float eps, float & mean, float & scale) {
+    const int P = K >> 6;
+    double p[4] = {0.0, 0.0, 0.0, 0.0}, q[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int j = 0; j < PC; j++)
+        if (j < P) p[j & 3] += (double)v[j];
+    const double s = wave_allsum_d((p[0] + p[1]) + (p[2] + p[3]));
+    mean = (float)(s / (double)K);
+#pragma unroll
+    for (int j = 0; j < PC; j++)
+        if (j < P) {
+            const float d = v[j] - mean;
+            q[j & 3] += (double)(d * d);
+        }
+    const double s2 = wave_allsum_d((q[0] + q[1]) + (q[2] + q[3]));
+    const float var = (float)(s2 / (double)K);
+    scale = 1.0f / sqrtf(var + eps);
+}
+
 template <int PC>
 __device__ __forceinline__ void ln_stats_wave(const float * x, int K, float eps, float & mean, float & scale) {
     const int lane = threadIdx.x & 63, P = K >> 6;
@@ -295,19 +323,9 @@ __device__ __forceinline__ void ln_stats_wave(const float * x, int K, float eps,
     if (P <= PC) {
         // one chunk: the second pass reuses the registers
         float v[PC];
-#pragma unroll
-        for (int j = 0; j < PC; j++) v[j] = x[lane + 64 * min(j, P - 1)];
-#pragma unroll
-        for (int j = 0; j < PC; j++)
-            if (j < P) p[j & 3] += (double)v[j];
-        const double s = wave_allsum_d((p[0] + p[1]) + (p[2] + p[3]));
-        mean = (float)(s / (double)K);
-#pragma unroll
-        for (int j = 0; j < PC; j++)
-            if (j < P) {
-                const float d = v[j] - mean;
-                q[j & 3] += (double)(d * d);
-            }
+        ln_load_regs<PC>(x, K, v);
+        ln_stats_regs<PC>(v, K, eps, mean, scale);
+        return;
     } else {
         // chunks of PC elements per lane, reloaded for the second pass (same association)
         for (int j0 = 0; j0 < P; j0 += PC) {

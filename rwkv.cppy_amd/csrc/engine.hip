@@ -291,6 +291,8 @@ bool Engine::init() {
     use_graphs_ = !(g && g[0] == '1');
     const char * gd = getenv("RWKV_MI355X_GENERIC_DECODE");
     generic_decode_ = gd && gd[0] == '1';
+    // the fused decode prologues hold LayerNorm inputs in registers up to n_embed 4096
+    if (m_->n_embed > 4096 || m_->n_embed % 64) generic_decode_ = true;
     return ensure_workspace(1) && init_state(dstate_[0]);
 }
 

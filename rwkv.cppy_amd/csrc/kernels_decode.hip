@@ -5,495 +5,37 @@
 // previous kernel's output): LayerNorm statistics, token-shift mix and the ggml Q8
 // activation quantization are recomputed per workgroup (a few KB of L2 reads) instead of
 // costing a separate launch.  Per-head attention work (decay LoRA tail, wkv, GroupNorm) is
-// one kernel with the head's state in registers.
-#include "device_common.hpp"
-#include "kernels.hpp"
-
-#include <stdio.h>
+// one kernel with the head's state in registers.  The matvec itself lives in mv_common.hpp;
+// its launch shapes are instantiated per weight type in mv_*.hip.
+#include "mv_common.hpp"
 
 namespace rwkvmi {
 
-// Phase timestamps for tools/mv_probe.hip (never defined in the library build).
-#ifdef MV_PROBE
-__device__ unsigned long long * g_probe;
-#define PROBE(k)                                                                               \
-    do {                                                                                       \
-        if (threadIdx.x == 0 && g_probe) g_probe[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
-    } while (0)
-#else
-#define PROBE(k) \
-    do {         \
-    } while (0)
-#endif
-
-// LDS image of one activation row in the consumer's format.
-__device__ __forceinline__ ActBuf lds_act(char * smem, int fmt, int K) {
-    ActBuf a;
-    a.fmt = fmt;
-    a.K = K;
-    a.q = nullptr;
-    a.d = a.s = nullptr;
-    a.qsum = nullptr;
-    a.h = nullptr;
-    a.f = nullptr;
-    if (fmt == A_F32) {
-        a.f = (float *)smem;
-    } else if (fmt == A_F16) {
-        a.h = (__half *)smem;
-    } else {
-        const int nb = K >> 5;
-        a.q = (int8_t *)smem;
-        a.d = (float *)(smem + ((K + 15) & ~15));
-        a.s = a.d + ((nb + 3) & ~3);
-        a.qsum = (int *)(a.s + ((nb + 3) & ~3));
-    }
-    return a;
-}
-
-static int lds_bytes_for(int fmt, int K) {
-    if (fmt == A_F32) return K * 4;
-    if (fmt == A_F16) return K * 2;
-    const int nb = K / 32;
-    return ((K + 15) & ~15) + 3 * ((nb + 3) & ~3) * 4;
-}
-
-// --------------------------------------------------------------------------- decode matvec
-// A lane owns 16-byte "units" of a row: quantized weights one 32-block (lane + 64u), F16 eight
-// halves (k = 8*lane + 512u), F32 four floats (k = 4*lane + 256u) -- the same lane/unit
-// assignment and accumulation order as the batched kernel k_mm, so decode and sequence
-// results are bit-identical.  All R*U weight units of a wave are loaded before anything else
-// waits (rows past M clamp to M-1, units past K clamp to the last unit and are skipped in the
-// dot), so the whole row-block is one HBM round trip, overlapped with the prologue.
-
-__host__ __device__ inline int mv_units(int type, int K) {
-    if (type == W_F32) return (K + 255) / 256;
-    if (type == W_F16) return (K + 511) / 512;
-    return (K / 32 + 63) / 64;
-}
-
-typedef int i32x4_t __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) const i32x4_t lds_i32x4_t;
-typedef __attribute__((address_space(3))) const float lds_float_t;
-typedef __attribute__((address_space(3))) const int lds_int_t;
-
-template <bool LDS>
-__device__ __forceinline__ int4 load16(const void * p) {
-    if constexpr (LDS) {
-        const i32x4_t t = *(const lds_i32x4_t *)(uintptr_t)p;
-        return make_int4(t.x, t.y, t.z, t.w);
-    } else {
-        return *(const int4 *)p;
-    }
-}
-template <bool LDS>
-__device__ __forceinline__ float loadf(const float * p) {
-    if constexpr (LDS) return *(const lds_float_t *)(uintptr_t)p;
-    else return *p;
-}
-template <bool LDS>
-__device__ __forceinline__ int loadi(const int * p) {
-    if constexpr (LDS) return *(const lds_int_t *)(uintptr_t)p;
-    else return *p;
-}
-
-template <int WF>
-__device__ __forceinline__ WBlk load_unit(const DMat & W, int row, int u, int lane) {
-    const int K = W.K;
-    if constexpr (WF == W_F32) {
-        WBlk w;
-        const int k = min(lane * 4 + u * 256, K - 4);
-        w.q0 = *(const int4 *)((const float *)W.qs + (size_t)row * K + k);
-        return w;
-    } else if constexpr (WF == W_F16) {
-        WBlk w;
-        const int k = min(lane * 8 + u * 512, K - 8);
-        w.q0 = *(const int4 *)((const __half *)W.qs + (size_t)row * K + k);
-        return w;
-    } else {
-        const int nb = K >> 5;
-        const int b = min(lane + u * 64, nb - 1);
-        return load_wblk<WF>(W, (size_t)row * nb + b);
-    }
-}
-
-struct AUnit {
-    int4 lo, hi;
-    float d, s;
-    int qs;
-};
-
-template <int WF, bool LDS>
-__device__ __forceinline__ AUnit load_act_unit(const ActBuf & a, int u, int lane) {
-    AUnit x;
-    const int K = a.K;
-    if constexpr (WF == W_F32) {
-        x.lo = load16<LDS>(a.f + min(lane * 4 + u * 256, K - 4));
-    } else if constexpr (WF == W_F16) {
-        x.lo = load16<LDS>(a.h + min(lane * 8 + u * 512, K - 8));
-    } else {
-        const int b = min(lane + u * 64, (K >> 5) - 1);
-        x.lo = load16<LDS>(a.q + (size_t)b * 32);
-        x.hi = load16<LDS>(a.q + (size_t)b * 32 + 16);
-        x.d = loadf<LDS>(a.d + b);
-        x.qs = loadi<LDS>(a.qsum + b);
-        x.s = (WF == W_Q4_1 || WF == W_Q5_1) ? loadf<LDS>(a.s + b) : 0.0f;
-    }
-    return x;
-}
-
-template <int WF>
-__device__ __forceinline__ bool unit_valid(int K, int u, int lane) {
-    if constexpr (WF == W_F32) return lane * 4 + u * 256 < K;
-    else if constexpr (WF == W_F16) return lane * 8 + u * 512 < K;
-    else return lane + u * 64 < (K >> 5);
-}
-
-template <int WF>
-__device__ __forceinline__ void dot_unit(const WBlk & w, const AUnit & x, float & acc, float & acc2) {
-    if constexpr (WF == W_F32) {
-        float s = acc;
-        s = fmaf(__int_as_float(w.q0.x), __int_as_float(x.lo.x), s);
-        s = fmaf(__int_as_float(w.q0.y), __int_as_float(x.lo.y), s);
-        s = fmaf(__int_as_float(w.q0.z), __int_as_float(x.lo.z), s);
-        s = fmaf(__int_as_float(w.q0.w), __int_as_float(x.lo.w), s);
-        acc = s;
-    } else if constexpr (WF == W_F16) {
-        float s = acc;
-        s = __builtin_amdgcn_fdot2(__builtin_bit_cast(half2_t, w.q0.x), __builtin_bit_cast(half2_t, x.lo.x), s, false);
-        s = __builtin_amdgcn_fdot2(__builtin_bit_cast(half2_t, w.q0.y), __builtin_bit_cast(half2_t, x.lo.y), s, false);
-        s = __builtin_amdgcn_fdot2(__builtin_bit_cast(half2_t, w.q0.z), __builtin_bit_cast(half2_t, x.lo.z), s, false);
-        s = __builtin_amdgcn_fdot2(__builtin_bit_cast(half2_t, w.q0.w), __builtin_bit_cast(half2_t, x.lo.w), s, false);
-        acc = s;
-    } else {
-        float dw, mw;
-        const int sumi = dot_wblk<WF>(w, x.lo, x.hi, x.qs, dw, mw);
-        acc = fmaf(dw * x.d, (float)sumi, acc);
-        if constexpr (WF == W_Q4_1 || WF == W_Q5_1) acc2 += mw * x.s;
-    }
-}
-
-// Per-thread register image of a K-vector: thread t owns k = i*NT + t (i < E).
-template <int E, int NT = 256>
-__device__ __forceinline__ void load_vec(float (&v)[E], const float * p, int K) {
-#pragma unroll
-    for (int i = 0; i < E; i++) {
-        // unconditional (clamped) loads: no per-load branches, so the waitcnt pass keeps
-        // them all in flight
-        const int k = i * NT + (int)threadIdx.x;
-        const float t = p[min(k, K - 1)];
-        v[i] = (k < K) ? t : 0.0f;
-    }
-}
-
-// Matvec prologue (SRC_F32 / SRC_LNMIX): the waves of a workgroup build the activation image
-// in LDS chunk by chunk (512 elements per wave-chunk, 8 consecutive elements per lane, so a
-// quantization block is one lane quad): token-shift mix of the LayerNorm output, then ggml's
-// Q8 quantization with quad DPP reductions (F16: packed halves, F32: as is).
-template <int WF>
-__device__ __forceinline__ void prologue_chunks(const MVEntry & E, const ActBuf & a, float mean, float scale,
-                                                bool write_carry, int wave, int nw, int lane) {
-    const int K = E.W.K;
-    for (int c = wave; c * 512 < K; c += nw) {
-        const int k0 = c * 512 + lane * 8;
-        const bool valid = k0 < K;  // quad-uniform (K % 32 == 0)
-        const int kc = min(k0, K - 8);
-        float v[8];
-        if (E.src == SRC_F32) {
-            const float4 t0 = *(const float4 *)(E.f + kc), t1 = *(const float4 *)(E.f + kc + 4);
-            v[0] = t0.x, v[1] = t0.y, v[2] = t0.z, v[3] = t0.w, v[4] = t1.x, v[5] = t1.y, v[6] = t1.z, v[7] = t1.w;
-        } else {
-            float xs[8], ws[8], bs[8], cs[8], ms[8];
-#pragma unroll
-            for (int h = 0; h < 8; h += 4) {
-                const float4 px = *(const float4 *)(E.x + kc + h);
-                const float4 pw = *(const float4 *)(E.lnw + kc + h);
-                const float4 pb = *(const float4 *)(E.lnb + kc + h);
-                xs[h] = px.x, xs[h + 1] = px.y, xs[h + 2] = px.z, xs[h + 3] = px.w;
-                ws[h] = pw.x, ws[h + 1] = pw.y, ws[h + 2] = pw.z, ws[h + 3] = pw.w;
-                bs[h] = pb.x, bs[h + 1] = pb.y, bs[h + 2] = pb.z, bs[h + 3] = pb.w;
-                if (E.form != 2) {
-                    const float4 pc = *(const float4 *)(E.carry + kc + h);
-                    const float4 pm = *(const float4 *)(E.mu + kc + h);
-                    cs[h] = pc.x, cs[h + 1] = pc.y, cs[h + 2] = pc.z, cs[h + 3] = pc.w;
-                    ms[h] = pm.x, ms[h + 1] = pm.y, ms[h + 2] = pm.z, ms[h + 3] = pm.w;
-                }
-            }
-            float xa[8];
-#pragma unroll
-            for (int j = 0; j < 8; j++) {
-                xa[j] = ln_apply(xs[j], mean, scale, ws[j], bs[j]);
-                if (E.form == 2) v[j] = xa[j];
-                else if (E.form == 0) v[j] = xa[j] * ms[j] + (cs[j] - cs[j] * ms[j]);
-                else v[j] = (cs[j] - xa[j]) * ms[j] + xa[j];
-            }
-            if (write_carry && valid) {
-                *(float4 *)(E.carry_out + k0) = make_float4(xa[0], xa[1], xa[2], xa[3]);
-                *(float4 *)(E.carry_out + k0 + 4) = make_float4(xa[4], xa[5], xa[6], xa[7]);
-            }
-        }
-        if constexpr (WF == W_F32) {
-            if (valid) {
-                *(float4 *)(a.f + k0) = make_float4(v[0], v[1], v[2], v[3]);
-                *(float4 *)(a.f + k0 + 4) = make_float4(v[4], v[5], v[6], v[7]);
-            }
-        } else if constexpr (WF == W_F16) {
-            int p[4];
-#pragma unroll
-            for (int j = 0; j < 4; j++)
-                p[j] = __builtin_bit_cast(int, __halves2half2(__float2half(v[2 * j]), __float2half(v[2 * j + 1])));
-            if (valid) *(int4 *)(a.h + k0) = make_int4(p[0], p[1], p[2], p[3]);
-        } else {
-            // ggml quantize_row_q8_0 / q8_1 (x86): d = amax/127, q = rint(x*127/amax)
-            float am = 0.0f;
-#pragma unroll
-            for (int j = 0; j < 8; j++) am = fmaxf(am, fabsf(v[j]));
-            am = fmaxf(am, __int_as_float(dpp_mov<0xB1>(__float_as_int(am))));
-            am = fmaxf(am, __int_as_float(dpp_mov<0x4E>(__float_as_int(am))));
-            const float d = am / 127.f;
-            const float id = (am != 0.0f) ? 127.f / am : 0.0f;
-            int lo = 0, hi = 0, sum = 0;
-#pragma unroll
-            for (int j = 0; j < 8; j++) {
-                const int q = (int)rintf(v[j] * id);
-                sum += q;
-                if (j < 4) lo |= (q & 0xff) << (8 * j);
-                else hi |= (q & 0xff) << (8 * (j - 4));
-            }
-            sum += dpp_mov<0xB1>(sum);
-            sum += dpp_mov<0x4E>(sum);
-            if (valid) {
-                *(int2 *)(a.q + k0) = make_int2(lo, hi);
-                if ((lane & 3) == 0) {
-                    const int bi = k0 >> 5;
-                    a.d[bi] = f16_round(d);
-                    a.qsum[bi] = sum;
-                    if (a.fmt == A_Q8_1) a.s[bi] = f16_round(d * (float)sum);
-                }
-            }
-        }
-    }
-}
-
-// Epilogue operands of one output row, loaded at kernel start (not after the dots).
-struct EpiIn {
-    float y, aux, bias;
-};
-__device__ __forceinline__ EpiIn epi_load(const MVEntry & E, int row) {
-    EpiIn p;
-    const bool yin = E.epi == EPI_ADD || E.epi == EPI_SIGMUL_ADD || E.epi == EPI_VMIX7;
-    const bool ain = E.epi == EPI_SIGMUL_ADD || E.epi == EPI_VMIX7;
-    const bool bin = E.epi == EPI_DECAY6 || E.epi == EPI_DECAY7 || E.epi == EPI_SIGMOID_BIAS || E.epi == EPI_VMIX7;
-    p.y = yin ? E.y[row] : 0.0f;
-    p.aux = ain ? E.aux[row] : 0.0f;
-    p.bias = bin ? E.bias[row] : 0.0f;
-    return p;
-}
-__device__ __forceinline__ float epi_apply(int epi, float acc, const EpiIn & p) {
-    switch (epi) {
-        case EPI_SIGMOID: return sigmoidf_(acc);
-        case EPI_TANH: return tanhf(acc);
-        case EPI_SILU: return siluf_(acc);
-        case EPI_RELU_SQ: {
-            const float r = acc > 0.0f ? acc : 0.0f;
-            return r * r;
-        }
-        case EPI_ADD: return p.y + acc;
-        case EPI_SIGMUL_ADD: return p.y + sigmoidf_(p.aux) * acc;
-        case EPI_DECAY6: return expf(-expf(acc + p.bias));
-        case EPI_DECAY7: return expf(sigmoidf_(acc + p.bias) * -0.606531f);
-        case EPI_SIGMOID_BIAS: return sigmoidf_(acc + p.bias);
-        case EPI_VMIX7: return p.y + (p.aux - p.y) * sigmoidf_(acc + p.bias);
-        default: return acc;
-    }
-}
-
-// One workgroup = NW waves x R rows (RW = NW*R rows per row block).  E == 0: the input is an
-// activation buffer in global memory (SRC_ACT, NW = 4); E > 0: the prologue builds it in LDS
-// (SRC_F32 / SRC_LNMIX, K <= 64*NW*E; NW = 16 so the per-wave prologue work is short).
-// stride > 0: the workgroup walks row blocks wgi, wgi+stride, ... with one prologue.
-template <int WF, int R, int U, bool PRO, bool EMIT, int NW>
-__device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, int stride, char * smem, float * red) {
-    constexpr int RW = NW * R;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const DMat & W = Ent.W;
-    const int M = W.M, K = W.K;
-    const int nblk = (M + RW - 1) / RW;
-    const int units = mv_units(WF, K);
-    PROBE(0);
-
-    // (1) this wave's weight units (HBM) and the epilogue operands, in flight during the
-    // prologue
-    int row0 = wgi * RW + wave * R;
-    int rows[R];
-#pragma unroll
-    for (int r = 0; r < R; r++) rows[r] = min(row0 + r, M - 1);
-    WBlk w[R][U];
-#pragma unroll
-    for (int u = 0; u < U; u++)
-#pragma unroll
-        for (int r = 0; r < R; r++) w[r][u] = load_unit<WF>(W, rows[r], u, lane);
-    EpiIn ep[R];
-    if constexpr (!EMIT) {
-#pragma unroll
-        for (int r = 0; r < R; r++) ep[r] = epi_load(Ent, rows[r]);
-    } else {
-        ep[0] = epi_load(Ent, min(wgi * RW + (tid < RW ? tid : 0), M - 1));
-    }
-    // (2) prologue: LayerNorm statistics (every wave for itself), then the activation image
-    ActBuf a;
-    if constexpr (PRO) {
-        a = lds_act(smem, act_fmt_for(WF), K);
-        float mean = 0.0f, scale = 0.0f;
-        if (Ent.src == SRC_LNMIX) ln_stats_any(Ent.x, K, 1e-5f, mean, scale);
-#ifdef MV_PROBE
-        if (mean == 1.2345f) g_probe[1] = 0;
-#endif
-        PROBE(4);
-        const bool write_carry = Ent.carry_out && wgi == (int)blockIdx.x - Ent.block0;
-        prologue_chunks<WF>(Ent, a, mean, scale, write_carry, wave, NW, lane);
-        PROBE(6);
-        __syncthreads();
-    } else {
-        a = Ent.act;
-    }
-    PROBE(1);
-
-    for (;;) {
-        // (4) dots
-        float acc[R], acc2[R];
-#pragma unroll
-        for (int r = 0; r < R; r++) acc[r] = acc2[r] = 0.0f;
-        for (int u0 = 0; u0 < units; u0 += U) {
-            if (u0 > 0) {
-#pragma unroll
-                for (int u = 0; u < U; u++)
-#pragma unroll
-                    for (int r = 0; r < R; r++) w[r][u] = load_unit<WF>(W, rows[r], u0 + u, lane);
-            }
-            AUnit x[U];
-#pragma unroll
-            for (int u = 0; u < U; u++) x[u] = load_act_unit<WF, PRO>(a, u0 + u, lane);
-#pragma unroll
-            for (int u = 0; u < U; u++) {
-                if (unit_valid<WF>(K, u0 + u, lane)) {
-#pragma unroll
-                    for (int r = 0; r < R; r++) dot_unit<WF>(w[r][u], x[u], acc[r], acc2[r]);
-                }
-            }
-        }
-
-        // (5) reduce + epilogue
-        constexpr bool one = WF == W_Q4_1 || WF == W_Q5_1;
-        float s[R];
-#pragma unroll
-        for (int r = 0; r < R; r++) s[r] = one ? wave_sum63(acc[r]) + wave_sum63(acc2[r]) : wave_sum63(acc[r]) + 0.0f;
-        if constexpr (!EMIT) {
-#ifdef MV_PROBE
-            if (s[0] == 1.2345f) g_probe[0] = 0;  // orders the stamp after the dots
-#endif
-            PROBE(2);
-#pragma unroll
-            for (int r = 0; r < R; r++) {
-                const int row = row0 + r;
-                if (lane == 63 && row < M) Ent.y[row] = epi_apply(Ent.epi, s[r], ep[r]);
-            }
-        } else {
-            // RW rows per block (a multiple of 32): apply the epilogue and emit each 32 rows as
-            // one quantization block of the next matmul's input (ggml Q8 / fp16 / fp32)
-#pragma unroll
-            for (int r = 0; r < R; r++)
-                if (lane == 63) red[wave * R + r] = s[r];
-            __syncthreads();
-            PROBE(2);
-            if (tid < RW) {
-                const int row = wgi * RW + tid;
-                float vv = 0.0f;
-                if (row < M) {
-                    vv = epi_apply(Ent.epi, red[tid], ep[0]);
-                    if (Ent.y) Ent.y[row] = vv;
-                }
-                if (Ent.act_out.fmt >= 0 && Ent.emit) emit32(Ent.act_out, 0, row, vv);
-            }
-        }
-        PROBE(3);
-        wgi += stride;
-        if (stride <= 0 || wgi >= nblk) break;
-        if constexpr (EMIT) __syncthreads();  // red[] reuse
-        row0 = wgi * RW + wave * R;
-#pragma unroll
-        for (int r = 0; r < R; r++) rows[r] = min(row0 + r, M - 1);
-#pragma unroll
-        for (int u = 0; u < U; u++)
-#pragma unroll
-            for (int r = 0; r < R; r++) w[r][u] = load_unit<WF>(W, rows[r], u, lane);
-        if constexpr (!EMIT) {
-#pragma unroll
-            for (int r = 0; r < R; r++) ep[r] = epi_load(Ent, rows[r]);
-        } else {
-            ep[0] = epi_load(Ent, min(wgi * RW + (tid < RW ? tid : 0), M - 1));
-        }
-    }
-}
-
-// WFIX >= 0: every entry of the group has weight type WFIX (one body, fewer registers);
-// WFIX < 0: per-entry switch.
-template <int R, int U, bool PRO, bool EMIT, int WFIX>
-__global__ __launch_bounds__(256) void k_mv(MVGroup g) {
-    constexpr int NW = 4;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    __shared__ float red[NW * R];
-    int e = 0;
-#pragma unroll 1
-    while (e + 1 < g.n && (int)blockIdx.x >= g.e[e + 1].block0) e++;
-    const MVEntry & Ent = g.e[e];
-    const int wgi = (int)blockIdx.x - Ent.block0;
-    if constexpr (WFIX >= 0) {
-        mv_body<WFIX, R, U, PRO, EMIT, NW>(Ent, wgi, g.stride, smem, red);
-    } else {
-        switch (Ent.W.type) {
-            case W_F32: mv_body<W_F32, R, U, PRO, EMIT, NW>(Ent, wgi, g.stride, smem, red); break;
-            case W_F16: mv_body<W_F16, R, U, PRO, EMIT, NW>(Ent, wgi, g.stride, smem, red); break;
-            case W_Q4_0: mv_body<W_Q4_0, R, U, PRO, EMIT, NW>(Ent, wgi, g.stride, smem, red); break;
-            case W_Q4_1: mv_body<W_Q4_1, R, U, PRO, EMIT, NW>(Ent, wgi, g.stride, smem, red); break;
-            case W_Q5_0: mv_body<W_Q5_0, R, U, PRO, EMIT, NW>(Ent, wgi, g.stride, smem, red); break;
-            case W_Q5_1: mv_body<W_Q5_1, R, U, PRO, EMIT, NW>(Ent, wgi, g.stride, smem, red); break;
-            case W_Q8_0: mv_body<W_Q8_0, R, U, PRO, EMIT, NW>(Ent, wgi, g.stride, smem, red); break;
-            default: break;
-        }
-    }
-}
+// instantiated in the mv_*.hip units
+extern template bool launch_mv_shape<-1>(hipStream_t, MVGroup &, int, int, int, bool, dim3);
+extern template bool launch_mv_shape<W_F16>(hipStream_t, MVGroup &, int, int, int, bool, dim3);
+extern template bool launch_mv_shape<W_Q4_0>(hipStream_t, MVGroup &, int, int, int, bool, dim3);
+extern template bool launch_mv_shape<W_Q4_1>(hipStream_t, MVGroup &, int, int, int, bool, dim3);
+extern template bool launch_mv_shape<W_Q5_0>(hipStream_t, MVGroup &, int, int, int, bool, dim3);
+extern template bool launch_mv_shape<W_Q5_1>(hipStream_t, MVGroup &, int, int, int, bool, dim3);
+extern template bool launch_mv_shape<W_Q8_0>(hipStream_t, MVGroup &, int, int, int, bool, dim3);
 
 static int g_mv_cus = 256;
 void set_mv_device_cus(int n) { g_mv_cus = n > 0 ? n : 256; }
 
-template <int U, int WFIX>
-static void launch_mv_w(hipStream_t st, MVGroup & g, bool pro, bool emit, dim3 grid) {
-    if (emit) hipLaunchKernelGGL((k_mv<8, U, true, true, WFIX>), grid, dim3(256), g.lds_bytes, st, g);
-    else if (pro) hipLaunchKernelGGL((k_mv<2, U, true, false, WFIX>), grid, dim3(256), g.lds_bytes, st, g);
-    else hipLaunchKernelGGL((k_mv<2, U, false, false, WFIX>), grid, dim3(256), 0, st, g);
-}
-
-template <int U>
-static void launch_mv_u(hipStream_t st, MVGroup & g, bool pro, bool emit, int wfix, dim3 grid) {
-    switch (wfix) {
-        case W_F16: launch_mv_w<U, W_F16>(st, g, pro, emit, grid); break;
-        case W_Q4_0: launch_mv_w<U, W_Q4_0>(st, g, pro, emit, grid); break;
-        case W_Q4_1: launch_mv_w<U, W_Q4_1>(st, g, pro, emit, grid); break;
-        case W_Q5_0: launch_mv_w<U, W_Q5_0>(st, g, pro, emit, grid); break;
-        case W_Q5_1: launch_mv_w<U, W_Q5_1>(st, g, pro, emit, grid); break;
-        case W_Q8_0: launch_mv_w<U, W_Q8_0>(st, g, pro, emit, grid); break;
-        default: launch_mv_w<U, -1>(st, g, pro, emit, grid); break;
-    }
-}
-
 bool launch_mv_group(hipStream_t st, MVGroup & g) {
-    bool emit = false, prologue = false, plain = false;
-    for (int i = 0; i < g.n; i++) {
-        emit |= g.e[i].emit != 0;
-        (g.e[i].src == SRC_ACT ? plain : prologue) = true;
-    }
-    if (prologue && plain) {
-        fprintf(stderr, "rwkv: matvec group mixes activation and prologue sources\n");
+    bool emit = false;
+    for (int i = 0; i < g.n; i++) emit |= g.e[i].emit != 0;
+    const int src = g.e[0].src, form = g.e[0].form;
+    for (int i = 1; i < g.n; i++)
+        if (g.e[i].src != src || (src == SRC_LNMIX && g.e[i].form != form)) {
+            fprintf(stderr, "rwkv: matvec group mixes input sources / token-shift forms\n");
+            return false;
+        }
+    const bool prologue = src != SRC_ACT;
+    const int srck = src == SRC_ACT ? MVK_ACT : src == SRC_F32 ? MVK_F32 : MVK_LN;
+    if (emit && src == SRC_LNMIX && form == 2) {
+        fprintf(stderr, "rwkv: emitting matvec with a plain LayerNorm input is not instantiated\n");
         return false;
     }
     if (emit && !prologue) {
@@ -535,15 +77,22 @@ bool launch_mv_group(hipStream_t st, MVGroup & g) {
         grid = 2 * g_mv_cus;
         g.stride = grid;
     }
-    const int U = umax <= 1 ? 1 : umax <= 2 ? 2 : 4;
+    int U = umax <= 1 ? 1 : umax <= 2 ? 2 : 4;
+    if (src != SRC_ACT && U == 2) U = 4;
     int wfix = g.e[0].W.type;
     for (int i = 1; i < g.n; i++)
         if (g.e[i].W.type != wfix) wfix = -1;
-    switch (U) {
-        case 1: launch_mv_u<1>(st, g, prologue, emit, wfix, dim3(grid)); break;
-        case 2: launch_mv_u<2>(st, g, prologue, emit, wfix, dim3(grid)); break;
-        default: launch_mv_u<4>(st, g, prologue, emit, wfix, dim3(grid)); break;
+    bool ok = false;
+    switch (wfix) {
+        case W_F16: ok = launch_mv_shape<W_F16>(st, g, U, srck, form, emit, dim3(grid)); break;
+        case W_Q4_0: ok = launch_mv_shape<W_Q4_0>(st, g, U, srck, form, emit, dim3(grid)); break;
+        case W_Q4_1: ok = launch_mv_shape<W_Q4_1>(st, g, U, srck, form, emit, dim3(grid)); break;
+        case W_Q5_0: ok = launch_mv_shape<W_Q5_0>(st, g, U, srck, form, emit, dim3(grid)); break;
+        case W_Q5_1: ok = launch_mv_shape<W_Q5_1>(st, g, U, srck, form, emit, dim3(grid)); break;
+        case W_Q8_0: ok = launch_mv_shape<W_Q8_0>(st, g, U, srck, form, emit, dim3(grid)); break;
+        default: ok = launch_mv_shape<-1>(st, g, U, srck, form, emit, dim3(grid)); break;
     }
+    if (!ok) return false;
     HIP_OK(hipGetLastError());
     return true;
 }
@@ -620,16 +169,17 @@ __device__ __forceinline__ float tree_wave32(const float (&p)[32]) {
     return (0.0f + 0.0f) + (r1 + r0);
 }
 
-// One row of the v6 decay LoRA tail by one thread (units <= 32, one per lane of k_mm);
-// PF units were prefetched into wp[].
-template <int WF, int PF>
+// One row of the v6 decay LoRA tail by one thread: lanes 0..nl-1 of k_mm's row (nl <= NL <= 32,
+// one unit each); the first PF units were prefetched into wp[].  Partials of lanes >= NL are
+// compile-time zeros, so the tree folds to the nonzero part.
+template <int WF, int PF, int NL>
 __device__ __forceinline__ float decay_row_thread(const DMat & W, int row, const ActBuf & act, int nl,
                                                   const WBlk (&wp)[PF > 0 ? PF : 1]) {
     float p[32], p2[32];
 #pragma unroll
     for (int l = 0; l < 32; l++) {
         p[l] = p2[l] = 0.0f;
-        if (l < nl) {
+        if (l < NL && l < nl) {
             const WBlk w = (l < PF) ? wp[l < PF ? l : 0] : load_unit<WF>(W, row, 0, l);
             const AUnit x = load_act_unit<WF, true>(act, 0, l);
             dot_unit<WF>(w, x, p[l], p2[l]);
@@ -664,10 +214,10 @@ template <int WF>
 __device__ __forceinline__ void decay_rows(const Att6Dec & a, const ActBuf & act, float * sw, int c0, int S) {
     const int tid = threadIdx.x;
     const int nl = one_unit_lanes(WF, a.wd2.K);
-    if (nl > 0 && nl <= 32) {
+    if (nl > 0 && nl <= 16) {
         const WBlk none[1] = {};
         if (tid < S) {
-            const float s = decay_row_thread<WF, 0>(a.wd2, c0 + tid, act, nl, none);
+            const float s = decay_row_thread<WF, 0, 16>(a.wd2, c0 + tid, act, nl, none);
             sw[tid] = expf(-expf(s + a.decay[c0 + tid]));
         }
     } else {
@@ -712,7 +262,7 @@ __global__ __launch_bounds__(256) void k_att6_dec(Att6Dec a) {
         if (a.w) sw[tid] = a.w[c0 + tid];
     }
     ActBuf act;
-    if (!a.w) {
+    if (WF != -2 && !a.w) {
         // v6 decay LoRA tail: w = exp(-exp(Wd2 . dl + decay)), rwkv_graph.inc:357-367
         const int D = a.wd2.K;
         act = lds_act(smem, act_fmt_for(a.wd2.type), D);
@@ -722,10 +272,11 @@ __global__ __launch_bounds__(256) void k_att6_dec(Att6Dec a) {
         }
     }
     __syncthreads();
-    if (!a.w) {
-        if constexpr (PF > 0) {
+    if (WF != -2 && !a.w) {
+        if constexpr (WF == -2) {
+        } else if constexpr (PF > 0) {
             if (tid < S) {
-                const float s = decay_row_thread<WF, PF>(a.wd2, c0 + tid, act, a.wd2.K >> 5, wp);
+                const float s = decay_row_thread<WF, PF, PF>(a.wd2, c0 + tid, act, a.wd2.K >> 5, wp);
                 sw[tid] = expf(-expf(s + a.decay[c0 + tid]));
             }
         } else {
@@ -809,7 +360,9 @@ bool launch_att6_dec(hipStream_t st, const Att6Dec & a) {
     }
     dim3 grid(a.H), block(std::max(threads, 64));
     const bool pf = !a.w && a.wd2.type >= W_Q4_0 && (a.wd2.K >> 5) <= 4;
-    if (!pf) {
+    if (a.w) {
+        hipLaunchKernelGGL((k_att6_dec<-2, 0>), grid, block, lds, st, a);  // v5: no decay LoRA
+    } else if (!pf) {
         hipLaunchKernelGGL((k_att6_dec<-1, 0>), grid, block, lds, st, a);
     } else {
         switch (a.wd2.type) {

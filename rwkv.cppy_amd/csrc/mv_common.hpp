@@ -1,0 +1,547 @@
+// mv_common.hpp -- the decode matvec (k_mv) and the device helpers it shares with the
+// per-head attention kernels.  Included by kernels_decode.hip and by the per-weight-type
+// instantiation units mv_*.hip (so the many launch shapes compile in parallel).
+#pragma once
+#include "device_common.hpp"
+#include "kernels.hpp"
+
+#include <stdio.h>
+
+namespace rwkvmi {
+
+// group input kinds (compile-time in k_mv)
+enum MVKind : int { MVK_ACT = 0, MVK_F32 = 1, MVK_LN = 2 };
+
+
+// Phase timestamps for tools/mv_probe.hip (never defined in the library build).
+#ifdef MV_PROBE
+__device__ unsigned long long * g_probe;
+#define PROBE(k)                                                                               \
+    do {                                                                                       \
+        if (threadIdx.x == 0 && g_probe) g_probe[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define PROBE(k) \
+    do {         \
+    } while (0)
+#endif
+
+// LDS image of one activation row in the consumer's format.
+__device__ __forceinline__ ActBuf lds_act(char * smem, int fmt, int K) {
+    ActBuf a;
+    a.fmt = fmt;
+    a.K = K;
+    a.q = nullptr;
+    a.d = a.s = nullptr;
+    a.qsum = nullptr;
+    a.h = nullptr;
+    a.f = nullptr;
+    if (fmt == A_F32) {
+        a.f = (float *)smem;
+    } else if (fmt == A_F16) {
+        a.h = (__half *)smem;
+    } else {
+        const int nb = K >> 5;
+        a.q = (int8_t *)smem;
+        a.d = (float *)(smem + ((K + 15) & ~15));
+        a.s = a.d + ((nb + 3) & ~3);
+        a.qsum = (int *)(a.s + ((nb + 3) & ~3));
+    }
+    return a;
+}
+
+inline int lds_bytes_for(int fmt, int K) {
+    if (fmt == A_F32) return K * 4;
+    if (fmt == A_F16) return K * 2;
+    const int nb = K / 32;
+    return ((K + 15) & ~15) + 3 * ((nb + 3) & ~3) * 4;
+}
+
+// --------------------------------------------------------------------------- decode matvec
+// A lane owns 16-byte "units" of a row: quantized weights one 32-block (lane + 64u), F16 eight
+// halves (k = 8*lane + 512u), F32 four floats (k = 4*lane + 256u) -- the same lane/unit
+// assignment and accumulation order as the batched kernel k_mm, so decode and sequence
+// results are bit-identical.  All R*U weight units of a wave are loaded before anything else
+// waits (rows past M clamp to M-1, units past K clamp to the last unit and are skipped in the
+// dot), so the whole row-block is one HBM round trip, overlapped with the prologue.
+
+__host__ __device__ inline int mv_units(int type, int K) {
+    if (type == W_F32) return (K + 255) / 256;
+    if (type == W_F16) return (K + 511) / 512;
+    return (K / 32 + 63) / 64;
+}
+
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) const i32x4_t lds_i32x4_t;
+typedef __attribute__((address_space(3))) const float lds_float_t;
+typedef __attribute__((address_space(3))) const int lds_int_t;
+
+template <bool LDS>
+__device__ __forceinline__ int4 load16(const void * p) {
+    if constexpr (LDS) {
+        const i32x4_t t = *(const lds_i32x4_t *)(uintptr_t)p;
+        return make_int4(t.x, t.y, t.z, t.w);
+    } else {
+        return *(const int4 *)p;
+    }
+}
+template <bool LDS>
+__device__ __forceinline__ float loadf(const float * p) {
+    if constexpr (LDS) return *(const lds_float_t *)(uintptr_t)p;
+    else return *p;
+}
+template <bool LDS>
+__device__ __forceinline__ int loadi(const int * p) {
+    if constexpr (LDS) return *(const lds_int_t *)(uintptr_t)p;
+    else return *p;
+}
+
+template <int WF>
+__device__ __forceinline__ WBlk load_unit(const DMat & W, int row, int u, int lane) {
+    const int K = W.K;
+    if constexpr (WF == W_F32) {
+        WBlk w;
+        const int k = min(lane * 4 + u * 256, K - 4);
+        w.q0 = *(const int4 *)((const float *)W.qs + (size_t)row * K + k);
+        return w;
+    } else if constexpr (WF == W_F16) {
+        WBlk w;
+        const int k = min(lane * 8 + u * 512, K - 8);
+        w.q0 = *(const int4 *)((const __half *)W.qs + (size_t)row * K + k);
+        return w;
+    } else {
+        const int nb = K >> 5;
+        const int b = min(lane + u * 64, nb - 1);
+        return load_wblk<WF>(W, (size_t)row * nb + b);
+    }
+}
+
+struct AUnit {
+    int4 lo, hi;
+    float d, s;
+    int qs;
+};
+
+template <int WF, bool LDS>
+__device__ __forceinline__ AUnit load_act_unit(const ActBuf & a, int u, int lane) {
+    AUnit x;
+    const int K = a.K;
+    if constexpr (WF == W_F32) {
+        x.lo = load16<LDS>(a.f + min(lane * 4 + u * 256, K - 4));
+    } else if constexpr (WF == W_F16) {
+        x.lo = load16<LDS>(a.h + min(lane * 8 + u * 512, K - 8));
+    } else {
+        const int b = min(lane + u * 64, (K >> 5) - 1);
+        x.lo = load16<LDS>(a.q + (size_t)b * 32);
+        x.hi = load16<LDS>(a.q + (size_t)b * 32 + 16);
+        x.d = loadf<LDS>(a.d + b);
+        x.qs = loadi<LDS>(a.qsum + b);
+        x.s = (WF == W_Q4_1 || WF == W_Q5_1) ? loadf<LDS>(a.s + b) : 0.0f;
+    }
+    return x;
+}
+
+template <int WF>
+__device__ __forceinline__ bool unit_valid(int K, int u, int lane) {
+    if constexpr (WF == W_F32) return lane * 4 + u * 256 < K;
+    else if constexpr (WF == W_F16) return lane * 8 + u * 512 < K;
+    else return lane + u * 64 < (K >> 5);
+}
+
+template <int WF>
+__device__ __forceinline__ void dot_unit(const WBlk & w, const AUnit & x, float & acc, float & acc2) {
+    if constexpr (WF == W_F32) {
+        float s = acc;
+        s = fmaf(__int_as_float(w.q0.x), __int_as_float(x.lo.x), s);
+        s = fmaf(__int_as_float(w.q0.y), __int_as_float(x.lo.y), s);
+        s = fmaf(__int_as_float(w.q0.z), __int_as_float(x.lo.z), s);
+        s = fmaf(__int_as_float(w.q0.w), __int_as_float(x.lo.w), s);
+        acc = s;
+    } else if constexpr (WF == W_F16) {
+        float s = acc;
+        s = __builtin_amdgcn_fdot2(__builtin_bit_cast(half2_t, w.q0.x), __builtin_bit_cast(half2_t, x.lo.x), s, false);
+        s = __builtin_amdgcn_fdot2(__builtin_bit_cast(half2_t, w.q0.y), __builtin_bit_cast(half2_t, x.lo.y), s, false);
+        s = __builtin_amdgcn_fdot2(__builtin_bit_cast(half2_t, w.q0.z), __builtin_bit_cast(half2_t, x.lo.z), s, false);
+        s = __builtin_amdgcn_fdot2(__builtin_bit_cast(half2_t, w.q0.w), __builtin_bit_cast(half2_t, x.lo.w), s, false);
+        acc = s;
+    } else {
+        float dw, mw;
+        const int sumi = dot_wblk<WF>(w, x.lo, x.hi, x.qs, dw, mw);
+        acc = fmaf(dw * x.d, (float)sumi, acc);
+        if constexpr (WF == W_Q4_1 || WF == W_Q5_1) acc2 += mw * x.s;
+    }
+}
+
+// Per-thread register image of a K-vector: thread t owns k = i*NT + t (i < E).
+template <int E, int NT = 256>
+__device__ __forceinline__ void load_vec(float (&v)[E], const float * p, int K) {
+#pragma unroll
+    for (int i = 0; i < E; i++) {
+        // unconditional (clamped) loads: no per-load branches, so the waitcnt pass keeps
+        // them all in flight
+        const int k = i * NT + (int)threadIdx.x;
+        const float t = p[min(k, K - 1)];
+        v[i] = (k < K) ? t : 0.0f;
+    }
+}
+
+// Matvec prologue (SRC_F32 / SRC_LNMIX): the waves of a workgroup build the activation image
+// in LDS chunk by chunk (512 elements per wave-chunk, 8 consecutive elements per lane, so a
+// quantization block is one lane quad): token-shift mix of the LayerNorm output, then ggml's
+// Q8 quantization with quad DPP reductions (F16: packed halves, F32: as is).  Loading a chunk
+// (chunk_load) is separate from using it (chunk_store) so the first chunk's loads can be
+// issued ahead of the weight stream.
+struct ChunkIn {
+    float x[8], w[8], b[8], c[8], m[8];
+};
+
+__device__ __forceinline__ void ld8(float (&v)[8], const float * p) {
+    const float4 t0 = *(const float4 *)p, t1 = *(const float4 *)(p + 4);
+    v[0] = t0.x, v[1] = t0.y, v[2] = t0.z, v[3] = t0.w, v[4] = t1.x, v[5] = t1.y, v[6] = t1.z, v[7] = t1.w;
+}
+
+template <int SRCK, int FORM>
+__device__ __forceinline__ void chunk_load(const MVEntry & E, int kc, ChunkIn & ci) {
+    if constexpr (SRCK == MVK_F32) {
+        ld8(ci.x, E.f + kc);
+    } else {
+        ld8(ci.x, E.x + kc);
+        ld8(ci.w, E.lnw + kc);
+        ld8(ci.b, E.lnb + kc);
+        if constexpr (FORM != 2) {
+            ld8(ci.c, E.carry + kc);
+            ld8(ci.m, E.mu + kc);
+        }
+    }
+}
+
+template <int WF, int SRCK, int FORM>
+__device__ __forceinline__ void chunk_store(const MVEntry & E, const ActBuf & a, const ChunkIn & ci, float mean,
+                                            float scale, bool write_carry, int k0, bool valid, int lane) {
+    float v[8];
+    if constexpr (SRCK == MVK_F32) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) v[j] = ci.x[j];
+    } else {
+        float xa[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            xa[j] = ln_apply(ci.x[j], mean, scale, ci.w[j], ci.b[j]);
+            if constexpr (FORM == 2) v[j] = xa[j];
+            else if constexpr (FORM == 0) v[j] = xa[j] * ci.m[j] + (ci.c[j] - ci.c[j] * ci.m[j]);
+            else v[j] = (ci.c[j] - xa[j]) * ci.m[j] + xa[j];
+        }
+        if (write_carry && valid) {
+            *(float4 *)(E.carry_out + k0) = make_float4(xa[0], xa[1], xa[2], xa[3]);
+            *(float4 *)(E.carry_out + k0 + 4) = make_float4(xa[4], xa[5], xa[6], xa[7]);
+        }
+    }
+    if constexpr (WF == W_F32) {
+        if (valid) {
+            *(float4 *)(a.f + k0) = make_float4(v[0], v[1], v[2], v[3]);
+            *(float4 *)(a.f + k0 + 4) = make_float4(v[4], v[5], v[6], v[7]);
+        }
+    } else if constexpr (WF == W_F16) {
+        int p[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            p[j] = __builtin_bit_cast(int, __halves2half2(__float2half(v[2 * j]), __float2half(v[2 * j + 1])));
+        if (valid) *(int4 *)(a.h + k0) = make_int4(p[0], p[1], p[2], p[3]);
+    } else {
+        // ggml quantize_row_q8_0 / q8_1 (x86): d = amax/127, q = rint(x*127/amax)
+        float am = 0.0f;
+#pragma unroll
+        for (int j = 0; j < 8; j++) am = fmaxf(am, fabsf(v[j]));
+        am = fmaxf(am, __int_as_float(dpp_mov<0xB1>(__float_as_int(am))));
+        am = fmaxf(am, __int_as_float(dpp_mov<0x4E>(__float_as_int(am))));
+        const float d = am / 127.f;
+        const float id = (am != 0.0f) ? 127.f / am : 0.0f;
+        int lo = 0, hi = 0, sum = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int q = (int)rintf(v[j] * id);
+            sum += q;
+            if (j < 4) lo |= (q & 0xff) << (8 * j);
+            else hi |= (q & 0xff) << (8 * (j - 4));
+        }
+        sum += dpp_mov<0xB1>(sum);
+        sum += dpp_mov<0x4E>(sum);
+        if (valid) {
+            *(int2 *)(a.q + k0) = make_int2(lo, hi);
+            if ((lane & 3) == 0) {
+                const int bi = k0 >> 5;
+                a.d[bi] = f16_round(d);
+                a.qsum[bi] = sum;
+                if (a.fmt == A_Q8_1) a.s[bi] = f16_round(d * (float)sum);
+            }
+        }
+    }
+}
+
+// Epilogue operands of one output row, loaded at kernel start (not after the dots).
+struct EpiIn {
+    float y, aux, bias;
+};
+// Branch-free: absent operands read a zero word instead (uniform pointer select), so these
+// loads never split the kernel into blocks that make the waitcnt pass drain the weight stream.
+static __device__ const float g_mv_zero[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+__device__ __forceinline__ EpiIn epi_load(const MVEntry & E, int row) {
+    EpiIn p;
+    const float * py = E.y ? E.y + row : g_mv_zero;
+    const float * pa = E.aux ? E.aux + row : g_mv_zero;
+    const float * pb = E.bias ? E.bias + row : g_mv_zero;
+    p.y = *py;
+    p.aux = *pa;
+    p.bias = *pb;
+    return p;
+}
+__device__ __forceinline__ float epi_apply(int epi, float acc, const EpiIn & p) {
+    switch (epi) {
+        case EPI_SIGMOID: return sigmoidf_(acc);
+        case EPI_TANH: return tanhf(acc);
+        case EPI_SILU: return siluf_(acc);
+        case EPI_RELU_SQ: {
+            const float r = acc > 0.0f ? acc : 0.0f;
+            return r * r;
+        }
+        case EPI_ADD: return p.y + acc;
+        case EPI_SIGMUL_ADD: return p.y + sigmoidf_(p.aux) * acc;
+        case EPI_DECAY6: return expf(-expf(acc + p.bias));
+        case EPI_DECAY7: return expf(sigmoidf_(acc + p.bias) * -0.606531f);
+        case EPI_SIGMOID_BIAS: return sigmoidf_(acc + p.bias);
+        case EPI_VMIX7: return p.y + (p.aux - p.y) * sigmoidf_(acc + p.bias);
+        default: return acc;
+    }
+}
+
+// One workgroup = NW waves x R rows (RW = NW*R rows per row block).  E == 0: the input is an
+// activation buffer in global memory (SRC_ACT, NW = 4); E > 0: the prologue builds it in LDS
+// (SRC_F32 / SRC_LNMIX, K <= 64*NW*E; NW = 16 so the per-wave prologue work is short).
+// stride > 0: the workgroup walks row blocks wgi, wgi+stride, ... with one prologue.
+// Workgroup roles: waves 0..NW-1 stream the weights and do the dots (R rows each); for
+// prologue sources NW more waves build the activation image (LayerNorm statistics each for
+// itself, one 512-element chunk each, ...).  Separate waves keep the two load streams apart:
+// vmcnt is in order per wave, so a prologue wave never waits behind the weight stream and a
+// dot wave's weights are in flight from its first instruction.
+template <int WF, int R, int U, int SRCK, int FORM, bool EMIT, int NW, int LNP>
+__device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, int stride, char * smem, float * red) {
+    constexpr bool PRO = SRCK != MVK_ACT;
+    constexpr int LNR = LNP > 0 ? LNP : 1;
+    constexpr int RW = NW * R;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const DMat & W = Ent.W;
+    const int M = W.M, K = W.K;
+    const int nblk = (M + RW - 1) / RW;
+    const int units = mv_units(WF, K);
+    PROBE(0);
+    ActBuf a;
+    if constexpr (PRO) {
+        a = lds_act(smem, act_fmt_for(WF), K);
+        if (wave >= NW) {
+            // ---- prologue wave
+            const int pw = wave - NW;
+            float lv[LNR];
+            ChunkIn ci;
+            const int k0 = pw * 512 + lane * 8;
+            if constexpr (SRCK == MVK_LN) ln_load_regs<LNR>(Ent.x, K, lv);
+            chunk_load<SRCK, FORM>(Ent, min(k0, K - 8), ci);
+            float mean = 0.0f, scale = 0.0f;
+            if constexpr (SRCK == MVK_LN) ln_stats_regs<LNR>(lv, K, 1e-5f, mean, scale);
+            const bool write_carry = Ent.carry_out && wgi == (int)blockIdx.x - Ent.block0;
+            chunk_store<WF, SRCK, FORM>(Ent, a, ci, mean, scale, write_carry, k0, k0 < K, lane);
+            for (int c = pw + NW; c * 512 < K; c += NW) {
+                const int kk = c * 512 + lane * 8;
+                chunk_load<SRCK, FORM>(Ent, min(kk, K - 8), ci);
+                chunk_store<WF, SRCK, FORM>(Ent, a, ci, mean, scale, write_carry, kk, kk < K, lane);
+            }
+            __syncthreads();
+            // take part in the dot waves' barriers, then leave
+            for (;;) {
+                if constexpr (EMIT) __syncthreads();
+                wgi += stride;
+                if (stride <= 0 || wgi >= nblk) break;
+                if constexpr (EMIT) __syncthreads();
+            }
+            return;
+        }
+    }
+    // ---- dot wave: this wave's weight units (HBM) and the epilogue operands
+    int row0 = wgi * RW + wave * R;
+    int rows[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) rows[r] = min(row0 + r, M - 1);
+    WBlk w[R][U];
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+        for (int r = 0; r < R; r++) w[r][u] = load_unit<WF>(W, rows[r], u, lane);
+    EpiIn ep[R];
+    if constexpr (!EMIT) {
+#pragma unroll
+        for (int r = 0; r < R; r++) ep[r] = epi_load(Ent, rows[r]);
+    } else {
+        ep[0] = epi_load(Ent, min(wgi * RW + (tid < RW ? tid : 0), M - 1));
+    }
+    if constexpr (PRO) __syncthreads();  // activation image ready
+    else a = Ent.act;
+    PROBE(1);
+
+    for (;;) {
+        // dots
+        float acc[R], acc2[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) acc[r] = acc2[r] = 0.0f;
+        for (int u0 = 0; u0 < units; u0 += U) {
+            if (u0 > 0) {
+#pragma unroll
+                for (int u = 0; u < U; u++)
+#pragma unroll
+                    for (int r = 0; r < R; r++) w[r][u] = load_unit<WF>(W, rows[r], u0 + u, lane);
+            }
+            AUnit x[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) x[u] = load_act_unit<WF, PRO>(a, u0 + u, lane);
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                if (unit_valid<WF>(K, u0 + u, lane)) {
+#pragma unroll
+                    for (int r = 0; r < R; r++) dot_unit<WF>(w[r][u], x[u], acc[r], acc2[r]);
+                }
+            }
+        }
+
+        // reduce + epilogue
+        constexpr bool one = WF == W_Q4_1 || WF == W_Q5_1;
+        float s[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) s[r] = one ? wave_sum63(acc[r]) + wave_sum63(acc2[r]) : wave_sum63(acc[r]) + 0.0f;
+        if constexpr (!EMIT) {
+#ifdef MV_PROBE
+            if (s[0] == 1.2345f) g_probe[0] = 0;  // orders the stamp after the dots
+#endif
+            PROBE(2);
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                const int row = row0 + r;
+                if (lane == 63 && row < M) Ent.y[row] = epi_apply(Ent.epi, s[r], ep[r]);
+            }
+        } else {
+            // RW rows per block (a multiple of 32): apply the epilogue and emit each 32 rows as
+            // one quantization block of the next matmul's input (ggml Q8 / fp16 / fp32)
+#pragma unroll
+            for (int r = 0; r < R; r++)
+                if (lane == 63) red[wave * R + r] = s[r];
+            __syncthreads();
+            PROBE(2);
+            if (tid < RW) {
+                const int row = wgi * RW + tid;
+                float vv = 0.0f;
+                if (row < M) {
+                    vv = epi_apply(Ent.epi, red[tid], ep[0]);
+                    if (Ent.y) Ent.y[row] = vv;
+                }
+                if (Ent.act_out.fmt >= 0 && Ent.emit) emit32(Ent.act_out, 0, row, vv);
+            }
+        }
+        PROBE(3);
+        wgi += stride;
+        if (stride <= 0 || wgi >= nblk) break;
+        if constexpr (EMIT) __syncthreads();  // red[] reuse
+        row0 = wgi * RW + wave * R;
+#pragma unroll
+        for (int r = 0; r < R; r++) rows[r] = min(row0 + r, M - 1);
+#pragma unroll
+        for (int u = 0; u < U; u++)
+#pragma unroll
+            for (int r = 0; r < R; r++) w[r][u] = load_unit<WF>(W, rows[r], u, lane);
+        if constexpr (!EMIT) {
+#pragma unroll
+            for (int r = 0; r < R; r++) ep[r] = epi_load(Ent, rows[r]);
+        } else {
+            ep[0] = epi_load(Ent, min(wgi * RW + (tid < RW ? tid : 0), M - 1));
+        }
+    }
+}
+
+// WFIX >= 0: every entry of the group has weight type WFIX (one body, fewer registers);
+// WFIX < 0: per-entry switch.  SRCK / FORM: the group's input source and token-shift form
+// (compile-time, so the prologue has no data-independent branches).
+template <int R, int U, int SRCK, int FORM, bool EMIT, int WFIX, int LNP>
+__global__ __launch_bounds__(512) void k_mv(MVGroup g) {
+    constexpr int NW = 4;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    __shared__ float red[NW * R];
+    int e = 0;
+#pragma unroll 1
+    while (e + 1 < g.n && (int)blockIdx.x >= g.e[e + 1].block0) e++;
+    const MVEntry & Ent = g.e[e];
+    const int wgi = (int)blockIdx.x - Ent.block0;
+    if constexpr (WFIX >= 0) {
+        mv_body<WFIX, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, g.stride, smem, red);
+    } else {
+        switch (Ent.W.type) {
+            case W_F32: mv_body<W_F32, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, g.stride, smem, red); break;
+            case W_F16: mv_body<W_F16, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, g.stride, smem, red); break;
+            case W_Q4_0: mv_body<W_Q4_0, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, g.stride, smem, red); break;
+            case W_Q4_1: mv_body<W_Q4_1, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, g.stride, smem, red); break;
+            case W_Q5_0: mv_body<W_Q5_0, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, g.stride, smem, red); break;
+            case W_Q5_1: mv_body<W_Q5_1, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, g.stride, smem, red); break;
+            case W_Q8_0: mv_body<W_Q8_0, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, g.stride, smem, red); break;
+            default: break;
+        }
+    }
+}
+
+// One weight-type translation unit (mv_*.hip) instantiates every launch shape for WFIX.
+// LayerNorm prologues hold the normalized vector in registers: LNP = 32 (K <= 2048) or 64
+// (K <= 4096) elements per lane.
+template <int WFIX>
+bool launch_mv_shape(hipStream_t st, MVGroup & g, int U, int srck, int form, bool emit, dim3 grid) {
+#define MV_L(Rv, Uv, S, F, E, P) \
+    hipLaunchKernelGGL((k_mv<Rv, Uv, S, F, E, WFIX, P>), grid, dim3((S) == MVK_ACT ? 256 : 512), g.lds_bytes, st, g)
+    const int K = g.e[0].W.K;
+    if (srck == MVK_ACT) {
+        if (U == 1) MV_L(2, 1, MVK_ACT, 0, false, 0);
+        else if (U == 2) MV_L(2, 2, MVK_ACT, 0, false, 0);
+        else MV_L(2, 4, MVK_ACT, 0, false, 0);
+        return true;
+    }
+    if (srck == MVK_F32) {
+        if (U == 1) MV_L(2, 1, MVK_F32, 0, false, 0);
+        else MV_L(2, 4, MVK_F32, 0, false, 0);
+        return true;
+    }
+    for (int i = 1; i < g.n; i++)
+        if (g.e[i].W.K != K) {
+            fprintf(stderr, "rwkv: LayerNorm matvec group needs one K\n");
+            return false;
+        }
+    if (K > 64 * 64) {
+        fprintf(stderr, "rwkv: LayerNorm matvec prologue needs K <= 4096 (K=%d)\n", K);
+        return false;
+    }
+#define MV_P(S, F, E)                                         \
+    do {                                                      \
+        constexpr int Rv = (E) ? 8 : 2;                       \
+        if (K <= 2048) {                                      \
+            if (U == 1) MV_L(Rv, 1, S, F, E, 32);             \
+            else MV_L(Rv, 4, S, F, E, 32);                    \
+        } else {                                              \
+            if (U == 1) MV_L(Rv, 1, S, F, E, 64);             \
+            else MV_L(Rv, 4, S, F, E, 64);                    \
+        }                                                     \
+    } while (0)
+    if (emit) {
+        if (form == 0) MV_P(MVK_LN, 0, true);
+        else MV_P(MVK_LN, 1, true);
+    } else {
+        if (form == 0) MV_P(MVK_LN, 0, false);
+        else if (form == 1) MV_P(MVK_LN, 1, false);
+        else MV_P(MVK_LN, 2, false);
+    }
+#undef MV_P
+#undef MV_L
+    return true;
+}
+
+}  // namespace rwkvmi

@@ -1,0 +1,6 @@
+// mv_f16.hip -- decode matvec launch shapes for weight type W_F16 (see mv_common.hpp).
+#include "mv_common.hpp"
+
+namespace rwkvmi {
+template bool launch_mv_shape<W_F16>(hipStream_t, MVGroup &, int, int, int, bool, dim3);
+}  // namespace rwkvmi

@@ -4,6 +4,16 @@
 // dots reduced, end.  Build: see tools/gpu_probe.sh.
 #include "kernels_decode.hip"
 
+namespace rwkvmi {
+template bool launch_mv_shape<-1>(hipStream_t, MVGroup &, int, int, int, bool, dim3);
+template bool launch_mv_shape<W_F16>(hipStream_t, MVGroup &, int, int, int, bool, dim3);
+template bool launch_mv_shape<W_Q4_0>(hipStream_t, MVGroup &, int, int, int, bool, dim3);
+template bool launch_mv_shape<W_Q4_1>(hipStream_t, MVGroup &, int, int, int, bool, dim3);
+template bool launch_mv_shape<W_Q5_0>(hipStream_t, MVGroup &, int, int, int, bool, dim3);
+template bool launch_mv_shape<W_Q5_1>(hipStream_t, MVGroup &, int, int, int, bool, dim3);
+template bool launch_mv_shape<W_Q8_0>(hipStream_t, MVGroup &, int, int, int, bool, dim3);
+}  // namespace rwkvmi
+
 #include <algorithm>
 #include <string.h>
 #include <stdlib.h>

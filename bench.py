@@ -138,14 +138,14 @@ def main():
     assert L.rwkv_mi355x_state_upload(ctx.ptr, None)
     assert L.rwkv_mi355x_eval_device(ctx.ptr, sp, len(seq), True, None, True)  # warm-up / workspace
     ts = []
-    for _ in range(args.seq_reps):
+    for _ in range(max(args.seq_reps, 0)):
         assert L.rwkv_mi355x_state_upload(ctx.ptr, None)
         L.rwkv_mi355x_sync(ctx.ptr)
         t1 = time.perf_counter()
         assert L.rwkv_mi355x_eval_device(ctx.ptr, sp, len(seq), True, None, True)
         ts.append(time.perf_counter() - t1)
-    seq_s = min(ts)
-    seq_tps = args.seq_len / seq_s
+    seq_s = min(ts) if ts else float('nan')
+    seq_tps = args.seq_len / seq_s if ts else 0.0
     log(f'seq-eval T={args.seq_len}: {seq_s * 1e3:.1f} ms, {seq_tps:.0f} tok/s')
 
     # ---------------- ABI-level decode (host state, reference contract) ----------------
@@ -158,7 +158,7 @@ def main():
     for i in range(args.abi_steps):
         assert L.rwkv_eval(ctx.ptr, int(dec_tokens[i]), state.ctypes.data_as(P_F), state.ctypes.data_as(P_F),
                            logits.ctypes.data_as(P_F))
-    abi_tps = args.abi_steps / (time.perf_counter() - t2)
+    abi_tps = args.abi_steps / (time.perf_counter() - t2) if args.abi_steps > 0 else 0.0
     log(f'ABI decode (host state {state_len * 4 / 1e6:.1f} MB each way): {abi_tps:.1f} tok/s')
 
     # ---------------- dominant-kernel roofline (HIP events on the context stream) ----------------
@@ -186,9 +186,15 @@ def main():
     achieved = bytes_per_launch / (avg_us * 1e-6) / 1e9
     mm_ms = sum(k['ms'] for k in kstats) / args.timing_steps
     mm_bytes = sum(k['bytes'] for k in kstats) / args.timing_steps
+    traffic = None
+    pmc = os.path.join(REPO, 'profiles', 'pmc_traffic.json')
+    if os.path.isfile(pmc):
+        t = json.load(open(pmc)).get(args.config, {}).get(dom['name'])
+        if t:
+            traffic = t['traffic_bytes_per_launch']
     roofline = {
         'kernel': dom['name'], 'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-        'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': None,
+        'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic,
         'avg_launch_us': round(avg_us, 3), 'algorithmic_bytes_per_launch': round(bytes_per_launch),
         'all_matmuls_GBps': round(mm_bytes / (mm_ms * 1e-3) / 1e9, 1),
         'decode_bytes_per_token': round(L.rwkv_mi355x_decode_bytes(ctx.ptr, True)),

@@ -260,9 +260,7 @@ __global__ void k_init_state(float * st, size_t n, int C, int v4) {
 
 Engine::~Engine() {
     if (stream_) (void)hipStreamSynchronize(stream_);
-    for (auto & row : graphs_)
-        for (auto & g : row)
-            if (g) (void)hipGraphExecDestroy(g);
+    drop_graphs();
     for (void * p : ws_allocs_) (void)hipFree(p);
     if (htokens_) (void)hipHostFree(htokens_);
     collect_timing();
@@ -296,15 +294,24 @@ bool Engine::init() {
     return ensure_workspace(1) && init_state(dstate_[0]);
 }
 
+void Engine::drop_graphs() {
+    for (int i = 0; i < 2; i++)
+        for (int j = 0; j < 2; j++) {
+            if (graphs_[i][j]) (void)hipGraphExecDestroy(graphs_[i][j]);
+            if (tgraphs_[i][j]) (void)hipGraphExecDestroy(tgraphs_[i][j]);
+            graphs_[i][j] = tgraphs_[i][j] = nullptr;
+            for (const Pending & p : tpairs_[i][j]) {
+                event_pool_.push_back(p.a);
+                event_pool_.push_back(p.b);
+            }
+            tpairs_[i][j].clear();
+        }
+}
+
 bool Engine::ensure_workspace(int T) {
     if (T <= tcap_) return true;
     HIP_OK(hipStreamSynchronize(stream_));
-    for (auto & row : graphs_)
-        for (auto & gr : row)
-            if (gr) {
-                (void)hipGraphExecDestroy(gr);
-                gr = nullptr;
-            }
+    drop_graphs();
     // keep state and logits, drop the rest
     std::vector<void *> keep = {dstate_[0], dstate_[1], logits_};
     for (void * p : ws_allocs_) {
@@ -447,16 +454,7 @@ bool Engine::mm_launch(MMGroup & g, int wtype) {
     }
     // kernel class = the template instantiation rocprofv3 reports: k_mm<WF, RPW, NT>
     const std::string name = "k_mm<" + std::to_string(wtype) + ", " + (emit ? "8" : "2") + ", " + (g.T == 1 ? "1" : "4") + ">";
-    int si = -1;
-    for (size_t i = 0; i < stats_.size(); i++)
-        if (stats_[i].name == name) si = (int)i;
-    if (si < 0) {
-        stats_.push_back(KernelStat{name});
-        si = (int)stats_.size() - 1;
-    }
-    stats_[si].total_bytes += bytes;
-    stats_[si].total_flops += flops;
-    stats_[si].launches++;
+    const int si = add_stat(name);
     hipEvent_t a, b;
     if (event_pool_.size() >= 2) {
         a = event_pool_.back();
@@ -470,15 +468,27 @@ bool Engine::mm_launch(MMGroup & g, int wtype) {
     HIP_OK(hipEventRecord(a, stream_));
     const bool ok = launch_mm_group(stream_, g, wtype);
     HIP_OK(hipEventRecord(b, stream_));
-    pending_.push_back(Pending{si, a, b});
+    pending_.push_back(Pending{si, a, b, bytes, flops});
     return ok;
+}
+
+int Engine::add_stat(const std::string & name) {
+    for (size_t i = 0; i < stats_.size(); i++)
+        if (stats_[i].name == name) return (int)i;
+    stats_.push_back(KernelStat{name});
+    return (int)stats_.size() - 1;
 }
 
 void Engine::collect_timing() {
     for (auto & p : pending_) {
         float ms = 0;
-        if (hipEventSynchronize(p.b) == hipSuccess && hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess)
-            stats_[p.stat].total_ms += ms;
+        if (hipEventSynchronize(p.b) == hipSuccess && hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+            KernelStat & s = stats_[p.stat];
+            s.total_ms += ms;
+            s.total_bytes += p.bytes;
+            s.total_flops += p.flops;
+            s.launches++;
+        }
         event_pool_.push_back(p.a);
         event_pool_.push_back(p.b);
     }
@@ -759,17 +769,7 @@ bool Engine::mv(MVGroup & g) {
         bytes += (double)e.W.M * 4 * ((e.epi == EPI_ADD || e.epi == EPI_SIGMUL_ADD || e.epi == EPI_VMIX7) ? 2 : 1);
         flops += 2.0 * e.W.M * e.W.K;
     }
-    const std::string name = "k_mv<2>";
-    int si = -1;
-    for (size_t i = 0; i < stats_.size(); i++)
-        if (stats_[i].name == name) si = (int)i;
-    if (si < 0) {
-        stats_.push_back(KernelStat{name});
-        si = (int)stats_.size() - 1;
-    }
-    stats_[si].total_bytes += bytes;
-    stats_[si].total_flops += flops;
-    stats_[si].launches++;
+    const int si = add_stat("k_mv");
     hipEvent_t a, b;
     if (event_pool_.size() >= 2) {
         a = event_pool_.back();
@@ -783,7 +783,7 @@ bool Engine::mv(MVGroup & g) {
     HIP_OK(hipEventRecord(a, stream_));
     const bool ok = launch_mv_group(stream_, g);
     HIP_OK(hipEventRecord(b, stream_));
-    pending_.push_back(Pending{si, a, b});
+    pending_.push_back(Pending{si, a, b, bytes, flops});
     return ok;
 }
 
@@ -1022,7 +1022,37 @@ bool Engine::run_tokens(const uint32_t * tokens, size_t T, bool want_logits) {
         HIP_OK(hipMemcpyAsync(dtokens_, htokens_, n * 4, hipMemcpyHostToDevice, stream_));
         HIP_OK(hipEventRecord(tok_event_, stream_));
         const bool lg = last && want_logits;
-        if (n == 1 && use_graphs_ && !timing_) {
+        if (n == 1 && use_graphs_ && timing_) {
+            // timed graph: same kernels, an event pair around each (see tgraphs_)
+            hipGraphExec_t & ge = tgraphs_[cur_][lg ? 1 : 0];
+            std::vector<Pending> & tp = tpairs_[cur_][lg ? 1 : 0];
+            if (!ge) {
+                collect_timing();
+                hipGraph_t g = nullptr;
+                HIP_OK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
+                const bool ok = forward(1, dstate_[cur_], dstate_[cur_ ^ 1], lg);
+                HIP_OK(hipStreamEndCapture(stream_, &g));
+                tp.swap(pending_);  // these events belong to the graph now
+                if (!ok) {
+                    (void)hipGraphDestroy(g);
+                    return false;
+                }
+                HIP_OK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+                (void)hipGraphDestroy(g);
+            }
+            HIP_OK(hipGraphLaunch(ge, stream_));
+            HIP_OK(hipStreamSynchronize(stream_));
+            for (const Pending & p : tp) {
+                float ms = 0;
+                if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+                    KernelStat & s = stats_[p.stat];
+                    s.total_ms += ms;
+                    s.total_bytes += p.bytes;
+                    s.total_flops += p.flops;
+                    s.launches++;
+                }
+            }
+        } else if (n == 1 && use_graphs_ && !timing_) {
             hipGraphExec_t & ge = graphs_[cur_][lg ? 1 : 0];
             if (!ge) {
                 hipGraph_t g = nullptr;

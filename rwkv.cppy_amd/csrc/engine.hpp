@@ -129,7 +129,15 @@ class Engine {
     struct Pending {
         int stat;
         hipEvent_t a, b;
+        double bytes, flops;
     };
+    // timing mode keeps the graph path: the decode step is captured with an event pair around
+    // every kernel (event record nodes), so per-kernel durations are measured inside the same
+    // graph replay the untimed path runs
+    hipGraphExec_t tgraphs_[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+    std::vector<Pending> tpairs_[2][2];
+    int add_stat(const std::string & name);
+    void drop_graphs();
     std::vector<Pending> pending_;
     std::vector<hipEvent_t> event_pool_;
     std::vector<KernelStat> stats_;

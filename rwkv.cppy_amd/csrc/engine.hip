@@ -300,10 +300,6 @@ void Engine::drop_graphs() {
             if (graphs_[i][j]) (void)hipGraphExecDestroy(graphs_[i][j]);
             if (tgraphs_[i][j]) (void)hipGraphExecDestroy(tgraphs_[i][j]);
             graphs_[i][j] = tgraphs_[i][j] = nullptr;
-            for (const Pending & p : tpairs_[i][j]) {
-                event_pool_.push_back(p.a);
-                event_pool_.push_back(p.b);
-            }
             tpairs_[i][j].clear();
         }
 }
@@ -314,6 +310,7 @@ bool Engine::ensure_workspace(int T) {
     drop_graphs();
     // keep state and logits, drop the rest
     std::vector<void *> keep = {dstate_[0], dstate_[1], logits_};
+    if (dts_) keep.push_back(dts_);
     for (void * p : ws_allocs_) {
         bool k = false;
         for (void * q : keep) k |= (p == q);
@@ -468,7 +465,7 @@ bool Engine::mm_launch(MMGroup & g, int wtype) {
     HIP_OK(hipEventRecord(a, stream_));
     const bool ok = launch_mm_group(stream_, g, wtype);
     HIP_OK(hipEventRecord(b, stream_));
-    pending_.push_back(Pending{si, a, b, bytes, flops});
+    pending_.push_back(Pending{si, a, b, bytes, flops, -1, 0});
     return ok;
 }
 
@@ -480,7 +477,9 @@ int Engine::add_stat(const std::string & name) {
 }
 
 void Engine::collect_timing() {
+    (void)harvest_stamps(pending_);
     for (auto & p : pending_) {
+        if (p.slot >= 0) continue;
         float ms = 0;
         if (hipEventSynchronize(p.b) == hipSuccess && hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
             KernelStat & s = stats_[p.stat];
@@ -770,21 +769,42 @@ bool Engine::mv(MVGroup & g) {
         flops += 2.0 * e.W.M * e.W.K;
     }
     const int si = add_stat("k_mv");
-    hipEvent_t a, b;
-    if (event_pool_.size() >= 2) {
-        a = event_pool_.back();
-        event_pool_.pop_back();
-        b = event_pool_.back();
-        event_pool_.pop_back();
-    } else {
-        HIP_OK(hipEventCreate(&a));
-        HIP_OK(hipEventCreate(&b));
+    if (!dts_) {
+        HIP_OK(hipMalloc(&dts_, sizeof(unsigned long long) * 2 * kTsCap));
+        ws_allocs_.push_back(dts_);
     }
-    HIP_OK(hipEventRecord(a, stream_));
+    if (ts_next_ + 8 * 1024 * 16 > kTsCap) {
+        fprintf(stderr, "rwkv: kernel timing slots exhausted\n");
+        return false;
+    }
+    g.tstamp = dts_ + 2 * (size_t)ts_next_;
     const bool ok = launch_mv_group(stream_, g);
-    HIP_OK(hipEventRecord(b, stream_));
-    pending_.push_back(Pending{si, a, b, bytes, flops});
+    pending_.push_back(Pending{si, nullptr, nullptr, bytes, flops, ts_next_, g.grid});
+    ts_next_ += g.grid;
     return ok;
+}
+
+bool Engine::harvest_stamps(const std::vector<Pending> & ps) {
+    int hi = 0;
+    for (const Pending & p : ps)
+        if (p.slot >= 0) hi = std::max(hi, p.slot + p.nwg);
+    if (!hi) return true;
+    std::vector<unsigned long long> h((size_t)2 * hi);
+    HIP_OK(hipMemcpy(h.data(), dts_, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    for (const Pending & p : ps) {
+        if (p.slot < 0) continue;
+        unsigned long long t0 = ~0ull, t1 = 0;
+        for (int i = p.slot; i < p.slot + p.nwg; i++) {
+            t0 = std::min(t0, h[2 * (size_t)i]);
+            t1 = std::max(t1, h[2 * (size_t)i + 1]);
+        }
+        KernelStat & s = stats_[p.stat];
+        s.total_ms += t1 > t0 ? (double)(t1 - t0) * 1e-5 : 0.0;  // s_memrealtime: 100 MHz
+        s.total_bytes += p.bytes;
+        s.total_flops += p.flops;
+        s.launches++;
+    }
+    return true;
 }
 
 // Builder for decode matvec groups.
@@ -1027,12 +1047,14 @@ bool Engine::run_tokens(const uint32_t * tokens, size_t T, bool want_logits) {
             hipGraphExec_t & ge = tgraphs_[cur_][lg ? 1 : 0];
             std::vector<Pending> & tp = tpairs_[cur_][lg ? 1 : 0];
             if (!ge) {
+                HIP_OK(hipStreamSynchronize(stream_));
                 collect_timing();
+                ts_next_ = 0;
                 hipGraph_t g = nullptr;
                 HIP_OK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
                 const bool ok = forward(1, dstate_[cur_], dstate_[cur_ ^ 1], lg);
                 HIP_OK(hipStreamEndCapture(stream_, &g));
-                tp.swap(pending_);  // these events belong to the graph now
+                tp.swap(pending_);  // the stamp slots belong to this graph now
                 if (!ok) {
                     (void)hipGraphDestroy(g);
                     return false;
@@ -1042,16 +1064,7 @@ bool Engine::run_tokens(const uint32_t * tokens, size_t T, bool want_logits) {
             }
             HIP_OK(hipGraphLaunch(ge, stream_));
             HIP_OK(hipStreamSynchronize(stream_));
-            for (const Pending & p : tp) {
-                float ms = 0;
-                if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
-                    KernelStat & s = stats_[p.stat];
-                    s.total_ms += ms;
-                    s.total_bytes += p.bytes;
-                    s.total_flops += p.flops;
-                    s.launches++;
-                }
-            }
+            if (!harvest_stamps(tp)) return false;
         } else if (n == 1 && use_graphs_ && !timing_) {
             hipGraphExec_t & ge = graphs_[cur_][lg ? 1 : 0];
             if (!ge) {

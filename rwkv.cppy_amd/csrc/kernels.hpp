@@ -106,6 +106,8 @@ struct MVGroup {
     int n;
     int lds_bytes;
     int stride;              // set by launch_mv_group: >0 = workgroups walk row blocks
+    int grid;                // set by launch_mv_group: workgroups launched
+    unsigned long long * tstamp;  // timing only: [grid][2] s_memrealtime at workgroup start / end
 };
 
 void set_mv_device_cus(int n);

@@ -77,6 +77,7 @@ bool launch_mv_group(hipStream_t st, MVGroup & g) {
         grid = 2 * g_mv_cus;
         g.stride = grid;
     }
+    g.grid = grid;
     int U = umax <= 1 ? 1 : umax <= 2 ? 2 : 4;
     if (src != SRC_ACT && U == 2) U = 4;
     int wfix = g.e[0].W.type;

@@ -433,6 +433,8 @@ static double act_bytes(const ActBuf & a, double T) {
 void Engine::set_timing(bool on) {
     (void)hipStreamSynchronize(stream_);
     collect_timing();
+    if (on && !dts_ && hipMalloc(&dts_, sizeof(unsigned long long) * 2 * kTsCap) == hipSuccess)
+        ws_allocs_.push_back(dts_);
     timing_ = on;
     if (on) stats_.clear();
 }
@@ -770,8 +772,8 @@ bool Engine::mv(MVGroup & g) {
     }
     const int si = add_stat("k_mv");
     if (!dts_) {
-        HIP_OK(hipMalloc(&dts_, sizeof(unsigned long long) * 2 * kTsCap));
-        ws_allocs_.push_back(dts_);
+        fprintf(stderr, "rwkv: kernel timing buffer missing\n");
+        return false;
     }
     if (ts_next_ + 8 * 1024 * 16 > kTsCap) {
         fprintf(stderr, "rwkv: kernel timing slots exhausted\n");

@@ -269,3 +269,40 @@ def test_synthetic_real_width_matches_oracle(tmp_path, arch, fmt):
     lg2, st2 = gpu_serial(m, toks)
     assert np.array_equal(st, st2) and np.array_equal(lg, lg2)
     m.free()
+
+
+def test_kernel_timing_mode_is_transparent():
+    """Kernel timing (bench.py's roofline source) runs the same graph path: results bit-identical to
+    the untimed path, and every decode matvec launch reports a duration."""
+    import ctypes
+    L = library()
+    lib = L.library
+    path = os.path.join(GOLD, 'tiny-rwkv-6v0-3m-Q5_0.bin')
+    m = RWKVModel(L, path)
+    P = ctypes.POINTER(ctypes.c_float)
+    PI = ctypes.POINTER(ctypes.c_int32)
+    outs = []
+    for timing in (False, True):
+        lib.rwkv_mi355x_set_kernel_timing(m._ctx.ptr, timing)
+        assert lib.rwkv_mi355x_state_upload(m._ctx.ptr, None)
+        lg = np.zeros(m._logits_buffer_element_count, np.float32)
+        for i, t in enumerate(LONG[:12]):
+            arr = (ctypes.c_int32 * 1)(t)
+            assert lib.rwkv_mi355x_eval_device(m._ctx.ptr, ctypes.cast(arr, PI), 1, True, lg.ctypes.data_as(P), True)
+        st = np.zeros(m._state_buffer_element_count, np.float32)
+        assert lib.rwkv_mi355x_state_download(m._ctx.ptr, st.ctypes.data_as(P))
+        outs.append((lg.copy(), st))
+    n = lib.rwkv_mi355x_kernel_stats(m._ctx.ptr, -1, None, 0, None, None, None, None)
+    found = False
+    for i in range(n):
+        name = ctypes.create_string_buffer(128)
+        la, ms, by, fl = ctypes.c_longlong(), ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        lib.rwkv_mi355x_kernel_stats(m._ctx.ptr, i, name, 128, ctypes.byref(la), ctypes.byref(ms), ctypes.byref(by),
+                                     ctypes.byref(fl))
+        if name.value == b'k_mv':
+            found = True
+            assert la.value > 0 and ms.value > 0 and by.value > 0
+    assert found
+    lib.rwkv_mi355x_set_kernel_timing(m._ctx.ptr, False)
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+    m.free()

@@ -298,9 +298,7 @@ void Engine::drop_graphs() {
     for (int i = 0; i < 2; i++)
         for (int j = 0; j < 2; j++) {
             if (graphs_[i][j]) (void)hipGraphExecDestroy(graphs_[i][j]);
-            if (tgraphs_[i][j]) (void)hipGraphExecDestroy(tgraphs_[i][j]);
-            graphs_[i][j] = tgraphs_[i][j] = nullptr;
-            tpairs_[i][j].clear();
+            graphs_[i][j] = nullptr;
         }
 }
 
@@ -310,7 +308,6 @@ bool Engine::ensure_workspace(int T) {
     drop_graphs();
     // keep state and logits, drop the rest
     std::vector<void *> keep = {dstate_[0], dstate_[1], logits_};
-    if (dts_) keep.push_back(dts_);
     for (void * p : ws_allocs_) {
         bool k = false;
         for (void * q : keep) k |= (p == q);
@@ -433,8 +430,6 @@ static double act_bytes(const ActBuf & a, double T) {
 void Engine::set_timing(bool on) {
     (void)hipStreamSynchronize(stream_);
     collect_timing();
-    if (on && !dts_ && hipMalloc(&dts_, sizeof(unsigned long long) * 2 * kTsCap) == hipSuccess)
-        ws_allocs_.push_back(dts_);
     timing_ = on;
     if (on) stats_.clear();
 }
@@ -467,7 +462,7 @@ bool Engine::mm_launch(MMGroup & g, int wtype) {
     HIP_OK(hipEventRecord(a, stream_));
     const bool ok = launch_mm_group(stream_, g, wtype);
     HIP_OK(hipEventRecord(b, stream_));
-    pending_.push_back(Pending{si, a, b, bytes, flops, -1, 0});
+    pending_.push_back(Pending{si, a, b, bytes, flops});
     return ok;
 }
 
@@ -479,9 +474,7 @@ int Engine::add_stat(const std::string & name) {
 }
 
 void Engine::collect_timing() {
-    (void)harvest_stamps(pending_);
     for (auto & p : pending_) {
-        if (p.slot >= 0) continue;
         float ms = 0;
         if (hipEventSynchronize(p.b) == hipSuccess && hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
             KernelStat & s = stats_[p.stat];
@@ -771,42 +764,21 @@ bool Engine::mv(MVGroup & g) {
         flops += 2.0 * e.W.M * e.W.K;
     }
     const int si = add_stat("k_mv");
-    if (!dts_) {
-        fprintf(stderr, "rwkv: kernel timing buffer missing\n");
-        return false;
+    hipEvent_t a, b;
+    if (event_pool_.size() >= 2) {
+        a = event_pool_.back();
+        event_pool_.pop_back();
+        b = event_pool_.back();
+        event_pool_.pop_back();
+    } else {
+        HIP_OK(hipEventCreate(&a));
+        HIP_OK(hipEventCreate(&b));
     }
-    if (ts_next_ + 8 * 1024 * 16 > kTsCap) {
-        fprintf(stderr, "rwkv: kernel timing slots exhausted\n");
-        return false;
-    }
-    g.tstamp = dts_ + 2 * (size_t)ts_next_;
+    HIP_OK(hipEventRecord(a, stream_));
     const bool ok = launch_mv_group(stream_, g);
-    pending_.push_back(Pending{si, nullptr, nullptr, bytes, flops, ts_next_, g.grid});
-    ts_next_ += g.grid;
+    HIP_OK(hipEventRecord(b, stream_));
+    pending_.push_back(Pending{si, a, b, bytes, flops});
     return ok;
-}
-
-bool Engine::harvest_stamps(const std::vector<Pending> & ps) {
-    int hi = 0;
-    for (const Pending & p : ps)
-        if (p.slot >= 0) hi = std::max(hi, p.slot + p.nwg);
-    if (!hi) return true;
-    std::vector<unsigned long long> h((size_t)2 * hi);
-    HIP_OK(hipMemcpy(h.data(), dts_, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-    for (const Pending & p : ps) {
-        if (p.slot < 0) continue;
-        unsigned long long t0 = ~0ull, t1 = 0;
-        for (int i = p.slot; i < p.slot + p.nwg; i++) {
-            t0 = std::min(t0, h[2 * (size_t)i]);
-            t1 = std::max(t1, h[2 * (size_t)i + 1]);
-        }
-        KernelStat & s = stats_[p.stat];
-        s.total_ms += t1 > t0 ? (double)(t1 - t0) * 1e-5 : 0.0;  // s_memrealtime: 100 MHz
-        s.total_bytes += p.bytes;
-        s.total_flops += p.flops;
-        s.launches++;
-    }
-    return true;
 }
 
 // Builder for decode matvec groups.
@@ -1044,30 +1016,12 @@ bool Engine::run_tokens(const uint32_t * tokens, size_t T, bool want_logits) {
         HIP_OK(hipMemcpyAsync(dtokens_, htokens_, n * 4, hipMemcpyHostToDevice, stream_));
         HIP_OK(hipEventRecord(tok_event_, stream_));
         const bool lg = last && want_logits;
-        if (n == 1 && use_graphs_ && timing_) {
-            // timed graph: same kernels, an event pair around each (see tgraphs_)
-            hipGraphExec_t & ge = tgraphs_[cur_][lg ? 1 : 0];
-            std::vector<Pending> & tp = tpairs_[cur_][lg ? 1 : 0];
-            if (!ge) {
-                HIP_OK(hipStreamSynchronize(stream_));
-                collect_timing();
-                ts_next_ = 0;
-                hipGraph_t g = nullptr;
-                HIP_OK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
-                const bool ok = forward(1, dstate_[cur_], dstate_[cur_ ^ 1], lg);
-                HIP_OK(hipStreamEndCapture(stream_, &g));
-                tp.swap(pending_);  // the stamp slots belong to this graph now
-                if (!ok) {
-                    (void)hipGraphDestroy(g);
-                    return false;
-                }
-                HIP_OK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
-                (void)hipGraphDestroy(g);
-            }
-            HIP_OK(hipGraphLaunch(ge, stream_));
-            HIP_OK(hipStreamSynchronize(stream_));
-            if (!harvest_stamps(tp)) return false;
-        } else if (n == 1 && use_graphs_ && !timing_) {
+        if (timing_) {
+            // eager launches bracketed by events; the delay kernel holds the GPU while the host
+            // queues the whole step, so the event pairs time kernels rather than submission gaps
+            if (!launch_delay(stream_, 4000)) return false;
+            if (!forward((int)n, dstate_[cur_], dstate_[cur_ ^ 1], lg)) return false;
+        } else if (n == 1 && use_graphs_) {
             hipGraphExec_t & ge = graphs_[cur_][lg ? 1 : 0];
             if (!ge) {
                 hipGraph_t g = nullptr;

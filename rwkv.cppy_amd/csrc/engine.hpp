@@ -128,20 +128,10 @@ class Engine {
     bool timing_ = false;
     struct Pending {
         int stat;
-        hipEvent_t a, b;         // event-timed launches (eager)
+        hipEvent_t a, b;
         double bytes, flops;
-        int slot, nwg;           // timestamp-timed matvec launches: workgroup slots [slot, slot+nwg)
     };
-    // Timing mode keeps the graph path for decode: the matvec kernels write per-workgroup
-    // s_memrealtime stamps (MVGroup::tstamp) into dts_, so a kernel's duration (first workgroup
-    // start to last workgroup end, as rocprofv3 counts it) is measured inside the same graph
-    // replay the untimed path runs.
-    hipGraphExec_t tgraphs_[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
-    std::vector<Pending> tpairs_[2][2];
-    unsigned long long * dts_ = nullptr;
-    int ts_next_ = 0;
-    static constexpr int kTsCap = 1 << 20;
-    bool harvest_stamps(const std::vector<Pending> & ps);
+
     int add_stat(const std::string & name);
     void drop_graphs();
     std::vector<Pending> pending_;

@@ -207,6 +207,18 @@ bool launch_mm_group(hipStream_t st, MMGroup & g, int wtype) {
     }
 }
 
+// --------------------------------------------------------------------------- timing helper
+__global__ void k_delay(unsigned long long ticks) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(10);
+}
+
+bool launch_delay(hipStream_t st, int us) {
+    hipLaunchKernelGGL(k_delay, dim3(1), dim3(64), 0, st, (unsigned long long)us * 100ull);  // 100 MHz clock
+    HIP_OK(hipGetLastError());
+    return true;
+}
+
 // --------------------------------------------------------------------------- LayerNorm family
 
 __global__ __launch_bounds__(256) void k_embed_ln(const uint32_t * tokens, DMat emb, const float * w,

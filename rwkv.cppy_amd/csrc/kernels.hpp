@@ -107,8 +107,11 @@ struct MVGroup {
     int lds_bytes;
     int stride;              // set by launch_mv_group: >0 = workgroups walk row blocks
     int grid;                // set by launch_mv_group: workgroups launched
-    unsigned long long * tstamp;  // timing only: [grid][2] s_memrealtime at workgroup start / end
 };
+
+// Busy-waits about `us` microseconds on the device (kernel timing: lets the host queue a whole
+// decode step before the GPU starts it, so event pairs time kernels, not host submission).
+bool launch_delay(hipStream_t st, int us);
 
 void set_mv_device_cus(int n);
 

@@ -476,7 +476,6 @@ __global__ __launch_bounds__(512) void k_mv(MVGroup g) {
     while (e + 1 < g.n && (int)blockIdx.x >= g.e[e + 1].block0) e++;
     const MVEntry & Ent = g.e[e];
     const int wgi = (int)blockIdx.x - Ent.block0;
-    if (g.tstamp && threadIdx.x == 0) g.tstamp[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
     if constexpr (WFIX >= 0) {
         mv_body<WFIX, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, g.stride, smem, red);
     } else {
@@ -490,10 +489,6 @@ __global__ __launch_bounds__(512) void k_mv(MVGroup g) {
             case W_Q8_0: mv_body<W_Q8_0, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, g.stride, smem, red); break;
             default: break;
         }
-    }
-    if (g.tstamp) {
-        __syncthreads();  // every wave (prologue waves included) is done
-        if (threadIdx.x == 0) g.tstamp[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
     }
 }
 

@@ -308,6 +308,7 @@ bool Engine::ensure_workspace(int T) {
     drop_graphs();
     // keep state and logits, drop the rest
     std::vector<void *> keep = {dstate_[0], dstate_[1], logits_};
+    if (mv_scratch_) keep.push_back(mv_scratch_);
     for (void * p : ws_allocs_) {
         bool k = false;
         for (void * q : keep) k |= (p == q);
@@ -763,22 +764,84 @@ bool Engine::mv(MVGroup & g) {
         bytes += (double)e.W.M * 4 * ((e.epi == EPI_ADD || e.epi == EPI_SIGMUL_ADD || e.epi == EPI_VMIX7) ? 2 : 1);
         flops += 2.0 * e.W.M * e.W.K;
     }
-    const int si = add_stat("k_mv");
-    hipEvent_t a, b;
-    if (event_pool_.size() >= 2) {
-        a = event_pool_.back();
-        event_pool_.pop_back();
-        b = event_pool_.back();
-        event_pool_.pop_back();
-    } else {
-        HIP_OK(hipEventCreate(&a));
-        HIP_OK(hipEventCreate(&b));
+    // decode matvecs are timed by replay (replay_mv_timing); the group is logged, and launched
+    // here untimed so the step's results are exactly the untimed path's
+    mv_log_.push_back(MVLog{g, bytes, flops});
+    return launch_mv_group(stream_, g);
+}
+
+// Timing of the decode matvecs: the step's k_mv groups are replayed back to back in one graph,
+// bracketed by a single HIP event pair on the engine stream, with every output pointer
+// redirected to scratch (the replay reads the step's real inputs and weights, and leaves state
+// and activations untouched).  Per-launch time = elapsed / launches: the kernels run as in the
+// decode graph (one inter-kernel gap each), without per-kernel event markers.
+bool Engine::replay_mv_timing() {
+    if (mv_log_.empty()) return true;
+    if (!mv_scratch_) {
+        HIP_OK(hipMalloc(&mv_scratch_, kMvScratch));
+        ws_allocs_.push_back(mv_scratch_);
+        HIP_OK(hipMemset(mv_scratch_, 0, kMvScratch));
     }
+    float * sf = (float *)mv_scratch_;
+    char * sa = (char *)mv_scratch_ + kMvScratch / 2;
+    std::vector<MVGroup> groups;
+    double bytes = 0, flops = 0;
+    for (const MVLog & l : mv_log_) {
+        MVGroup g = l.g;
+        for (int i = 0; i < g.n; i++) {
+            MVEntry & e = g.e[i];
+            if ((size_t)e.W.M * 4 > kMvScratch / 4 || (size_t)e.W.K * 4 > kMvScratch / 4) return false;
+            e.y = sf;
+            if (e.carry_out) e.carry_out = sf + kMvScratch / 16;
+            if (e.emit) {
+                ActBuf & o = e.act_out;
+                o.f = (float *)sa;
+                o.h = (__half *)sa;
+                o.q = (int8_t *)sa;
+                o.d = (float *)(sa + kMvScratch / 8);
+                o.s = o.d + kMvScratch / 64;
+                o.qsum = (int *)(o.s + kMvScratch / 64);
+            }
+        }
+        groups.push_back(g);
+        bytes += l.bytes;
+        flops += l.flops;
+    }
+    hipGraph_t gr = nullptr;
+    hipGraphExec_t ge = nullptr;
+    HIP_OK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
+    bool ok = true;
+    for (MVGroup & g : groups) ok = ok && launch_mv_group(stream_, g);
+    HIP_OK(hipStreamEndCapture(stream_, &gr));
+    if (!ok) {
+        (void)hipGraphDestroy(gr);
+        return false;
+    }
+    HIP_OK(hipGraphInstantiate(&ge, gr, nullptr, nullptr, 0));
+    (void)hipGraphDestroy(gr);
+    if (event_pool_.size() < 2) {
+        hipEvent_t x, y;
+        HIP_OK(hipEventCreate(&x));
+        HIP_OK(hipEventCreate(&y));
+        event_pool_.push_back(x);
+        event_pool_.push_back(y);
+    }
+    hipEvent_t a = event_pool_[0], b = event_pool_[1];
+    HIP_OK(hipGraphLaunch(ge, stream_));  // warm (instruction caches, code objects)
     HIP_OK(hipEventRecord(a, stream_));
-    const bool ok = launch_mv_group(stream_, g);
+    HIP_OK(hipGraphLaunch(ge, stream_));
     HIP_OK(hipEventRecord(b, stream_));
-    pending_.push_back(Pending{si, a, b, bytes, flops});
-    return ok;
+    HIP_OK(hipEventSynchronize(b));
+    float ms = 0;
+    HIP_OK(hipEventElapsedTime(&ms, a, b));
+    (void)hipGraphExecDestroy(ge);
+    KernelStat & s = stats_[add_stat("k_mv")];
+    s.total_ms += ms;
+    s.total_bytes += bytes;
+    s.total_flops += flops;
+    s.launches += (long long)groups.size();
+    mv_log_.clear();
+    return true;
 }
 
 // Builder for decode matvec groups.
@@ -1019,8 +1082,10 @@ bool Engine::run_tokens(const uint32_t * tokens, size_t T, bool want_logits) {
         if (timing_) {
             // eager launches bracketed by events; the delay kernel holds the GPU while the host
             // queues the whole step, so the event pairs time kernels rather than submission gaps
-            if (!launch_delay(stream_, 4000)) return false;
+            mv_log_.clear();
             if (!forward((int)n, dstate_[cur_], dstate_[cur_ ^ 1], lg)) return false;
+            if (n == 1 && !replay_mv_timing()) return false;
+            mv_log_.clear();
         } else if (n == 1 && use_graphs_) {
             hipGraphExec_t & ge = graphs_[cur_][lg ? 1 : 0];
             if (!ge) {

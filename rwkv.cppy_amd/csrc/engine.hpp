@@ -133,6 +133,14 @@ class Engine {
     };
 
     int add_stat(const std::string & name);
+    struct MVLog {
+        MVGroup g;
+        double bytes, flops;
+    };
+    std::vector<MVLog> mv_log_;
+    void * mv_scratch_ = nullptr;
+    static constexpr size_t kMvScratch = 4u << 20;
+    bool replay_mv_timing();
     void drop_graphs();
     std::vector<Pending> pending_;
     std::vector<hipEvent_t> event_pool_;

@@ -78,6 +78,10 @@ RWKV_API bool rwkv_mi355x_selftest_quantize_act(int wtype, const float * x, int 
  * host) and x [T][K] (host): y [T][M] = W x with the library's activation quantization. */
 RWKV_API bool rwkv_mi355x_selftest_matmul(int wtype, const void * W, int K, int M, const float * x, int T, float * y);
 
+// Self-test of the sequence GEMM: the same product as rwkv_mi355x_selftest_matmul computed by
+// the int8-MFMA kernel (quantized weight types only; T >= 2).
+RWKV_API bool rwkv_mi355x_selftest_gemm(int wtype, const void * W, int K, int M, const float * x, int T, float * y);
+
 #if defined(__cplusplus)
 }
 #endif

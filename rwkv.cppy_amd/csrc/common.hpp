@@ -60,6 +60,8 @@ struct DMat {
     const uint8_t * qs;     // quantized nibbles / int8, or raw F16/F32 rows
     const uint32_t * qh;    // Q5 high bits
     const void * sc;        // u16 d  or u32 (d | m<<16)
+    const void * sct;       // the same scales block-major [nb][ldt] (sequence GEMM epilogue)
+    int ldt;                // row pitch of sct (M rounded up to 4)
 };
 
 enum Epi : int {

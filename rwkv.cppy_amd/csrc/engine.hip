@@ -109,14 +109,29 @@ bool upload_mat(DeviceModel & dm, const HostTensor * t, DMat & out, bool count_b
             if (!dh || hipMemcpy(dh, qh.data(), qh.size() * 4, hipMemcpyHostToDevice) != hipSuccess) return false;
             out.qh = dh;
         }
+        // block-major copy of the scales for the sequence GEMM: [nb][ldt], ldt = M rounded to 4
+        const size_t ldt = (M + 3) & ~(size_t)3;
+        out.ldt = (int)ldt;
         if (one) {
             uint32_t * ds = dalloc<uint32_t>(dm, sc32.size());
             if (!ds || hipMemcpy(ds, sc32.data(), sc32.size() * 4, hipMemcpyHostToDevice) != hipSuccess) return false;
             out.sc = ds;
+            std::vector<uint32_t> tr(nb * ldt, 0);
+            for (size_t m = 0; m < M; m++)
+                for (size_t b = 0; b < nb; b++) tr[b * ldt + m] = sc32[m * nb + b];
+            uint32_t * dt = dalloc<uint32_t>(dm, tr.size());
+            if (!dt || hipMemcpy(dt, tr.data(), tr.size() * 4, hipMemcpyHostToDevice) != hipSuccess) return false;
+            out.sct = dt;
         } else {
             uint16_t * ds = dalloc<uint16_t>(dm, sc16.size());
             if (!ds || hipMemcpy(ds, sc16.data(), sc16.size() * 2, hipMemcpyHostToDevice) != hipSuccess) return false;
             out.sc = ds;
+            std::vector<uint16_t> tr(nb * ldt, 0);
+            for (size_t m = 0; m < M; m++)
+                for (size_t b = 0; b < nb; b++) tr[b * ldt + m] = sc16[m * nb + b];
+            uint16_t * dt = dalloc<uint16_t>(dm, tr.size());
+            if (!dt || hipMemcpy(dt, tr.data(), tr.size() * 2, hipMemcpyHostToDevice) != hipSuccess) return false;
+            out.sct = dt;
         }
     }
     if (count_bytes) {
@@ -261,6 +276,7 @@ __global__ void k_init_state(float * st, size_t n, int C, int v4) {
 Engine::~Engine() {
     if (stream_) (void)hipStreamSynchronize(stream_);
     drop_graphs();
+    if (gy_) (void)hipFree(gy_);
     for (void * p : ws_allocs_) (void)hipFree(p);
     if (htokens_) (void)hipHostFree(htokens_);
     collect_timing();
@@ -289,6 +305,8 @@ bool Engine::init() {
     use_graphs_ = !(g && g[0] == '1');
     const char * gd = getenv("RWKV_MI355X_GENERIC_DECODE");
     generic_decode_ = gd && gd[0] == '1';
+    const char * um = getenv("RWKV_MI355X_SEQ_MATVEC");  // sequence matmuls on k_mm (comparison)
+    use_mm_ = um && um[0] == '1';
     // the fused decode prologues hold LayerNorm inputs in registers up to n_embed 4096
     if (m_->n_embed > 4096 || m_->n_embed % 64) generic_decode_ = true;
     return ensure_workspace(1) && init_state(dstate_[0]);
@@ -435,8 +453,43 @@ void Engine::set_timing(bool on) {
     if (on) stats_.clear();
 }
 
+// Sequence matmuls on quantized weights go to the int8-MFMA GEMM; entries that only emit get
+// a scratch y, and emission is a separate quantization pass (same bits as k_mm's epilogue).
+bool Engine::mm_dispatch(MMGroup & g, int wtype) {
+    if (g.T < 2 || !wtype_quantized(wtype) || use_mm_) return launch_mm_group(stream_, g, wtype);
+    size_t need = 0;
+    for (int i = 0; i < g.n; i++)
+        if (!g.e[i].y) need += (size_t)g.T * g.e[i].W.M;
+    if (need > gy_cap_) {
+        HIP_OK(hipStreamSynchronize(stream_));
+        if (gy_) (void)hipFree(gy_);
+        gy_ = nullptr;
+        HIP_OK(hipMalloc(&gy_, need * 4 + 64));
+        gy_cap_ = need;
+    }
+    size_t off = 0;
+    for (int i = 0; i < g.n; i++) {
+        MMEntry & e = g.e[i];
+        if (!e.y) {
+            e.y = gy_ + off;
+            e.ldy = e.W.M;
+            off += (size_t)g.T * e.W.M;
+        }
+    }
+    if (!launch_qgemm(stream_, g, wtype)) return false;
+    for (int i = 0; i < g.n; i++) {
+        const MMEntry & e = g.e[i];
+        if (e.emit && e.ldy == e.W.M && !launch_act_from_f32(stream_, e.y, g.T, e.W.M, e.out)) return false;
+        if (e.emit && e.ldy != e.W.M) {
+            fprintf(stderr, "rwkv: emitting GEMM entry needs ldy == M\n");
+            return false;
+        }
+    }
+    return true;
+}
+
 bool Engine::mm_launch(MMGroup & g, int wtype) {
-    if (!timing_) return launch_mm_group(stream_, g, wtype);
+    if (!timing_) return mm_dispatch(g, wtype);
     bool emit = false;
     double bytes = 0, flops = 0;
     for (int i = 0; i < g.n; i++) {
@@ -448,7 +501,9 @@ bool Engine::mm_launch(MMGroup & g, int wtype) {
         flops += 2.0 * e.W.M * e.W.K * g.T;
     }
     // kernel class = the template instantiation rocprofv3 reports: k_mm<WF, RPW, NT>
-    const std::string name = "k_mm<" + std::to_string(wtype) + ", " + (emit ? "8" : "2") + ", " + (g.T == 1 ? "1" : "4") + ">";
+    const bool mfma = g.T >= 2 && wtype_quantized(wtype) && !use_mm_;
+    const std::string name = mfma ? "k_qgemm<" + std::to_string(wtype) + ">"
+                                  : "k_mm<" + std::to_string(wtype) + ", " + (emit ? "8" : "2") + ", " + (g.T == 1 ? "1" : "4") + ">";
     const int si = add_stat(name);
     hipEvent_t a, b;
     if (event_pool_.size() >= 2) {
@@ -461,7 +516,7 @@ bool Engine::mm_launch(MMGroup & g, int wtype) {
         HIP_OK(hipEventCreate(&b));
     }
     HIP_OK(hipEventRecord(a, stream_));
-    const bool ok = launch_mm_group(stream_, g, wtype);
+    const bool ok = mm_dispatch(g, wtype);
     HIP_OK(hipEventRecord(b, stream_));
     pending_.push_back(Pending{si, a, b, bytes, flops});
     return ok;

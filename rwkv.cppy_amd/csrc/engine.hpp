@@ -141,6 +141,10 @@ class Engine {
     void * mv_scratch_ = nullptr;
     static constexpr size_t kMvScratch = 4u << 20;
     bool replay_mv_timing();
+    bool mm_dispatch(MMGroup & g, int wtype);
+    float * gy_ = nullptr;     // scratch y of emit-only GEMM entries
+    size_t gy_cap_ = 0;
+    bool use_mm_ = false;
     void drop_graphs();
     std::vector<Pending> pending_;
     std::vector<hipEvent_t> event_pool_;

@@ -8,6 +8,9 @@ namespace rwkvmi {
 // ---- matmul (dequant-matvec / batched) --------------------------------------------------
 // Launches one grouped matmul: every entry shares the weight type `wtype`.
 bool launch_mm_group(hipStream_t st, MMGroup & g, int wtype);
+// int8-MFMA sequence GEMM for quantized weights (qgemm.hip); same results as launch_mm_group.
+// Every entry needs y; emission is left to the caller (launch_act_from_f32).
+bool launch_qgemm(hipStream_t st, MMGroup & g, int wtype);
 
 // ---- elementwise / recurrence kernels -----------------------------------------------------
 // x[t] = LN(emb[tokens[t]]; w, b)   (rwkv_graph.inc:654-658)

@@ -61,8 +61,7 @@ extern "C" RWKV_API bool rwkv_mi355x_selftest_quantize_act(int wtype, const floa
     return true;
 }
 
-extern "C" RWKV_API bool rwkv_mi355x_selftest_matmul(int wtype, const void * W, int K, int M, const float * x, int T,
-                                                     float * y) {
+static bool selftest_mm(int wtype, const void * W, int K, int M, const float * x, int T, float * y, bool mfma) {
     if (K % 32 || T <= 0 || M <= 0) return false;
     HostTensor ht;
     ht.name = "selftest";
@@ -93,10 +92,21 @@ extern "C" RWKV_API bool rwkv_mi355x_selftest_matmul(int wtype, const void * W, 
         g.e[0].y = dy;
         g.e[0].ldy = M;
         g.e[0].epi = EPI_STORE;
-        ok = launch_mm_group(nullptr, g, wtype);
+        ok = mfma ? launch_qgemm(nullptr, g, wtype) : launch_mm_group(nullptr, g, wtype);
     }
     ok = ok && hipDeviceSynchronize() == hipSuccess;
     ok = ok && hipMemcpy(y, dy, (size_t)T * M * 4, hipMemcpyDeviceToHost) == hipSuccess;
     free_model(dm);
     return ok;
+}
+
+extern "C" RWKV_API bool rwkv_mi355x_selftest_matmul(int wtype, const void * W, int K, int M, const float * x, int T,
+                                                     float * y) {
+    return selftest_mm(wtype, W, K, M, x, T, y, false);
+}
+
+extern "C" RWKV_API bool rwkv_mi355x_selftest_gemm(int wtype, const void * W, int K, int M, const float * x, int T,
+                                                   float * y) {
+    if (!wtype_quantized(wtype) || T < 2) return false;
+    return selftest_mm(wtype, W, K, M, x, T, y, true);
 }

@@ -6,6 +6,8 @@
 - matmul kernel (every weight format, decode T=1 and batched T>1, ragged M/K) vs
   oracle_matmul: identical integer block dots, so only the fp32 summation order differs:
   |y_gpu - y_oracle| <= 1e-5 * (|W| |x|) + 1e-6 elementwise.
+- int8-MFMA sequence GEMM vs the matvec/matmul kernel: bit-exact (same block dots, same fp32
+  association), across formats, ragged M/T and K spanning 1..7 lane classes per row.
 """
 import ctypes
 
@@ -28,6 +30,8 @@ def lib():
     L.rwkv_mi355x_selftest_matmul.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                               ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
     L.rwkv_mi355x_selftest_matmul.restype = ctypes.c_bool
+    L.rwkv_mi355x_selftest_gemm.argtypes = L.rwkv_mi355x_selftest_matmul.argtypes
+    L.rwkv_mi355x_selftest_gemm.restype = ctypes.c_bool
     return L
 
 
@@ -70,3 +74,19 @@ def test_matmul_kernel(fmt, M, K, T):
     bound = np.abs(x.astype(np.float64)) @ np.abs(dequantize(fmt, wb, K, M).astype(np.float64)).T
     err = np.abs(y.astype(np.float64) - ref)
     assert np.all(err <= 1e-5 * bound + 1e-6), float((err / (bound + 1e-12)).max())
+
+
+@pytest.mark.parametrize('fmt', ['Q4_0', 'Q4_1', 'Q5_0', 'Q5_1', 'Q8_0'])
+@pytest.mark.parametrize('M,K,T', [(2048, 2048, 70), (100, 96, 3), (64, 7168, 33), (160, 2048, 64), (72, 320, 9),
+                                   (2048, 64, 17), (40, 4096, 2)])
+def test_mfma_gemm_matches_matmul_bit_exact(fmt, M, K, T):
+    rng = np.random.default_rng(M * 3 + K * 5 + T)
+    w = (rng.standard_normal((M, K)) / np.sqrt(K)).astype(np.float32)
+    x = rng.standard_normal((T, K)).astype(np.float32)
+    wb = quantize_rows(fmt, w)
+    y_mm = np.zeros((T, M), np.float32)
+    y_g = np.zeros((T, M), np.float32)
+    L = lib()
+    assert L.rwkv_mi355x_selftest_matmul(TYPE_IDS[fmt], wb.ctypes.data, K, M, x.ctypes.data, T, y_mm.ctypes.data)
+    assert L.rwkv_mi355x_selftest_gemm(TYPE_IDS[fmt], wb.ctypes.data, K, M, x.ctypes.data, T, y_g.ctypes.data)
+    assert np.array_equal(y_g.view(np.uint32), y_mm.view(np.uint32)), float(np.abs(y_g - y_mm).max())

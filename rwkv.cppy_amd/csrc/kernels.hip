@@ -427,9 +427,98 @@ static int pick_groups(int S) {
     return G;
 }
 
+// Head size 64 (every released v5/v6 model): one wave per (head, 16 value columns), grid
+// (H, 4).  Lane (g = lane >> 4, jl = lane & 15) owns column j = 16*blockIdx.y + jl for keys
+// i in [16g, 16g+16) -- the (j, g) work split and per-thread arithmetic of k_wkv6 / k_att6_dec,
+// and the same 4-group fold (xor 2, then xor 1 on g).  Chunks of 32 tokens of k, r, w and v are
+// staged in LDS with coalesced loads, the next chunk's loads in flight while this one runs; the
+// per-token critical path is only the state update S = S*w + k*v.
+constexpr int WKV_TC = 32;
+
+__global__ __launch_bounds__(64) void k_wkv6_s64(int T, int H, const float * k, const float * v, const float * r,
+                                                 const float * u, const float * w, int w_per_token,
+                                                 const float * sin, float * sout, float * y) {
+    constexpr int S = 64;
+    __shared__ __attribute__((aligned(16))) float sk[WKV_TC][S], sr[WKV_TC][S], sw[WKV_TC][S], sv[WKV_TC][16];
+    const int h = blockIdx.x, jb = blockIdx.y, lane = threadIdx.x;
+    const int jl = lane & 15, g = lane >> 4, j = jb * 16 + jl;
+    const int C = H * S;
+    const size_t hb = (size_t)h * S * S;
+    float st[16], uu[16], wc[16];
+#pragma unroll
+    for (int ii = 0; ii < 16; ii++) {
+        st[ii] = sin[hb + (size_t)(g * 16 + ii) * S + j];
+        uu[ii] = u[h * S + g * 16 + ii];
+        wc[ii] = w_per_token ? 0.0f : w[h * S + g * 16 + ii];
+    }
+    // chunk staging: k/r/w rows of 64 floats = 16 float4 per token; lane moves float4 #(lane & 15)
+    // of tokens (lane >> 4) + 4q, q < 8
+    float4 pk[8], pr[8], pw[8];
+    float4 pv[2];
+    auto load_chunk = [&](int t0) {
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const int t = min(t0 + (lane >> 4) + 4 * q, T - 1);
+            const size_t base = (size_t)t * C + (size_t)h * S + 4 * (lane & 15);
+            pk[q] = *(const float4 *)(k + base);
+            pr[q] = *(const float4 *)(r + base);
+            pw[q] = w_per_token ? *(const float4 *)(w + base) : make_float4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            // v: 16 columns = 4 float4 per token; lane moves float4 #(lane & 3) of token (lane >> 2) + 16q
+            const int t = min(t0 + (lane >> 2) + 16 * q, T - 1);
+            pv[q] = *(const float4 *)(v + (size_t)t * C + (size_t)h * S + jb * 16 + 4 * (lane & 3));
+        }
+    };
+    auto store_chunk = [&]() {
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const int tt = (lane >> 4) + 4 * q;
+            *(float4 *)&sk[tt][4 * (lane & 15)] = pk[q];
+            *(float4 *)&sr[tt][4 * (lane & 15)] = pr[q];
+            *(float4 *)&sw[tt][4 * (lane & 15)] = pw[q];
+        }
+#pragma unroll
+        for (int q = 0; q < 2; q++) *(float4 *)&sv[(lane >> 2) + 16 * q][4 * (lane & 3)] = pv[q];
+    };
+    load_chunk(0);
+    for (int t0 = 0; t0 < T; t0 += WKV_TC) {
+        store_chunk();
+        __syncthreads();
+        if (t0 + WKV_TC < T) load_chunk(t0 + WKV_TC);  // in flight during this chunk
+        const int n = min(WKV_TC, T - t0);
+        for (int tt = 0; tt < n; tt++) {
+            const float vj = sv[tt][jl];
+            float acc = 0.0f;
+#pragma unroll
+            for (int ii = 0; ii < 16; ii++) {
+                const int i = g * 16 + ii;
+                const float kv = vj * sk[tt][i];
+                const float prev = st[ii];
+                const float temp = kv * uu[ii] + prev;
+                acc += temp * sr[tt][i];
+                st[ii] = prev * (w_per_token ? sw[tt][i] : wc[ii]) + kv;
+            }
+            acc += __shfl_xor(acc, 32);
+            acc += __shfl_xor(acc, 16);
+            if (g == 0) y[(size_t)(t0 + tt) * C + h * S + j] = acc;
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int ii = 0; ii < 16; ii++) sout[hb + (size_t)(g * 16 + ii) * S + j] = st[ii];
+}
+
 bool launch_wkv6(hipStream_t st, int T, int H, int S, const float * k, const float * v, const float * r,
                  const float * u, const float * w, int w_per_token, const float * state_in, float * state_out,
                  float * y) {
+    if (S == 64) {
+        hipLaunchKernelGGL(k_wkv6_s64, dim3(H, 4), dim3(64), 0, st, T, H, k, v, r, u, w, w_per_token, state_in,
+                           state_out, y);
+        HIP_OK(hipGetLastError());
+        return true;
+    }
     const int G = pick_groups(S), IPG = S / G;
     dim3 grid(H), block(S * G);
     switch (IPG) {

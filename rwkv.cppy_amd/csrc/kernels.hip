@@ -307,20 +307,35 @@ struct Mix5Args {
     ActBuf out[5];
 };
 
+// Thread per channel c, 16 tokens per workgroup: each W2 column (time_maa_w2 transposed,
+// [5][D][C]) is loaded once into registers and reused for the block's tokens; per token the
+// D-long dot accumulates in fp64 in i order (the oracle's and k_v6_mix5_dec's order).
+constexpr int MIX5_TT = 16;
+
 __global__ __launch_bounds__(256) void k_v6_mix5(Mix5Args a) {
-    const int t = blockIdx.y;
+    const int t0 = blockIdx.y * MIX5_TT;
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if ((int)(blockIdx.x * blockDim.x + (threadIdx.x & ~63)) >= a.C) return;  // wave-uniform
-    const int C = a.C, D = a.D;
-    const size_t ti = (size_t)t * C + c;
-    const float xa = a.xa[ti], sx = a.sx[ti];
+    const int C = a.C, D = a.D, nt = min(MIX5_TT, a.T - t0);
     for (int n = 0; n < 5; n++) {
-        const float * w2 = a.w2 + (size_t)n * D * C + c;   // transposed [5][D][C]
-        const float * lv = a.lora + (size_t)t * 5 * D + n * D;
-        double acc = 0.0;
-        for (int i = 0; i < D; i++) acc += (double)(w2[(size_t)i * C] * lv[i]);
-        const float m = (float)acc;
-        emit32(a.out[n], t, c, (m + a.maa[n][c]) * sx + xa);
+        float w2v[64];
+        const float * w2 = a.w2 + (size_t)n * D * C + c;
+#pragma unroll
+        for (int i = 0; i < 64; i++) {
+            const float t = w2[(size_t)min(i, D - 1) * C];
+            w2v[i] = i < D ? t : 0.0f;
+        }
+        const float mu = a.maa[n][c];
+        for (int tt = 0; tt < nt; tt++) {
+            const int t = t0 + tt;
+            const float * lv = a.lora + (size_t)t * 5 * D + n * D;
+            double acc = 0.0;
+#pragma unroll
+            for (int i = 0; i < 64; i++)
+                if (i < D) acc += (double)(w2v[i] * lv[i]);
+            const size_t ti = (size_t)t * C + c;
+            emit32(a.out[n], t, c, ((float)acc + mu) * a.sx[ti] + a.xa[ti]);
+        }
     }
 }
 
@@ -338,7 +353,11 @@ bool launch_v6_mix5(hipStream_t st, int T, int C, int D, const float * lora, con
     }
     a.xa = xa;
     a.sx = sx;
-    hipLaunchKernelGGL(k_v6_mix5, dim3((C + 255) / 256, T), dim3(256), 0, st, a);
+    if (D > 64) {
+        fprintf(stderr, "rwkv: v6 maa LoRA width %d unsupported\n", D);
+        return false;
+    }
+    hipLaunchKernelGGL(k_v6_mix5, dim3((C + 255) / 256, (T + MIX5_TT - 1) / MIX5_TT), dim3(256), 0, st, a);
     HIP_OK(hipGetLastError());
     return true;
 }
@@ -488,17 +507,33 @@ __global__ __launch_bounds__(64) void k_wkv6_s64(int T, int H, const float * k, 
         __syncthreads();
         if (t0 + WKV_TC < T) load_chunk(t0 + WKV_TC);  // in flight during this chunk
         const int n = min(WKV_TC, T - t0);
+#pragma unroll 2
         for (int tt = 0; tt < n; tt++) {
+            // this token's 16 keys / receptances / decays of group g: 12 ds_read_b128
+            float kk[16], rr[16], ww[16];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const float4 a = *(const float4 *)&sk[tt][g * 16 + 4 * q];
+                const float4 b = *(const float4 *)&sr[tt][g * 16 + 4 * q];
+                kk[4 * q] = a.x, kk[4 * q + 1] = a.y, kk[4 * q + 2] = a.z, kk[4 * q + 3] = a.w;
+                rr[4 * q] = b.x, rr[4 * q + 1] = b.y, rr[4 * q + 2] = b.z, rr[4 * q + 3] = b.w;
+                if (w_per_token) {
+                    const float4 c = *(const float4 *)&sw[tt][g * 16 + 4 * q];
+                    ww[4 * q] = c.x, ww[4 * q + 1] = c.y, ww[4 * q + 2] = c.z, ww[4 * q + 3] = c.w;
+                } else {
+                    ww[4 * q] = wc[4 * q], ww[4 * q + 1] = wc[4 * q + 1], ww[4 * q + 2] = wc[4 * q + 2],
+                    ww[4 * q + 3] = wc[4 * q + 3];
+                }
+            }
             const float vj = sv[tt][jl];
             float acc = 0.0f;
 #pragma unroll
             for (int ii = 0; ii < 16; ii++) {
-                const int i = g * 16 + ii;
-                const float kv = vj * sk[tt][i];
+                const float kv = vj * kk[ii];
                 const float prev = st[ii];
                 const float temp = kv * uu[ii] + prev;
-                acc += temp * sr[tt][i];
-                st[ii] = prev * (w_per_token ? sw[tt][i] : wc[ii]) + kv;
+                acc += temp * rr[ii];
+                st[ii] = prev * ww[ii] + kv;
             }
             acc += __shfl_xor(acc, 32);
             acc += __shfl_xor(acc, 16);
@@ -605,9 +640,107 @@ __global__ void k_wkv7(int T, int H, int S, int G, const float * r, const float 
     for (int jj = 0; jj < JPG; jj++) sout[hb + jj] = st[jj];
 }
 
+// Head size 64: one wave per (head, 16 value rows i), grid (H, 4); lane (g = lane >> 4, il =
+// lane & 15) owns row i = 16*blockIdx.y + il, keys j in [16g, 16g+16) -- k_wkv7's / k_att7_dec's
+// split and arithmetic with the same 4-group folds -- with 32-token chunks of r, w, k, a, b
+// (and v) staged in LDS, the next chunk's loads in flight.
+__global__ __launch_bounds__(64) void k_wkv7_s64(int T, int H, const float * r, const float * w, const float * k,
+                                                 const float * v, const float * a, const float * b,
+                                                 const float * sin, float * sout, float * y) {
+    constexpr int S = 64;
+    __shared__ __attribute__((aligned(16))) float sr[WKV_TC][S], sw[WKV_TC][S], sk[WKV_TC][S], sa_[WKV_TC][S],
+        sb[WKV_TC][S], sv[WKV_TC][16];
+    const int h = blockIdx.x, ib = blockIdx.y, lane = threadIdx.x;
+    const int il = lane & 15, g = lane >> 4, i = ib * 16 + il;
+    const int C = H * S;
+    const size_t hb = (size_t)h * S * S + (size_t)i * S + g * 16;
+    float st[16];
+#pragma unroll
+    for (int jj = 0; jj < 16; jj++) st[jj] = sin[hb + jj];
+    float4 p[5][8], pv[2];
+    const float * src[5] = {r, w, k, a, b};
+    auto load_chunk = [&](int t0) {
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const int t = min(t0 + (lane >> 4) + 4 * q, T - 1);
+            const size_t base = (size_t)t * C + (size_t)h * S + 4 * (lane & 15);
+#pragma unroll
+            for (int s = 0; s < 5; s++) p[s][q] = *(const float4 *)(src[s] + base);
+        }
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            const int t = min(t0 + (lane >> 2) + 16 * q, T - 1);
+            pv[q] = *(const float4 *)(v + (size_t)t * C + (size_t)h * S + ib * 16 + 4 * (lane & 3));
+        }
+    };
+    auto store_chunk = [&]() {
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const int tt = (lane >> 4) + 4 * q, c4 = 4 * (lane & 15);
+            *(float4 *)&sr[tt][c4] = p[0][q];
+            *(float4 *)&sw[tt][c4] = p[1][q];
+            *(float4 *)&sk[tt][c4] = p[2][q];
+            *(float4 *)&sa_[tt][c4] = p[3][q];
+            *(float4 *)&sb[tt][c4] = p[4][q];
+        }
+#pragma unroll
+        for (int q = 0; q < 2; q++) *(float4 *)&sv[(lane >> 2) + 16 * q][4 * (lane & 3)] = pv[q];
+    };
+    load_chunk(0);
+    for (int t0 = 0; t0 < T; t0 += WKV_TC) {
+        store_chunk();
+        __syncthreads();
+        if (t0 + WKV_TC < T) load_chunk(t0 + WKV_TC);
+        const int n = min(WKV_TC, T - t0);
+        for (int tt = 0; tt < n; tt++) {
+            float aa[16];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const float4 x = *(const float4 *)&sa_[tt][g * 16 + 4 * q];
+                aa[4 * q] = x.x, aa[4 * q + 1] = x.y, aa[4 * q + 2] = x.z, aa[4 * q + 3] = x.w;
+            }
+            float sa = 0.0f;
+#pragma unroll
+            for (int jj = 0; jj < 16; jj++) sa += aa[jj] * st[jj];
+            sa += __shfl_xor(sa, 32);
+            sa += __shfl_xor(sa, 16);
+            const float vi = sv[tt][il];
+            float acc = 0.0f;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const float4 kq = *(const float4 *)&sk[tt][g * 16 + 4 * q];
+                const float4 wq = *(const float4 *)&sw[tt][g * 16 + 4 * q];
+                const float4 bq = *(const float4 *)&sb[tt][g * 16 + 4 * q];
+                const float4 rq = *(const float4 *)&sr[tt][g * 16 + 4 * q];
+                const float kk[4] = {kq.x, kq.y, kq.z, kq.w}, ww[4] = {wq.x, wq.y, wq.z, wq.w};
+                const float bb[4] = {bq.x, bq.y, bq.z, bq.w}, rr[4] = {rq.x, rq.y, rq.z, rq.w};
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    const int jj = 4 * q + e;
+                    const float kv = vi * kk[e];
+                    const float ns = st[jj] * ww[e] + kv + sa * bb[e];
+                    st[jj] = ns;
+                    acc += ns * rr[e];
+                }
+            }
+            acc += __shfl_xor(acc, 32);
+            acc += __shfl_xor(acc, 16);
+            if (g == 0) y[(size_t)(t0 + tt) * C + (size_t)h * S + i] = acc;
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int jj = 0; jj < 16; jj++) sout[hb + jj] = st[jj];
+}
+
 bool launch_wkv7(hipStream_t st, int T, int H, int S, const float * r, const float * w, const float * k,
                  const float * v, const float * a, const float * b, const float * state_in, float * state_out,
                  float * y) {
+    if (S == 64) {
+        hipLaunchKernelGGL(k_wkv7_s64, dim3(H, 4), dim3(64), 0, st, T, H, r, w, k, v, a, b, state_in, state_out, y);
+        HIP_OK(hipGetLastError());
+        return true;
+    }
     const int G = pick_groups(S), JPG = S / G;
     dim3 grid(H), block(S * G);
     switch (JPG) {

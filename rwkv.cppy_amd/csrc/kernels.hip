@@ -307,35 +307,20 @@ struct Mix5Args {
     ActBuf out[5];
 };
 
-// Thread per channel c, 16 tokens per workgroup: each W2 column (time_maa_w2 transposed,
-// [5][D][C]) is loaded once into registers and reused for the block's tokens; per token the
-// D-long dot accumulates in fp64 in i order (the oracle's and k_v6_mix5_dec's order).
-constexpr int MIX5_TT = 16;
-
 __global__ __launch_bounds__(256) void k_v6_mix5(Mix5Args a) {
-    const int t0 = blockIdx.y * MIX5_TT;
+    const int t = blockIdx.y;
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if ((int)(blockIdx.x * blockDim.x + (threadIdx.x & ~63)) >= a.C) return;  // wave-uniform
-    const int C = a.C, D = a.D, nt = min(MIX5_TT, a.T - t0);
+    const int C = a.C, D = a.D;
+    const size_t ti = (size_t)t * C + c;
+    const float xa = a.xa[ti], sx = a.sx[ti];
     for (int n = 0; n < 5; n++) {
-        float w2v[64];
-        const float * w2 = a.w2 + (size_t)n * D * C + c;
-#pragma unroll
-        for (int i = 0; i < 64; i++) {
-            const float t = w2[(size_t)min(i, D - 1) * C];
-            w2v[i] = i < D ? t : 0.0f;
-        }
-        const float mu = a.maa[n][c];
-        for (int tt = 0; tt < nt; tt++) {
-            const int t = t0 + tt;
-            const float * lv = a.lora + (size_t)t * 5 * D + n * D;
-            double acc = 0.0;
-#pragma unroll
-            for (int i = 0; i < 64; i++)
-                if (i < D) acc += (double)(w2v[i] * lv[i]);
-            const size_t ti = (size_t)t * C + c;
-            emit32(a.out[n], t, c, ((float)acc + mu) * a.sx[ti] + a.xa[ti]);
-        }
+        const float * w2 = a.w2 + (size_t)n * D * C + c;   // transposed [5][D][C]
+        const float * lv = a.lora + (size_t)t * 5 * D + n * D;
+        double acc = 0.0;
+        for (int i = 0; i < D; i++) acc += (double)(w2[(size_t)i * C] * lv[i]);
+        const float m = (float)acc;
+        emit32(a.out[n], t, c, (m + a.maa[n][c]) * sx + xa);
     }
 }
 
@@ -353,11 +338,7 @@ bool launch_v6_mix5(hipStream_t st, int T, int C, int D, const float * lora, con
     }
     a.xa = xa;
     a.sx = sx;
-    if (D > 64) {
-        fprintf(stderr, "rwkv: v6 maa LoRA width %d unsupported\n", D);
-        return false;
-    }
-    hipLaunchKernelGGL(k_v6_mix5, dim3((C + 255) / 256, (T + MIX5_TT - 1) / MIX5_TT), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_v6_mix5, dim3((C + 255) / 256, T), dim3(256), 0, st, a);
     HIP_OK(hipGetLastError());
     return true;
 }
@@ -454,6 +435,15 @@ static int pick_groups(int S) {
 // per-token critical path is only the state update S = S*w + k*v.
 constexpr int WKV_TC = 32;
 
+// Sum over the four lane groups g = lane >> 4: partner g ^ 2 (permlane32 swap), then g ^ 1
+// (permlane16 swap) -- the (p0 + p2) + (p1 + p3) of group_sum(., 4) on adjacent lanes.
+__device__ __forceinline__ float fold_g4(float v) {
+    const auto a = __builtin_amdgcn_permlane32_swap(__float_as_int(v), __float_as_int(v), false, false);
+    v = __int_as_float(a[0]) + __int_as_float(a[1]);
+    const auto b = __builtin_amdgcn_permlane16_swap(__float_as_int(v), __float_as_int(v), false, false);
+    return __int_as_float(b[0]) + __int_as_float(b[1]);
+}
+
 __global__ __launch_bounds__(64) void k_wkv6_s64(int T, int H, const float * k, const float * v, const float * r,
                                                  const float * u, const float * w, int w_per_token,
                                                  const float * sin, float * sout, float * y) {
@@ -535,8 +525,7 @@ __global__ __launch_bounds__(64) void k_wkv6_s64(int T, int H, const float * k, 
                 acc += temp * rr[ii];
                 st[ii] = prev * ww[ii] + kv;
             }
-            acc += __shfl_xor(acc, 32);
-            acc += __shfl_xor(acc, 16);
+            acc = fold_g4(acc);
             if (g == 0) y[(size_t)(t0 + tt) * C + h * S + j] = acc;
         }
         __syncthreads();
@@ -702,8 +691,7 @@ __global__ __launch_bounds__(64) void k_wkv7_s64(int T, int H, const float * r, 
             float sa = 0.0f;
 #pragma unroll
             for (int jj = 0; jj < 16; jj++) sa += aa[jj] * st[jj];
-            sa += __shfl_xor(sa, 32);
-            sa += __shfl_xor(sa, 16);
+            sa = fold_g4(sa);
             const float vi = sv[tt][il];
             float acc = 0.0f;
 #pragma unroll
@@ -723,8 +711,7 @@ __global__ __launch_bounds__(64) void k_wkv7_s64(int T, int H, const float * r, 
                     acc += ns * rr[e];
                 }
             }
-            acc += __shfl_xor(acc, 32);
-            acc += __shfl_xor(acc, 16);
+            acc = fold_g4(acc);
             if (g == 0) y[(size_t)(t0 + tt) * C + (size_t)h * S + i] = acc;
         }
         __syncthreads();

@@ -51,7 +51,28 @@ struct ActBuf {
     float * d;       // [T][K/32]    fp16-rounded block scale, stored as fp32
     float * s;       // [T][K/32]    A_Q8_1: fp16-rounded d*sum(q)
     int * qsum;      // [T][K/32]    sum(q) (exact, used for the -8/-16 offset of _0 formats)
+    // Sequence-GEMM layout (tiled != 0): Q8 blocks are written as token-tile records into tq
+    // instead of q/d/s/qsum (qg_* below); only the int8-MFMA GEMM reads it.
+    uint8_t * tq = nullptr;
+    int tiled = 0;
 };
+
+// --------------------------------------------------------------------------- sequence-GEMM tiles
+// Records the int8-MFMA GEMM (qgemm.hip) copies global->LDS as whole, contiguous pieces:
+//   weights     per (row tile of qg_rows rows, block b), ordered [row tile][b]:
+//                 [rows x 32 int8 (the block's integer weights, offset applied: q-8 / q-16 for
+//                  _0, q for _1, 5th bit merged)][rows x fp16 d][_1: rows x fp16 m]
+//   activations per (QG_TOK-token tile, block b), ordered [token tile][b]:
+//                 [2 halves x QG_TOK tokens x 16 B int8][QG_TOK x f32 d][Q8_1: QG_TOK x f32 s]
+constexpr int QG_TOK = 64;
+__host__ __device__ constexpr bool qg_one(int wt) { return wt == W_Q4_1 || wt == W_Q5_1; }
+__host__ __device__ constexpr int qg_rows(int wt) { return qg_one(wt) ? 32 : 64; }
+__host__ __device__ constexpr int qg_w_d(int wt) { return qg_rows(wt) * 32; }
+__host__ __device__ constexpr int qg_w_m(int wt) { return qg_w_d(wt) + qg_rows(wt) * 2; }
+__host__ __device__ constexpr int qg_w_bytes(int wt) { return qg_w_m(wt) + (qg_one(wt) ? qg_rows(wt) * 2 : 0); }
+constexpr int QG_A_D = 2 * QG_TOK * 16;
+constexpr int QG_A_S = QG_A_D + QG_TOK * 4;
+__host__ __device__ constexpr int qg_a_bytes(bool one) { return QG_A_S + (one ? QG_TOK * 4 : 0); }
 
 // Device weight matrix, ggml ne=[K, M] (M output rows of K elements).
 struct DMat {
@@ -60,8 +81,7 @@ struct DMat {
     const uint8_t * qs;     // quantized nibbles / int8, or raw F16/F32 rows
     const uint32_t * qh;    // Q5 high bits
     const void * sc;        // u16 d  or u32 (d | m<<16)
-    const void * sct;       // the same scales block-major [nb][ldt] (sequence GEMM epilogue)
-    int ldt;                // row pitch of sct (M rounded up to 4)
+    const uint8_t * gt;     // the same blocks as sequence-GEMM tile records (qg_w_*), quantized types
 };
 
 enum Epi : int {

@@ -124,6 +124,17 @@ __device__ __forceinline__ Q32 quant32(float v) {
 
 // Store element k of row t (and, from the block's first lane, its scales).
 __device__ __forceinline__ void store32(const ActBuf & a, int t, int k, const Q32 & r) {
+    if (a.tiled) {  // sequence-GEMM token-tile record (common.hpp qg_*)
+        const bool one = a.fmt == A_Q8_1;
+        uint8_t * rec = a.tq + ((size_t)(t / QG_TOK) * (a.K >> 5) + (k >> 5)) * qg_a_bytes(one);
+        const int tl = t % QG_TOK;
+        rec[((k >> 4) & 1) * QG_TOK * 16 + tl * 16 + (k & 15)] = (uint8_t)(int8_t)r.q;
+        if ((k & 31) == 0) {
+            ((float *)(rec + QG_A_D))[tl] = f16_round(r.d);
+            if (one) ((float *)(rec + QG_A_S))[tl] = f16_round(r.d * (float)r.sum);
+        }
+        return;
+    }
     const size_t idx = (size_t)t * a.K + k;
     a.q[idx] = (int8_t)r.q;
     if ((k & 31) == 0) {
@@ -247,6 +258,29 @@ __device__ __forceinline__ int block_dot(const DMat & W, int row, int b, int nb,
 }
 
 typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
+
+// apply_epi with y[t][row] (yv) and aux[t][row] (av) already loaded (only read by the epilogues
+// that use them: ADD / SIGMUL_ADD / VMIX7)
+__device__ __forceinline__ float apply_epi_v(const MMEntry & E, int row, float acc, float yv, float av) {
+    switch (E.epi) {
+        case EPI_SIGMOID: return sigmoidf_(acc);
+        case EPI_TANH: return tanhf(acc);
+        case EPI_SILU: return siluf_(acc);
+        case EPI_RELU_SQ: {
+            const float r = acc > 0.0f ? acc : 0.0f;
+            return r * r;
+        }
+        case EPI_ADD: return yv + acc;
+        case EPI_SIGMUL_ADD: return yv + sigmoidf_(av) * acc;
+        case EPI_DECAY6: return expf(-expf(acc + E.bias[row]));
+        case EPI_DECAY7: return expf(sigmoidf_(acc + E.bias[row]) * -0.606531f);
+        case EPI_SIGMOID_BIAS: return sigmoidf_(acc + E.bias[row]);
+        case EPI_VMIX7: return yv + (av - yv) * sigmoidf_(acc + E.bias[row]);
+        default: return acc;
+    }
+}
+__device__ __forceinline__ bool epi_reads_y(int epi) { return epi == EPI_ADD || epi == EPI_SIGMUL_ADD || epi == EPI_VMIX7; }
+__device__ __forceinline__ bool epi_reads_aux(int epi) { return epi == EPI_SIGMUL_ADD || epi == EPI_VMIX7; }
 
 __device__ __forceinline__ float apply_epi(const MMEntry & E, int t, int row, float acc) {
     const size_t yi = (size_t)t * E.ldy + row;

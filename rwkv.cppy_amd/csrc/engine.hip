@@ -64,6 +64,7 @@ bool upload_mat(DeviceModel & dm, const HostTensor * t, DMat & out, bool count_b
         return false;
     }
     out.type = (int)t->type;
+    out.gt = nullptr;
     out.K = (int)t->ne[0];
     out.M = (int)t->ne[1];
     const size_t M = out.M, K = out.K;
@@ -109,29 +110,51 @@ bool upload_mat(DeviceModel & dm, const HostTensor * t, DMat & out, bool count_b
             if (!dh || hipMemcpy(dh, qh.data(), qh.size() * 4, hipMemcpyHostToDevice) != hipSuccess) return false;
             out.qh = dh;
         }
-        // block-major copy of the scales for the sequence GEMM: [nb][ldt], ldt = M rounded to 4
-        const size_t ldt = (M + 3) & ~(size_t)3;
-        out.ldt = (int)ldt;
         if (one) {
             uint32_t * ds = dalloc<uint32_t>(dm, sc32.size());
             if (!ds || hipMemcpy(ds, sc32.data(), sc32.size() * 4, hipMemcpyHostToDevice) != hipSuccess) return false;
             out.sc = ds;
-            std::vector<uint32_t> tr(nb * ldt, 0);
-            for (size_t m = 0; m < M; m++)
-                for (size_t b = 0; b < nb; b++) tr[b * ldt + m] = sc32[m * nb + b];
-            uint32_t * dt = dalloc<uint32_t>(dm, tr.size());
-            if (!dt || hipMemcpy(dt, tr.data(), tr.size() * 4, hipMemcpyHostToDevice) != hipSuccess) return false;
-            out.sct = dt;
         } else {
             uint16_t * ds = dalloc<uint16_t>(dm, sc16.size());
             if (!ds || hipMemcpy(ds, sc16.data(), sc16.size() * 2, hipMemcpyHostToDevice) != hipSuccess) return false;
             out.sc = ds;
-            std::vector<uint16_t> tr(nb * ldt, 0);
-            for (size_t m = 0; m < M; m++)
-                for (size_t b = 0; b < nb; b++) tr[b * ldt + m] = sc16[m * nb + b];
-            uint16_t * dt = dalloc<uint16_t>(dm, tr.size());
-            if (!dt || hipMemcpy(dt, tr.data(), tr.size() * 2, hipMemcpyHostToDevice) != hipSuccess) return false;
-            out.sct = dt;
+        }
+        // the same blocks again as sequence-GEMM tile records (common.hpp qg_*); the head only
+        // ever runs on one token
+        if (!is_head) {
+            const int wt = (int)t->type, R = qg_rows(wt);
+            const size_t tiles = (M + R - 1) / R, rb = qg_w_bytes(wt);
+            std::vector<uint8_t> gt(tiles * nb * rb, 0);
+            for (size_t rt = 0; rt < tiles; rt++)
+                for (size_t b = 0; b < nb; b++) {
+                    uint8_t * rec = &gt[(rt * nb + b) * rb];
+                    for (int r = 0; r < R && rt * R + r < M; r++) {
+                        const size_t i = (rt * R + r) * nb + b;
+                        int8_t * w8 = (int8_t *)rec + r * 32;
+                        for (int j = 0; j < 32; j++) {
+                            int v;
+                            if (wt == W_Q8_0) {
+                                v = (int8_t)qs[i * 32 + j];
+                            } else {
+                                const uint8_t byte = qs[i * 16 + (j & 15)];
+                                v = j < 16 ? (byte & 0xF) : (byte >> 4);
+                                if (q5) v |= (int)((qh[i] >> j) & 1u) << 4;
+                                if (wt == W_Q4_0) v -= 8;
+                                if (wt == W_Q5_0) v -= 16;
+                            }
+                            w8[j] = (int8_t)v;
+                        }
+                        const uint16_t d = one ? (uint16_t)(sc32[i] & 0xFFFFu) : sc16[i];
+                        memcpy(rec + qg_w_d(wt) + r * 2, &d, 2);
+                        if (one) {
+                            const uint16_t m = (uint16_t)(sc32[i] >> 16);
+                            memcpy(rec + qg_w_m(wt) + r * 2, &m, 2);
+                        }
+                    }
+                }
+            uint8_t * dg = dalloc<uint8_t>(dm, gt.size());
+            if (!dg || hipMemcpy(dg, gt.data(), gt.size(), hipMemcpyHostToDevice) != hipSuccess) return false;
+            out.gt = dg;
         }
     }
     if (count_bytes) {
@@ -365,7 +388,10 @@ bool Engine::ensure_workspace(int T) {
         s.qsum = (int *)A(nb * 4);
         s.h = (__half *)A(n * 2);
         s.f = (float *)A(n * 4);
-        if (!s.q || !s.d || !s.s || !s.qsum || !s.h || !s.f) return false;
+        // sequence-GEMM token tiles: whole QG_TOK-token tiles, records of up to qg_a_bytes(true)
+        const size_t ttiles = ((size_t)cap + QG_TOK - 1) / QG_TOK;
+        s.tq = (uint8_t *)A(ttiles * (kmax / 32 + 1) * qg_a_bytes(true));
+        if (!s.q || !s.d || !s.s || !s.qsum || !s.h || !s.f || !s.tq) return false;
     }
     HIP_OK(hipHostMalloc((void **)&htokens_, (size_t)cap * 4, hipHostMallocDefault));
     return true;
@@ -390,6 +416,8 @@ ActBuf Engine::Aview(int slot, int K, int fmt) const {
     a.d = s.d;
     a.s = s.s;
     a.qsum = s.qsum;
+    a.tq = s.tq;
+    a.tiled = tile_acts_ && (fmt == A_Q8_0 || fmt == A_Q8_1);
     return a;
 }
 
@@ -784,6 +812,8 @@ bool Engine::forward(int T, const float * sin, float * sout, bool logits) {
     const size_t C = m_->n_embed;
     if (!launch_embed_ln(stream_, dtokens_, T, m_->emb, m_->ln0_w, m_->ln0_b, x_)) return false;
     const size_t per_layer = m_->major >= 5 ? C * (2 + (size_t)m_->S) : 5 * C;
+    // layer matmuls run over all T tokens: Q8 activations go straight into GEMM tiles
+    tile_acts_ = T >= 2 && !use_mm_;
     for (uint32_t l = 0; l < m_->n_layer; l++) {
         const float * si = sin + l * per_layer;
         float * so = sout + l * per_layer;
@@ -795,8 +825,12 @@ bool Engine::forward(int T, const float * sin, float * sout, bool logits) {
             case 7: ok = layer_v7((int)l, T, si, so); break;
             default: break;
         }
-        if (!ok) return false;
+        if (!ok) {
+            tile_acts_ = false;
+            return false;
+        }
     }
+    tile_acts_ = false;  // the head runs on the last token only
     if (logits) {
         // rwkv_graph.inc:704-708 / :850-854
         ActBuf hin = A(0, m_->head);

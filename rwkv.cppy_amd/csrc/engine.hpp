@@ -62,6 +62,7 @@ struct ActSlot {
     int * qsum = nullptr;
     __half * h = nullptr;
     float * f = nullptr;
+    uint8_t * tq = nullptr;  // sequence-GEMM token-tile records
 };
 
 // Per-kernel-class timing collected with hipEvents on the context stream (bench roofline).
@@ -145,6 +146,7 @@ class Engine {
     float * gy_ = nullptr;     // scratch y of emit-only GEMM entries
     size_t gy_cap_ = 0;
     bool use_mm_ = false;
+    bool tile_acts_ = false;  // Aview: Q8 activations in sequence-GEMM tiles (forward, T >= 2)
     void drop_graphs();
     std::vector<Pending> pending_;
     std::vector<hipEvent_t> event_pool_;

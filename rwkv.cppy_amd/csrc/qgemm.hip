@@ -9,164 +9,290 @@
 // ascending b, and the 64 class sums are folded with wave_sum63's perfect binary tree (a binary
 // counter over the classes).  So serial decode and sequence evaluation stay bit-identical.
 //
-// Workgroup = 4 waves as 2 (rows) x 2 (tokens); a wave owns TI 16-row tiles x 2 16-token tiles.
+// Operands come as tile records (common.hpp qg_*): per (row tile, block) one contiguous weight
+// record, per (64-token tile, block) one contiguous activation record, so every copy
+// instruction moves 1 KiB of consecutive bytes.  Workgroup = 4 waves as 2 (rows) x 2 (tokens)
+// over a 32*TI-row x 64-token tile; a wave owns TI 16-row tiles x 2 16-token tiles.  Blocks are
+// consumed in class-major order in chunks of 8 steps; each chunk's records are copied
+// global->LDS (LDS DMA) by the four waves while the previous chunk is computed from the other
+// LDS buffer, and within a chunk the LDS operands of step k+1 are read while step k's epilogue
+// runs.
 #include "device_common.hpp"
 #include "kernels.hpp"
 
 #include <stdio.h>
+#include <type_traits>
+
+// m0 in the copy asm's clobber list is a reserved register: the compiler re-sets m0 before each of
+// its own uses (none in this file besides these copies)
+#pragma clang diagnostic ignored "-Winline-asm"
 
 namespace rwkvmi {
 
 typedef int v4i_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void_t;
 
-// 8 int8 weights of `row`, block b, elements k = 8h..8h+7: the A operand of the 16x16x32 MFMA
-// (lane = (h << 4) | (row & 15)).  ggml order: low nibble of qs[j] = element j, high = j + 16.
-template <int WF>
-__device__ __forceinline__ long wfrag(const DMat & W, int row, int b, int nb, int h) {
-    const size_t bi = (size_t)row * nb + b;
-    if constexpr (WF == W_Q8_0) {
-        return *(const long *)(W.qs + bi * 32 + 8 * h);
-    } else {
-        const uint2 q = *(const uint2 *)(W.qs + bi * 16 + (h & 1) * 8);
-        uint32_t lo = q.x, hi = q.y;
-        if (h >= 2) {
-            lo >>= 4;
-            hi >>= 4;
+// Global->LDS copy (LDS DMA) of one 1-KiB piece: buffer_load_dwordx4 ... lds puts lane i's 16
+// bytes from base + soff + voff + OFF at LDS m0 + OFF + 16 i (tools/bufdma_check.hip).  Issued as
+// inline asm on purpose: the compiler cannot tell a copy into one LDS buffer from reads of the
+// other and would drain vmcnt before every LDS read; the kernel orders the copies itself
+// (s_waitcnt vmcnt(0) + barrier per chunk, qg_chunk_done).  M0 is written in the same statement
+// (the compiler does not preserve it) and needs one wait state before the load.
+template <int OFF>
+__device__ __forceinline__ void qg_bdma(v4i_t rsrc, unsigned soff, unsigned m0, unsigned voff) {
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %2, %3 offen offset:%4 lds" ::"v"(voff),
+                 "s"(m0), "s"(rsrc), "s"(soff), "i"(OFF)
+                 : "m0");
+}
+
+// raw buffer descriptor over [base, base + 4 GiB) (gfx9 dword3 0x00020000)
+__device__ __forceinline__ v4i_t qg_rsrc(const void * base) {
+    v4i_t r;
+    r.x = __builtin_amdgcn_readfirstlane((int)(unsigned long)base);
+    r.y = __builtin_amdgcn_readfirstlane((int)((unsigned long)base >> 32));
+    r.z = -1;
+    r.w = 0x00020000;
+    return r;
+}
+
+// One record of BYTES into LDS at m0: full 1-KiB pieces plus a partial last piece
+template <int BYTES, int P = 0>
+__device__ __forceinline__ void qg_record(v4i_t rsrc, unsigned soff, unsigned m0, int lane) {
+    if constexpr (P * 1024 < BYTES) {
+        if constexpr ((P + 1) * 1024 <= BYTES) {
+            qg_bdma<P * 1024>(rsrc, soff, m0, lane * 16);
+        } else if (lane * 16 < BYTES - P * 1024) {
+            qg_bdma<P * 1024>(rsrc, soff, m0, lane * 16);
         }
-        lo &= 0x0F0F0F0Fu;
-        hi &= 0x0F0F0F0Fu;
-        if constexpr (WF == W_Q5_0 || WF == W_Q5_1) {
-            const uint32_t qh = W.qh[bi] >> (8 * h);
-            lo |= spread4(qh & 0xFu);
-            hi |= spread4((qh >> 4) & 0xFu);
-        }
-        // per-byte subtraction without borrows: ((v | 0x80) - off) ^ 0x80 == v - off (mod 256)
-        if constexpr (WF == W_Q4_0) {
-            lo = ((lo | 0x80808080u) - 0x08080808u) ^ 0x80808080u;
-            hi = ((hi | 0x80808080u) - 0x08080808u) ^ 0x80808080u;
-        } else if constexpr (WF == W_Q5_0) {
-            lo = ((lo | 0x80808080u) - 0x10101010u) ^ 0x80808080u;
-            hi = ((hi | 0x80808080u) - 0x10101010u) ^ 0x80808080u;
-        }
-        return (long)(((unsigned long)hi << 32) | lo);
+        qg_record<BYTES, P + 1>(rsrc, soff, m0, lane);
     }
 }
 
-template <int WF, int TI>
-struct QOp {
-    long a[TI];          // weight fragments per row tile
-    long x[2];           // activation fragments per token tile
-    uint32_t sc[TI][4];  // scales of the lane's 4 output rows per row tile (d | m << 16)
+// All of this wave's copies have landed; the barrier then publishes every wave's copies.
+__device__ __forceinline__ void qg_chunk_done() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+}
+
+constexpr int QG_STEPS = 8;  // blocks per chunk
+
+template <int WF>
+struct QGLayout {
+    static constexpr bool ONE = qg_one(WF);
+    static constexpr int TI = ONE ? 1 : 2;
+    static constexpr int ROWS = qg_rows(WF);        // = 32 * TI
+    static constexpr int WB = qg_w_bytes(WF);       // weight record
+    static constexpr int AB = qg_a_bytes(ONE);      // activation record
+    static constexpr int STEP = WB + AB;            // LDS bytes per step: [weight rec][act rec]
+    static constexpr int BUF = STEP * QG_STEPS;
+    static constexpr int WP = (WB + 1023) / 1024;   // copy instructions per record
+    static constexpr int AP = (AB + 1023) / 1024;
+    static constexpr int JOBS = WP + AP;
+    static_assert(ROWS == 32 * TI && WB % 16 == 0 && AB % 16 == 0, "qgemm layout");
+};
+
+// Class-major walk over the blocks: class l (= b mod 64) has n = q + (l < rem) blocks, q = nb/64,
+// rem = nb%64; step s of the walk is block l + 64 u.  Scalar state, advanced one step at a time.
+struct QGWalk {
+    int q, rem, l, u, n;
+    __device__ __forceinline__ void init(int nb) {
+        q = nb >> 6;
+        rem = nb & 63;
+        l = 0;
+        u = 0;
+        n = q + (rem > 0 ? 1 : 0);
+    }
+    __device__ __forceinline__ int block() const { return l + 64 * u; }
+    __device__ __forceinline__ void next() {
+        if (++u == n) {
+            l++;
+            u = 0;
+            n = q + (l < rem ? 1 : 0);
+        }
+    }
+};
+
+// This wave's share of chunk c: steps 8c + wave and 8c + wave + 4 (the walk is at the first of
+// them and is left at 8(c+1) + wave).
+template <int WF>
+__device__ __forceinline__ void qg_load_chunk(v4i_t rw, v4i_t ra, unsigned lds_buf, int c, QGWalk & wk, int nb,
+                                              int wave, int lane) {
+    using Lt = QGLayout<WF>;
+#pragma unroll
+    for (int h2 = 0; h2 < 2; h2++) {
+        const int k = wave + 4 * h2;
+        if (c * QG_STEPS + k < nb) {
+            const int b = wk.block();
+            const unsigned m = lds_buf + k * Lt::STEP;
+            qg_record<Lt::WB>(rw, (unsigned)(b * Lt::WB), m, lane);
+            qg_record<Lt::AB>(ra, (unsigned)(b * Lt::AB), m + Lt::WB, lane);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++) wk.next();
+    }
+}
+
+// LDS operands of one step for one wave
+template <int TI>
+struct QGOps {
+    long af[TI], xf[2];
+    uint2 sd[TI], sm[TI];  // fp16 d (m) of the 4 D-layout rows 4h..4h+3 of each 16-row tile
     float dx[2], sx[2];
 };
 
-template <int WF, int TI>
-__device__ __forceinline__ void qop_load(QOp<WF, TI> & o, const MMEntry & E, int b, int nb, int rowA0, int rowO0,
-                                         int tokB0, int M, int T, int h, int r16) {
-    constexpr bool ONE = WF == W_Q4_1 || WF == W_Q5_1;
-    const DMat & W = E.W;
-    const int K = W.K;
+template <int WF>
+__device__ __forceinline__ void qg_read_ops(const char * sp, QGOps<QGLayout<WF>::TI> & o, int wr, int wt, int r16,
+                                            int h) {
+    using Lt = QGLayout<WF>;
 #pragma unroll
-    for (int i = 0; i < TI; i++) {
-        o.a[i] = wfrag<WF>(W, min(rowA0 + 16 * i + r16, M - 1), b, nb, h);
-        const int ro = min(rowO0 + 16 * i + 4 * h, W.ldt - 4);  // 4 consecutive rows, 4-aligned
-        if constexpr (ONE) {
-            const uint4 s = *(const uint4 *)((const uint32_t *)W.sct + (size_t)b * W.ldt + ro);
-            o.sc[i][0] = s.x, o.sc[i][1] = s.y, o.sc[i][2] = s.z, o.sc[i][3] = s.w;
-        } else {
-            const uint2 s = *(const uint2 *)((const uint16_t *)W.sct + (size_t)b * W.ldt + ro);
-            o.sc[i][0] = s.x & 0xFFFFu, o.sc[i][1] = s.x >> 16, o.sc[i][2] = s.y & 0xFFFFu, o.sc[i][3] = s.y >> 16;
-        }
+    for (int i = 0; i < Lt::TI; i++) {
+        o.af[i] = *(const long *)(sp + (wr + 16 * i + r16) * 32 + h * 8);  // int8 row, k = 8h..8h+7
+        const int ro = wr + 16 * i + 4 * h;
+        o.sd[i] = *(const uint2 *)(sp + qg_w_d(WF) + ro * 2);
+        if constexpr (Lt::ONE) o.sm[i] = *(const uint2 *)(sp + qg_w_m(WF) + ro * 2);
     }
+    const char * ap = sp + Lt::WB;
 #pragma unroll
     for (int j = 0; j < 2; j++) {
-        const int t = min(tokB0 + 16 * j + r16, T - 1);
-        o.x[j] = *(const long *)(E.in.q + (size_t)t * K + (size_t)b * 32 + 8 * h);
-        o.dx[j] = E.in.d[(size_t)t * nb + b];
-        o.sx[j] = ONE ? E.in.s[(size_t)t * nb + b] : 0.0f;
+        const int tl = wt + 16 * j + r16;
+        o.xf[j] = *(const long *)(ap + (h >> 1) * QG_TOK * 16 + tl * 16 + (h & 1) * 8);
+        o.dx[j] = *(const float *)(ap + QG_A_D + tl * 4);
+        if constexpr (Lt::ONE) o.sx[j] = *(const float *)(ap + QG_A_S + tl * 4);
     }
 }
 
-// one block: 2*TI MFMAs, then acc = fmaf(d_w*d_x, sumi, acc) (+ acc2 += m_w*s_x)
-template <int WF, int TI>
-__device__ __forceinline__ void qop_compute(const QOp<WF, TI> & o, float (&c)[TI][2][4], float (&c2)[TI][2][4]) {
-    constexpr bool ONE = WF == W_Q4_1 || WF == W_Q5_1;
-    const v4i_t zero = {0, 0, 0, 0};
-#pragma unroll
-    for (int i = 0; i < TI; i++)
-#pragma unroll
-        for (int j = 0; j < 2; j++) {
-            const v4i_t s = __builtin_amdgcn_mfma_i32_16x16x32_i8(o.a[i], o.x[j], zero, 0, 0, 0);
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const float dw = h2f((uint16_t)(o.sc[i][q] & 0xFFFFu));
-                c[i][j][q] = fmaf(dw * o.dx[j], (float)s[q], c[i][j][q]);
-                if constexpr (ONE) {
-                    const float mw = h2f((uint16_t)(o.sc[i][q] >> 16));
-                    c2[i][j][q] = c2[i][j][q] + mw * o.sx[j];
-                }
-            }
-        }
+__device__ __forceinline__ uint32_t qg_h16(uint2 v, int q) {
+    const uint32_t w = q < 2 ? v.x : v.y;
+    return (q & 1) ? (w >> 16) : (w & 0xFFFFu);
 }
 
-template <int WF, int TI>
+template <int WF>
 __global__ __launch_bounds__(256) void k_qgemm(MMGroup g) {
-    constexpr bool ONE = WF == W_Q4_1 || WF == W_Q5_1;
-    constexpr int NE = TI * 2 * 4;  // outputs per lane
+    using Lt = QGLayout<WF>;
+    constexpr bool ONE = Lt::ONE;
+    constexpr int TI = Lt::TI;
+    __shared__ __attribute__((aligned(16))) char smem[2][Lt::BUF];
     int e = 0;
 #pragma unroll 1
     while (e + 1 < g.n && (int)blockIdx.x >= g.e[e + 1].block0) e++;
     const MMEntry & E = g.e[e];
     const int M = E.W.M, K = E.W.K, T = g.T, nb = K >> 5;
-    const int tilesT = (T + 63) / 64;
+    const int tilesT = (T + QG_TOK - 1) / QG_TOK;
     const int local = (int)blockIdx.x - E.block0;
     const int mtile = local / tilesT, ttile = local % tilesT;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int r16 = lane & 15, h = lane >> 4;
-    const int row0 = mtile * (32 * TI) + (wave & 1) * (16 * TI);  // this wave's first row
-    const int tok0 = ttile * 64 + (wave >> 1) * 32;                // this wave's first token
+    const int row0 = mtile * Lt::ROWS, tok0 = ttile * QG_TOK;
+    const int wr = (wave & 1) * 16 * TI, wt = (wave >> 1) * 32;  // this wave's tile-local row / token
+    const v4i_t rw = qg_rsrc(E.W.gt + (size_t)mtile * nb * Lt::WB);
+    const v4i_t ra = qg_rsrc(E.in.tq + (size_t)ttile * nb * Lt::AB);
+    const unsigned lds0 = __builtin_amdgcn_readfirstlane((unsigned)(unsigned long)(lds_void_t *)&smem[0][0]);
+    QGWalk ld;  // the loader's walk (this wave's steps)
+    ld.init(nb);
+    for (int i = 0; i < wave; i++) ld.next();
+    const int cq = nb >> 6, crem = nb & 63;  // class sizes for the consumer
 
-    // binary-counter tree over the 64 classes (levels 0..5), per output
+    // Per output: class sums in a binary counter (wave_sum63's tree).  Classes are walked in
+    // pairs: the even class accumulates straight into level 0 (st[0]), the odd one into c, and
+    // the pair then folds upward -- no copies or resets of accumulators between classes (each
+    // class's first block starts its chain from 0 in a peeled step).
     float st[6][TI][2][4], st2[6][TI][2][4];
     float tot[TI][2][4], tot2[TI][2][4];
-    QOp<WF, TI> op;
-    if (nb > 0) qop_load<WF, TI>(op, E, 0, nb, row0, row0, tok0, M, T, h, r16);
-#pragma unroll 1
-    for (int l = 0; l < 64; l++) {
-        float c[TI][2][4], c2[TI][2][4];
+    float c[TI][2][4], c2[TI][2][4];
+    const v4i_t zero = {0, 0, 0, 0};
+    const int nchunks = (nb + QG_STEPS - 1) / QG_STEPS;
+
+    int k = 0, cb = 0, cn = 1;  // step within the chunk, its buffer, next chunk to issue
+    // one block: MFMAs from this step's LDS operands, then the fp32 block epilogue into acc
+    auto step = [&](auto first, float (&acc)[TI][2][4], float (&acc2)[TI][2][4]) {
+        constexpr bool FIRST = decltype(first)::value;
+        // Chunk consumed: switch buffers (wave-uniform).  Done before this step's MFMAs, not
+        // after them, so no branch separates an MFMA from the reads of its result.
+        if (k == QG_STEPS) {
+            k = 0;
+            qg_chunk_done();  // the next chunk has landed and this buffer is free
+#if defined(QG_PROBE) && QG_PROBE == 2
+            if (cn < nchunks && cn < 2)  // tools/gemm_probe: compute only
+#else
+            if (cn < nchunks)
+#endif
+                qg_load_chunk<WF>(rw, ra, lds0 + cb * Lt::BUF, cn, ld, nb, wave, lane);
+            cn++;
+            cb ^= 1;
+        }
+#if defined(QG_PROBE) && QG_PROBE == 1
+        if (0)  // tools/gemm_probe: copies only
+#endif
+        {
+            QGOps<TI> o;
+            qg_read_ops<WF>(smem[cb] + k * Lt::STEP, o, wr, wt, r16, h);
+            v4i_t sv[TI][2];
+#pragma unroll
+            for (int i = 0; i < TI; i++)
+#pragma unroll
+                for (int j = 0; j < 2; j++) sv[i][j] = __builtin_amdgcn_mfma_i32_16x16x32_i8(o.af[i], o.xf[j], zero, 0, 0, 0);
+#pragma unroll
+            for (int i = 0; i < TI; i++)
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const float dw = h2f((uint16_t)qg_h16(o.sd[i], q));
+                    const float mw = ONE ? h2f((uint16_t)qg_h16(o.sm[i], q)) : 0.0f;
+#pragma unroll
+                    for (int j = 0; j < 2; j++) {
+                        acc[i][j][q] = fmaf(dw * o.dx[j], (float)sv[i][j][q], FIRST ? 0.0f : acc[i][j][q]);
+                        if constexpr (ONE) acc2[i][j][q] = (FIRST ? 0.0f : acc2[i][j][q]) + mw * o.sx[j];
+                    }
+                }
+        }
+        k++;
+    };
+    using T1 = std::integral_constant<bool, true>;
+    using T0 = std::integral_constant<bool, false>;
+    auto zero_acc = [&](float (&acc)[TI][2][4], float (&acc2)[TI][2][4]) {
 #pragma unroll
         for (int i = 0; i < TI; i++)
 #pragma unroll
             for (int j = 0; j < 2; j++)
 #pragma unroll
-                for (int q = 0; q < 4; q++) c[i][j][q] = c2[i][j][q] = 0.0f;
-#pragma unroll 1
-        for (int b = l; b < nb; b += 64) {
-            const QOp<WF, TI> cur = op;
-            const int bn = b + 64 < nb ? b + 64 : (l + 1 < nb ? l + 1 : -1);
-            if (bn >= 0) qop_load<WF, TI>(op, E, bn, nb, row0, row0, tok0, M, T, h, r16);
-            qop_compute<WF, TI>(cur, c, c2);
+                for (int q = 0; q < 4; q++) acc[i][j][q] = acc2[i][j][q] = 0.0f;
+    };
+    // all blocks of class l into acc (a class without blocks, nb < 64, is a zero leaf)
+    auto run_class = [&](int l, float (&acc)[TI][2][4], float (&acc2)[TI][2][4]) {
+        const int n = cq + (l < crem ? 1 : 0);
+        if (n == 0) {
+            zero_acc(acc, acc2);
+            return;
         }
-        // fold class l into the tree (wave_sum63's pairs (2i, 2i+1), then pairs of pairs, ...):
-        // a binary counter -- class l closes as many levels as l has trailing one bits
-        const int n = __builtin_ctz(~l);
-#define QG_ELEMS for (int i = 0; i < TI; i++) for (int j = 0; j < 2; j++) for (int q = 0; q < 4; q++)
-#define QG_CASE(N, DST, DST2)                                                                    \
-    case N: {                                                                                    \
-        _Pragma("unroll") QG_ELEMS {                                                             \
-            float v = c[i][j][q];                                                                \
-            for (int k = 0; k < N; k++) v = st[k][i][j][q] + v;                                  \
-            DST[i][j][q] = v;                                                                    \
-            if constexpr (ONE) {                                                                 \
-                float v2 = c2[i][j][q];                                                          \
-                for (int k = 0; k < N; k++) v2 = st2[k][i][j][q] + v2;                           \
-                DST2[i][j][q] = v2;                                                              \
-            }                                                                                    \
-        }                                                                                        \
-        break;                                                                                   \
+        step(T1{}, acc, acc2);
+        for (int u = 1; u < n; u++) step(T0{}, acc, acc2);
+    };
+
+    // odd class l (in c) closes ctz(~l) >= 1 levels: v = c, then v = st[k] + v for k < N
+#define QG_CASE(N, DST, DST2)                                                     \
+    case N: {                                                                     \
+        _Pragma("unroll") for (int i = 0; i < TI; i++)                            \
+        _Pragma("unroll") for (int j = 0; j < 2; j++)                             \
+        _Pragma("unroll") for (int q = 0; q < 4; q++) {                           \
+            float v = c[i][j][q];                                                 \
+            for (int kk = 0; kk < N; kk++) v = st[kk][i][j][q] + v;               \
+            DST[i][j][q] = v;                                                     \
+            if constexpr (ONE) {                                                  \
+                float v2 = c2[i][j][q];                                           \
+                for (int kk = 0; kk < N; kk++) v2 = st2[kk][i][j][q] + v2;        \
+                DST2[i][j][q] = v2;                                               \
+            }                                                                     \
+        }                                                                         \
+        break;                                                                    \
     }
-        switch (n) {
-            QG_CASE(0, st[0], st2[0])
+
+    if (nchunks > 0) qg_load_chunk<WF>(rw, ra, lds0, 0, ld, nb, wave, lane);
+    qg_chunk_done();
+    if (nchunks > 1) qg_load_chunk<WF>(rw, ra, lds0 + Lt::BUF, 1, ld, nb, wave, lane);
+    cn = 2;
+    for (int pr = 0; pr < 32; pr++) {
+        run_class(2 * pr, st[0], st2[0]);
+        run_class(2 * pr + 1, c, c2);
+        switch (__builtin_ctz(~(2 * pr + 1))) {
             QG_CASE(1, st[1], st2[1])
             QG_CASE(2, st[2], st2[2])
             QG_CASE(3, st[3], st2[3])
@@ -175,55 +301,68 @@ __global__ __launch_bounds__(256) void k_qgemm(MMGroup g) {
             default:
             QG_CASE(6, tot, tot2)
         }
-#undef QG_CASE
-#undef QG_ELEMS
     }
-    (void)NE;
-    // epilogue: y[t][m] = epi(total (+ total2)), as k_mm's red + red2
+#undef QG_CASE
+    // copies of a partial last chunk (or of none) were never waited for: drain before exit
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+    // epilogue: y[t][m] = epi(total (+ total2)), as k_mm's red + red2.  A lane holds rows
+    // 4h..4h+3 of one token: one 16-byte access per (token, 4 rows) when aligned.
+    const bool vec = ((E.ldy | M) & 3) == 0 && (((uintptr_t)E.y | (uintptr_t)E.aux) & 15) == 0;
 #pragma unroll
     for (int i = 0; i < TI; i++)
 #pragma unroll
         for (int j = 0; j < 2; j++) {
-            const int t = tok0 + 16 * j + r16;
+            const int t = tok0 + wt + 16 * j + r16;
+            const int m0 = row0 + wr + 16 * i + 4 * h;
+            if (t >= T || m0 >= M) continue;
+            float acc[4];
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const int m = row0 + 16 * i + 4 * h + q;
-                if (t < T && m < M) {
-                    const float acc = ONE ? tot[i][j][q] + tot2[i][j][q] : tot[i][j][q] + 0.0f;
-                    E.y[(size_t)t * E.ldy + m] = apply_epi(E, t, m, acc);
-                }
+            for (int q = 0; q < 4; q++) acc[q] = ONE ? tot[i][j][q] + tot2[i][j][q] : tot[i][j][q] + 0.0f;
+            float * yp = E.y + (size_t)t * E.ldy + m0;
+            if (vec) {
+                float4 yv = make_float4(0.f, 0.f, 0.f, 0.f), av = yv;
+                if (epi_reads_y(E.epi)) yv = *(const float4 *)yp;
+                if (epi_reads_aux(E.epi)) av = *(const float4 *)(E.aux + (size_t)t * E.ldy + m0);
+                float4 o;
+                o.x = apply_epi_v(E, m0, acc[0], yv.x, av.x);
+                o.y = apply_epi_v(E, m0 + 1, acc[1], yv.y, av.y);
+                o.z = apply_epi_v(E, m0 + 2, acc[2], yv.z, av.z);
+                o.w = apply_epi_v(E, m0 + 3, acc[3], yv.w, av.w);
+                *(float4 *)yp = o;
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    if (m0 + q < M) yp[q] = apply_epi(E, t, m0 + q, acc[q]);
             }
         }
 }
 
-template <int WF>
-static void launch_qgemm_wf(hipStream_t st, MMGroup & g, int blocks) {
-    constexpr int TI = (WF == W_Q4_1 || WF == W_Q5_1) ? 1 : 2;
-    hipLaunchKernelGGL((k_qgemm<WF, TI>), dim3(blocks), dim3(256), 0, st, g);
-}
-
 // Every entry must have y (the engine gives emitting entries a scratch y); emission into the
-// next matmul's activation format is a separate launch_act_from_f32 pass by the caller.
+// next matmul's activation format is a separate launch_act_from_f32 pass by the caller.  The
+// weights need their tile records (upload_mat) and the activations must be token tiles.
 bool launch_qgemm(hipStream_t st, MMGroup & g, int wtype) {
-    const int TI = (wtype == W_Q4_1 || wtype == W_Q5_1) ? 1 : 2;
-    const int tilesT = (g.T + 63) / 64;
+    const int rows = qg_rows(wtype);
+    const int tilesT = (g.T + QG_TOK - 1) / QG_TOK;
     int blocks = 0;
     for (int i = 0; i < g.n; i++) {
         MMEntry & e = g.e[i];
-        if (e.W.type != wtype || !e.W.sct || e.W.K % 32 || !e.y || e.in.fmt != act_fmt_for(wtype)) {
+        if (e.W.type != wtype || !e.W.gt || e.W.K % 32 || !e.y || e.in.fmt != act_fmt_for(wtype) || !e.in.tiled ||
+            !e.in.tq) {
             fprintf(stderr, "rwkv: qgemm entry %d not supported (type %d)\n", i, e.W.type);
             return false;
         }
         e.block0 = blocks;
-        blocks += (e.W.M + 32 * TI - 1) / (32 * TI) * tilesT;
+        blocks += (e.W.M + rows - 1) / rows * tilesT;
     }
     if (!blocks) return true;
+    const dim3 grid(blocks), block(256);
     switch (wtype) {
-        case W_Q4_0: launch_qgemm_wf<W_Q4_0>(st, g, blocks); break;
-        case W_Q4_1: launch_qgemm_wf<W_Q4_1>(st, g, blocks); break;
-        case W_Q5_0: launch_qgemm_wf<W_Q5_0>(st, g, blocks); break;
-        case W_Q5_1: launch_qgemm_wf<W_Q5_1>(st, g, blocks); break;
-        case W_Q8_0: launch_qgemm_wf<W_Q8_0>(st, g, blocks); break;
+        case W_Q4_0: hipLaunchKernelGGL(k_qgemm<W_Q4_0>, grid, block, 0, st, g); break;
+        case W_Q4_1: hipLaunchKernelGGL(k_qgemm<W_Q4_1>, grid, block, 0, st, g); break;
+        case W_Q5_0: hipLaunchKernelGGL(k_qgemm<W_Q5_0>, grid, block, 0, st, g); break;
+        case W_Q5_1: hipLaunchKernelGGL(k_qgemm<W_Q5_1>, grid, block, 0, st, g); break;
+        case W_Q8_0: hipLaunchKernelGGL(k_qgemm<W_Q8_0>, grid, block, 0, st, g); break;
         default: fprintf(stderr, "rwkv: qgemm type %d unsupported\n", wtype); return false;
     }
     HIP_OK(hipGetLastError());

@@ -38,7 +38,8 @@ bool make_act(DevBufs & b, int fmt, int T, int K, ActBuf & a) {
     a.d = (float *)b.alloc(nb * 4);
     a.s = (float *)b.alloc(nb * 4);
     a.qsum = (int *)b.alloc(nb * 4);
-    return a.f && a.h && a.q && a.d && a.s && a.qsum;
+    a.tq = (uint8_t *)b.alloc(((size_t)T + QG_TOK - 1) / QG_TOK * (K / 32) * qg_a_bytes(true));
+    return a.f && a.h && a.q && a.d && a.s && a.qsum && a.tq;
 }
 
 }  // namespace
@@ -80,6 +81,7 @@ static bool selftest_mm(int wtype, const void * W, int K, int M, const float * x
     float * dx = (float *)b.alloc((size_t)T * K * 4);
     float * dy = (float *)b.alloc((size_t)T * M * 4);
     ok = ok && dx && dy && make_act(b, act_fmt_for(wtype), T, K, a);
+    a.tiled = mfma ? 1 : 0;  // the GEMM reads token tiles, k_mm row-major blocks
     ok = ok && hipMemcpy(dx, x, (size_t)T * K * 4, hipMemcpyHostToDevice) == hipSuccess;
     ok = ok && launch_act_from_f32(nullptr, dx, T, K, a);
     if (ok) {

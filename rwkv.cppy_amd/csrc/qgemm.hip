@@ -204,6 +204,9 @@ __global__ __launch_bounds__(256) void k_qgemm(MMGroup g) {
 
     int k = 0, cb = 0, cn = 1;  // step within the chunk, its buffer, next chunk to issue
     // one block: MFMAs from this step's LDS operands, then the fp32 block epilogue into acc
+    // LDS operands of the current step live in registers (cur); the next step's are read while
+    // this step's epilogue runs, except across a chunk boundary (its buffer is not ready yet).
+    QGOps<TI> cur;
     auto step = [&](auto first, float (&acc)[TI][2][4], float (&acc2)[TI][2][4]) {
         constexpr bool FIRST = decltype(first)::value;
         // Chunk consumed: switch buffers (wave-uniform).  Done before this step's MFMAs, not
@@ -219,30 +222,32 @@ __global__ __launch_bounds__(256) void k_qgemm(MMGroup g) {
                 qg_load_chunk<WF>(rw, ra, lds0 + cb * Lt::BUF, cn, ld, nb, wave, lane);
             cn++;
             cb ^= 1;
+            qg_read_ops<WF>(smem[cb], cur, wr, wt, r16, h);
         }
 #if defined(QG_PROBE) && QG_PROBE == 1
         if (0)  // tools/gemm_probe: copies only
 #endif
         {
-            QGOps<TI> o;
-            qg_read_ops<WF>(smem[cb] + k * Lt::STEP, o, wr, wt, r16, h);
             v4i_t sv[TI][2];
 #pragma unroll
             for (int i = 0; i < TI; i++)
 #pragma unroll
-                for (int j = 0; j < 2; j++) sv[i][j] = __builtin_amdgcn_mfma_i32_16x16x32_i8(o.af[i], o.xf[j], zero, 0, 0, 0);
+                for (int j = 0; j < 2; j++) sv[i][j] = __builtin_amdgcn_mfma_i32_16x16x32_i8(cur.af[i], cur.xf[j], zero, 0, 0, 0);
+            QGOps<TI> nxt = cur;
+            if (k + 1 < QG_STEPS) qg_read_ops<WF>(smem[cb] + (k + 1) * Lt::STEP, nxt, wr, wt, r16, h);
 #pragma unroll
             for (int i = 0; i < TI; i++)
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
-                    const float dw = h2f((uint16_t)qg_h16(o.sd[i], q));
-                    const float mw = ONE ? h2f((uint16_t)qg_h16(o.sm[i], q)) : 0.0f;
+                    const float dw = h2f((uint16_t)qg_h16(cur.sd[i], q));
+                    const float mw = ONE ? h2f((uint16_t)qg_h16(cur.sm[i], q)) : 0.0f;
 #pragma unroll
                     for (int j = 0; j < 2; j++) {
-                        acc[i][j][q] = fmaf(dw * o.dx[j], (float)sv[i][j][q], FIRST ? 0.0f : acc[i][j][q]);
-                        if constexpr (ONE) acc2[i][j][q] = (FIRST ? 0.0f : acc2[i][j][q]) + mw * o.sx[j];
+                        acc[i][j][q] = fmaf(dw * cur.dx[j], (float)sv[i][j][q], FIRST ? 0.0f : acc[i][j][q]);
+                        if constexpr (ONE) acc2[i][j][q] = (FIRST ? 0.0f : acc2[i][j][q]) + mw * cur.sx[j];
                     }
                 }
+            cur = nxt;
         }
         k++;
     };
@@ -289,6 +294,7 @@ __global__ __launch_bounds__(256) void k_qgemm(MMGroup g) {
     qg_chunk_done();
     if (nchunks > 1) qg_load_chunk<WF>(rw, ra, lds0 + Lt::BUF, 1, ld, nb, wave, lane);
     cn = 2;
+    qg_read_ops<WF>(smem[0], cur, wr, wt, r16, h);
     for (int pr = 0; pr < 32; pr++) {
         run_class(2 * pr, st[0], st2[0]);
         run_class(2 * pr + 1, c, c2);

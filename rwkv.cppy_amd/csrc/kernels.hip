@@ -444,25 +444,57 @@ __device__ __forceinline__ float fold_g4(float v) {
     return __int_as_float(b[0]) + __int_as_float(b[1]);
 }
 
+typedef float f2_t __attribute__((ext_vector_type(2)));
+
+// One key group's operands of one token: 16 keys / receptances / decays as 8 packed pairs
+struct Wkv6Tok {
+    f2_t k[8], r[8], w[8];
+    float v;
+};
+
+template <bool WPT>
+__device__ __forceinline__ void wkv6_read_tok(Wkv6Tok & o, const float (*sk)[64], const float (*sr)[64],
+                                              const float (*sw)[64], const float (*sv)[16], int tt, int g, int jl) {
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const float4 a = *(const float4 *)&sk[tt][g * 16 + 4 * q];
+        const float4 b = *(const float4 *)&sr[tt][g * 16 + 4 * q];
+        o.k[2 * q] = f2_t{a.x, a.y}, o.k[2 * q + 1] = f2_t{a.z, a.w};
+        o.r[2 * q] = f2_t{b.x, b.y}, o.r[2 * q + 1] = f2_t{b.z, b.w};
+        if constexpr (WPT) {
+            const float4 c = *(const float4 *)&sw[tt][g * 16 + 4 * q];
+            o.w[2 * q] = f2_t{c.x, c.y}, o.w[2 * q + 1] = f2_t{c.z, c.w};
+        }
+    }
+    o.v = sv[tt][jl];
+}
+
+// WPT: per-token decays w[t][c] (v6); otherwise one decay per channel (v5).  The arithmetic per
+// state element is the decode kernel's (kernels_decode.hip k_att6_dec), element pairs in packed
+// f32 instructions (the same IEEE mul / add per element, no contraction); the output sum runs
+// over the 16 keys of the lane's group in order, then fold_g4 across the 4 groups.
+template <bool WPT>
 __global__ __launch_bounds__(64) void k_wkv6_s64(int T, int H, const float * k, const float * v, const float * r,
-                                                 const float * u, const float * w, int w_per_token,
-                                                 const float * sin, float * sout, float * y) {
+                                                 const float * u, const float * w, const float * sin, float * sout,
+                                                 float * y) {
     constexpr int S = 64;
-    __shared__ __attribute__((aligned(16))) float sk[WKV_TC][S], sr[WKV_TC][S], sw[WKV_TC][S], sv[WKV_TC][16];
+    __shared__ __attribute__((aligned(16))) float sk[WKV_TC][S], sr[WKV_TC][S], sw[WPT ? WKV_TC : 1][S],
+        sv[WKV_TC][16];
     const int h = blockIdx.x, jb = blockIdx.y, lane = threadIdx.x;
     const int jl = lane & 15, g = lane >> 4, j = jb * 16 + jl;
     const int C = H * S;
     const size_t hb = (size_t)h * S * S;
-    float st[16], uu[16], wc[16];
+    f2_t st[8], uu[8], wc[8];
 #pragma unroll
-    for (int ii = 0; ii < 16; ii++) {
-        st[ii] = sin[hb + (size_t)(g * 16 + ii) * S + j];
-        uu[ii] = u[h * S + g * 16 + ii];
-        wc[ii] = w_per_token ? 0.0f : w[h * S + g * 16 + ii];
+    for (int p = 0; p < 8; p++) {
+        const int i0 = g * 16 + 2 * p;
+        st[p] = f2_t{sin[hb + (size_t)i0 * S + j], sin[hb + (size_t)(i0 + 1) * S + j]};
+        uu[p] = f2_t{u[h * S + i0], u[h * S + i0 + 1]};
+        wc[p] = WPT ? f2_t{0.f, 0.f} : f2_t{w[h * S + i0], w[h * S + i0 + 1]};
     }
     // chunk staging: k/r/w rows of 64 floats = 16 float4 per token; lane moves float4 #(lane & 15)
     // of tokens (lane >> 4) + 4q, q < 8
-    float4 pk[8], pr[8], pw[8];
+    float4 pk[8], pr[8], pw[WPT ? 8 : 1];
     float4 pv[2];
     auto load_chunk = [&](int t0) {
 #pragma unroll
@@ -471,7 +503,7 @@ __global__ __launch_bounds__(64) void k_wkv6_s64(int T, int H, const float * k, 
             const size_t base = (size_t)t * C + (size_t)h * S + 4 * (lane & 15);
             pk[q] = *(const float4 *)(k + base);
             pr[q] = *(const float4 *)(r + base);
-            pw[q] = w_per_token ? *(const float4 *)(w + base) : make_float4(0, 0, 0, 0);
+            if constexpr (WPT) pw[q] = *(const float4 *)(w + base);
         }
 #pragma unroll
         for (int q = 0; q < 2; q++) {
@@ -486,7 +518,7 @@ __global__ __launch_bounds__(64) void k_wkv6_s64(int T, int H, const float * k, 
             const int tt = (lane >> 4) + 4 * q;
             *(float4 *)&sk[tt][4 * (lane & 15)] = pk[q];
             *(float4 *)&sr[tt][4 * (lane & 15)] = pr[q];
-            *(float4 *)&sw[tt][4 * (lane & 15)] = pw[q];
+            if constexpr (WPT) *(float4 *)&sw[tt][4 * (lane & 15)] = pw[q];
         }
 #pragma unroll
         for (int q = 0; q < 2; q++) *(float4 *)&sv[(lane >> 2) + 16 * q][4 * (lane & 3)] = pv[q];
@@ -497,49 +529,50 @@ __global__ __launch_bounds__(64) void k_wkv6_s64(int T, int H, const float * k, 
         __syncthreads();
         if (t0 + WKV_TC < T) load_chunk(t0 + WKV_TC);  // in flight during this chunk
         const int n = min(WKV_TC, T - t0);
-#pragma unroll 2
-        for (int tt = 0; tt < n; tt++) {
-            // this token's 16 keys / receptances / decays of group g: 12 ds_read_b128
-            float kk[16], rr[16], ww[16];
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const float4 a = *(const float4 *)&sk[tt][g * 16 + 4 * q];
-                const float4 b = *(const float4 *)&sr[tt][g * 16 + 4 * q];
-                kk[4 * q] = a.x, kk[4 * q + 1] = a.y, kk[4 * q + 2] = a.z, kk[4 * q + 3] = a.w;
-                rr[4 * q] = b.x, rr[4 * q + 1] = b.y, rr[4 * q + 2] = b.z, rr[4 * q + 3] = b.w;
-                if (w_per_token) {
-                    const float4 c = *(const float4 *)&sw[tt][g * 16 + 4 * q];
-                    ww[4 * q] = c.x, ww[4 * q + 1] = c.y, ww[4 * q + 2] = c.z, ww[4 * q + 3] = c.w;
-                } else {
-                    ww[4 * q] = wc[4 * q], ww[4 * q + 1] = wc[4 * q + 1], ww[4 * q + 2] = wc[4 * q + 2],
-                    ww[4 * q + 3] = wc[4 * q + 3];
-                }
-            }
-            const float vj = sv[tt][jl];
+        auto token = [&](const Wkv6Tok & o, int tt) {
+            const f2_t vj = f2_t{o.v, o.v};
             float acc = 0.0f;
 #pragma unroll
-            for (int ii = 0; ii < 16; ii++) {
-                const float kv = vj * kk[ii];
-                const float prev = st[ii];
-                const float temp = kv * uu[ii] + prev;
-                acc += temp * rr[ii];
-                st[ii] = prev * ww[ii] + kv;
+            for (int p = 0; p < 8; p++) {
+                const f2_t kv = vj * o.k[p];
+                const f2_t prev = st[p];
+                const f2_t temp = kv * uu[p] + prev;
+                const f2_t x = temp * o.r[p];
+                acc += x.x;
+                acc += x.y;
+                st[p] = prev * (WPT ? o.w[p] : wc[p]) + kv;
             }
             acc = fold_g4(acc);
             if (g == 0) y[(size_t)(t0 + tt) * C + h * S + j] = acc;
+        };
+        // two operand sets in turn: the next token's LDS reads overlap this token's arithmetic
+        Wkv6Tok A, B;
+        wkv6_read_tok<WPT>(A, sk, sr, sw, sv, 0, g, jl);
+        for (int tt = 0; tt < n; tt += 2) {
+            wkv6_read_tok<WPT>(B, sk, sr, sw, sv, min(tt + 1, n - 1), g, jl);
+            token(A, tt);
+            if (tt + 1 >= n) break;
+            wkv6_read_tok<WPT>(A, sk, sr, sw, sv, min(tt + 2, n - 1), g, jl);
+            token(B, tt + 1);
         }
         __syncthreads();
     }
 #pragma unroll
-    for (int ii = 0; ii < 16; ii++) sout[hb + (size_t)(g * 16 + ii) * S + j] = st[ii];
+    for (int p = 0; p < 8; p++) {
+        const int i0 = g * 16 + 2 * p;
+        sout[hb + (size_t)i0 * S + j] = st[p].x;
+        sout[hb + (size_t)(i0 + 1) * S + j] = st[p].y;
+    }
 }
 
 bool launch_wkv6(hipStream_t st, int T, int H, int S, const float * k, const float * v, const float * r,
                  const float * u, const float * w, int w_per_token, const float * state_in, float * state_out,
                  float * y) {
     if (S == 64) {
-        hipLaunchKernelGGL(k_wkv6_s64, dim3(H, 4), dim3(64), 0, st, T, H, k, v, r, u, w, w_per_token, state_in,
-                           state_out, y);
+        if (w_per_token)
+            hipLaunchKernelGGL(k_wkv6_s64<true>, dim3(H, 4), dim3(64), 0, st, T, H, k, v, r, u, w, state_in, state_out, y);
+        else
+            hipLaunchKernelGGL(k_wkv6_s64<false>, dim3(H, 4), dim3(64), 0, st, T, H, k, v, r, u, w, state_in, state_out, y);
         HIP_OK(hipGetLastError());
         return true;
     }

@@ -29,6 +29,19 @@ RWKV_API bool rwkv_mi355x_eval_device(struct rwkv_context * ctx, const uint32_t 
                                       bool compute_logits, float * logits_out, bool sync);
 RWKV_API bool rwkv_mi355x_sync(struct rwkv_context * ctx);
 
+/* One stage of the layer pipeline (the reference has no such entry point -- it is
+ * the unit the multi-GPU sequence evaluation is built from, rwkv.cppy_amd/python/rwkv_cpp/pipeline.py).
+ * Runs layers [layer_begin, layer_end) over T tokens on the device-resident state; only those
+ * layers' state slices change.  x_dev / vfirst_dev: device buffers [T][n_embed] fp32 on the
+ * context's GPU with the residual stream (and, v7 only, the layer-0 values v_first) entering
+ * layer_begin; on return they hold the ones leaving layer_end - 1.  layer_begin == 0 embeds
+ * `tokens` instead of reading x_dev (which may then be NULL).  When layer_end == n_layer and
+ * compute_logits, the head runs on the last token (logits_out host, may be NULL).  Synchronous.
+ * The same tensors, chunked along T, give results bit-identical to rwkv_eval_sequence. */
+RWKV_API bool rwkv_mi355x_eval_layers(struct rwkv_context * ctx, const uint32_t * tokens, size_t T,
+                                      uint32_t layer_begin, uint32_t layer_end, float * x_dev, float * vfirst_dev,
+                                      bool compute_logits, float * logits_out);
+
 /* The context's HIP stream (hipStream_t), so callers can time kernels with events on it. */
 RWKV_API void * rwkv_mi355x_stream(struct rwkv_context * ctx);
 

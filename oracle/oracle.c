@@ -1215,25 +1215,41 @@ static void ffn_v7(const oracle_model * m, const olayer * L, float * x, int64_t 
     free(xa); free(xp); free(xk); free(k); free(o);
 }
 
-int oracle_eval(const oracle_model * m, const uint32_t * tokens, size_t Tsz, const float * state_in,
-                float * state_out, float * logits_out) {
+/* Layers [l0, l1) over T tokens (the unit of a layer pipeline stage).  x_io /
+ * vfirst_io: [T][C] residual stream and (v7) layer-0 values entering l0, replaced by the ones
+ * leaving l1 - 1; with l0 == 0 the tokens are embedded instead (x_io / vfirst_io may then be
+ * NULL).  Only the state slices of layers [l0, l1) change.  Head on the last token when
+ * l1 == n_layer and logits_out is given. */
+int oracle_eval_layers(const oracle_model * m, const uint32_t * tokens, size_t Tsz, uint32_t l0, uint32_t l1,
+                       float * x_io, float * vfirst_io, const float * state_in, float * state_out,
+                       float * logits_out) {
     const int64_t T = (int64_t)Tsz, C = m->n_embed;
-    if (T <= 0) return 1;
-    for (int64_t t = 0; t < T; t++)
-        if (tokens[t] >= m->n_vocab) return 2;
+    if (T <= 0 || l0 > l1 || l1 > m->n_layer) return 1;
+    if (l0 == 0) {
+        if (!tokens) return 2;
+        for (int64_t t = 0; t < T; t++)
+            if (tokens[t] >= m->n_vocab) return 2;
+    } else if (!x_io || (m->major == 7 && !vfirst_io)) {
+        return 1;
+    }
     const int64_t SL = state_len(m);
     float * st = ALLOC(SL);
     if (state_in) memcpy(st, state_in, sizeof(float) * (size_t)SL); else oracle_init_state(m, st);
     float * x = ALLOC(T * C), * v_first = ALLOC(T * C);
-    /* rwkv_graph.inc:654-658 / :786-790 */
     float * row = ALLOC(C);
-    for (int64_t t = 0; t < T; t++) {
-        oracle_dequantize_row((int)m->emb->type, m->emb->data + tensor_nbytes(m->emb->type, (uint64_t)tokens[t] * C),
-                              row, C);
-        norm_row(row, x + t * C, C, 1e-5f, m->ln0_w, m->ln0_b);
+    if (l0 == 0) {
+        /* rwkv_graph.inc:654-658 / :786-790 */
+        for (int64_t t = 0; t < T; t++) {
+            oracle_dequantize_row((int)m->emb->type,
+                                  m->emb->data + tensor_nbytes(m->emb->type, (uint64_t)tokens[t] * C), row, C);
+            norm_row(row, x + t * C, C, 1e-5f, m->ln0_w, m->ln0_b);
+        }
+    } else {
+        memcpy(x, x_io, sizeof(float) * (size_t)(T * C));
+        if (m->major == 7) memcpy(v_first, vfirst_io, sizeof(float) * (size_t)(T * C));
     }
     const int64_t per_layer = m->major >= 5 ? C * (2 + m->head_size) : 5 * C;
-    for (uint32_t i = 0; i < m->n_layer; i++) {
+    for (uint32_t i = l0; i < l1; i++) {
         const olayer * L = &m->layers[i];
         float * ls = st + i * per_layer;
         switch (m->major) {
@@ -1244,14 +1260,21 @@ int oracle_eval(const oracle_model * m, const uint32_t * tokens, size_t Tsz, con
             default: break;
         }
     }
-    if (logits_out) {
+    if (logits_out && l1 == m->n_layer) {
         /* rwkv_graph.inc:704-708 / :850-854: head(LN(x[T-1])) */
         norm_row(x + (T - 1) * C, row, C, 1e-5f, m->lnout_w, m->lnout_b);
         mm(m->head, row, 1, logits_out);
     }
+    if (x_io) memcpy(x_io, x, sizeof(float) * (size_t)(T * C));
+    if (vfirst_io && m->major == 7) memcpy(vfirst_io, v_first, sizeof(float) * (size_t)(T * C));
     if (state_out) memcpy(state_out, st, sizeof(float) * (size_t)SL);
     free(st); free(x); free(v_first); free(row);
     return 0;
+}
+
+int oracle_eval(const oracle_model * m, const uint32_t * tokens, size_t Tsz, const float * state_in,
+                float * state_out, float * logits_out) {
+    return oracle_eval_layers(m, tokens, Tsz, 0, m->n_layer, NULL, NULL, state_in, state_out, logits_out);
 }
 
 /* ------------------------------------------------------------- quantizer */

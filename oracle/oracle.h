@@ -41,6 +41,13 @@ void oracle_init_state(const oracle_model * m, float * state);
 int oracle_eval(const oracle_model * m, const uint32_t * tokens, size_t T,
                 const float * state_in, float * state_out, float * logits_out);
 
+/* Layers [l0, l1) only (a layer-pipeline stage): x_io / vfirst_io [T][C] carry the residual
+ * stream (and v7's layer-0 values) in and out; l0 == 0 embeds the tokens instead.  Only the
+ * state slices of those layers change; logits when l1 == n_layer.  Returns 0 on success. */
+int oracle_eval_layers(const oracle_model * m, const uint32_t * tokens, size_t T, uint32_t l0, uint32_t l1,
+                       float * x_io, float * vfirst_io, const float * state_in, float * state_out,
+                       float * logits_out);
+
 /* rwkv_quantize_model_file semantics (rwkv_quantize.inc:16-171).  0 on success. */
 int oracle_quantize_file(const char * in_path, const char * out_path, const char * format);
 

@@ -809,12 +809,18 @@ bool Engine::layer_v7(int l, int T, const float * si, float * so) {
 
 bool Engine::forward(int T, const float * sin, float * sout, bool logits) {
     if (T == 1 && !generic_decode_) return forward_decode(sin, sout, logits);
+    return forward_range(T, sin, sout, 0, m_->n_layer, logits);
+}
+
+// Layers [l0, l1) over T tokens; l0 == 0 embeds the tokens into x_, otherwise x_ (and, v7,
+// vfirst_) already hold the stream entering l0.  Head on the last token when l1 == n_layer.
+bool Engine::forward_range(int T, const float * sin, float * sout, uint32_t l0, uint32_t l1, bool logits) {
     const size_t C = m_->n_embed;
-    if (!launch_embed_ln(stream_, dtokens_, T, m_->emb, m_->ln0_w, m_->ln0_b, x_)) return false;
+    if (l0 == 0 && !launch_embed_ln(stream_, dtokens_, T, m_->emb, m_->ln0_w, m_->ln0_b, x_)) return false;
     const size_t per_layer = m_->major >= 5 ? C * (2 + (size_t)m_->S) : 5 * C;
     // layer matmuls run over all T tokens: Q8 activations go straight into GEMM tiles
     tile_acts_ = T >= 2 && !use_mm_;
-    for (uint32_t l = 0; l < m_->n_layer; l++) {
+    for (uint32_t l = l0; l < l1; l++) {
         const float * si = sin + l * per_layer;
         float * so = sout + l * per_layer;
         bool ok = false;
@@ -831,7 +837,7 @@ bool Engine::forward(int T, const float * sin, float * sout, bool logits) {
         }
     }
     tile_acts_ = false;  // the head runs on the last token only
-    if (logits) {
+    if (logits && l1 == m_->n_layer) {
         // rwkv_graph.inc:704-708 / :850-854
         ActBuf hin = A(0, m_->head);
         if (!launch_ln_emit(stream_, (int)C, x_ + (size_t)(T - 1) * C, m_->lnout_w, m_->lnout_b, hin)) return false;
@@ -1228,6 +1234,38 @@ bool Engine::eval(const uint32_t * tokens, size_t T, const float * state_in, flo
         HIP_OK(hipMemcpyAsync(logits_out, logits_, (size_t)m_->n_vocab * 4, hipMemcpyDeviceToHost, stream_));
     if (state_out)
         HIP_OK(hipMemcpyAsync(state_out, dstate_[cur_], m_->state_len * 4, hipMemcpyDeviceToHost, stream_));
+    HIP_OK(hipStreamSynchronize(stream_));
+    return true;
+}
+
+// One layer-pipeline stage step on the device-resident state: x_io / vfirst_io
+// are device buffers [T][C] on this engine's device carrying the residual stream (and v7's
+// layer-0 values) between stages.  Synchronous: on return x_io holds this stage's output.
+bool Engine::eval_layers(const uint32_t * tokens, size_t T, uint32_t l0, uint32_t l1, float * x_io, float * vfirst_io,
+                         bool want_logits, float * logits_out) {
+    HIP_OK(hipSetDevice(m_->device));
+    if (!ensure_workspace((int)T)) return false;
+    const size_t bytes = T * (size_t)m_->n_embed * 4;
+    if (l0 == 0) {
+        HIP_OK(hipEventSynchronize(tok_event_));
+        memcpy(htokens_, tokens, T * 4);
+        HIP_OK(hipMemcpyAsync(dtokens_, htokens_, T * 4, hipMemcpyHostToDevice, stream_));
+        HIP_OK(hipEventRecord(tok_event_, stream_));
+    } else {
+        HIP_OK(hipMemcpyAsync(x_, x_io, bytes, hipMemcpyDeviceToDevice, stream_));
+        if (m_->major == 7) HIP_OK(hipMemcpyAsync(vfirst_, vfirst_io, bytes, hipMemcpyDeviceToDevice, stream_));
+    }
+    const bool lg = (want_logits || logits_out) && l1 == m_->n_layer;
+    if (!forward_range((int)T, dstate_[cur_], dstate_[cur_ ^ 1], l0, l1, lg)) return false;
+    // only this range's slices were written: copy them back instead of flipping the ping-pong
+    // pair, so later calls on other ranges still read a complete current state
+    const size_t C = m_->n_embed, per_layer = m_->major >= 5 ? C * (2 + (size_t)m_->S) : 5 * C;
+    HIP_OK(hipMemcpyAsync(dstate_[cur_] + l0 * per_layer, dstate_[cur_ ^ 1] + l0 * per_layer,
+                          (size_t)(l1 - l0) * per_layer * 4, hipMemcpyDeviceToDevice, stream_));
+    if (x_io) HIP_OK(hipMemcpyAsync(x_io, x_, bytes, hipMemcpyDeviceToDevice, stream_));
+    if (vfirst_io && m_->major == 7) HIP_OK(hipMemcpyAsync(vfirst_io, vfirst_, bytes, hipMemcpyDeviceToDevice, stream_));
+    if (lg && logits_out)
+        HIP_OK(hipMemcpyAsync(logits_out, logits_, (size_t)m_->n_vocab * 4, hipMemcpyDeviceToHost, stream_));
     HIP_OK(hipStreamSynchronize(stream_));
     return true;
 }

@@ -84,6 +84,8 @@ class Engine {
     bool eval(const uint32_t * tokens, size_t T, const float * state_in, float * state_out, float * logits_out);
     // device-resident evaluation on the context's own state
     bool eval_device(const uint32_t * tokens, size_t T, bool want_logits, float * logits_out, bool sync);
+    bool eval_layers(const uint32_t * tokens, size_t T, uint32_t l0, uint32_t l1, float * x_io, float * vfirst_io,
+                     bool want_logits, float * logits_out);
     bool state_upload(const float * state);
     bool state_download(float * state);
     bool sync();
@@ -97,6 +99,7 @@ class Engine {
     bool ensure_workspace(int T);
     bool init_state(float * st);
     bool forward(int T, const float * sin, float * sout, bool logits);
+    bool forward_range(int T, const float * sin, float * sout, uint32_t l0, uint32_t l1, bool logits);
     bool forward_decode(const float * sin, float * sout, bool logits);
     bool mv(MVGroup & g);
     bool run_tokens(const uint32_t * tokens, size_t T, bool want_logits);

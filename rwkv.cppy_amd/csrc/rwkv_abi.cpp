@@ -219,6 +219,26 @@ RWKV_API bool rwkv_mi355x_eval_device(struct rwkv_context * ctx, const uint32_t 
     return true;
 }
 
+RWKV_API bool rwkv_mi355x_eval_layers(struct rwkv_context * ctx, const uint32_t * tokens, size_t T,
+                                      uint32_t layer_begin, uint32_t layer_end, float * x_dev, float * vfirst_dev,
+                                      bool compute_logits, float * logits_out) {
+    ctx->last_error = RWKV_ERROR_NONE;
+    const DeviceModel & dm = ctx->model->dm;
+    CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, T > 0, "Sequence length is 0");
+    CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, layer_begin < layer_end && layer_end <= dm.n_layer, "Bad layer range");
+    CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, layer_begin == 0 || x_dev != nullptr, "x_dev required after layer 0");
+    CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, layer_begin == 0 || dm.major != 7 || vfirst_dev != nullptr,
+              "vfirst_dev required after layer 0 (v7)");
+    if (layer_begin == 0) {
+        CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, tokens != nullptr, "Tokens required at layer 0");
+        for (size_t i = 0; i < T; i++) CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, tokens[i] < dm.n_vocab, "Token out of range");
+    }
+    CTX_CHECK(ctx, RWKV_ERROR_CTX, false,
+              ctx->engine->eval_layers(tokens, T, layer_begin, layer_end, x_dev, vfirst_dev, compute_logits, logits_out),
+              "GPU evaluation failed");
+    return true;
+}
+
 RWKV_API bool rwkv_mi355x_sync(struct rwkv_context * ctx) { return ctx->engine->sync(); }
 RWKV_API void * rwkv_mi355x_stream(struct rwkv_context * ctx) { return (void *)ctx->engine->stream(); }
 RWKV_API float * rwkv_mi355x_device_state(struct rwkv_context * ctx) { return ctx->engine->device_state(); }

@@ -72,6 +72,8 @@ class RWKVSharedLibrary:
         L.rwkv_mi355x_state_download.restype = ctypes.c_bool
         L.rwkv_mi355x_eval_device.argtypes = [vp, P_INT, sz, ctypes.c_bool, P_FLOAT, ctypes.c_bool]
         L.rwkv_mi355x_eval_device.restype = ctypes.c_bool
+        L.rwkv_mi355x_eval_layers.argtypes = [vp, vp, sz, u32, u32, vp, vp, ctypes.c_bool, P_FLOAT]
+        L.rwkv_mi355x_eval_layers.restype = ctypes.c_bool
         L.rwkv_mi355x_sync.argtypes = [vp]
         L.rwkv_mi355x_sync.restype = ctypes.c_bool
         L.rwkv_mi355x_stream.argtypes = [vp]

@@ -34,6 +34,8 @@ def lib():
         L.oracle_init_state.argtypes = [vp, vp]
         L.oracle_eval.argtypes = [vp, vp, sz, vp, vp, vp]
         L.oracle_eval.restype = ctypes.c_int
+        L.oracle_eval_layers.argtypes = [vp, vp, sz, ctypes.c_uint32, ctypes.c_uint32, vp, vp, vp, vp, vp]
+        L.oracle_eval_layers.restype = ctypes.c_int
         L.oracle_quantize_file.argtypes = [ctypes.c_char_p] * 3
         L.oracle_quantize_file.restype = ctypes.c_int
         L.oracle_set_threads.argtypes = [ctypes.c_int]
@@ -76,6 +78,19 @@ class OracleModel:
         rc = lib().oracle_eval(self.ptr, _p(toks), len(toks), _p(state_in), _p(st), _p(lg))
         if rc:
             raise ValueError(f'oracle_eval failed rc={rc}')
+        return lg, st
+
+    def eval_layers(self, tokens, l0, l1, x=None, vfirst=None, state_in=None, want_logits=False):
+        """Layers [l0, l1) over len(tokens) tokens (a pipeline stage).  x / vfirst: [T, C] float32
+        arrays updated in place (required when l0 > 0; vfirst for v7 only).  Returns
+        (logits or None, full state with only this range's slices updated)."""
+        toks = np.ascontiguousarray(np.asarray(tokens, dtype=np.uint32))
+        st = np.zeros(self.state_len, np.float32)
+        lg = np.zeros(self.n_vocab, np.float32) if want_logits and l1 == self.n_layer else None
+        rc = lib().oracle_eval_layers(self.ptr, _p(toks), len(toks), l0, l1, _p(x), _p(vfirst), _p(state_in),
+                                      _p(st), _p(lg))
+        if rc:
+            raise ValueError(f'oracle_eval_layers failed rc={rc}')
         return lg, st
 
     def eval_serial(self, tokens, state_in=None):

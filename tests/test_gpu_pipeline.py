@@ -1,0 +1,121 @@
+"""Layer pipeline on the GPU: rwkv_mi355x_eval_layers stages composed over layer
+ranges and T-chunks give the whole-sequence result bit for bit, and the multi-process driver
+(rwkv_cpp.pipeline) does too.  The one-GPU box runs the 2-rank driver with gloo as the wire
+(both ranks on cuda:0; RCCL needs one GPU per rank) -- the nccl path is the same code with
+device-resident messages, exercised by bench.py --gpus N."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+from rwkv_lib import LIB_PATH, RWKVModel, library
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(__file__), 'golden')
+
+
+def _ctx_eval_layers(L, ctx, toks, l0, l1, x, want_logits, n_vocab):
+    import ctypes
+    lg = np.zeros(n_vocab, np.float32) if want_logits else None
+    t = np.ascontiguousarray(np.asarray(toks, np.uint32))
+    ok = L.library.rwkv_mi355x_eval_layers(ctx.ptr, t.ctypes.data, len(t), l0, l1, x[0].data_ptr(),
+                                           x[1].data_ptr() if x.shape[0] > 1 else None, want_logits,
+                                           lg.ctypes.data_as(ctypes.POINTER(ctypes.c_float)) if want_logits else None)
+    assert ok
+    return lg
+
+
+def _synthetic(tmp_path, arch, fmt, n_layer=5):
+    L = library()
+    p = str(tmp_path / f'pipe{arch}{fmt}.bin')
+    assert L.library.rwkv_mi355x_write_synthetic_model(p.encode(), arch, 1024, 2048, n_layer, 0, fmt.encode(), 5)
+    return p
+
+
+@pytest.mark.parametrize('arch,fmt', [(6, 'Q4_0'), (7, 'Q5_1'), (5, 'Q4_1'), (4, 'Q8_0')])
+def test_stage_composition_bit_exact(tmp_path, arch, fmt):
+    """[0, a) then [a, b) then [b, L) per chunk of 24 tokens == one rwkv_eval_sequence of 70."""
+    L = library()
+    p = _synthetic(tmp_path, arch, fmt)
+    m = RWKVModel(L, p)
+    toks = [int(t) for t in np.random.default_rng(9).integers(0, 1024, 70)]
+    ref_lg, ref_st = m.eval_sequence(toks, None, use_numpy=True)
+    m.free()
+    ctx = L.rwkv_init_from_file(p, 1, 99)
+    n_layer, C, n_vocab = L.rwkv_get_n_layer(ctx), L.rwkv_get_n_embed(ctx), L.rwkv_get_n_vocab(ctx)
+    assert L.library.rwkv_mi355x_state_upload(ctx.ptr, None)
+    planes = 2 if arch == 7 else 1
+    cuts = [(0, 2), (2, 3), (3, n_layer)]
+    lg = None
+    for a in range(0, len(toks), 24):
+        ch = toks[a:a + 24]
+        x = torch.zeros((planes, len(ch), C), dtype=torch.float32, device='cuda')
+        for l0, l1 in cuts:
+            lg = _ctx_eval_layers(L, ctx, ch, l0, l1, x, l1 == n_layer, n_vocab)
+    st = np.zeros(L.rwkv_get_state_buffer_element_count(ctx), np.float32)
+    assert L.library.rwkv_mi355x_state_download(ctx.ptr, st.ctypes.data_as(
+        __import__('ctypes').POINTER(__import__('ctypes').c_float)))
+    L.rwkv_free(ctx)
+    assert np.array_equal(lg.view(np.uint32), ref_lg.view(np.uint32))
+    assert np.array_equal(st.view(np.uint32), ref_st.view(np.uint32))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def _rank_main(rank, world, port, path, toks, chunk, out_dir):
+    import ctypes
+    import sys
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.join(os.path.dirname(LIB_PATH), '..', 'python'))
+    from rwkv_cpp import RWKVSharedLibrary
+    from rwkv_cpp.pipeline import LibraryStage, pipeline_eval_sequence, stage_layers
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        L = RWKVSharedLibrary(LIB_PATH)
+        ctx = L.rwkv_init_from_file(path, 1, 99)
+        arch = (ctypes.c_int64 * 4)()
+        L.library.rwkv_mi355x_arch(ctx.ptr, arch)
+        stage = LibraryStage(L, ctx, L.rwkv_get_n_vocab(ctx), int(arch[0]))
+        stage.reset_state()
+        n_layer, C = L.rwkv_get_n_layer(ctx), L.rwkv_get_n_embed(ctx)
+        lg = pipeline_eval_sequence(stage, toks, chunk, n_layer, C, stage.planes, rank, world,
+                                    torch.device('cuda', 0), wire_device=torch.device('cpu'))
+        st = np.zeros(L.rwkv_get_state_buffer_element_count(ctx), np.float32)
+        assert L.library.rwkv_mi355x_state_download(ctx.ptr, st.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
+        l0, l1 = stage_layers(n_layer, world, rank)
+        per = len(st) // n_layer
+        np.save(os.path.join(out_dir, f'state{rank}.npy'), st[l0 * per:l1 * per])
+        if lg is not None:
+            np.save(os.path.join(out_dir, 'logits.npy'), lg)
+        L.rwkv_free(ctx)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('arch,fmt,chunk', [(6, 'Q4_0', 16), (7, 'Q5_1', 33)])
+def test_two_process_pipeline_bit_exact(tmp_path, arch, fmt, chunk):
+    import torch.multiprocessing as mp
+    L = library()
+    p = _synthetic(tmp_path, arch, fmt)
+    toks = [int(t) for t in np.random.default_rng(4).integers(0, 1024, 70)]
+    m = RWKVModel(L, p)
+    ref_lg, ref_st = m.eval_sequence(toks, None, use_numpy=True)
+    n_layer = L.rwkv_get_n_layer(m._ctx)
+    m.free()
+    mp.start_processes(_rank_main, args=(2, _free_port(), p, toks, chunk, str(tmp_path)), nprocs=2,
+                       start_method='spawn', join=True)
+    assert np.array_equal(np.load(tmp_path / 'logits.npy').view(np.uint32), ref_lg.view(np.uint32))
+    per = len(ref_st) // n_layer
+    from rwkv_cpp.pipeline import stage_layers
+    for r in range(2):
+        l0, l1 = stage_layers(n_layer, 2, r)
+        got = np.load(tmp_path / f'state{r}.npy')
+        assert np.array_equal(got.view(np.uint32), ref_st[l0 * per:l1 * per].view(np.uint32)), r

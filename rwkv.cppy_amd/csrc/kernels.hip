@@ -531,16 +531,25 @@ __global__ __launch_bounds__(64) void k_wkv6_s64(int T, int H, const float * k, 
         const int n = min(WKV_TC, T - t0);
         auto token = [&](const Wkv6Tok & o, int tt) {
             const f2_t vj = f2_t{o.v, o.v};
+            // phase by phase over the 8 independent pairs (no dependent packed op back to back)
+            f2_t kv[8], x[8];
+#pragma unroll
+            for (int p = 0; p < 8; p++) kv[p] = vj * o.k[p];
+#pragma unroll
+            for (int p = 0; p < 8; p++) x[p] = kv[p] * uu[p];
+#pragma unroll
+            for (int p = 0; p < 8; p++) x[p] = x[p] + st[p];
+#pragma unroll
+            for (int p = 0; p < 8; p++) x[p] = x[p] * o.r[p];
+#pragma unroll
+            for (int p = 0; p < 8; p++) st[p] = st[p] * (WPT ? o.w[p] : wc[p]);
+#pragma unroll
+            for (int p = 0; p < 8; p++) st[p] = st[p] + kv[p];
             float acc = 0.0f;
 #pragma unroll
             for (int p = 0; p < 8; p++) {
-                const f2_t kv = vj * o.k[p];
-                const f2_t prev = st[p];
-                const f2_t temp = kv * uu[p] + prev;
-                const f2_t x = temp * o.r[p];
-                acc += x.x;
-                acc += x.y;
-                st[p] = prev * (WPT ? o.w[p] : wc[p]) + kv;
+                acc += x[p].x;
+                acc += x[p].y;
             }
             acc = fold_g4(acc);
             if (g == 0) y[(size_t)(t0 + tt) * C + h * S + j] = acc;

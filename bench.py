@@ -6,7 +6,8 @@ logits produced) of RWKV-v6-World-1B6 Q4_0 with the recurrent state resident in 
 (rwkv_mi355x_eval_device).  Steps are enqueued back to back on the context's stream.
 value = tokens decoded by all ranks / max-over-ranks wall time of the K timed steps.
 Multi-GPU: decode does not shard -- each rank runs an independent replica
-("scaling": "weak").
+("scaling": "weak").  Sequence evaluation is reported both ways: independent replicas, and one
+sequence through a layer pipeline over all ranks (rwkv_cpp/pipeline.py, RCCL point-to-point).
 
 Also reported (same run): 1024-token rwkv_eval_sequence throughput, ABI-level decode
 (13 MB of host state in and out per token, the reference's contract), the dominant kernel's
@@ -54,6 +55,7 @@ def main():
     ap.add_argument('--seq-len', type=int, default=1024)
     ap.add_argument('--seq-reps', type=int, default=3)
     ap.add_argument('--abi-steps', type=int, default=16)
+    ap.add_argument('--pipe-chunk', type=int, default=0, help='pipeline chunk (0: max(64, T / (2 N)))')
     ap.add_argument('--timing-steps', type=int, default=8)
     ap.add_argument('--cpu-seconds', type=float, default=12.0)
     ap.add_argument('--skip-cpu', action='store_true')
@@ -63,16 +65,29 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local_rank = int(os.environ.get('LOCAL_RANK', '0'))
-    os.environ.setdefault('RWKV_MI355X_DEVICE', str(local_rank))
+    # RWKV_BENCH_BACKEND=gloo: rehearsal of the multi-rank code on fewer GPUs (ranks share GPUs,
+    # messages go through host memory); the real runs use nccl (RCCL), one GPU per rank
+    backend = os.environ.get('RWKV_BENCH_BACKEND', 'nccl')
     import torch
     import torch.distributed as dist
+    gpu = local_rank % max(1, torch.cuda.device_count()) if backend == 'gloo' else local_rank
+    os.environ.setdefault('RWKV_MI355X_DEVICE', str(gpu))
     if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local_rank))
+        torch.cuda.set_device(gpu)
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', gpu))
+        else:
+            dist.init_process_group(backend)
+    wire = torch.device('cuda', gpu) if backend == 'nccl' else torch.device('cpu')
 
     def barrier():
         if world > 1:
             dist.barrier()
+
+    def allmax(v):
+        t = torch.tensor([v], device=wire)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
 
     import rwkv_cpp
     lib = rwkv_cpp.RWKVSharedLibrary(os.path.join(REPO, 'rwkv.cppy_amd', 'build', 'librwkv.so'))
@@ -125,9 +140,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        tt = torch.tensor([elapsed], device='cuda')
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+        elapsed = allmax(elapsed)
     ms_per_step = elapsed * 1e3 / args.steps
     value = world * args.steps / elapsed
     log(f'decode: {ms_per_step * 1e3:.1f} us/token, {value:.1f} tok/s aggregate over {world} GPU(s)')
@@ -147,6 +160,42 @@ def main():
     seq_s = min(ts) if ts else float('nan')
     seq_tps = args.seq_len / seq_s if ts else 0.0
     log(f'seq-eval T={args.seq_len}: {seq_s * 1e3:.1f} ms, {seq_tps:.0f} tok/s')
+
+    # ---------------- sequence eval as a layer pipeline over all ranks ----------------
+    pipe = None
+    if world > 1 and args.seq_reps > 0:
+        try:
+            from rwkv_cpp.pipeline import LibraryStage, pipeline_eval_sequence, stage_layers
+            archv = (ctypes.c_int64 * 4)()
+            L.rwkv_mi355x_arch(ctx.ptr, archv)
+            stage = LibraryStage(lib, ctx, n_vocab, int(archv[0]))
+            chunk = args.pipe_chunk or max(64, args.seq_len // (2 * world))
+            pseq = np.random.default_rng(4321).integers(0, n_vocab, size=args.seq_len)  # same on every rank
+            dev = torch.device('cuda', gpu)
+
+            def run_pipe():
+                stage.reset_state()
+                return pipeline_eval_sequence(stage, pseq, chunk, NL, C, stage.planes, rank, world, dev,
+                                              wire_device=wire)
+
+            run_pipe()  # warm-up: P2P communicators, workspaces
+            pts = []
+            for _ in range(args.seq_reps):
+                torch.cuda.synchronize()
+                barrier()
+                t1 = time.perf_counter()
+                run_pipe()
+                torch.cuda.synchronize()
+                barrier()
+                pts.append(allmax(time.perf_counter() - t1))
+            l0, l1 = stage_layers(NL, world, rank)
+            pipe = {'tokens_per_s': round(args.seq_len / min(pts), 1), 'ms_per_sequence': round(min(pts) * 1e3, 3),
+                    'parallelism': f'layer pipeline x{world}', 'scaling': 'strong', 'chunk': chunk,
+                    'transport': f'torch.distributed {backend} isend/irecv of x [chunk, C] fp32'}
+            log(f'pipeline seq-eval over {world} stages (rank {rank}: layers [{l0}, {l1})): '
+                f'{min(pts) * 1e3:.1f} ms, {args.seq_len / min(pts):.0f} tok/s, chunk {chunk}')
+        except Exception as e:  # reported, never required for the decode line
+            log(f'pipeline seq-eval failed: {e!r}')
 
     # ---------------- ABI-level decode (host state, reference contract) ----------------
     state = np.zeros(state_len, np.float32)
@@ -240,7 +289,8 @@ def main():
                                    f'state resident in HBM', 'n_embed': C, 'n_layer': NL, 'n_vocab': V,
                        'weights': fmt, 'parallelism': f'replicas x{world}'},
             'seq_eval': {'tokens_per_s': round(seq_tps * world, 1), 'T': args.seq_len,
-                         'ms_per_sequence': round(seq_s * 1e3, 3)},
+                         'ms_per_sequence': round(seq_s * 1e3, 3), 'parallelism': f'replicas x{world}',
+                         'pipeline': pipe},
             'abi_decode_tokens_per_s': round(abi_tps * world, 2),
             'roofline': roofline,
             'cpu_baseline': cpu,

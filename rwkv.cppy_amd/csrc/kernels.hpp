@@ -104,12 +104,31 @@ struct MVEntry {
     int block0;
 };
 
+// The scalars k_mva reads, copied out of the entry by launch_mv_group into one contiguous
+// record so the kernel fetches them as a few back-to-back wide scalar loads (one round trip).
+struct MVHot {
+    const uint8_t * qs;
+    const uint32_t * qh;
+    const void * sc;
+    const int8_t * aq;
+    const float * ad;
+    const float * as;
+    const int * aqsum;
+    const void * ahf;       // A_F16 halves or A_F32 floats
+    float * y;
+    const float * aux;      // g_mv_zero-free: null -> step 0 over a zero word (set by the kernel)
+    const float * bias;
+    int M, K, epi, steps;   // steps: bit0 aux present, bit1 bias present
+};
+
 struct MVGroup {
+    MVHot hot[MM_MAX_ENTRIES];
     MVEntry e[MM_MAX_ENTRIES];
     int n;
     int lds_bytes;
     int stride;              // set by launch_mv_group: >0 = workgroups walk row blocks
     int grid;                // set by launch_mv_group: workgroups launched
+    int units_max;           // set by launch_mv_group: max 16-byte units per lane over entries
 };
 
 // Busy-waits about `us` microseconds on the device (kernel timing: lets the host queue a whole

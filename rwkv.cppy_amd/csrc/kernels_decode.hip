@@ -68,6 +68,26 @@ bool launch_mv_group(hipStream_t st, MVGroup & g) {
         if (e.src != SRC_ACT) lds = std::max(lds, lds_bytes_for(act_fmt_for(e.W.type), e.W.K));
     }
     g.lds_bytes = lds;
+    g.units_max = umax;
+    for (int i = 0; i < g.n; i++) {
+        const MVEntry & e = g.e[i];
+        MVHot & h = g.hot[i];
+        h.qs = e.W.qs;
+        h.qh = e.W.qh;
+        h.sc = e.W.sc;
+        h.aq = e.act.q;
+        h.ad = e.act.d;
+        h.as = e.act.s;
+        h.aqsum = e.act.qsum;
+        h.ahf = e.act.fmt == A_F16 ? (const void *)e.act.h : (const void *)e.act.f;
+        h.y = e.y;
+        h.aux = e.aux;
+        h.bias = e.bias;
+        h.M = e.W.M;
+        h.K = e.W.K;
+        h.epi = e.epi;
+        h.steps = (e.aux ? 1 : 0) | (e.bias ? 2 : 0);
+    }
     if (!blocks) return true;
     // a single large prologue entry (the head): persistent walk over its row blocks, one
     // LayerNorm per workgroup

@@ -5,6 +5,7 @@
 #include "device_common.hpp"
 #include "kernels.hpp"
 
+#include <limits.h>
 #include <stdio.h>
 
 namespace rwkvmi {
@@ -324,7 +325,7 @@ __device__ __forceinline__ float epi_apply(int epi, float acc, const EpiIn & p) 
 // vmcnt is in order per wave, so a prologue wave never waits behind the weight stream and a
 // dot wave's weights are in flight from its first instruction.
 template <int WF, int R, int U, int SRCK, int FORM, bool EMIT, int NW, int LNP>
-__device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, int stride, char * smem, float * red) {
+__device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, int b0, int stride, char * smem, float * red) {
     constexpr bool PRO = SRCK != MVK_ACT;
     constexpr int LNR = LNP > 0 ? LNP : 1;
     constexpr int RW = NW * R;
@@ -347,7 +348,7 @@ __device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, int stride
             chunk_load<SRCK, FORM>(Ent, min(k0, K - 8), ci);
             float mean = 0.0f, scale = 0.0f;
             if constexpr (SRCK == MVK_LN) ln_stats_regs<LNR>(lv, K, 1e-5f, mean, scale);
-            const bool write_carry = Ent.carry_out && wgi == (int)blockIdx.x - Ent.block0;
+            const bool write_carry = Ent.carry_out && wgi == (int)blockIdx.x - b0;
             chunk_store<WF, SRCK, FORM>(Ent, a, ci, mean, scale, write_carry, k0, k0 < K, lane);
             for (int c = pw + NW; c * 512 < K; c += NW) {
                 const int kk = c * 512 + lane * 8;
@@ -466,29 +467,115 @@ __device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, int stride
 // WFIX >= 0: every entry of the group has weight type WFIX (one body, fewer registers);
 // WFIX < 0: per-entry switch.  SRCK / FORM: the group's input source and token-shift form
 // (compile-time, so the prologue has no data-independent branches).
+//
+// The entry's first workgroups b1..b7 (b_i = e[i].block0, or INT_MAX past the last entry) are
+// scalar arguments ahead of the group so the code object preloads them into SGPRs
+// (-amdgpu-kernarg-preload-count): the entry index is SALU compares, and the entry's weight
+// pointers are one scalar-load round trip away from the kernel's first instruction (a loop
+// over g.e[].block0 would be one dependent kernarg load per entry).
 template <int R, int U, int SRCK, int FORM, bool EMIT, int WFIX, int LNP>
-__global__ __launch_bounds__(512) void k_mv(MVGroup g) {
+__global__ __launch_bounds__(512) void k_mv(int b1, int b2, int b3, int b4, int b5, int b6, int b7, MVGroup g) {
     constexpr int NW = 4;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ float red[NW * R];
-    int e = 0;
-#pragma unroll 1
-    while (e + 1 < g.n && (int)blockIdx.x >= g.e[e + 1].block0) e++;
+    const int bx = (int)blockIdx.x;
+    const int e = (bx >= b1) + (bx >= b2) + (bx >= b3) + (bx >= b4) + (bx >= b5) + (bx >= b6) + (bx >= b7);
+    const int b0 = e == 0 ? 0 : e == 1 ? b1 : e == 2 ? b2 : e == 3 ? b3 : e == 4 ? b4 : e == 5 ? b5 : e == 6 ? b6 : b7;
     const MVEntry & Ent = g.e[e];
-    const int wgi = (int)blockIdx.x - Ent.block0;
+    const int wgi = bx - b0;
     if constexpr (WFIX >= 0) {
-        mv_body<WFIX, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, g.stride, smem, red);
+        mv_body<WFIX, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red);
     } else {
         switch (Ent.W.type) {
-            case W_F32: mv_body<W_F32, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, g.stride, smem, red); break;
-            case W_F16: mv_body<W_F16, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, g.stride, smem, red); break;
-            case W_Q4_0: mv_body<W_Q4_0, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, g.stride, smem, red); break;
-            case W_Q4_1: mv_body<W_Q4_1, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, g.stride, smem, red); break;
-            case W_Q5_0: mv_body<W_Q5_0, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, g.stride, smem, red); break;
-            case W_Q5_1: mv_body<W_Q5_1, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, g.stride, smem, red); break;
-            case W_Q8_0: mv_body<W_Q8_0, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, g.stride, smem, red); break;
+            case W_F32: mv_body<W_F32, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red); break;
+            case W_F16: mv_body<W_F16, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red); break;
+            case W_Q4_0: mv_body<W_Q4_0, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red); break;
+            case W_Q4_1: mv_body<W_Q4_1, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red); break;
+            case W_Q5_0: mv_body<W_Q5_0, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red); break;
+            case W_Q5_1: mv_body<W_Q5_1, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red); break;
+            case W_Q8_0: mv_body<W_Q8_0, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red); break;
             default: break;
         }
+    }
+}
+
+// Activation-input matvec (SRC_ACT, no emission, one weight type): the lean form of mv_body's
+// dot-wave path.  Every scalar the launch needs (weights, activation, epilogue) is read from
+// the group before any arithmetic, so they arrive in one scalar-load round trip and the weight
+// stream is issued right after it; no persistent walk, no prologue waves.  Same lane/unit
+// assignment and accumulation order as mv_body (bit-identical results).
+template <int WF, int R, int U>
+__global__ __launch_bounds__(256) void k_mva(int b1, int b2, int b3, int b4, int b5, int b6, int b7, MVGroup g) {
+    const int bx = (int)blockIdx.x;
+    const int e = (bx >= b1) + (bx >= b2) + (bx >= b3) + (bx >= b4) + (bx >= b5) + (bx >= b6) + (bx >= b7);
+    const int b0 = e == 0 ? 0 : e == 1 ? b1 : e == 2 ? b2 : e == 3 ? b3 : e == 4 ? b4 : e == 5 ? b5 : e == 6 ? b6 : b7;
+    const MVHot h = g.hot[e];
+    DMat W;
+    W.type = WF;
+    W.M = h.M;
+    W.K = h.K;
+    W.qs = h.qs;
+    W.qh = h.qh;
+    W.sc = h.sc;
+    ActBuf a;
+    a.K = h.K;
+    a.q = (int8_t *)h.aq;
+    a.d = (float *)h.ad;
+    a.s = (float *)h.as;
+    a.qsum = (int *)h.aqsum;
+    a.h = (__half *)h.ahf;
+    a.f = (float *)h.ahf;
+    const float * const aux = (h.steps & 1) ? h.aux : g_mv_zero;
+    const float * const bias = (h.steps & 2) ? h.bias : g_mv_zero;
+    const int astep = h.steps & 1, bstep = (h.steps >> 1) & 1;
+
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int M = h.M, K = h.K;
+    const int row0 = (bx - b0) * (4 * R) + wave * R;
+    int rows[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) rows[r] = min(row0 + r, M - 1);
+    // all U units of every row in flight before anything waits (clamped loads, no branches)
+    WBlk w[R][U];
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+        for (int r = 0; r < R; r++) w[r][u] = load_unit<WF>(W, rows[r], u, lane);
+    AUnit x[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) x[u] = load_act_unit<WF, false>(a, u, lane);
+    EpiIn ep[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        ep[r].y = h.y[rows[r]];
+        ep[r].aux = aux[rows[r] * astep];
+        ep[r].bias = bias[rows[r] * bstep];
+    }
+    // keep the machine scheduler from interleaving later rows' loads with earlier rows' dots
+    __builtin_amdgcn_sched_barrier(0);
+    float acc[R], acc2[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) acc[r] = acc2[r] = 0.0f;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const bool valid = unit_valid<WF>(K, u, lane);
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            float t = acc[r], t2 = acc2[r];
+            dot_unit<WF>(w[r][u], x[u], t, t2);
+            acc[r] = valid ? t : acc[r];
+            acc2[r] = valid ? t2 : acc2[r];
+        }
+    }
+    constexpr bool one = WF == W_Q4_1 || WF == W_Q5_1;
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const float sr = one ? wave_sum63(acc[r]) + wave_sum63(acc2[r]) : wave_sum63(acc[r]) + 0.0f;
+        const int row = row0 + r;
+        // epilogue on every lane: its operand loads then stay ahead of the dots instead of being
+        // sunk into the lane-63 store branch (a dependent round trip at the kernel's end)
+        const float v = epi_apply(h.epi, sr, ep[r]);
+        if (lane == 63 && row < M) h.y[row] = v;
     }
 }
 
@@ -497,9 +584,24 @@ __global__ __launch_bounds__(512) void k_mv(MVGroup g) {
 // (K <= 4096) elements per lane.
 template <int WFIX>
 bool launch_mv_shape(hipStream_t st, MVGroup & g, int U, int srck, int form, bool emit, dim3 grid) {
-#define MV_L(Rv, Uv, S, F, E, P) \
-    hipLaunchKernelGGL((k_mv<Rv, Uv, S, F, E, WFIX, P>), grid, dim3((S) == MVK_ACT ? 256 : 512), g.lds_bytes, st, g)
+    static_assert(MM_MAX_ENTRIES == 8, "k_mv takes b1..b7");
+    int b[MM_MAX_ENTRIES];
+    for (int i = 1; i < MM_MAX_ENTRIES; i++) b[i] = i < g.n ? g.e[i].block0 : INT_MAX;
+#define MV_L(Rv, Uv, S, F, E, P)                                                                              \
+    hipLaunchKernelGGL((k_mv<Rv, Uv, S, F, E, WFIX, P>), grid, dim3((S) == MVK_ACT ? 256 : 512), g.lds_bytes, st, \
+                       b[1], b[2], b[3], b[4], b[5], b[6], b[7], g)
     const int K = g.e[0].W.K;
+    if constexpr (WFIX >= 0) {
+        if (srck == MVK_ACT && !emit && g.units_max <= U) {
+#define MVA_L(Uv) \
+    hipLaunchKernelGGL((k_mva<WFIX, 2, Uv>), grid, dim3(256), 0, st, b[1], b[2], b[3], b[4], b[5], b[6], b[7], g)
+            if (U == 1) MVA_L(1);
+            else if (U == 2) MVA_L(2);
+            else MVA_L(4);
+#undef MVA_L
+            return true;
+        }
+    }
     if (srck == MVK_ACT) {
         if (U == 1) MV_L(2, 1, MVK_ACT, 0, false, 0);
         else if (U == 2) MV_L(2, 2, MVK_ACT, 0, false, 0);

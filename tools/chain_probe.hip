@@ -10,6 +10,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <vector>
+#include <string.h>
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("err %s line %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
 
@@ -68,6 +69,61 @@ __global__ __launch_bounds__(256) void k_syn(const int4 * __restrict__ W, const 
         if (lane == 63 && row0 + r < M) {
             y[row0 + r] = f;
             if (row0 + r < 2048) act_out[row0 + r] = (int8_t)((int)f & 0x7f);
+        }
+    }
+}
+
+// The same body behind a k_mv-like group argument: 8 entries of 304 bytes by value, the entry
+// found by a loop over block0 (dependent scalar loads), then its pointers loaded.
+struct SynEnt {
+    const int4 * W;
+    const unsigned short * sc;
+    const int8_t * act;
+    const float * ad;
+    float * y;
+    int8_t * act_out;
+    int M;
+    int block0;
+    char pad[304 - 56];
+};
+struct SynGrp {
+    SynEnt e[8];
+    int n;
+};
+template <int R>
+__global__ __launch_bounds__(256) void k_syn_grp(SynGrp g) {
+    int e = 0;
+#pragma unroll 1
+    while (e + 1 < g.n && (int)blockIdx.x >= g.e[e + 1].block0) e++;
+    const SynEnt & E = g.e[e];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int M = E.M;
+    const int row0 = (((int)blockIdx.x - E.block0) * 4 + wave) * R;
+    int4 w[R];
+    unsigned short s[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const int row = min(row0 + r, M - 1);
+        w[r] = E.W[(size_t)row * 64 + lane];
+        s[r] = E.sc[(size_t)row * 64 + lane];
+    }
+    const int4 xl = *(const int4 *)(E.act + lane * 32);
+    const int4 xh = *(const int4 *)(E.act + lane * 32 + 16);
+    const float d = E.ad[lane];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const int q[4] = {w[r].x, w[r].y, w[r].z, w[r].w};
+        const int xs[8] = {xl.x, xl.y, xl.z, xl.w, xh.x, xh.y, xh.z, xh.w};
+        int acc = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            acc = __builtin_amdgcn_sdot4((q[j] & 0x0f0f0f0f) - 0x08080808, xs[j], acc, false);
+            acc = __builtin_amdgcn_sdot4(((q[j] >> 4) & 0x0f0f0f0f) - 0x08080808, xs[4 + j], acc, false);
+        }
+        const float f = wave_sum63(__half2float(__ushort_as_half(s[r])) * d * (float)acc);
+        if (lane == 63 && row0 + r < M) {
+            E.y[row0 + r] = f;
+            if (row0 + r < 2048) E.act_out[row0 + r] = (int8_t)((int)f & 0x7f);
         }
     }
 }
@@ -141,6 +197,31 @@ int main(int argc, char ** argv) {
                     char * base = pool + (size_t)(i % R) * per;
                     hipLaunchKernelGGL(k_syn<2>, dim3((M + 7) / 8), dim3(256), 0, st, (const int4 *)base,
                                        (const unsigned short *)(base + wbytes), act[i & 1], ad, y, act[(i + 1) & 1], M);
+                }
+            }, name, algo);
+        }
+        for (int ne : {1, 4}) {
+            const int R = (int)(total / per);
+            char name[128];
+            snprintf(name, sizeof name, "M=%d group of %d, copies=%d (HBM)", M, ne, R);
+            time_graph([&] {
+                for (int i = 0; i < N; i++) {
+                    char * base = pool + (size_t)(i % R) * per;
+                    SynGrp g;
+                    memset(&g, 0, sizeof g);
+                    g.n = ne;
+                    const int Me = M / ne;
+                    for (int j = 0; j < ne; j++) {
+                        g.e[j].W = (const int4 *)(base + (size_t)j * Me * 64 * 16);
+                        g.e[j].sc = (const unsigned short *)(base + wbytes + (size_t)j * Me * 64 * 2);
+                        g.e[j].act = act[i & 1];
+                        g.e[j].ad = ad;
+                        g.e[j].y = y + j * Me;
+                        g.e[j].act_out = act[(i + 1) & 1];
+                        g.e[j].M = Me;
+                        g.e[j].block0 = j * ((Me + 7) / 8);
+                    }
+                    hipLaunchKernelGGL(k_syn_grp<2>, dim3(ne * ((Me + 7) / 8)), dim3(256), 0, st, g);
                 }
             }, name, algo);
         }

@@ -330,6 +330,8 @@ bool Engine::init() {
     generic_decode_ = gd && gd[0] == '1';
     const char * um = getenv("RWKV_MI355X_SEQ_MATVEC");  // sequence matmuls on k_mm (comparison)
     use_mm_ = um && um[0] == '1';
+    const char * sm = getenv("RWKV_MI355X_SPLIT_MAA");  // v6 decode: W1 and mix as two launches (comparison)
+    split_maa_ = sm && sm[0] == '1';
     // the fused decode prologues hold LayerNorm inputs in registers up to n_embed 4096
     if (m_->n_embed > 4096 || m_->n_embed % 64) generic_decode_ = true;
     return ensure_workspace(1) && init_state(dstate_[0]);
@@ -1041,12 +1043,19 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits) {
             if (!mv(c_wo.g)) return false;
         } else if (m_->major == 6) {
             const int D = m_->maa_D;
-            MV b;
-            src_lnmix(b.add(L.maa_w1, lora_, EPI_TANH), x_, si + C, L.ln1_w, L.ln1_b, L.maa_x, 1, so + C);
-            if (!mv(b.g)) return false;
             ActBuf outs[5] = {A(1, L.decay_w1), A(2, L.att_k), A(3, L.att_v), A(4, L.att_r), A(5, L.att_g)};
-            if (!launch_v6_mix5_dec(stream_, C, D, so + C, si + C, lora_, L.maa_w2t, L.maa, outs))
-                return false;
+            if (v6_maa_dec_supported(C, D, L.maa_w1.type) && !split_maa_) {
+                // W1 rows + mix in one launch (mv_maa.hip)
+                if (!launch_v6_maa_dec(stream_, C, D, L.maa_w1, x_, si + C, so + C, L.ln1_w, L.ln1_b, L.maa_x,
+                                       L.maa_w2t, L.maa, outs))
+                    return false;
+            } else {
+                MV b;
+                src_lnmix(b.add(L.maa_w1, lora_, EPI_TANH), x_, si + C, L.ln1_w, L.ln1_b, L.maa_x, 1, so + C);
+                if (!mv(b.g)) return false;
+                if (!launch_v6_mix5_dec(stream_, C, D, so + C, si + C, lora_, L.maa_w2t, L.maa, outs))
+                    return false;
+            }
             MV c;
             const int mats[5] = {3, 1, 2, 4, 0};  // r, k, v, g, w
             float * ys[5] = {r_, k_, v_, g_, dsmall_[0]};

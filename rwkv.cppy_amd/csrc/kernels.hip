@@ -427,12 +427,18 @@ static int pick_groups(int S) {
     return G;
 }
 
-// Head size 64 (every released v5/v6 model): one wave per (head, 16 value columns), grid
-// (H, 4).  Lane (g = lane >> 4, jl = lane & 15) owns column j = 16*blockIdx.y + jl for keys
-// i in [16g, 16g+16) -- the (j, g) work split and per-thread arithmetic of k_wkv6 / k_att6_dec,
-// and the same 4-group fold (xor 2, then xor 1 on g).  Chunks of 32 tokens of k, r, w and v are
-// staged in LDS with coalesced loads, the next chunk's loads in flight while this one runs; the
-// per-token critical path is only the state update S = S*w + k*v.
+typedef float f2_t __attribute__((ext_vector_type(2)));
+
+// Head size 64 (every released v5/v6 model), four keys per lane.  Workgroup = 4 waves over 16
+// value columns of one head, grid (H, 4).  Lane (g = lane >> 4, jl = (lane >> 2) & 3, q = lane & 3)
+// of wave wv owns column j = 16*blockIdx.y + 4*wv + jl for keys i = 16g + 4q + e (e < 4): the
+// per-element arithmetic is k_att6_dec's (packed pairs, the same IEEE mul / add per element, no
+// contraction).  The output sum keeps the decode association exactly -- for each key group g a
+// sequential sum over its 16 keys in order, starting from 0 -- by running it across the four
+// q-lanes of the group: lane q continues the partial of lane q-1 (DPP row_shr:1), so the chain is
+// 16 dependent adds as before while the state work is spread over 4x the lanes.  The 4 group
+// partials are folded with fold_g4 ((p0 + p2) + (p1 + p3)).  Chunks of 32 tokens of k, r, w and v
+// are staged in LDS with coalesced loads, the next chunk in flight while this one runs.
 constexpr int WKV_TC = 32;
 
 // Sum over the four lane groups g = lane >> 4: partner g ^ 2 (permlane32 swap), then g ^ 1
@@ -444,84 +450,79 @@ __device__ __forceinline__ float fold_g4(float v) {
     return __int_as_float(b[0]) + __int_as_float(b[1]);
 }
 
-typedef float f2_t __attribute__((ext_vector_type(2)));
-
-// One key group's operands of one token: 16 keys / receptances / decays as 8 packed pairs
-struct Wkv6Tok {
-    f2_t k[8], r[8], w[8];
-    float v;
-};
-
-template <bool WPT>
-__device__ __forceinline__ void wkv6_read_tok(Wkv6Tok & o, const float (*sk)[64], const float (*sr)[64],
-                                              const float (*sw)[64], const float (*sv)[16], int tt, int g, int jl) {
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-        const float4 a = *(const float4 *)&sk[tt][g * 16 + 4 * q];
-        const float4 b = *(const float4 *)&sr[tt][g * 16 + 4 * q];
-        o.k[2 * q] = f2_t{a.x, a.y}, o.k[2 * q + 1] = f2_t{a.z, a.w};
-        o.r[2 * q] = f2_t{b.x, b.y}, o.r[2 * q + 1] = f2_t{b.z, b.w};
-        if constexpr (WPT) {
-            const float4 c = *(const float4 *)&sw[tt][g * 16 + 4 * q];
-            o.w[2 * q] = f2_t{c.x, c.y}, o.w[2 * q + 1] = f2_t{c.z, c.w};
-        }
-    }
-    o.v = sv[tt][jl];
+__device__ __forceinline__ float dpp_shr1(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x111, 0xF, 0xF, false));
 }
 
-// WPT: per-token decays w[t][c] (v6); otherwise one decay per channel (v5).  The arithmetic per
-// state element is the decode kernel's (kernels_decode.hip k_att6_dec), element pairs in packed
-// f32 instructions (the same IEEE mul / add per element, no contraction); the output sum runs
-// over the 16 keys of the lane's group in order, then fold_g4 across the 4 groups.
+// acc continued over the lane's 4 terms in order
+__device__ __forceinline__ float chain4(float acc, const f2_t (&x)[2]) {
+    acc += x[0].x;
+    acc += x[0].y;
+    acc += x[1].x;
+    acc += x[1].y;
+    return acc;
+}
+
 template <bool WPT>
-__global__ __launch_bounds__(64) void k_wkv6_s64(int T, int H, const float * k, const float * v, const float * r,
-                                                 const float * u, const float * w, const float * sin, float * sout,
-                                                 float * y) {
+__global__ __launch_bounds__(256) void k_wkv6_s64(int T, int H, const float * k, const float * v, const float * r,
+                                                  const float * u, const float * w, const float * sin, float * sout,
+                                                  float * y) {
     constexpr int S = 64;
     __shared__ __attribute__((aligned(16))) float sk[WKV_TC][S], sr[WKV_TC][S], sw[WPT ? WKV_TC : 1][S],
         sv[WKV_TC][16];
-    const int h = blockIdx.x, jb = blockIdx.y, lane = threadIdx.x;
-    const int jl = lane & 15, g = lane >> 4, j = jb * 16 + jl;
+    const int h = blockIdx.x, jb = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int q = lane & 3, jl = (lane >> 2) & 3, g = lane >> 4;
+    const int jc = 4 * wv + jl, j = jb * 16 + jc, i0 = g * 16 + 4 * q;
     const int C = H * S;
     const size_t hb = (size_t)h * S * S;
-    f2_t st[8], uu[8], wc[8];
+    f2_t st[2], uu[2], wc[2];
 #pragma unroll
-    for (int p = 0; p < 8; p++) {
-        const int i0 = g * 16 + 2 * p;
-        st[p] = f2_t{sin[hb + (size_t)i0 * S + j], sin[hb + (size_t)(i0 + 1) * S + j]};
-        uu[p] = f2_t{u[h * S + i0], u[h * S + i0 + 1]};
-        wc[p] = WPT ? f2_t{0.f, 0.f} : f2_t{w[h * S + i0], w[h * S + i0 + 1]};
+    for (int p = 0; p < 2; p++) {
+        const int i = i0 + 2 * p;
+        st[p] = f2_t{sin[hb + (size_t)i * S + j], sin[hb + (size_t)(i + 1) * S + j]};
+        uu[p] = f2_t{u[h * S + i], u[h * S + i + 1]};
+        wc[p] = WPT ? f2_t{0.f, 0.f} : f2_t{w[h * S + i], w[h * S + i + 1]};
     }
-    // chunk staging: k/r/w rows of 64 floats = 16 float4 per token; lane moves float4 #(lane & 15)
-    // of tokens (lane >> 4) + 4q, q < 8
-    float4 pk[8], pr[8], pw[WPT ? 8 : 1];
-    float4 pv[2];
+    // chunk staging: k/r/w rows of 64 floats = 16 float4 per token; thread moves float4
+    // #(tid & 15) of tokens (tid >> 4) + 16 qq, qq < 2; v: 16 columns = 4 float4 per token,
+    // threads < 128 move float4 #(tid & 3) of token tid >> 2
+    float4 pk[2], pr[2], pw[WPT ? 2 : 1], pv;
     auto load_chunk = [&](int t0) {
 #pragma unroll
-        for (int q = 0; q < 8; q++) {
-            const int t = min(t0 + (lane >> 4) + 4 * q, T - 1);
-            const size_t base = (size_t)t * C + (size_t)h * S + 4 * (lane & 15);
-            pk[q] = *(const float4 *)(k + base);
-            pr[q] = *(const float4 *)(r + base);
-            if constexpr (WPT) pw[q] = *(const float4 *)(w + base);
+        for (int qq = 0; qq < 2; qq++) {
+            const int t = min(t0 + (tid >> 4) + 16 * qq, T - 1);
+            const size_t base = (size_t)t * C + (size_t)h * S + 4 * (tid & 15);
+            pk[qq] = *(const float4 *)(k + base);
+            pr[qq] = *(const float4 *)(r + base);
+            if constexpr (WPT) pw[qq] = *(const float4 *)(w + base);
         }
-#pragma unroll
-        for (int q = 0; q < 2; q++) {
-            // v: 16 columns = 4 float4 per token; lane moves float4 #(lane & 3) of token (lane >> 2) + 16q
-            const int t = min(t0 + (lane >> 2) + 16 * q, T - 1);
-            pv[q] = *(const float4 *)(v + (size_t)t * C + (size_t)h * S + jb * 16 + 4 * (lane & 3));
-        }
+        const int t = min(t0 + ((tid & 127) >> 2), T - 1);
+        pv = *(const float4 *)(v + (size_t)t * C + (size_t)h * S + jb * 16 + 4 * (tid & 3));
     };
     auto store_chunk = [&]() {
 #pragma unroll
-        for (int q = 0; q < 8; q++) {
-            const int tt = (lane >> 4) + 4 * q;
-            *(float4 *)&sk[tt][4 * (lane & 15)] = pk[q];
-            *(float4 *)&sr[tt][4 * (lane & 15)] = pr[q];
-            if constexpr (WPT) *(float4 *)&sw[tt][4 * (lane & 15)] = pw[q];
+        for (int qq = 0; qq < 2; qq++) {
+            const int tt = (tid >> 4) + 16 * qq;
+            *(float4 *)&sk[tt][4 * (tid & 15)] = pk[qq];
+            *(float4 *)&sr[tt][4 * (tid & 15)] = pr[qq];
+            if constexpr (WPT) *(float4 *)&sw[tt][4 * (tid & 15)] = pw[qq];
         }
-#pragma unroll
-        for (int q = 0; q < 2; q++) *(float4 *)&sv[(lane >> 2) + 16 * q][4 * (lane & 3)] = pv[q];
+        if (tid < 128) *(float4 *)&sv[tid >> 2][4 * (tid & 3)] = pv;
+    };
+    struct Tok {
+        f2_t k[2], r[2], w[2];
+        float v;
+    };
+    auto read_tok = [&](Tok & o, int tt) {
+        const float4 a = *(const float4 *)&sk[tt][i0];
+        const float4 b = *(const float4 *)&sr[tt][i0];
+        o.k[0] = f2_t{a.x, a.y}, o.k[1] = f2_t{a.z, a.w};
+        o.r[0] = f2_t{b.x, b.y}, o.r[1] = f2_t{b.z, b.w};
+        if constexpr (WPT) {
+            const float4 c = *(const float4 *)&sw[tt][i0];
+            o.w[0] = f2_t{c.x, c.y}, o.w[1] = f2_t{c.z, c.w};
+        }
+        o.v = sv[tt][jc];
     };
     load_chunk(0);
     for (int t0 = 0; t0 < T; t0 += WKV_TC) {
@@ -529,48 +530,48 @@ __global__ __launch_bounds__(64) void k_wkv6_s64(int T, int H, const float * k, 
         __syncthreads();
         if (t0 + WKV_TC < T) load_chunk(t0 + WKV_TC);  // in flight during this chunk
         const int n = min(WKV_TC, T - t0);
-        auto token = [&](const Wkv6Tok & o, int tt) {
+        auto token = [&](const Tok & o, int tt) {
             const f2_t vj = f2_t{o.v, o.v};
-            // phase by phase over the 8 independent pairs (no dependent packed op back to back)
-            f2_t kv[8], x[8];
+            f2_t kv[2], x[2];
 #pragma unroll
-            for (int p = 0; p < 8; p++) kv[p] = vj * o.k[p];
+            for (int p = 0; p < 2; p++) kv[p] = vj * o.k[p];
 #pragma unroll
-            for (int p = 0; p < 8; p++) x[p] = kv[p] * uu[p];
+            for (int p = 0; p < 2; p++) x[p] = kv[p] * uu[p];
 #pragma unroll
-            for (int p = 0; p < 8; p++) x[p] = x[p] + st[p];
+            for (int p = 0; p < 2; p++) x[p] = x[p] + st[p];
 #pragma unroll
-            for (int p = 0; p < 8; p++) x[p] = x[p] * o.r[p];
+            for (int p = 0; p < 2; p++) x[p] = x[p] * o.r[p];
 #pragma unroll
-            for (int p = 0; p < 8; p++) st[p] = st[p] * (WPT ? o.w[p] : wc[p]);
+            for (int p = 0; p < 2; p++) st[p] = st[p] * (WPT ? o.w[p] : wc[p]);
 #pragma unroll
-            for (int p = 0; p < 8; p++) st[p] = st[p] + kv[p];
-            float acc = 0.0f;
+            for (int p = 0; p < 2; p++) st[p] = st[p] + kv[p];
+            // 16-key sequential sum of group g across its q-lanes
+            float acc = chain4(0.0f, x);
 #pragma unroll
-            for (int p = 0; p < 8; p++) {
-                acc += x[p].x;
-                acc += x[p].y;
+            for (int s = 1; s < 4; s++) {
+                const float c = chain4(dpp_shr1(acc), x);
+                acc = q >= s ? c : acc;
             }
             acc = fold_g4(acc);
-            if (g == 0) y[(size_t)(t0 + tt) * C + h * S + j] = acc;
+            if (g == 0 && q == 3) y[(size_t)(t0 + tt) * C + h * S + j] = acc;
         };
         // two operand sets in turn: the next token's LDS reads overlap this token's arithmetic
-        Wkv6Tok A, B;
-        wkv6_read_tok<WPT>(A, sk, sr, sw, sv, 0, g, jl);
+        Tok A, B;
+        read_tok(A, 0);
         for (int tt = 0; tt < n; tt += 2) {
-            wkv6_read_tok<WPT>(B, sk, sr, sw, sv, min(tt + 1, n - 1), g, jl);
+            read_tok(B, min(tt + 1, n - 1));
             token(A, tt);
             if (tt + 1 >= n) break;
-            wkv6_read_tok<WPT>(A, sk, sr, sw, sv, min(tt + 2, n - 1), g, jl);
+            read_tok(A, min(tt + 2, n - 1));
             token(B, tt + 1);
         }
         __syncthreads();
     }
 #pragma unroll
-    for (int p = 0; p < 8; p++) {
-        const int i0 = g * 16 + 2 * p;
-        sout[hb + (size_t)i0 * S + j] = st[p].x;
-        sout[hb + (size_t)(i0 + 1) * S + j] = st[p].y;
+    for (int p = 0; p < 2; p++) {
+        const int i = i0 + 2 * p;
+        sout[hb + (size_t)i * S + j] = st[p].x;
+        sout[hb + (size_t)(i + 1) * S + j] = st[p].y;
     }
 }
 
@@ -579,9 +580,9 @@ bool launch_wkv6(hipStream_t st, int T, int H, int S, const float * k, const flo
                  float * y) {
     if (S == 64) {
         if (w_per_token)
-            hipLaunchKernelGGL(k_wkv6_s64<true>, dim3(H, 4), dim3(64), 0, st, T, H, k, v, r, u, w, state_in, state_out, y);
+            hipLaunchKernelGGL(k_wkv6_s64<true>, dim3(H, 4), dim3(256), 0, st, T, H, k, v, r, u, w, state_in, state_out, y);
         else
-            hipLaunchKernelGGL(k_wkv6_s64<false>, dim3(H, 4), dim3(64), 0, st, T, H, k, v, r, u, w, state_in, state_out, y);
+            hipLaunchKernelGGL(k_wkv6_s64<false>, dim3(H, 4), dim3(256), 0, st, T, H, k, v, r, u, w, state_in, state_out, y);
         HIP_OK(hipGetLastError());
         return true;
     }

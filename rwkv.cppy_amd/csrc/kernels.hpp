@@ -145,6 +145,14 @@ bool launch_mv_group(hipStream_t st, MVGroup & g);
 bool launch_v6_mix5_dec(hipStream_t st, int C, int D, const float * xa, const float * carry, const float * lora,
                         const float * w2t, const float * const * maa, const ActBuf * outs);
 
+// v6 maa LoRA in one launch (mv_maa.hip): LN(x) + token shift -> lora_n = tanh(W1[n] . xxx) ->
+// the five mixed vectors w,k,v,r,g, emitted in their matmuls' input formats; writes the new
+// att_xx carry.  Bit-identical to the W1 k_mv + launch_v6_mix5_dec pair it replaces.
+bool v6_maa_dec_supported(int C, int D, int w1_type);
+bool launch_v6_maa_dec(hipStream_t st, int C, int D, const DMat & w1, const float * x, const float * carry,
+                       float * carry_out, const float * lnw, const float * lnb, const float * maa_x,
+                       const float * w2t, const float * const * maa, const ActBuf * outs);
+
 // v5/v6 attention core for one token, one workgroup per head: (v6: decay LoRA second stage
 // w = exp(-exp(Wd2 . dl + decay))) + wkv6 + GroupNorm*ln_x (+ *g).  Writes fp32 y [C].
 struct Att6Dec {

@@ -275,6 +275,12 @@ __global__ __launch_bounds__(256) void k_att6_dec(Att6Dec a) {
 #pragma unroll
         for (int l = 0; l < PF; l++) wp[l] = load_wblk<WF>(a.wd2, (size_t)row * nb + min(l, nb - 1));
     }
+    // per-channel operands of the decay tail and the GroupNorm epilogue, loaded now so they
+    // are not a dependent round trip behind the barriers
+    const int cme = c0 + min(tid, S - 1);
+    const float lnw_c = a.lnx_w[cme], lnb_c = a.lnx_b[cme];
+    const float g_c = a.g ? a.g[cme] : 1.0f;
+    const float dec_c = a.w ? 0.0f : a.decay[cme];
     if (tid < S) {
         sr[tid] = a.r[c0 + tid];
         sk[tid] = a.k[c0 + tid];
@@ -298,7 +304,7 @@ __global__ __launch_bounds__(256) void k_att6_dec(Att6Dec a) {
         } else if constexpr (PF > 0) {
             if (tid < S) {
                 const float s = decay_row_thread<WF, PF, PF>(a.wd2, c0 + tid, act, a.wd2.K >> 5, wp);
-                sw[tid] = expf(-expf(s + a.decay[c0 + tid]));
+                sw[tid] = expf(-expf(s + dec_c));
             }
         } else {
             switch (a.wd2.type) {
@@ -350,9 +356,9 @@ __global__ __launch_bounds__(256) void k_att6_dec(Att6Dec a) {
         const float var = (float)(s2 / (double)S);
         const float scale = 1.0f / sqrtf(var + a.eps);
         float o = d * scale;
-        o = o * a.lnx_w[c0 + tid];
-        o = o + a.lnx_b[c0 + tid];
-        if (a.g) o = o * a.g[c0 + tid];
+        o = o * lnw_c;
+        o = o + lnb_c;
+        if (a.g) o = o * g_c;
         if (a.yq.fmt >= 0) emit32(a.yq, 0, c0 + tid, o);  // S >= 32: whole half-wave blocks
         else a.y[c0 + tid] = o;
     }
@@ -405,6 +411,16 @@ __global__ __launch_bounds__(256) void k_att7_dec(Att7Dec a) {
     __shared__ float sbonus;
     const int h = blockIdx.x, S = a.S, G = S / JPG;
     const int tid = threadIdx.x, c0 = h * S;
+    // state rows and the GroupNorm epilogue operands are loaded first: no dependent round trip
+    // behind the barriers
+    const bool wact = tid < S * G;
+    const int wi = min(tid / G, S - 1), wg = tid % G;
+    const size_t wbase = (size_t)h * S * S + (size_t)wi * S + wg * JPG;
+    float st[JPG];
+#pragma unroll
+    for (int jj = 0; jj < JPG; jj++) st[jj] = a.sin[wbase + jj];
+    const int cme = c0 + min(tid, S - 1);
+    const float lnw_c = a.lnx_w[cme], lnb_c = a.lnx_b[cme], g_c = a.g[cme];
     if (tid < S) {
         // prep (rwkv_graph.inc:432-437 + rwkv_operators.inc:40-82)
         const int c = c0 + tid;
@@ -427,13 +443,10 @@ __global__ __launch_bounds__(256) void k_att7_dec(Att7Dec a) {
         if (tid == 0) sbonus = bs;
     }
     __syncthreads();
-    if (tid < S * G) {
+    if (wact) {
         // wkv7 (rwkv_operators_wkv_v7.inc:37-107): state [h][i(value)][j(key)], g splits j
-        const int i = tid / G, g = tid % G;
-        const size_t base = (size_t)h * S * S + (size_t)i * S + g * JPG;
-        float st[JPG];
-#pragma unroll
-        for (int jj = 0; jj < JPG; jj++) st[jj] = a.sin[base + jj];
+        const int i = wi, g = wg;
+        const size_t base = wbase;
         float sa = 0.0f;
 #pragma unroll
         for (int jj = 0; jj < JPG; jj++) sa += snb[g * JPG + jj] * st[jj];
@@ -462,10 +475,10 @@ __global__ __launch_bounds__(256) void k_att7_dec(Att7Dec a) {
         const float var = (float)(s2 / (double)S);
         const float scale = 1.0f / sqrtf(var + 64e-5f);
         float o = d * scale;
-        o = o * a.lnx_w[c];
-        o = o + a.lnx_b[c];
+        o = o * lnw_c;
+        o = o + lnb_c;
         o = o + sv[tid] * sbonus;
-        o = o * a.g[c];
+        o = o * g_c;
         if (a.yq.fmt >= 0) emit32(a.yq, 0, c, o);  // S >= 32: whole half-wave blocks
         else a.y[c] = o;
     }

@@ -1,0 +1,201 @@
+// mv_maa.hip -- v6 decode: the maa LoRA in one launch (rwkv_graph.inc:306-346).
+//
+// Before: W1 matvec with the LN prologue (lora = tanh(W1 . xxx), one launch) then the W2 mix
+// (k_v6_mix5_dec, a second launch that waits for the whole lora vector).  The mixed vector n
+// only needs lora_n = rows [n*D, (n+1)*D) of W1, so workgroup (cx, n) computes those D rows
+// itself -- LayerNorm + token shift + Q8 quantization of xxx in LDS (exactly the k_mv prologue),
+// D rows dotted by the dot waves (exactly k_mv's lane/unit order and wave_sum63 tree, so the
+// lora values are bit-identical) -- and then mixes its 256 channels (exactly k_v6_mix5_dec).
+// The five row chunks are each recomputed by C/256 workgroups (W1 is 5*D x C: 37 KB per chunk
+// for v6-1B6 Q4_0, read from L2), which replaces one dependent launch per layer.
+#include "mv_common.hpp"
+
+namespace rwkvmi {
+
+struct MaaDec {
+    int C, D;
+    DMat w1;                    // time_maa_w1 (M = 5*D, K = C)
+    const float * x;            // residual stream [C]
+    const float * carry;        // previous att_xx [C]
+    float * carry_out;          // new att_xx [C] (= LN(x)), written by workgroup (0, 0)
+    const float * lnw, * lnb;
+    const float * maa_x;        // time_maa_x [C]
+    const float * w2t;          // time_maa_w2 transposed [5][D][C]
+    const float * maa[5];       // time_maa_{w,k,v,r,g} [C]
+    ActBuf out[5];
+    int xa_off;                 // LDS byte offset of the fp32 xa image
+};
+
+// 512 threads.  Waves 0..3: W1 rows (R each, D <= 4R), then the mix of one channel per thread
+// (its W2 column prefetched with the weights).  Waves 4..7: the activation image (LayerNorm +
+// token shift + quantization, one 512-element chunk per wave per pass) and the fp32 xa image.
+// Each wave keeps well under 63 loads in flight, so none stalls on the vmcnt limit.
+template <int WF, int R, int U, int LNP, int DM>
+__global__ __launch_bounds__(512) void k_v6_maa_dec(MaaDec a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    __shared__ float s_lora[64];
+    const int n = blockIdx.y, C = a.C, D = a.D, K = C;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const ActBuf act = lds_act(smem, act_fmt_for(WF), K);
+    float * s_xa = (float *)(smem + a.xa_off);
+    if (wave < 4) {
+        // ---- dot wave: rows n*D + wave*R + r of W1
+        const DMat & W = a.w1;
+        const int units = mv_units(WF, K);
+        const int row0 = n * D + wave * R, rlast = n * D + D - 1;
+        int rows[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) rows[r] = min(row0 + r, rlast);
+        WBlk w[R][U];
+#pragma unroll
+        for (int u = 0; u < U; u++)
+#pragma unroll
+            for (int r = 0; r < R; r++) w[r][u] = load_unit<WF>(W, rows[r], u, lane);
+        // this thread's mix channel: W2 column, carry, maa
+        const int c = blockIdx.x * 256 + tid;
+        const bool cval = (int)(blockIdx.x * 256 + (tid & ~31)) < C;  // half-wave uniform
+        const int cc = min(c, C - 1);
+        float w2v[DM];
+        const float * w2 = a.w2t + (size_t)n * D * C + cc;
+#pragma unroll
+        for (int i = 0; i < DM; i++) {
+            const float t = w2[(size_t)min(i, D - 1) * C];
+            w2v[i] = (i < D) ? t : 0.0f;
+        }
+        const float carry_c = a.carry[cc], mu_c = a.maa[n][cc];
+        __syncthreads();  // (1) activation image ready
+        float acc[R], acc2[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) acc[r] = acc2[r] = 0.0f;
+        for (int u0 = 0; u0 < units; u0 += U) {
+            if (u0 > 0) {
+#pragma unroll
+                for (int u = 0; u < U; u++)
+#pragma unroll
+                    for (int r = 0; r < R; r++) w[r][u] = load_unit<WF>(W, rows[r], u0 + u, lane);
+            }
+            AUnit xu[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) xu[u] = load_act_unit<WF, true>(act, u0 + u, lane);
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                if (unit_valid<WF>(K, u0 + u, lane)) {
+#pragma unroll
+                    for (int r = 0; r < R; r++) dot_unit<WF>(w[r][u], xu[u], acc[r], acc2[r]);
+                }
+            }
+        }
+        constexpr bool one = WF == W_Q4_1 || WF == W_Q5_1;
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            const float s = one ? wave_sum63(acc[r]) + wave_sum63(acc2[r]) : wave_sum63(acc[r]) + 0.0f;
+            if (lane == 63 && wave * R + r < D) s_lora[wave * R + r] = tanhf(s);  // EPI_TANH
+        }
+        __syncthreads();  // (2) lora_n ready
+        // k_v6_mix5_dec's arithmetic: m = sum_i (double)(w2[i] * lora[i]) in order
+        const float xa = s_xa[cc];
+        const float sx = carry_c - xa;
+        double accd = 0.0;
+#pragma unroll
+        for (int i = 0; i < DM; i++)
+            if (i < D) accd += (double)(w2v[i] * s_lora[i]);
+        const float m = (float)accd;
+        if (cval) emit32(a.out[n], 0, c, (m + mu_c) * sx + xa);
+        return;
+    }
+    // ---- prologue wave
+    const int pw = wave - 4;
+    MVEntry E;
+    E.x = a.x;
+    E.carry = a.carry;
+    E.lnw = a.lnw;
+    E.lnb = a.lnb;
+    E.mu = a.maa_x;
+    E.carry_out = a.carry_out;
+    E.f = nullptr;
+    float lv[LNP];
+    ln_load_regs<LNP>(a.x, K, lv);
+    ChunkIn ci;
+    int k0 = pw * 512 + lane * 8;
+    chunk_load<MVK_LN, 1>(E, min(k0, K - 8), ci);
+    float mean = 0.0f, scale = 0.0f;
+    ln_stats_regs<LNP>(lv, K, 1e-5f, mean, scale);
+    const bool write_carry = blockIdx.x == 0 && n == 0;
+    for (;;) {
+        if (k0 < K) {
+#pragma unroll
+            for (int j = 0; j < 8; j++) s_xa[k0 + j] = ln_apply(ci.x[j], mean, scale, ci.w[j], ci.b[j]);
+        }
+        chunk_store<WF, MVK_LN, 1>(E, act, ci, mean, scale, write_carry, k0, k0 < K, lane);
+        k0 += 4 * 512;
+        if (k0 - lane * 8 >= K) break;
+        chunk_load<MVK_LN, 1>(E, min(k0, K - 8), ci);
+    }
+    __syncthreads();  // (1)
+    __syncthreads();  // (2)
+}
+
+template <int WF>
+static bool launch_maa_t(hipStream_t st, const MaaDec & a, int lds, int units) {
+    const dim3 grid((a.C + 255) / 256, 5);
+#define MAA_L(Rv, Uv, P) hipLaunchKernelGGL((k_v6_maa_dec<WF, Rv, Uv, P, (Rv) * 4>), grid, dim3(512), lds, st, a)
+#define MAA_P(Rv, Uv) \
+    do { if (a.C <= 2048) MAA_L(Rv, Uv, 32); else MAA_L(Rv, Uv, 64); } while (0)
+    const bool u1 = units <= 1;
+    if (a.D <= 32) {
+        if (u1) MAA_P(8, 1); else MAA_P(8, 2);
+    } else {
+        if (u1) MAA_P(16, 1); else MAA_P(16, 2);
+    }
+#undef MAA_P
+#undef MAA_L
+    HIP_OK(hipGetLastError());
+    return true;
+}
+
+bool v6_maa_dec_supported(int C, int D, int w1_type) {
+    return D >= 1 && D <= 64 && C % 64 == 0 && C <= 4096 && w1_type >= 0;
+}
+
+bool launch_v6_maa_dec(hipStream_t st, int C, int D, const DMat & w1, const float * x, const float * carry,
+                       float * carry_out, const float * lnw, const float * lnb, const float * maa_x,
+                       const float * w2t, const float * const * maa, const ActBuf * outs) {
+    if (!v6_maa_dec_supported(C, D, w1.type) || (int)w1.M != 5 * D || (int)w1.K != C) {
+        fprintf(stderr, "rwkv: fused v6 maa decode: unsupported shape (C %d, D %d, W1 %dx%d)\n", C, D,
+                (int)w1.M, (int)w1.K);
+        return false;
+    }
+    MaaDec a;
+    a.C = C;
+    a.D = D;
+    a.w1 = w1;
+    a.x = x;
+    a.carry = carry;
+    a.carry_out = carry_out;
+    a.lnw = lnw;
+    a.lnb = lnb;
+    a.maa_x = maa_x;
+    a.w2t = w2t;
+    for (int i = 0; i < 5; i++) {
+        a.maa[i] = maa[i];
+        a.out[i] = outs[i];
+    }
+    const int fmt = act_fmt_for(w1.type);
+    a.xa_off = (lds_bytes_for(fmt, C) + 15) & ~15;
+    const int lds = a.xa_off + C * 4;
+    const int units = mv_units(w1.type, C);
+    switch (w1.type) {
+        case W_F32: return launch_maa_t<W_F32>(st, a, lds, units);
+        case W_F16: return launch_maa_t<W_F16>(st, a, lds, units);
+        case W_Q4_0: return launch_maa_t<W_Q4_0>(st, a, lds, units);
+        case W_Q4_1: return launch_maa_t<W_Q4_1>(st, a, lds, units);
+        case W_Q5_0: return launch_maa_t<W_Q5_0>(st, a, lds, units);
+        case W_Q5_1: return launch_maa_t<W_Q5_1>(st, a, lds, units);
+        case W_Q8_0: return launch_maa_t<W_Q8_0>(st, a, lds, units);
+        default: break;
+    }
+    fprintf(stderr, "rwkv: fused v6 maa decode: weight type %d\n", (int)w1.type);
+    return false;
+}
+
+}  // namespace rwkvmi

@@ -323,3 +323,22 @@ def test_kernel_timing_mode_is_transparent():
     lib.rwkv_mi355x_set_kernel_timing(m._ctx.ptr, False)
     assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
     m.free()
+
+
+@pytest.mark.parametrize('fmt', ['Q4_0', 'Q5_1', 'FP16'])
+def test_v6_fused_maa_decode_equals_split(tmp_path, fmt):
+    """The one-launch v6 maa LoRA (mv_maa.hip) reproduces the W1 matvec + mix launch pair bit for bit."""
+    L = library()
+    p = str(tmp_path / f'maa{fmt}.bin')
+    assert L.library.rwkv_mi355x_write_synthetic_model(p.encode(), 6, 1024, 2048, 2, 0, fmt.encode(), 13)
+    toks = [int(t) for t in np.random.default_rng(5).integers(0, 1024, 12)]
+    outs = []
+    for split in ('1', '0'):
+        os.environ['RWKV_MI355X_SPLIT_MAA'] = split
+        try:
+            m = RWKVModel(L, p)
+        finally:
+            os.environ.pop('RWKV_MI355X_SPLIT_MAA', None)
+        outs.append(gpu_serial(m, toks))
+        m.free()
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])

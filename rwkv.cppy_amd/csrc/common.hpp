@@ -61,15 +61,16 @@ struct ActBuf {
 // Records the int8-MFMA GEMM (qgemm.hip) copies global->LDS as whole, contiguous pieces:
 //   weights     per (row tile of qg_rows rows, block b), ordered [row tile][b]:
 //                 [rows x 32 int8 (the block's integer weights, offset applied: q-8 / q-16 for
-//                  _0, q for _1, 5th bit merged)][rows x fp16 d][_1: rows x fp16 m]
+//                  _0, q for _1, 5th bit merged)][rows x f32 d][_1: rows x f32 m] (the fp16
+//                  scales widened exactly, so the GEMM epilogue needs no conversion)
 //   activations per (QG_TOK-token tile, block b), ordered [token tile][b]:
 //                 [2 halves x QG_TOK tokens x 16 B int8][QG_TOK x f32 d][Q8_1: QG_TOK x f32 s]
 constexpr int QG_TOK = 64;
 __host__ __device__ constexpr bool qg_one(int wt) { return wt == W_Q4_1 || wt == W_Q5_1; }
 __host__ __device__ constexpr int qg_rows(int wt) { return qg_one(wt) ? 32 : 64; }
 __host__ __device__ constexpr int qg_w_d(int wt) { return qg_rows(wt) * 32; }
-__host__ __device__ constexpr int qg_w_m(int wt) { return qg_w_d(wt) + qg_rows(wt) * 2; }
-__host__ __device__ constexpr int qg_w_bytes(int wt) { return qg_w_m(wt) + (qg_one(wt) ? qg_rows(wt) * 2 : 0); }
+__host__ __device__ constexpr int qg_w_m(int wt) { return qg_w_d(wt) + qg_rows(wt) * 4; }
+__host__ __device__ constexpr int qg_w_bytes(int wt) { return qg_w_m(wt) + (qg_one(wt) ? qg_rows(wt) * 4 : 0); }
 constexpr int QG_A_D = 2 * QG_TOK * 16;
 constexpr int QG_A_S = QG_A_D + QG_TOK * 4;
 __host__ __device__ constexpr int qg_a_bytes(bool one) { return QG_A_S + (one ? QG_TOK * 4 : 0); }

@@ -144,11 +144,11 @@ bool upload_mat(DeviceModel & dm, const HostTensor * t, DMat & out, bool count_b
                             }
                             w8[j] = (int8_t)v;
                         }
-                        const uint16_t d = one ? (uint16_t)(sc32[i] & 0xFFFFu) : sc16[i];
-                        memcpy(rec + qg_w_d(wt) + r * 2, &d, 2);
+                        const float d = f16_to_f32(one ? (uint16_t)(sc32[i] & 0xFFFFu) : sc16[i]);
+                        memcpy(rec + qg_w_d(wt) + r * 4, &d, 4);
                         if (one) {
-                            const uint16_t m = (uint16_t)(sc32[i] >> 16);
-                            memcpy(rec + qg_w_m(wt) + r * 2, &m, 2);
+                            const float m = f16_to_f32((uint16_t)(sc32[i] >> 16));
+                            memcpy(rec + qg_w_m(wt) + r * 4, &m, 4);
                         }
                     }
                 }

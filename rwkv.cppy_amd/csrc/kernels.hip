@@ -307,20 +307,50 @@ struct Mix5Args {
     ActBuf out[5];
 };
 
+// Workgroup = 256 channels x MIX_TT tokens: each thread holds its channel's W2 column for all five
+// mixes in registers (read once per token tile instead of once per token) and the tile's lora rows
+// sit in LDS; per token the five D-long fp64 sums (k_v6_mix5_dec's order: sequential over i) run
+// side by side.
+constexpr int MIX_TT = 16;
+
+template <int DM>
 __global__ __launch_bounds__(256) void k_v6_mix5(Mix5Args a) {
-    const int t = blockIdx.y;
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if ((int)(blockIdx.x * blockDim.x + (threadIdx.x & ~63)) >= a.C) return;  // wave-uniform
-    const int C = a.C, D = a.D;
-    const size_t ti = (size_t)t * C + c;
-    const float xa = a.xa[ti], sx = a.sx[ti];
+    __shared__ __attribute__((aligned(16))) float sl[MIX_TT][5 * DM];
+    const int C = a.C, D = a.D, T = a.T;
+    const int tid = threadIdx.x, c = blockIdx.x * blockDim.x + tid;
+    const bool cval = (int)(blockIdx.x * blockDim.x + (tid & ~31)) < C;  // half-wave uniform
+    const int cc = min(c, C - 1);
+    const int t0 = blockIdx.y * MIX_TT, nt = min(MIX_TT, T - t0);
+    for (int e = tid; e < MIX_TT * 5 * DM; e += 256) {
+        const int tt = e / (5 * DM), f = e % (5 * DM), n = f / DM, i = f % DM;
+        sl[tt][f] = (tt < nt && i < D) ? a.lora[(size_t)(t0 + tt) * 5 * D + n * D + i] : 0.0f;
+    }
+    float w2v[5][DM], mu[5];
+#pragma unroll
     for (int n = 0; n < 5; n++) {
-        const float * w2 = a.w2 + (size_t)n * D * C + c;   // transposed [5][D][C]
-        const float * lv = a.lora + (size_t)t * 5 * D + n * D;
-        double acc = 0.0;
-        for (int i = 0; i < D; i++) acc += (double)(w2[(size_t)i * C] * lv[i]);
-        const float m = (float)acc;
-        emit32(a.out[n], t, c, (m + a.maa[n][c]) * sx + xa);
+        mu[n] = a.maa[n][cc];
+#pragma unroll
+        for (int i = 0; i < DM; i++) {
+            const float t = a.w2[((size_t)n * D + min(i, D - 1)) * C + cc];   // transposed [5][D][C]
+            w2v[n][i] = i < D ? t : 0.0f;
+        }
+    }
+    __syncthreads();
+    for (int tt = 0; tt < nt; tt++) {
+        const size_t ti = (size_t)(t0 + tt) * C + cc;
+        const float xa = a.xa[ti], sx = a.sx[ti];
+        double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int i = 0; i < DM; i++) {
+            if (i < D) {
+#pragma unroll
+                for (int n = 0; n < 5; n++) acc[n] += (double)(w2v[n][i] * sl[tt][n * DM + i]);
+            }
+        }
+        if (cval) {
+#pragma unroll
+            for (int n = 0; n < 5; n++) emit32(a.out[n], t0 + tt, c, ((float)acc[n] + mu[n]) * sx + xa);
+        }
     }
 }
 
@@ -338,7 +368,13 @@ bool launch_v6_mix5(hipStream_t st, int T, int C, int D, const float * lora, con
     }
     a.xa = xa;
     a.sx = sx;
-    hipLaunchKernelGGL(k_v6_mix5, dim3((C + 255) / 256, T), dim3(256), 0, st, a);
+    if (D > 64 || C % 32) {
+        fprintf(stderr, "rwkv: v6 maa LoRA width %d / n_embed %d unsupported\n", D, C);
+        return false;
+    }
+    const dim3 grid((C + 255) / 256, (T + MIX_TT - 1) / MIX_TT);
+    if (D <= 32) hipLaunchKernelGGL(k_v6_mix5<32>, grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(k_v6_mix5<64>, grid, dim3(256), 0, st, a);
     HIP_OK(hipGetLastError());
     return true;
 }
@@ -463,16 +499,17 @@ __device__ __forceinline__ float chain4(float acc, const f2_t (&x)[2]) {
     return acc;
 }
 
-template <bool WPT>
-__global__ __launch_bounds__(256) void k_wkv6_s64(int T, int H, const float * k, const float * v, const float * r,
-                                                  const float * u, const float * w, const float * sin, float * sout,
-                                                  float * y) {
+template <bool WPT, int NWV>
+__global__ __launch_bounds__(64 * NWV) void k_wkv6_s64(int T, int H, const float * k, const float * v, const float * r,
+                                                       const float * u, const float * w, const float * sin, float * sout,
+                                                       float * y) {
     constexpr int S = 64;
+    constexpr int CW = 4 * NWV, NT = 64 * NWV, QQ = WKV_TC * 16 / NT;
     __shared__ __attribute__((aligned(16))) float sk[WKV_TC][S], sr[WKV_TC][S], sw[WPT ? WKV_TC : 1][S],
-        sv[WKV_TC][16];
+        sv[WKV_TC][CW];
     const int h = blockIdx.x, jb = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int q = lane & 3, jl = (lane >> 2) & 3, g = lane >> 4;
-    const int jc = 4 * wv + jl, j = jb * 16 + jc, i0 = g * 16 + 4 * q;
+    const int jc = 4 * wv + jl, j = jb * CW + jc, i0 = g * 16 + 4 * q;
     const int C = H * S;
     const size_t hb = (size_t)h * S * S;
     f2_t st[2], uu[2], wc[2];
@@ -484,30 +521,31 @@ __global__ __launch_bounds__(256) void k_wkv6_s64(int T, int H, const float * k,
         wc[p] = WPT ? f2_t{0.f, 0.f} : f2_t{w[h * S + i], w[h * S + i + 1]};
     }
     // chunk staging: k/r/w rows of 64 floats = 16 float4 per token; thread moves float4
-    // #(tid & 15) of tokens (tid >> 4) + 16 qq, qq < 2; v: 16 columns = 4 float4 per token,
-    // threads < 128 move float4 #(tid & 3) of token tid >> 2
-    float4 pk[2], pr[2], pw[WPT ? 2 : 1], pv;
+    // #(tid & 15) of tokens (tid >> 4) + (NT/16) qq, qq < QQ; v: CW columns = NWV float4 per
+    // token, threads < 32*NWV move float4 #(tid % NWV) of token tid / NWV
+    float4 pk[QQ], pr[QQ], pw[WPT ? QQ : 1], pv;
     auto load_chunk = [&](int t0) {
 #pragma unroll
-        for (int qq = 0; qq < 2; qq++) {
-            const int t = min(t0 + (tid >> 4) + 16 * qq, T - 1);
+        for (int qq = 0; qq < QQ; qq++) {
+            const int t = min(t0 + (tid >> 4) + (NT / 16) * qq, T - 1);
             const size_t base = (size_t)t * C + (size_t)h * S + 4 * (tid & 15);
             pk[qq] = *(const float4 *)(k + base);
             pr[qq] = *(const float4 *)(r + base);
             if constexpr (WPT) pw[qq] = *(const float4 *)(w + base);
         }
-        const int t = min(t0 + ((tid & 127) >> 2), T - 1);
-        pv = *(const float4 *)(v + (size_t)t * C + (size_t)h * S + jb * 16 + 4 * (tid & 3));
+        const int tv = min(tid, 32 * NWV - 1);
+        const int t = min(t0 + tv / NWV, T - 1);
+        pv = *(const float4 *)(v + (size_t)t * C + (size_t)h * S + jb * CW + 4 * (tv % NWV));
     };
     auto store_chunk = [&]() {
 #pragma unroll
-        for (int qq = 0; qq < 2; qq++) {
-            const int tt = (tid >> 4) + 16 * qq;
+        for (int qq = 0; qq < QQ; qq++) {
+            const int tt = (tid >> 4) + (NT / 16) * qq;
             *(float4 *)&sk[tt][4 * (tid & 15)] = pk[qq];
             *(float4 *)&sr[tt][4 * (tid & 15)] = pr[qq];
             if constexpr (WPT) *(float4 *)&sw[tt][4 * (tid & 15)] = pw[qq];
         }
-        if (tid < 128) *(float4 *)&sv[tid >> 2][4 * (tid & 3)] = pv;
+        if (tid < 32 * NWV) *(float4 *)&sv[tid / NWV][4 * (tid % NWV)] = pv;
     };
     struct Tok {
         f2_t k[2], r[2], w[2];
@@ -530,40 +568,61 @@ __global__ __launch_bounds__(256) void k_wkv6_s64(int T, int H, const float * k,
         __syncthreads();
         if (t0 + WKV_TC < T) load_chunk(t0 + WKV_TC);  // in flight during this chunk
         const int n = min(WKV_TC, T - t0);
-        auto token = [&](const Tok & o, int tt) {
-            const f2_t vj = f2_t{o.v, o.v};
-            f2_t kv[2], x[2];
+        // Tokens in groups of TG: the state updates run token after token, then the TG output
+        // chains (independent of each other) are interleaved step by step.
+        constexpr int TG = 4;
+        auto group = [&](const Tok (&o)[TG], int tt0) {
+            f2_t x[TG][2];
 #pragma unroll
-            for (int p = 0; p < 2; p++) kv[p] = vj * o.k[p];
+            for (int e = 0; e < TG; e++) {
+                const bool val = tt0 + e < n;
+                const f2_t vj = f2_t{o[e].v, o[e].v};
+                f2_t kv[2];
 #pragma unroll
-            for (int p = 0; p < 2; p++) x[p] = kv[p] * uu[p];
+                for (int p = 0; p < 2; p++) kv[p] = vj * o[e].k[p];
 #pragma unroll
-            for (int p = 0; p < 2; p++) x[p] = x[p] + st[p];
+                for (int p = 0; p < 2; p++) x[e][p] = kv[p] * uu[p];
 #pragma unroll
-            for (int p = 0; p < 2; p++) x[p] = x[p] * o.r[p];
+                for (int p = 0; p < 2; p++) x[e][p] = x[e][p] + st[p];
 #pragma unroll
-            for (int p = 0; p < 2; p++) st[p] = st[p] * (WPT ? o.w[p] : wc[p]);
+                for (int p = 0; p < 2; p++) x[e][p] = x[e][p] * o[e].r[p];
 #pragma unroll
-            for (int p = 0; p < 2; p++) st[p] = st[p] + kv[p];
-            // 16-key sequential sum of group g across its q-lanes
-            float acc = chain4(0.0f, x);
+                for (int p = 0; p < 2; p++) {
+                    f2_t ns = st[p] * (WPT ? o[e].w[p] : wc[p]);
+                    ns = ns + kv[p];
+                    st[p] = val ? ns : st[p];
+                }
+            }
+            // 16-key sequential sum of group g across its q-lanes, TG chains side by side
+            float acc[TG];
+#pragma unroll
+            for (int e = 0; e < TG; e++) acc[e] = chain4(0.0f, x[e]);
 #pragma unroll
             for (int s = 1; s < 4; s++) {
-                const float c = chain4(dpp_shr1(acc), x);
-                acc = q >= s ? c : acc;
+#pragma unroll
+                for (int e = 0; e < TG; e++) {
+                    const float c = chain4(dpp_shr1(acc[e]), x[e]);
+                    acc[e] = q >= s ? c : acc[e];
+                }
             }
-            acc = fold_g4(acc);
-            if (g == 0 && q == 3) y[(size_t)(t0 + tt) * C + h * S + j] = acc;
+#pragma unroll
+            for (int e = 0; e < TG; e++) {
+                acc[e] = fold_g4(acc[e]);
+                if (g == 0 && q == 3 && tt0 + e < n) y[(size_t)(t0 + tt0 + e) * C + h * S + j] = acc[e];
+            }
         };
-        // two operand sets in turn: the next token's LDS reads overlap this token's arithmetic
-        Tok A, B;
-        read_tok(A, 0);
-        for (int tt = 0; tt < n; tt += 2) {
-            read_tok(B, min(tt + 1, n - 1));
-            token(A, tt);
-            if (tt + 1 >= n) break;
-            read_tok(A, min(tt + 2, n - 1));
-            token(B, tt + 1);
+        // two operand sets in turn: the next group's LDS reads overlap this group's arithmetic
+        Tok A[TG], B[TG];
+#pragma unroll
+        for (int e = 0; e < TG; e++) read_tok(A[e], min(e, n - 1));
+        for (int tt = 0; tt < n; tt += 2 * TG) {
+#pragma unroll
+            for (int e = 0; e < TG; e++) read_tok(B[e], min(tt + TG + e, n - 1));
+            group(A, tt);
+            if (tt + TG >= n) break;
+#pragma unroll
+            for (int e = 0; e < TG; e++) read_tok(A[e], min(tt + 2 * TG + e, n - 1));
+            group(B, tt + TG);
         }
         __syncthreads();
     }
@@ -575,14 +634,24 @@ __global__ __launch_bounds__(256) void k_wkv6_s64(int T, int H, const float * k,
     }
 }
 
+int g_wkv6_nwv = 4;  // waves per workgroup of k_wkv6_s64 (tools/wkv_probe.hip varies it)
+
 bool launch_wkv6(hipStream_t st, int T, int H, int S, const float * k, const float * v, const float * r,
                  const float * u, const float * w, int w_per_token, const float * state_in, float * state_out,
                  float * y) {
     if (S == 64) {
-        if (w_per_token)
-            hipLaunchKernelGGL(k_wkv6_s64<true>, dim3(H, 4), dim3(256), 0, st, T, H, k, v, r, u, w, state_in, state_out, y);
-        else
-            hipLaunchKernelGGL(k_wkv6_s64<false>, dim3(H, 4), dim3(256), 0, st, T, H, k, v, r, u, w, state_in, state_out, y);
+#define WKV6_L(P, N) hipLaunchKernelGGL((k_wkv6_s64<P, N>), dim3(H, 16 / (N)), dim3(64 * (N)), 0, st, T, H, k, v, r, u, w, state_in, state_out, y)
+        const int nwv = g_wkv6_nwv;
+        if (w_per_token) {
+            if (nwv == 1) WKV6_L(true, 1);
+            else if (nwv == 2) WKV6_L(true, 2);
+            else WKV6_L(true, 4);
+        } else {
+            if (nwv == 1) WKV6_L(false, 1);
+            else if (nwv == 2) WKV6_L(false, 2);
+            else WKV6_L(false, 4);
+        }
+#undef WKV6_L
         HIP_OK(hipGetLastError());
         return true;
     }

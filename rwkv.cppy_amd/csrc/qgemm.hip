@@ -136,7 +136,7 @@ __device__ __forceinline__ void qg_load_chunk(v4i_t rw, v4i_t ra, unsigned lds_b
 template <int TI>
 struct QGOps {
     long af[TI], xf[2];
-    uint2 sd[TI], sm[TI];  // fp16 d (m) of the 4 D-layout rows 4h..4h+3 of each 16-row tile
+    float4 sd[TI], sm[TI];  // d (m) of the 4 D-layout rows 4h..4h+3 of each 16-row tile
     float dx[2], sx[2];
 };
 
@@ -148,8 +148,8 @@ __device__ __forceinline__ void qg_read_ops(const char * sp, QGOps<QGLayout<WF>:
     for (int i = 0; i < Lt::TI; i++) {
         o.af[i] = *(const long *)(sp + (wr + 16 * i + r16) * 32 + h * 8);  // int8 row, k = 8h..8h+7
         const int ro = wr + 16 * i + 4 * h;
-        o.sd[i] = *(const uint2 *)(sp + qg_w_d(WF) + ro * 2);
-        if constexpr (Lt::ONE) o.sm[i] = *(const uint2 *)(sp + qg_w_m(WF) + ro * 2);
+        o.sd[i] = *(const float4 *)(sp + qg_w_d(WF) + ro * 4);
+        if constexpr (Lt::ONE) o.sm[i] = *(const float4 *)(sp + qg_w_m(WF) + ro * 4);
     }
     const char * ap = sp + Lt::WB;
 #pragma unroll
@@ -161,9 +161,192 @@ __device__ __forceinline__ void qg_read_ops(const char * sp, QGOps<QGLayout<WF>:
     }
 }
 
-__device__ __forceinline__ uint32_t qg_h16(uint2 v, int q) {
-    const uint32_t w = q < 2 ? v.x : v.y;
-    return (q & 1) ? (w >> 16) : (w & 0xFFFFu);
+typedef float qf2_t __attribute__((ext_vector_type(2)));
+
+// The MFMA accumulates each block's integer dot onto QG_BIAS = 0x4B400000 (1.5 * 2^23 as a float),
+// so the result read as a float is 12582912 + sumi exactly (|sumi| < 2^22), and one packed
+// subtraction recovers (float)sumi for two outputs: no per-output int->float conversion.
+constexpr int QG_BIAS = 0x4B400000;
+constexpr float QG_BIAS_F = 12582912.0f;
+
+// The TI x 2 MFMAs of one step (one quantization block) from this step's LDS operands
+template <int TI>
+__device__ __forceinline__ void qg_mfma(const QGOps<TI> & cur, v4i_t (&sv)[TI][2]) {
+    const v4i_t bias = {QG_BIAS, QG_BIAS, QG_BIAS, QG_BIAS};
+#pragma unroll
+    for (int i = 0; i < TI; i++)
+#pragma unroll
+        for (int j = 0; j < 2; j++) sv[i][j] = __builtin_amdgcn_mfma_i32_16x16x32_i8(cur.af[i], cur.xf[j], bias, 0, 0, 0);
+}
+
+// The fp32 block epilogue: acc = fma(d_w * d_x, sumi, acc) (+ acc2 += m_w * s_x), rows in pairs;
+// FIRST: the class's first block (its chain starts from 0)
+template <bool ONE, bool FIRST, int TI>
+__device__ __forceinline__ void qg_epi(const QGOps<TI> & cur, const v4i_t (&sv)[TI][2], float (&acc)[TI][2][4],
+                                       float (&acc2)[TI][2][4]) {
+    const qf2_t nbias = {-QG_BIAS_F, -QG_BIAS_F};
+#pragma unroll
+    for (int i = 0; i < TI; i++)
+#pragma unroll
+        for (int qp = 0; qp < 2; qp++) {
+            const qf2_t dw = qp ? qf2_t{cur.sd[i].z, cur.sd[i].w} : qf2_t{cur.sd[i].x, cur.sd[i].y};
+            const qf2_t mw = qp ? qf2_t{cur.sm[i].z, cur.sm[i].w} : qf2_t{cur.sm[i].x, cur.sm[i].y};
+#pragma unroll
+            for (int j = 0; j < 2; j++) {
+                const qf2_t dx = {cur.dx[j], cur.dx[j]};
+                const qf2_t si = qf2_t{__int_as_float(sv[i][j][2 * qp]), __int_as_float(sv[i][j][2 * qp + 1])} + nbias;
+                const qf2_t a0 = FIRST ? qf2_t{0.0f, 0.0f} : qf2_t{acc[i][j][2 * qp], acc[i][j][2 * qp + 1]};
+                const qf2_t a = __builtin_elementwise_fma(dw * dx, si, a0);
+                acc[i][j][2 * qp] = a.x;
+                acc[i][j][2 * qp + 1] = a.y;
+                if constexpr (ONE) {
+                    const qf2_t sx = {cur.sx[j], cur.sx[j]};
+                    const qf2_t b0 = FIRST ? qf2_t{0.0f, 0.0f} : qf2_t{acc2[i][j][2 * qp], acc2[i][j][2 * qp + 1]};
+                    const qf2_t b = b0 + mw * sx;
+                    acc2[i][j][2 * qp] = b.x;
+                    acc2[i][j][2 * qp + 1] = b.y;
+                }
+            }
+        }
+}
+
+// y[t][m] = epi(total (+ total2)), as k_mm's red + red2.  A lane holds rows 4h..4h+3 of one
+// token: one 16-byte access per (token, 4 rows) when aligned.
+template <bool ONE, int TI>
+__device__ __forceinline__ void qg_store(const MMEntry & E, int T, int M, int tok0, int row0, int wt, int wr, int r16,
+                                         int h, const float (&tot)[TI][2][4], const float (&tot2)[TI][2][4]) {
+    const bool vec = ((E.ldy | M) & 3) == 0 && (((uintptr_t)E.y | (uintptr_t)E.aux) & 15) == 0;
+#pragma unroll
+    for (int i = 0; i < TI; i++)
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            const int t = tok0 + wt + 16 * j + r16;
+            const int m0 = row0 + wr + 16 * i + 4 * h;
+            if (t >= T || m0 >= M) continue;
+            float acc[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) acc[q] = ONE ? tot[i][j][q] + tot2[i][j][q] : tot[i][j][q] + 0.0f;
+            float * yp = E.y + (size_t)t * E.ldy + m0;
+            if (vec) {
+                float4 yv = make_float4(0.f, 0.f, 0.f, 0.f), av = yv;
+                if (epi_reads_y(E.epi)) yv = *(const float4 *)yp;
+                if (epi_reads_aux(E.epi)) av = *(const float4 *)(E.aux + (size_t)t * E.ldy + m0);
+                float4 o;
+                o.x = apply_epi_v(E, m0, acc[0], yv.x, av.x);
+                o.y = apply_epi_v(E, m0 + 1, acc[1], yv.y, av.y);
+                o.z = apply_epi_v(E, m0 + 2, acc[2], yv.z, av.z);
+                o.w = apply_epi_v(E, m0 + 3, acc[3], yv.w, av.w);
+                *(float4 *)yp = o;
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    if (m0 + q < M) yp[q] = apply_epi(E, t, m0 + q, acc[q]);
+            }
+        }
+}
+
+// Class-pair fold: the odd class (in c) closes N >= 1 levels of the binary counter: v = c, then
+// v = st[k] + v for k < N, into st[N] (N < 6) or the total (N = 6)
+template <bool ONE, int TI, int N>
+__device__ __forceinline__ void qg_fold(float (&st)[6][TI][2][4], float (&st2)[6][TI][2][4], const float (&c)[TI][2][4],
+                                        const float (&c2)[TI][2][4], float (&tot)[TI][2][4], float (&tot2)[TI][2][4]) {
+#pragma unroll
+    for (int i = 0; i < TI; i++)
+#pragma unroll
+        for (int j = 0; j < 2; j++)
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                float v = c[i][j][q];
+#pragma unroll
+                for (int kk = 0; kk < N; kk++) v = st[kk][i][j][q] + v;
+                if constexpr (N < 6) st[N][i][j][q] = v;
+                else tot[i][j][q] = v;
+                if constexpr (ONE) {
+                    float v2 = c2[i][j][q];
+#pragma unroll
+                    for (int kk = 0; kk < N; kk++) v2 = st2[kk][i][j][q] + v2;
+                    if constexpr (N < 6) st2[N][i][j][q] = v2;
+                    else tot2[i][j][q] = v2;
+                }
+            }
+}
+
+// K = 2048 (64 blocks: every class is one block, the walk is block order): the same arithmetic
+// as k_qgemm with the step bookkeeping resolved at compile time -- each 8-step chunk is
+// straight-line code (the class-pair folds after steps 1, 3, 5 close 1, 2, 1 levels; after step
+// 7, 3 + ctz(~chunk) levels), and the copy walk is blocks 8c + wave, 8c + wave + 4.
+template <int WF>
+__global__ __launch_bounds__(256) void k_qgemm_k64(MMGroup g) {
+    using Lt = QGLayout<WF>;
+    constexpr bool ONE = Lt::ONE;
+    constexpr int TI = Lt::TI;
+    constexpr int NB = 64, NCH = NB / QG_STEPS;
+    __shared__ __attribute__((aligned(16))) char smem[2][Lt::BUF];
+    int e = 0;
+#pragma unroll 1
+    while (e + 1 < g.n && (int)blockIdx.x >= g.e[e + 1].block0) e++;
+    const MMEntry & E = g.e[e];
+    const int M = E.W.M, T = g.T;
+    const int tilesT = (T + QG_TOK - 1) / QG_TOK;
+    const int local = (int)blockIdx.x - E.block0;
+    const int mtile = local / tilesT, ttile = local % tilesT;
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int r16 = lane & 15, h = lane >> 4;
+    const int row0 = mtile * Lt::ROWS, tok0 = ttile * QG_TOK;
+    const int wr = (wave & 1) * 16 * TI, wt = (wave >> 1) * 32;
+    const v4i_t rw = qg_rsrc(E.W.gt + (size_t)mtile * NB * Lt::WB);
+    const v4i_t ra = qg_rsrc(E.in.tq + (size_t)ttile * NB * Lt::AB);
+    const unsigned lds0 = __builtin_amdgcn_readfirstlane((unsigned)(unsigned long)(lds_void_t *)&smem[0][0]);
+    auto load = [&](int c, unsigned buf) {
+#pragma unroll
+        for (int h2 = 0; h2 < 2; h2++) {
+            const int k = wave + 4 * h2, b = c * QG_STEPS + k;
+            const unsigned m = buf + k * Lt::STEP;
+            qg_record<Lt::WB>(rw, (unsigned)(b * Lt::WB), m, lane);
+            qg_record<Lt::AB>(ra, (unsigned)(b * Lt::AB), m + Lt::WB, lane);
+        }
+    };
+    float st[6][TI][2][4], st2[6][TI][2][4];
+    float tot[TI][2][4], tot2[TI][2][4];
+    float c[TI][2][4], c2[TI][2][4];
+    load(0, lds0);
+    qg_chunk_done();
+    load(1, lds0 + Lt::BUF);
+    QGOps<TI> cur;
+    qg_read_ops<WF>(smem[0], cur, wr, wt, r16, h);
+#pragma unroll 1
+    for (int ch = 0; ch < NCH; ch++) {
+        const char * buf = smem[ch & 1];
+#pragma unroll
+        for (int k = 0; k < QG_STEPS; k++) {
+            v4i_t sv[TI][2];
+            qg_mfma<TI>(cur, sv);
+            QGOps<TI> nxt = cur;
+            if (k + 1 < QG_STEPS) qg_read_ops<WF>(buf + (k + 1) * Lt::STEP, nxt, wr, wt, r16, h);
+            if (k & 1) {
+                qg_epi<ONE, true, TI>(cur, sv, c, c2);
+                if (k == 1 || k == 5) qg_fold<ONE, TI, 1>(st, st2, c, c2, tot, tot2);
+                else if (k == 3) qg_fold<ONE, TI, 2>(st, st2, c, c2, tot, tot2);
+                else {
+                    switch (__builtin_ctz(~ch)) {
+                        case 0: qg_fold<ONE, TI, 3>(st, st2, c, c2, tot, tot2); break;
+                        case 1: qg_fold<ONE, TI, 4>(st, st2, c, c2, tot, tot2); break;
+                        case 2: qg_fold<ONE, TI, 5>(st, st2, c, c2, tot, tot2); break;
+                        default: qg_fold<ONE, TI, 6>(st, st2, c, c2, tot, tot2); break;
+                    }
+                }
+            } else {
+                qg_epi<ONE, true, TI>(cur, sv, st[0], st2[0]);
+            }
+            cur = nxt;
+        }
+        if (ch + 1 < NCH) {
+            qg_chunk_done();  // chunk ch+1 has landed and buffer ch&1 is free
+            if (ch + 2 < NCH) load(ch + 2, lds0 + (ch & 1) * Lt::BUF);
+            qg_read_ops<WF>(smem[(ch + 1) & 1], cur, wr, wt, r16, h);
+        }
+    }
+    qg_store<ONE, TI>(E, T, M, tok0, row0, wt, wr, r16, h, tot, tot2);
 }
 
 template <int WF>
@@ -199,7 +382,6 @@ __global__ __launch_bounds__(256) void k_qgemm(MMGroup g) {
     float st[6][TI][2][4], st2[6][TI][2][4];
     float tot[TI][2][4], tot2[TI][2][4];
     float c[TI][2][4], c2[TI][2][4];
-    const v4i_t zero = {0, 0, 0, 0};
     const int nchunks = (nb + QG_STEPS - 1) / QG_STEPS;
 
     int k = 0, cb = 0, cn = 1;  // step within the chunk, its buffer, next chunk to issue
@@ -229,24 +411,10 @@ __global__ __launch_bounds__(256) void k_qgemm(MMGroup g) {
 #endif
         {
             v4i_t sv[TI][2];
-#pragma unroll
-            for (int i = 0; i < TI; i++)
-#pragma unroll
-                for (int j = 0; j < 2; j++) sv[i][j] = __builtin_amdgcn_mfma_i32_16x16x32_i8(cur.af[i], cur.xf[j], zero, 0, 0, 0);
+            qg_mfma<TI>(cur, sv);
             QGOps<TI> nxt = cur;
             if (k + 1 < QG_STEPS) qg_read_ops<WF>(smem[cb] + (k + 1) * Lt::STEP, nxt, wr, wt, r16, h);
-#pragma unroll
-            for (int i = 0; i < TI; i++)
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    const float dw = h2f((uint16_t)qg_h16(cur.sd[i], q));
-                    const float mw = ONE ? h2f((uint16_t)qg_h16(cur.sm[i], q)) : 0.0f;
-#pragma unroll
-                    for (int j = 0; j < 2; j++) {
-                        acc[i][j][q] = fmaf(dw * cur.dx[j], (float)sv[i][j][q], FIRST ? 0.0f : acc[i][j][q]);
-                        if constexpr (ONE) acc2[i][j][q] = (FIRST ? 0.0f : acc2[i][j][q]) + mw * cur.sx[j];
-                    }
-                }
+            qg_epi<ONE, FIRST, TI>(cur, sv, acc, acc2);
             cur = nxt;
         }
         k++;
@@ -312,41 +480,14 @@ __global__ __launch_bounds__(256) void k_qgemm(MMGroup g) {
     // copies of a partial last chunk (or of none) were never waited for: drain before exit
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-    // epilogue: y[t][m] = epi(total (+ total2)), as k_mm's red + red2.  A lane holds rows
-    // 4h..4h+3 of one token: one 16-byte access per (token, 4 rows) when aligned.
-    const bool vec = ((E.ldy | M) & 3) == 0 && (((uintptr_t)E.y | (uintptr_t)E.aux) & 15) == 0;
-#pragma unroll
-    for (int i = 0; i < TI; i++)
-#pragma unroll
-        for (int j = 0; j < 2; j++) {
-            const int t = tok0 + wt + 16 * j + r16;
-            const int m0 = row0 + wr + 16 * i + 4 * h;
-            if (t >= T || m0 >= M) continue;
-            float acc[4];
-#pragma unroll
-            for (int q = 0; q < 4; q++) acc[q] = ONE ? tot[i][j][q] + tot2[i][j][q] : tot[i][j][q] + 0.0f;
-            float * yp = E.y + (size_t)t * E.ldy + m0;
-            if (vec) {
-                float4 yv = make_float4(0.f, 0.f, 0.f, 0.f), av = yv;
-                if (epi_reads_y(E.epi)) yv = *(const float4 *)yp;
-                if (epi_reads_aux(E.epi)) av = *(const float4 *)(E.aux + (size_t)t * E.ldy + m0);
-                float4 o;
-                o.x = apply_epi_v(E, m0, acc[0], yv.x, av.x);
-                o.y = apply_epi_v(E, m0 + 1, acc[1], yv.y, av.y);
-                o.z = apply_epi_v(E, m0 + 2, acc[2], yv.z, av.z);
-                o.w = apply_epi_v(E, m0 + 3, acc[3], yv.w, av.w);
-                *(float4 *)yp = o;
-            } else {
-#pragma unroll
-                for (int q = 0; q < 4; q++)
-                    if (m0 + q < M) yp[q] = apply_epi(E, t, m0 + q, acc[q]);
-            }
-        }
+    qg_store<ONE, TI>(E, T, M, tok0, row0, wt, wr, r16, h, tot, tot2);
 }
 
 // Every entry must have y (the engine gives emitting entries a scratch y); emission into the
 // next matmul's activation format is a separate launch_act_from_f32 pass by the caller.  The
 // weights need their tile records (upload_mat) and the activations must be token tiles.
+int g_qgemm_generic = 0;  // 1: K = 2048 through the generic kernel too (tools, comparison)
+
 bool launch_qgemm(hipStream_t st, MMGroup & g, int wtype) {
     const int rows = qg_rows(wtype);
     const int tilesT = (g.T + QG_TOK - 1) / QG_TOK;
@@ -363,6 +504,20 @@ bool launch_qgemm(hipStream_t st, MMGroup & g, int wtype) {
     }
     if (!blocks) return true;
     const dim3 grid(blocks), block(256);
+    bool k64 = true;
+    for (int i = 0; i < g.n; i++) k64 = k64 && g.e[i].W.K == 2048;
+    if (k64 && !g_qgemm_generic) {
+        switch (wtype) {
+            case W_Q4_0: hipLaunchKernelGGL(k_qgemm_k64<W_Q4_0>, grid, block, 0, st, g); break;
+            case W_Q4_1: hipLaunchKernelGGL(k_qgemm_k64<W_Q4_1>, grid, block, 0, st, g); break;
+            case W_Q5_0: hipLaunchKernelGGL(k_qgemm_k64<W_Q5_0>, grid, block, 0, st, g); break;
+            case W_Q5_1: hipLaunchKernelGGL(k_qgemm_k64<W_Q5_1>, grid, block, 0, st, g); break;
+            case W_Q8_0: hipLaunchKernelGGL(k_qgemm_k64<W_Q8_0>, grid, block, 0, st, g); break;
+            default: fprintf(stderr, "rwkv: qgemm type %d unsupported\n", wtype); return false;
+        }
+        HIP_OK(hipGetLastError());
+        return true;
+    }
     switch (wtype) {
         case W_Q4_0: hipLaunchKernelGGL(k_qgemm<W_Q4_0>, grid, block, 0, st, g); break;
         case W_Q4_1: hipLaunchKernelGGL(k_qgemm<W_Q4_1>, grid, block, 0, st, g); break;

@@ -55,7 +55,7 @@ static ActBuf act(int T, int K) {
 }
 
 int main(int argc, char ** argv) {
-    const int npath = argc > 1 ? atoi(argv[1]) : 2;
+    const int npath = argc > 1 ? atoi(argv[1]) : 3;
     const int T = 1024;
     hipStream_t st;
     CK(hipStreamCreate(&st));
@@ -70,6 +70,7 @@ int main(int argc, char ** argv) {
         ActBuf x = act(T, s.K);
         float * y;
         CK(hipMalloc(&y, (size_t)T * s.M * 4));
+        std::vector<float> ref((size_t)T * s.M), out(ref.size());
         for (int path = 0; path < npath; path++) {
             MMGroup g;
             memset(&g, 0, sizeof g);
@@ -77,22 +78,27 @@ int main(int argc, char ** argv) {
             g.T = T;
             g.e[0].W = W;
             g.e[0].in = x;
-            g.e[0].in.tiled = path ? 0 : 1;
+            g.e[0].in.tiled = path < 2 ? 1 : 0;
             g.e[0].y = y;
             g.e[0].ldy = s.M;
             g.e[0].epi = EPI_STORE;
-            auto run = [&]() { return path ? launch_mm_group(st, g, W_Q4_0) : launch_qgemm(st, g, W_Q4_0); };
+            g_qgemm_generic = path == 1;
+            auto run = [&]() { return path == 2 ? launch_mm_group(st, g, W_Q4_0) : launch_qgemm(st, g, W_Q4_0); };
             if (!run()) return 1;
             CK(hipStreamSynchronize(st));
-            const int reps = path ? 1 : 5;
+            const int reps = path == 2 ? 1 : 5;
             CK(hipEventRecord(a, st));
             for (int i = 0; i < reps; i++) run();
             CK(hipEventRecord(b, st));
             CK(hipEventSynchronize(b));
             float ms;
             CK(hipEventElapsedTime(&ms, a, b));
+            CK(hipMemcpy(out.data(), y, out.size() * 4, hipMemcpyDeviceToHost));
+            if (path == 0) ref = out;
+            const bool same = !memcmp(ref.data(), out.data(), out.size() * 4);
             const double us = ms * 1e3 / reps, ops = 2.0 * s.M * s.K * T;
-            printf("%-26s %-6s %9.1f us  %7.1f TOPS\n", s.name, path ? "k_mm" : "qgemm", us, ops / us * 1e-6);
+            printf("%-26s %-14s %9.1f us  %7.1f TOPS  %s\n", s.name, path == 2 ? "k_mm" : path ? "qgemm-generic" : "qgemm",
+                   us, ops / us * 1e-6, path && path < 2 ? (same ? "bit-identical" : "DIFFERENT") : "");
         }
     }
     return 0;

@@ -2,7 +2,7 @@
 
 FETCH_SIZE is doubled (gfx950 tallies 128-B requests of wide streaming reads at 64 B,
 MI355X_MICROARCH.md HBM section); WRITE_SIZE is taken as is.  Both are in KiB per dispatch.
-All decode matvec instantiations (k_mv<...>) are pooled under the name bench.py reports, "k_mv".
+All decode matvec instantiations (k_mv<...>, k_mva<...>) are pooled under the name bench.py reports, "k_mv".
 Usage: python tools/pmc_summary.py TAG CONFIG  ->  updates profiles/pmc_traffic.json
 """
 import csv
@@ -24,7 +24,7 @@ def per_kernel(d, counter):
             if r.get('Counter_Name') != counter:
                 continue
             name = r['Kernel_Name']
-            key = 'k_mv' if 'k_mv<' in name else name.split('(')[0]
+            key = 'k_mv' if ('k_mv<' in name or 'k_mva<' in name) else name.split('(')[0]
             tot[key] += float(r['Counter_Value']) * 1024.0
             cnt[key] += 1
     return tot, cnt

@@ -336,20 +336,29 @@ __global__ __launch_bounds__(256) void k_v6_mix5(Mix5Args a) {
         }
     }
     __syncthreads();
-    for (int tt = 0; tt < nt; tt++) {
-        const size_t ti = (size_t)(t0 + tt) * C + cc;
-        const float xa = a.xa[ti], sx = a.sx[ti];
-        double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+    // two tokens at a time: ten independent fp64 chains side by side
+    for (int tt = 0; tt < nt; tt += 2) {
+        const int t1 = min(tt + 1, nt - 1);
+        const size_t ti0 = (size_t)(t0 + tt) * C + cc, ti1 = (size_t)(t0 + t1) * C + cc;
+        const float xa0 = a.xa[ti0], sx0 = a.sx[ti0], xa1 = a.xa[ti1], sx1 = a.sx[ti1];
+        double acc0[5] = {0.0, 0.0, 0.0, 0.0, 0.0}, acc1[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int i = 0; i < DM; i++) {
             if (i < D) {
 #pragma unroll
-                for (int n = 0; n < 5; n++) acc[n] += (double)(w2v[n][i] * sl[tt][n * DM + i]);
+                for (int n = 0; n < 5; n++) {
+                    acc0[n] += (double)(w2v[n][i] * sl[tt][n * DM + i]);
+                    acc1[n] += (double)(w2v[n][i] * sl[t1][n * DM + i]);
+                }
             }
         }
         if (cval) {
 #pragma unroll
-            for (int n = 0; n < 5; n++) emit32(a.out[n], t0 + tt, c, ((float)acc[n] + mu[n]) * sx + xa);
+            for (int n = 0; n < 5; n++) emit32(a.out[n], t0 + tt, c, ((float)acc0[n] + mu[n]) * sx0 + xa0);
+            if (tt + 1 < nt) {
+#pragma unroll
+                for (int n = 0; n < 5; n++) emit32(a.out[n], t0 + tt + 1, c, ((float)acc1[n] + mu[n]) * sx1 + xa1);
+            }
         }
     }
 }

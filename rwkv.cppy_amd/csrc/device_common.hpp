@@ -181,20 +181,39 @@ struct WBlk {
     uint32_t sc;     // fp16 d (low half) | fp16 m << 16 (_1 formats)
 };
 
-template <int WF>
+// Weight loads.  NT: non-temporal (`nt`) loads for bytes that ONE workgroup reads once per
+// token (the decode matvec stream, 1 GB per v6-1B6 token, far larger than L2 + MALL): they do
+// not displace the activations and state the chain re-reads (MI355X_MICROARCH.md nt-weights).
+typedef int wld_i32x4 __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ int4 ld16w(const void * p) {
+    if constexpr (NT) {
+        const wld_i32x4 t = __builtin_nontemporal_load((const wld_i32x4 *)p);
+        return make_int4(t.x, t.y, t.z, t.w);
+    } else {
+        return *(const int4 *)p;
+    }
+}
+template <bool NT, typename T>
+__device__ __forceinline__ T ldw(const T * p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+
+template <int WF, bool NT = false>
 __device__ __forceinline__ WBlk load_wblk(const DMat & W, size_t bi) {
     WBlk w;
     if constexpr (WF == W_Q8_0) {
         const int4 * p = (const int4 *)(W.qs + bi * 32);
-        w.q0 = p[0];
-        w.q1 = p[1];
+        w.q0 = ld16w<NT>(p);
+        w.q1 = ld16w<NT>(p + 1);
     } else {
-        w.q0 = *(const int4 *)(W.qs + bi * 16);
+        w.q0 = ld16w<NT>(W.qs + bi * 16);
         w.q1 = make_int4(0, 0, 0, 0);
     }
-    w.qh = (WF == W_Q5_0 || WF == W_Q5_1) ? W.qh[bi] : 0u;
-    if constexpr (WF == W_Q4_1 || WF == W_Q5_1) w.sc = ((const uint32_t *)W.sc)[bi];
-    else w.sc = ((const uint16_t *)W.sc)[bi];
+    w.qh = (WF == W_Q5_0 || WF == W_Q5_1) ? ldw<NT>(W.qh + bi) : 0u;
+    if constexpr (WF == W_Q4_1 || WF == W_Q5_1) w.sc = ldw<NT>((const uint32_t *)W.sc + bi);
+    else w.sc = ldw<NT>((const uint16_t *)W.sc + bi);
     return w;
 }
 

@@ -97,23 +97,24 @@ __device__ __forceinline__ int loadi(const int * p) {
     else return *p;
 }
 
-template <int WF>
+// NT (default): the row is streamed once per token by this wave -- non-temporal loads
+template <int WF, bool NT = true>
 __device__ __forceinline__ WBlk load_unit(const DMat & W, int row, int u, int lane) {
     const int K = W.K;
     if constexpr (WF == W_F32) {
         WBlk w;
         const int k = min(lane * 4 + u * 256, K - 4);
-        w.q0 = *(const int4 *)((const float *)W.qs + (size_t)row * K + k);
+        w.q0 = ld16w<NT>((const float *)W.qs + (size_t)row * K + k);
         return w;
     } else if constexpr (WF == W_F16) {
         WBlk w;
         const int k = min(lane * 8 + u * 512, K - 8);
-        w.q0 = *(const int4 *)((const __half *)W.qs + (size_t)row * K + k);
+        w.q0 = ld16w<NT>((const __half *)W.qs + (size_t)row * K + k);
         return w;
     } else {
         const int nb = K >> 5;
         const int b = min(lane + u * 64, nb - 1);
-        return load_wblk<WF>(W, (size_t)row * nb + b);
+        return load_wblk<WF, NT>(W, (size_t)row * nb + b);
     }
 }
 

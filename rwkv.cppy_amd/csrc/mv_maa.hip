@@ -50,7 +50,7 @@ __global__ __launch_bounds__(512) void k_v6_maa_dec(MaaDec a) {
 #pragma unroll
         for (int u = 0; u < U; u++)
 #pragma unroll
-            for (int r = 0; r < R; r++) w[r][u] = load_unit<WF>(W, rows[r], u, lane);
+            for (int r = 0; r < R; r++) w[r][u] = load_unit<WF, false>(W, rows[r], u, lane);
         // this thread's mix channel: W2 column, carry, maa
         const int c = blockIdx.x * 256 + tid;
         const bool cval = (int)(blockIdx.x * 256 + (tid & ~31)) < C;  // half-wave uniform
@@ -72,7 +72,7 @@ __global__ __launch_bounds__(512) void k_v6_maa_dec(MaaDec a) {
 #pragma unroll
                 for (int u = 0; u < U; u++)
 #pragma unroll
-                    for (int r = 0; r < R; r++) w[r][u] = load_unit<WF>(W, rows[r], u0 + u, lane);
+                    for (int r = 0; r < R; r++) w[r][u] = load_unit<WF, false>(W, rows[r], u0 + u, lane);
             }
             AUnit xu[U];
 #pragma unroll

@@ -478,11 +478,11 @@ typedef float f2_t __attribute__((ext_vector_type(2)));
 // value columns of one head, grid (H, 4).  Lane (g = lane >> 4, jl = (lane >> 2) & 3, q = lane & 3)
 // of wave wv owns column j = 16*blockIdx.y + 4*wv + jl for keys i = 16g + 4q + e (e < 4): the
 // per-element arithmetic is k_att6_dec's (packed pairs, the same IEEE mul / add per element, no
-// contraction).  The output sum keeps the decode association exactly -- for each key group g a
-// sequential sum over its 16 keys in order, starting from 0 -- by running it across the four
-// q-lanes of the group: lane q continues the partial of lane q-1 (DPP row_shr:1), so the chain is
-// 16 dependent adds as before while the state work is spread over 4x the lanes.  The 4 group
-// partials are folded with fold_g4 ((p0 + p2) + (p1 + p3)).  Chunks of 32 tokens of k, r, w and v
+// contraction).  The output sum has k_att6_dec's association exactly: each lane sums its 4 keys
+// in order starting from 0 (p_q), the quad folds them as (p0 + p1) + (p2 + p3) (DPP quad
+// permutes xor 1, xor 2; float addition commutes, so every lane of the quad holds the same bits),
+// and the 4 key groups are folded with fold_g4 ((s0 + s2) + (s1 + s3)): 8 dependent VALU ops per
+// token instead of a 16-add chain through the lanes.  Chunks of 32 tokens of k, r, w and v
 // are staged in LDS with coalesced loads, the next chunk in flight while this one runs.
 constexpr int WKV_TC = 32;
 
@@ -495,8 +495,12 @@ __device__ __forceinline__ float fold_g4(float v) {
     return __int_as_float(b[0]) + __int_as_float(b[1]);
 }
 
-__device__ __forceinline__ float dpp_shr1(float v) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x111, 0xF, 0xF, false));
+// v + (v of lane ^ 1) and v + (v of lane ^ 2) inside each quad
+__device__ __forceinline__ float quad_add_x1(float v) {
+    return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float quad_add_x2(float v) {
+    return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));
 }
 
 // acc continued over the lane's 4 terms in order
@@ -602,22 +606,18 @@ __global__ __launch_bounds__(64 * NWV) void k_wkv6_s64(int T, int H, const float
                     st[p] = val ? ns : st[p];
                 }
             }
-            // 16-key sequential sum of group g across its q-lanes, TG chains side by side
+            // p_q (4 keys in order), (p0 + p1) + (p2 + p3) over the quad, TG sums side by side
             float acc[TG];
 #pragma unroll
             for (int e = 0; e < TG; e++) acc[e] = chain4(0.0f, x[e]);
 #pragma unroll
-            for (int s = 1; s < 4; s++) {
+            for (int e = 0; e < TG; e++) acc[e] = quad_add_x1(acc[e]);
 #pragma unroll
-                for (int e = 0; e < TG; e++) {
-                    const float c = chain4(dpp_shr1(acc[e]), x[e]);
-                    acc[e] = q >= s ? c : acc[e];
-                }
-            }
+            for (int e = 0; e < TG; e++) acc[e] = quad_add_x2(acc[e]);
 #pragma unroll
             for (int e = 0; e < TG; e++) {
                 acc[e] = fold_g4(acc[e]);
-                if (g == 0 && q == 3 && tt0 + e < n) y[(size_t)(t0 + tt0 + e) * C + h * S + j] = acc[e];
+                if (g == 0 && q == 0 && tt0 + e < n) y[(size_t)(t0 + tt0 + e) * C + h * S + j] = acc[e];
             }
         };
         // two operand sets in turn: the next group's LDS reads overlap this group's arithmetic

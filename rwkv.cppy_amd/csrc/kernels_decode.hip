@@ -320,10 +320,12 @@ __global__ __launch_bounds__(256) void k_att6_dec(Att6Dec a) {
         }
         __syncthreads();
     }
-    // wkv6 for one token (ggml_rwkv_wkv6 semantics, same arithmetic as k_wkv6)
+    // wkv6 for one token (ggml_rwkv_wkv6 semantics, same arithmetic as the sequence kernels).
+    // Head size 64 (IPG 16): the group's sum is (p0 + p1) + (p2 + p3) over its four 4-key runs,
+    // k_wkv6_s64's association; other head sizes: one sequential run (k_wkv6's).
     if (active) {
         const float vj = sv[j];
-        float acc = 0.0f;
+        float acc = 0.0f, p4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
         for (int ii = 0; ii < 16; ii++) {
             if (ii < IPG) {
@@ -331,11 +333,13 @@ __global__ __launch_bounds__(256) void k_att6_dec(Att6Dec a) {
                 const float prev = st[ii];
                 const float kv = vj * sk[i];
                 const float temp = kv * su[i] + prev;
-                acc += temp * sr[i];
+                const float t = temp * sr[i];
+                acc += t;
+                p4[ii >> 2] += t;
                 a.sout[hb + (size_t)i * S + j] = prev * sw[i] + kv;
             }
         }
-        part[g][j] = acc;
+        part[g][j] = IPG == 16 ? (p4[0] + p4[1]) + (p4[2] + p4[3]) : acc;
     }
     __syncthreads();
     // GroupNorm over the head (ggml_norm, fp64 sums) * ln_x (+ b) (* g)

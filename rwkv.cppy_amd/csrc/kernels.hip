@@ -482,7 +482,7 @@ typedef float f2_t __attribute__((ext_vector_type(2)));
 // in order starting from 0 (p_q), the quad folds them as (p0 + p1) + (p2 + p3) (DPP quad
 // permutes xor 1, xor 2; float addition commutes, so every lane of the quad holds the same bits),
 // and the 4 key groups are folded with fold_g4 ((s0 + s2) + (s1 + s3)): 8 dependent VALU ops per
-// token instead of a 16-add chain through the lanes.  Chunks of 32 tokens of k, r, w and v
+// token instead of a 16-add chain through the lanes.  Chunks of 64 tokens of k, r, w and v
 // are staged in LDS with coalesced loads, the next chunk in flight while this one runs.
 constexpr int WKV_TC = 32;
 
@@ -512,14 +512,17 @@ __device__ __forceinline__ float chain4(float acc, const f2_t (&x)[2]) {
     return acc;
 }
 
+// wkv6 chunk: 64 tokens, so the next chunk's loads have a whole chunk of compute to land in
+constexpr int WKV6_TC = 64;
+
 template <bool WPT, int NWV>
 __global__ __launch_bounds__(64 * NWV) void k_wkv6_s64(int T, int H, const float * k, const float * v, const float * r,
                                                        const float * u, const float * w, const float * sin, float * sout,
                                                        float * y) {
     constexpr int S = 64;
-    constexpr int CW = 4 * NWV, NT = 64 * NWV, QQ = WKV_TC * 16 / NT;
-    __shared__ __attribute__((aligned(16))) float sk[WKV_TC][S], sr[WKV_TC][S], sw[WPT ? WKV_TC : 1][S],
-        sv[WKV_TC][CW];
+    constexpr int CW = 4 * NWV, NT = 64 * NWV, QQ = WKV6_TC * 16 / NT;
+    __shared__ __attribute__((aligned(16))) float sk[WKV6_TC][S], sr[WKV6_TC][S], sw[WPT ? WKV6_TC : 1][S],
+        sv[WKV6_TC][CW];
     const int h = blockIdx.x, jb = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int q = lane & 3, jl = (lane >> 2) & 3, g = lane >> 4;
     const int jc = 4 * wv + jl, j = jb * CW + jc, i0 = g * 16 + 4 * q;
@@ -535,7 +538,7 @@ __global__ __launch_bounds__(64 * NWV) void k_wkv6_s64(int T, int H, const float
     }
     // chunk staging: k/r/w rows of 64 floats = 16 float4 per token; thread moves float4
     // #(tid & 15) of tokens (tid >> 4) + (NT/16) qq, qq < QQ; v: CW columns = NWV float4 per
-    // token, threads < 32*NWV move float4 #(tid % NWV) of token tid / NWV
+    // token, threads < WKV6_TC*NWV move float4 #(tid % NWV) of token tid / NWV
     float4 pk[QQ], pr[QQ], pw[WPT ? QQ : 1], pv;
     auto load_chunk = [&](int t0) {
 #pragma unroll
@@ -546,7 +549,7 @@ __global__ __launch_bounds__(64 * NWV) void k_wkv6_s64(int T, int H, const float
             pr[qq] = *(const float4 *)(r + base);
             if constexpr (WPT) pw[qq] = *(const float4 *)(w + base);
         }
-        const int tv = min(tid, 32 * NWV - 1);
+        const int tv = min(tid, WKV6_TC * NWV - 1);
         const int t = min(t0 + tv / NWV, T - 1);
         pv = *(const float4 *)(v + (size_t)t * C + (size_t)h * S + jb * CW + 4 * (tv % NWV));
     };
@@ -558,7 +561,7 @@ __global__ __launch_bounds__(64 * NWV) void k_wkv6_s64(int T, int H, const float
             *(float4 *)&sr[tt][4 * (tid & 15)] = pr[qq];
             if constexpr (WPT) *(float4 *)&sw[tt][4 * (tid & 15)] = pw[qq];
         }
-        if (tid < 32 * NWV) *(float4 *)&sv[tid / NWV][4 * (tid % NWV)] = pv;
+        if (tid < WKV6_TC * NWV) *(float4 *)&sv[tid / NWV][4 * (tid % NWV)] = pv;
     };
     struct Tok {
         f2_t k[2], r[2], w[2];
@@ -576,11 +579,11 @@ __global__ __launch_bounds__(64 * NWV) void k_wkv6_s64(int T, int H, const float
         o.v = sv[tt][jc];
     };
     load_chunk(0);
-    for (int t0 = 0; t0 < T; t0 += WKV_TC) {
+    for (int t0 = 0; t0 < T; t0 += WKV6_TC) {
         store_chunk();
         __syncthreads();
-        if (t0 + WKV_TC < T) load_chunk(t0 + WKV_TC);  // in flight during this chunk
-        const int n = min(WKV_TC, T - t0);
+        if (t0 + WKV6_TC < T) load_chunk(t0 + WKV6_TC);  // in flight during this chunk
+        const int n = min(WKV6_TC, T - t0);
         // Tokens in groups of TG: the state updates run token after token, then the TG output
         // chains (independent of each other) are interleaved step by step.
         constexpr int TG = 4;

@@ -1177,11 +1177,16 @@ bool Engine::run_tokens(const uint32_t * tokens, size_t T, bool want_logits) {
         const size_t n = std::min(T - done, kChunkMax);
         const bool last = done + n == T;
         if (!ensure_workspace((int)n)) return false;
-        // the pinned token buffer may still feed the previous (async) call's copy
-        HIP_OK(hipEventSynchronize(tok_event_));
-        memcpy(htokens_, tokens + done, n * 4);
-        HIP_OK(hipMemcpyAsync(dtokens_, htokens_, n * 4, hipMemcpyHostToDevice, stream_));
-        HIP_OK(hipEventRecord(tok_event_, stream_));
+        if (n == 1) {
+            // one token: a CP write packet in stream order (no blit kernel, no pinned buffer)
+            HIP_OK(hipStreamWriteValue32(stream_, dtokens_, tokens[done], 0));
+        } else {
+            // the pinned token buffer may still feed the previous (async) call's copy
+            HIP_OK(hipEventSynchronize(tok_event_));
+            memcpy(htokens_, tokens + done, n * 4);
+            HIP_OK(hipMemcpyAsync(dtokens_, htokens_, n * 4, hipMemcpyHostToDevice, stream_));
+            HIP_OK(hipEventRecord(tok_event_, stream_));
+        }
         const bool lg = last && want_logits;
         if (timing_) {
             // eager launches bracketed by events; the delay kernel holds the GPU while the host

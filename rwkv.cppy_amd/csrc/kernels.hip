@@ -244,17 +244,24 @@ bool launch_embed_ln(hipStream_t st, const uint32_t * tokens, int T, const DMat 
     return true;
 }
 
+// Token-row kernels that emit Q8 activations into sequence-GEMM token tiles run TOKS_PER_WG
+// consecutive tokens per workgroup (one 256-thread group each): a tile record's 64-byte sectors
+// hold 16-byte pieces of 4 consecutive tokens, so the four partial writes of a sector meet in one
+// XCD's L2 instead of leaving four L2s as four partial-line write-backs.
+constexpr int TOKS_PER_WG = 4;
+
 // rwkv_carry_x (rwkv_graph.inc:56-82) + the token-shift mixes of each version.
-__global__ __launch_bounds__(256) void k_ln_mix(LnMixArgs a) {
+__global__ __launch_bounds__(1024) void k_ln_mix(LnMixArgs a) {
     __shared__ double sh[8];
-    const int t = blockIdx.x, C = a.C;
+    const int t = blockIdx.x * TOKS_PER_WG + (threadIdx.x >> 8), C = a.C, tid = threadIdx.x & 255;
+    if (t >= a.T) return;  // whole 256-thread token groups
     const float * xt = a.x + (size_t)t * C;
     float mean, scale, pmean = 0.0f, pscale = 0.0f;
     ln_stats(xt, C, 1e-5f, mean, scale, sh);
     if (t > 0) ln_stats(xt - C, C, 1e-5f, pmean, pscale, sh);
-    for (int c0 = 0; c0 < C; c0 += blockDim.x) {
-        const int c = c0 + threadIdx.x;
-        if (c0 + (int)(threadIdx.x & ~63) >= C) continue;  // whole wave out of range (C % 64 == 0)
+    for (int c0 = 0; c0 < C; c0 += 256) {
+        const int c = c0 + tid;
+        if (c0 + (tid & ~63) >= C) continue;  // whole wave out of range (C % 64 == 0)
         const float xa = ln_apply(xt[c], mean, scale, a.lnw[c], a.lnb[c]);
         const float xp = (t > 0) ? ln_apply(xt[c - C], pmean, pscale, a.lnw[c], a.lnb[c]) : a.carry_in[c];
         if (t == a.T - 1 && a.carry_out) a.carry_out[c] = xa;
@@ -274,7 +281,7 @@ __global__ __launch_bounds__(256) void k_ln_mix(LnMixArgs a) {
 }
 
 bool launch_ln_mix(hipStream_t st, const LnMixArgs & a) {
-    hipLaunchKernelGGL(k_ln_mix, dim3(a.T), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_ln_mix, dim3((a.T + TOKS_PER_WG - 1) / TOKS_PER_WG), dim3(256 * TOKS_PER_WG), 0, st, a);
     HIP_OK(hipGetLastError());
     return true;
 }
@@ -868,13 +875,14 @@ bool launch_wkv7(hipStream_t st, int T, int H, int S, const float * r, const flo
 }
 
 // --------------------------------------------------------------------------- GroupNorm
-__global__ __launch_bounds__(256) void k_groupnorm(int T, int H, int S, float eps, const float * y, const float * w,
-                                                   const float * b, int mode, const float * g, const float * v,
-                                                   const float * bonus, ActBuf out) {
-    const int t = blockIdx.x, C = H * S;
-    for (int c0 = 0; c0 < C; c0 += blockDim.x) {
-        const int c = c0 + threadIdx.x;
-        if (c0 + (int)(threadIdx.x & ~63) >= C) continue;
+__global__ __launch_bounds__(1024) void k_groupnorm(int T, int H, int S, float eps, const float * y, const float * w,
+                                                    const float * b, int mode, const float * g, const float * v,
+                                                    const float * bonus, ActBuf out) {
+    const int t = blockIdx.x * TOKS_PER_WG + (threadIdx.x >> 8), C = H * S, tid = threadIdx.x & 255;
+    if (t >= T) return;
+    for (int c0 = 0; c0 < C; c0 += 256) {
+        const int c = c0 + tid;
+        if (c0 + (tid & ~63) >= C) continue;
         const size_t i = (size_t)t * C + c;
         const float x = y[i];
         const double s = group_sum((double)x, S);
@@ -899,7 +907,8 @@ bool launch_groupnorm(hipStream_t st, int T, int H, int S, float eps, const floa
         fprintf(stderr, "rwkv: head size %d unsupported by groupnorm\n", S);
         return false;
     }
-    hipLaunchKernelGGL(k_groupnorm, dim3(T), dim3(256), 0, st, T, H, S, eps, y, w, b, mode, g, v, bonus, out);
+    hipLaunchKernelGGL(k_groupnorm, dim3((T + TOKS_PER_WG - 1) / TOKS_PER_WG), dim3(256 * TOKS_PER_WG), 0, st, T, H, S, eps, y, w,
+                       b, mode, g, v, bonus, out);
     HIP_OK(hipGetLastError());
     return true;
 }
@@ -920,18 +929,18 @@ bool launch_fill(hipStream_t st, float * p, size_t n, float value) {
 
 namespace rwkvmi {
 
-__global__ __launch_bounds__(256) void k_act_from_f32(const float * x, int K, ActBuf out) {
-    const int t = blockIdx.x;
-    for (int k0 = 0; k0 < K; k0 += blockDim.x) {
-        const int k = k0 + threadIdx.x;
-        if (k0 + (int)(threadIdx.x & ~31) >= K) continue;  // half-wave uniform (K % 32 == 0)
+__global__ __launch_bounds__(1024) void k_act_from_f32(const float * x, int T, int K, ActBuf out) {
+    const int t = blockIdx.x * TOKS_PER_WG + (threadIdx.x >> 8), tid = threadIdx.x & 255;
+    if (t >= T) return;
+    for (int k0 = 0; k0 < K; k0 += 256) {
+        const int k = k0 + tid;
+        if (k0 + (tid & ~31) >= K) continue;  // half-wave uniform (K % 32 == 0)
         emit32(out, t, k, x[(size_t)t * K + k]);
     }
 }
-
 bool launch_act_from_f32(hipStream_t st, const float * x, int T, int K, const ActBuf & out) {
     if (K % 32) return false;
-    hipLaunchKernelGGL(k_act_from_f32, dim3(T), dim3(256), 0, st, x, K, out);
+    hipLaunchKernelGGL(k_act_from_f32, dim3((T + TOKS_PER_WG - 1) / TOKS_PER_WG), dim3(256 * TOKS_PER_WG), 0, st, x, T, K, out);
     HIP_OK(hipGetLastError());
     return true;
 }

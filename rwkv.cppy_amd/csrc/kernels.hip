@@ -320,7 +320,10 @@ struct Mix5Args {
 // side by side.
 constexpr int MIX_TT = 16;
 
-template <int DM>
+// TQ > 0: all five outputs are Q8 sequence-GEMM token tiles (TQ = 2: Q8_1); each lane's record
+// address is formed once (a workgroup's MIX_TT tokens lie in one QG_TOK-token tile) and the
+// per-output emission is quant32 + store (store32's tiled values), no runtime format dispatch.
+template <int DM, int TQ>
 __global__ __launch_bounds__(256) void k_v6_mix5(Mix5Args a) {
     __shared__ __attribute__((aligned(16))) float sl[MIX_TT][5 * DM];
     const int C = a.C, D = a.D, T = a.T;
@@ -342,6 +345,15 @@ __global__ __launch_bounds__(256) void k_v6_mix5(Mix5Args a) {
             w2v[n][i] = i < D ? t : 0.0f;
         }
     }
+    uint8_t * rec[5];
+    int qoff = 0;
+    if constexpr (TQ > 0) {
+        // record of (token tile t0 / QG_TOK, block c / 32); byte of element c in half (c >> 4) & 1
+        const size_t ri = (size_t)(t0 / QG_TOK) * (C >> 5) + (cc >> 5);
+#pragma unroll
+        for (int n = 0; n < 5; n++) rec[n] = a.out[n].tq + ri * qg_a_bytes(TQ == 2);
+        qoff = ((cc >> 4) & 1) * QG_TOK * 16 + (cc & 15);
+    }
     __syncthreads();
     // two tokens at a time: ten independent fp64 chains side by side
     for (int tt = 0; tt < nt; tt += 2) {
@@ -359,7 +371,32 @@ __global__ __launch_bounds__(256) void k_v6_mix5(Mix5Args a) {
                 }
             }
         }
-        if (cval) {
+        if constexpr (TQ > 0) {
+            if (cval) {
+                Q32 q0[5], q1[5];
+#pragma unroll
+                for (int n = 0; n < 5; n++) {
+                    q0[n] = quant32(((float)acc0[n] + mu[n]) * sx0 + xa0);
+                    q1[n] = quant32(((float)acc1[n] + mu[n]) * sx1 + xa1);
+                }
+                const int tl0 = (t0 + tt) % QG_TOK, tl1 = (t0 + t1) % QG_TOK;
+#pragma unroll
+                for (int n = 0; n < 5; n++) {
+                    rec[n][qoff + tl0 * 16] = (uint8_t)(int8_t)q0[n].q;
+                    if (tt + 1 < nt) rec[n][qoff + tl1 * 16] = (uint8_t)(int8_t)q1[n].q;
+                    if ((c & 31) == 0) {
+                        float * dp = (float *)(rec[n] + QG_A_D);
+                        dp[tl0] = f16_round(q0[n].d);
+                        if (tt + 1 < nt) dp[tl1] = f16_round(q1[n].d);
+                        if constexpr (TQ == 2) {
+                            float * sp = (float *)(rec[n] + QG_A_S);
+                            sp[tl0] = f16_round(q0[n].d * (float)q0[n].sum);
+                            if (tt + 1 < nt) sp[tl1] = f16_round(q1[n].d * (float)q1[n].sum);
+                        }
+                    }
+                }
+            }
+        } else if (cval) {
 #pragma unroll
             for (int n = 0; n < 5; n++) emit32(a.out[n], t0 + tt, c, ((float)acc0[n] + mu[n]) * sx0 + xa0);
             if (tt + 1 < nt) {
@@ -389,8 +426,25 @@ bool launch_v6_mix5(hipStream_t st, int T, int C, int D, const float * lora, con
         return false;
     }
     const dim3 grid((C + 255) / 256, (T + MIX_TT - 1) / MIX_TT);
-    if (D <= 32) hipLaunchKernelGGL(k_v6_mix5<32>, grid, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL(k_v6_mix5<64>, grid, dim3(256), 0, st, a);
+    int tq = 0;
+    if (QG_TOK % MIX_TT == 0) {
+        bool all = true;
+        for (int n = 0; n < 5; n++)
+            all = all && outs[n].tiled && outs[n].fmt == outs[0].fmt && outs[n].K == C &&
+                  (outs[n].fmt == A_Q8_0 || outs[n].fmt == A_Q8_1);
+        if (all) tq = outs[0].fmt == A_Q8_1 ? 2 : 1;
+    }
+#define MIX5_L(DMv, TQv) hipLaunchKernelGGL((k_v6_mix5<DMv, TQv>), grid, dim3(256), 0, st, a)
+    if (D <= 32) {
+        if (tq == 1) MIX5_L(32, 1);
+        else if (tq == 2) MIX5_L(32, 2);
+        else MIX5_L(32, 0);
+    } else {
+        if (tq == 1) MIX5_L(64, 1);
+        else if (tq == 2) MIX5_L(64, 2);
+        else MIX5_L(64, 0);
+    }
+#undef MIX5_L
     HIP_OK(hipGetLastError());
     return true;
 }

@@ -250,7 +250,32 @@ bool launch_embed_ln(hipStream_t st, const uint32_t * tokens, int T, const DMat 
 // XCD's L2 instead of leaving four L2s as four partial-line write-backs.
 constexpr int TOKS_PER_WG = 4;
 
+// emit32 for an output known at compile time to be Q8 sequence-GEMM token tiles (TQ 1: Q8_0,
+// 2: Q8_1) of row length K: store32's tiled values, no runtime format dispatch
+template <int TQ>
+__device__ __forceinline__ void emit32_tile(uint8_t * tq, int K, int t, int k, float v) {
+    const Q32 r = quant32(v);
+    uint8_t * rec = tq + ((size_t)(t / QG_TOK) * (K >> 5) + (k >> 5)) * qg_a_bytes(TQ == 2);
+    const int tl = t % QG_TOK;
+    rec[((k >> 4) & 1) * QG_TOK * 16 + tl * 16 + (k & 15)] = (uint8_t)(int8_t)r.q;
+    if ((k & 31) == 0) {
+        ((float *)(rec + QG_A_D))[tl] = f16_round(r.d);
+        if constexpr (TQ == 2) ((float *)(rec + QG_A_S))[tl] = f16_round(r.d * (float)r.sum);
+    }
+}
+
+// TQ of a set of outputs: 1 / 2 when all are Q8_0 / Q8_1 token tiles of row length K, else 0
+static int tile_q(const ActBuf * outs, int n, int K) {
+    if (n < 1) return 0;
+    for (int i = 0; i < n; i++)
+        if (!outs[i].tiled || outs[i].fmt != outs[0].fmt || outs[i].K != K ||
+            (outs[i].fmt != A_Q8_0 && outs[i].fmt != A_Q8_1))
+            return 0;
+    return outs[0].fmt == A_Q8_1 ? 2 : 1;
+}
+
 // rwkv_carry_x (rwkv_graph.inc:56-82) + the token-shift mixes of each version.
+template <int TQ>
 __global__ __launch_bounds__(1024) void k_ln_mix(LnMixArgs a) {
     __shared__ double sh[8];
     const int t = blockIdx.x * TOKS_PER_WG + (threadIdx.x >> 8), C = a.C, tid = threadIdx.x & 255;
@@ -275,13 +300,18 @@ __global__ __launch_bounds__(1024) void k_ln_mix(LnMixArgs a) {
             } else {
                 v = (xp - xa) * mu + xa;
             }
-            emit32(a.out[n], t, c, v);
+            if constexpr (TQ > 0) emit32_tile<TQ>(a.out[n].tq, C, t, c, v);
+            else emit32(a.out[n], t, c, v);
         }
     }
 }
 
 bool launch_ln_mix(hipStream_t st, const LnMixArgs & a) {
-    hipLaunchKernelGGL(k_ln_mix, dim3((a.T + TOKS_PER_WG - 1) / TOKS_PER_WG), dim3(256 * TOKS_PER_WG), 0, st, a);
+    const dim3 grid((a.T + TOKS_PER_WG - 1) / TOKS_PER_WG), block(256 * TOKS_PER_WG);
+    const int tq = tile_q(a.out, a.n_out, a.C);
+    if (tq == 1) hipLaunchKernelGGL(k_ln_mix<1>, grid, block, 0, st, a);
+    else if (tq == 2) hipLaunchKernelGGL(k_ln_mix<2>, grid, block, 0, st, a);
+    else hipLaunchKernelGGL(k_ln_mix<0>, grid, block, 0, st, a);
     HIP_OK(hipGetLastError());
     return true;
 }
@@ -929,6 +959,7 @@ bool launch_wkv7(hipStream_t st, int T, int H, int S, const float * r, const flo
 }
 
 // --------------------------------------------------------------------------- GroupNorm
+template <int TQ>
 __global__ __launch_bounds__(1024) void k_groupnorm(int T, int H, int S, float eps, const float * y, const float * w,
                                                     const float * b, int mode, const float * g, const float * v,
                                                     const float * bonus, ActBuf out) {
@@ -950,7 +981,8 @@ __global__ __launch_bounds__(1024) void k_groupnorm(int T, int H, int S, float e
         o = o + b[c];
         if (mode == 2) o = o + v[i] * bonus[(size_t)t * H + c / S];
         if (mode >= 1) o = o * g[i];
-        emit32(out, t, c, o);
+        if constexpr (TQ > 0) emit32_tile<TQ>(out.tq, C, t, c, o);
+        else emit32(out, t, c, o);
     }
 }
 
@@ -961,8 +993,11 @@ bool launch_groupnorm(hipStream_t st, int T, int H, int S, float eps, const floa
         fprintf(stderr, "rwkv: head size %d unsupported by groupnorm\n", S);
         return false;
     }
-    hipLaunchKernelGGL(k_groupnorm, dim3((T + TOKS_PER_WG - 1) / TOKS_PER_WG), dim3(256 * TOKS_PER_WG), 0, st, T, H, S, eps, y, w,
-                       b, mode, g, v, bonus, out);
+    const dim3 grid((T + TOKS_PER_WG - 1) / TOKS_PER_WG), block(256 * TOKS_PER_WG);
+    const int tq = tile_q(&out, 1, H * S);
+    if (tq == 1) hipLaunchKernelGGL(k_groupnorm<1>, grid, block, 0, st, T, H, S, eps, y, w, b, mode, g, v, bonus, out);
+    else if (tq == 2) hipLaunchKernelGGL(k_groupnorm<2>, grid, block, 0, st, T, H, S, eps, y, w, b, mode, g, v, bonus, out);
+    else hipLaunchKernelGGL(k_groupnorm<0>, grid, block, 0, st, T, H, S, eps, y, w, b, mode, g, v, bonus, out);
     HIP_OK(hipGetLastError());
     return true;
 }
@@ -983,18 +1018,24 @@ bool launch_fill(hipStream_t st, float * p, size_t n, float value) {
 
 namespace rwkvmi {
 
+template <int TQ>
 __global__ __launch_bounds__(1024) void k_act_from_f32(const float * x, int T, int K, ActBuf out) {
     const int t = blockIdx.x * TOKS_PER_WG + (threadIdx.x >> 8), tid = threadIdx.x & 255;
     if (t >= T) return;
     for (int k0 = 0; k0 < K; k0 += 256) {
         const int k = k0 + tid;
         if (k0 + (tid & ~31) >= K) continue;  // half-wave uniform (K % 32 == 0)
-        emit32(out, t, k, x[(size_t)t * K + k]);
+        if constexpr (TQ > 0) emit32_tile<TQ>(out.tq, K, t, k, x[(size_t)t * K + k]);
+        else emit32(out, t, k, x[(size_t)t * K + k]);
     }
 }
 bool launch_act_from_f32(hipStream_t st, const float * x, int T, int K, const ActBuf & out) {
     if (K % 32) return false;
-    hipLaunchKernelGGL(k_act_from_f32, dim3((T + TOKS_PER_WG - 1) / TOKS_PER_WG), dim3(256 * TOKS_PER_WG), 0, st, x, T, K, out);
+    const dim3 grid((T + TOKS_PER_WG - 1) / TOKS_PER_WG), block(256 * TOKS_PER_WG);
+    const int tq = tile_q(&out, 1, K);
+    if (tq == 1) hipLaunchKernelGGL(k_act_from_f32<1>, grid, block, 0, st, x, T, K, out);
+    else if (tq == 2) hipLaunchKernelGGL(k_act_from_f32<2>, grid, block, 0, st, x, T, K, out);
+    else hipLaunchKernelGGL(k_act_from_f32<0>, grid, block, 0, st, x, T, K, out);
     HIP_OK(hipGetLastError());
     return true;
 }

@@ -613,7 +613,7 @@ __global__ __launch_bounds__(64 * NWV) void k_wkv6_s64(int T, int H, const float
     constexpr int S = 64;
     constexpr int CW = 4 * NWV, NT = 64 * NWV, QQ = WKV6_TC * 16 / NT;
     __shared__ __attribute__((aligned(16))) float sk[WKV6_TC][S], sr[WKV6_TC][S], sw[WPT ? WKV6_TC : 1][S],
-        sv[WKV6_TC][CW];
+        sv[WKV6_TC][CW], sy[WKV6_TC][CW];
     const int h = blockIdx.x, jb = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int q = lane & 3, jl = (lane >> 2) & 3, g = lane >> 4;
     const int jc = 4 * wv + jl, j = jb * CW + jc, i0 = g * 16 + 4 * q;
@@ -708,10 +708,11 @@ __global__ __launch_bounds__(64 * NWV) void k_wkv6_s64(int T, int H, const float
             for (int e = 0; e < TG; e++) acc[e] = quad_add_x1(acc[e]);
 #pragma unroll
             for (int e = 0; e < TG; e++) acc[e] = quad_add_x2(acc[e]);
+            // every lane of the column holds the same sum: all write it to the chunk's y tile
 #pragma unroll
             for (int e = 0; e < TG; e++) {
                 acc[e] = fold_g4(acc[e]);
-                if (g == 0 && q == 0 && tt0 + e < n) y[(size_t)(t0 + tt0 + e) * C + h * S + j] = acc[e];
+                if (tt0 + e < n) sy[tt0 + e][jc] = acc[e];
             }
         };
         // two operand sets in turn: the next group's LDS reads overlap this group's arithmetic
@@ -728,6 +729,13 @@ __global__ __launch_bounds__(64 * NWV) void k_wkv6_s64(int T, int H, const float
             group(B, tt + TG);
         }
         __syncthreads();
+        // the chunk's y tile [n tokens][CW columns], one float4 per thread
+        {
+            const int tk = tid / NWV;
+            if (tk < n)
+                *(float4 *)(y + (size_t)(t0 + tk) * C + (size_t)h * S + jb * CW + 4 * (tid % NWV)) =
+                    *(const float4 *)&sy[tk][4 * (tid % NWV)];
+        }
     }
 #pragma unroll
     for (int p = 0; p < 2; p++) {

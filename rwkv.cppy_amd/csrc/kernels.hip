@@ -5,6 +5,8 @@
 // where the reference rounds; fused multiply-adds appear only where ggml's x86 kernels use
 // them (the quantized block accumulation).
 #include "kernels.hpp"
+
+#include <type_traits>
 #include "device_common.hpp"
 
 #include <stdio.h>
@@ -605,6 +607,7 @@ __device__ __forceinline__ float chain4(float acc, const f2_t (&x)[2]) {
 
 // wkv6 chunk: 64 tokens, so the next chunk's loads have a whole chunk of compute to land in
 constexpr int WKV6_TC = 64;
+constexpr int WKV6_PAD = 8;  // >= 2 * the token group
 
 template <bool WPT, int NWV>
 __global__ __launch_bounds__(64 * NWV) void k_wkv6_s64(int T, int H, const float * k, const float * v, const float * r,
@@ -612,8 +615,11 @@ __global__ __launch_bounds__(64 * NWV) void k_wkv6_s64(int T, int H, const float
                                                        float * y) {
     constexpr int S = 64;
     constexpr int CW = 4 * NWV, NT = 64 * NWV, QQ = WKV6_TC * 16 / NT;
-    __shared__ __attribute__((aligned(16))) float sk[WKV6_TC][S], sr[WKV6_TC][S], sw[WPT ? WKV6_TC : 1][S],
-        sv[WKV6_TC][CW], sy[WKV6_TC][CW];
+    // WKV6_PAD rows past the chunk: a full chunk's look-ahead reads need no clamp (their tokens
+    // are never used)
+    constexpr int RW = WKV6_TC + WKV6_PAD;
+    __shared__ __attribute__((aligned(16))) float sk[RW][S], sr[RW][S], sw[WPT ? RW : 1][S], sv[RW][CW],
+        sy[WKV6_TC][CW];
     const int h = blockIdx.x, jb = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int q = lane & 3, jl = (lane >> 2) & 3, g = lane >> 4;
     const int jc = 4 * wv + jl, j = jb * CW + jc, i0 = g * 16 + 4 * q;
@@ -678,11 +684,14 @@ __global__ __launch_bounds__(64 * NWV) void k_wkv6_s64(int T, int H, const float
         // Tokens in groups of TG: the state updates run token after token, then the TG output
         // chains (independent of each other) are interleaved step by step.
         constexpr int TG = 4;
-        auto group = [&](const Tok (&o)[TG], int tt0) {
+        static_assert(2 * TG <= WKV6_PAD, "look-ahead rows");
+        // FULL: a whole chunk (n == WKV6_TC), every token valid
+        auto group = [&](const Tok (&o)[TG], int tt0, auto full) {
+            constexpr bool FULL = decltype(full)::value;
             f2_t x[TG][2];
 #pragma unroll
             for (int e = 0; e < TG; e++) {
-                const bool val = tt0 + e < n;
+                const bool val = FULL || tt0 + e < n;
                 const f2_t vj = f2_t{o[e].v, o[e].v};
                 f2_t kv[2];
 #pragma unroll
@@ -712,21 +721,36 @@ __global__ __launch_bounds__(64 * NWV) void k_wkv6_s64(int T, int H, const float
 #pragma unroll
             for (int e = 0; e < TG; e++) {
                 acc[e] = fold_g4(acc[e]);
-                if (tt0 + e < n) sy[tt0 + e][jc] = acc[e];
+                if (FULL || tt0 + e < n) sy[tt0 + e][jc] = acc[e];
             }
         };
         // two operand sets in turn: the next group's LDS reads overlap this group's arithmetic
         Tok A[TG], B[TG];
+        if (n == WKV6_TC) {
+            const std::integral_constant<bool, true> full;
 #pragma unroll
-        for (int e = 0; e < TG; e++) read_tok(A[e], min(e, n - 1));
-        for (int tt = 0; tt < n; tt += 2 * TG) {
+            for (int e = 0; e < TG; e++) read_tok(A[e], e);
+            for (int tt = 0; tt < WKV6_TC; tt += 2 * TG) {
 #pragma unroll
-            for (int e = 0; e < TG; e++) read_tok(B[e], min(tt + TG + e, n - 1));
-            group(A, tt);
-            if (tt + TG >= n) break;
+                for (int e = 0; e < TG; e++) read_tok(B[e], tt + TG + e);
+                group(A, tt, full);
 #pragma unroll
-            for (int e = 0; e < TG; e++) read_tok(A[e], min(tt + 2 * TG + e, n - 1));
-            group(B, tt + TG);
+                for (int e = 0; e < TG; e++) read_tok(A[e], tt + 2 * TG + e);
+                group(B, tt + TG, full);
+            }
+        } else {
+            const std::integral_constant<bool, false> part;
+#pragma unroll
+            for (int e = 0; e < TG; e++) read_tok(A[e], min(e, n - 1));
+            for (int tt = 0; tt < n; tt += 2 * TG) {
+#pragma unroll
+                for (int e = 0; e < TG; e++) read_tok(B[e], min(tt + TG + e, n - 1));
+                group(A, tt, part);
+                if (tt + TG >= n) break;
+#pragma unroll
+                for (int e = 0; e < TG; e++) read_tok(A[e], min(tt + 2 * TG + e, n - 1));
+                group(B, tt + TG, part);
+            }
         }
         __syncthreads();
         // the chunk's y tile [n tokens][CW columns], one float4 per thread

@@ -723,14 +723,23 @@ bool Engine::layer_v6(int l, int T, const float * si, float * so) {
     ActBuf outs[5] = {A(1, L.decay_w1), A(2, L.att_k), A(3, L.att_v), A(4, L.att_r), A(5, L.att_g)};
     if (!launch_v6_mix5(stream_, T, C, D, lora_, L.maa_w2t, L.maa, xa_, sx_, outs)) return false;
     ActBuf dl = A(6, L.decay_w2);
+    // decay tail by threads (k_att6_dec's rows) when Wd2 is quantized; dl fp32 then reuses lora_
+    // (consumed by mix5 above)
+    const int DD = L.decay_w2.K;  // decay LoRA width (64 for the released checkpoints)
+    const bool dseq = v6_decay_seq_supported(L.decay_w2.type, DD) && L.decay_w1.M == DD;
     b.add(L.att_r, outs[3], r_, C, EPI_STORE);
     b.add(L.att_k, outs[1], k_, C, EPI_STORE);
     b.add(L.att_v, outs[2], v_, C, EPI_STORE);
     b.add(L.att_g, outs[4], g_, C, EPI_SILU);
-    b.add(L.decay_w1, outs[0], nullptr, 0, EPI_TANH, nullptr, nullptr, &dl);
+    if (dseq) b.add(L.decay_w1, outs[0], lora_, DD, EPI_TANH);
+    else b.add(L.decay_w1, outs[0], nullptr, 0, EPI_TANH, nullptr, nullptr, &dl);
     if (!b.run(*this, T)) return false;
-    b.add(L.decay_w2, dl, w_, C, EPI_DECAY6, nullptr, L.decay6);
-    if (!b.run(*this, T)) return false;
+    if (dseq) {
+        if (!launch_v6_decay_seq(stream_, T, C, L.decay_w2, lora_, L.decay6, w_)) return false;
+    } else {
+        b.add(L.decay_w2, dl, w_, C, EPI_DECAY6, nullptr, L.decay6);
+        if (!b.run(*this, T)) return false;
+    }
     if (!launch_wkv6(stream_, T, H, S, k_, v_, r_, L.att_u, w_, 1, si + 2 * C, so + 2 * C, y_)) return false;
     ActBuf o = A(7, L.att_o);
     if (!launch_groupnorm(stream_, T, H, S, 64e-5f, y_, L.att_lnx_w, L.att_lnx_b, 1, g_, nullptr, nullptr, o)) return false;

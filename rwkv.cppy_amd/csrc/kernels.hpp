@@ -171,6 +171,12 @@ struct Att6Dec {
 };
 bool launch_att6_dec(hipStream_t st, const Att6Dec & a);
 
+// Sequence v6 decay LoRA tail (T >= 2): w[t][c] = exp(-exp(Wd2[c] . Q8(dl[t]) + decay[c])) with
+// k_att6_dec's per-row arithmetic; dl fp32 [T][D].  Quantized Wd2 with D <= 512 only.
+bool v6_decay_seq_supported(int wd2_type, int D);
+bool launch_v6_decay_seq(hipStream_t st, int T, int C, const DMat & wd2, const float * dl, const float * decay,
+                         float * w);
+
 // v7 attention core for one token, one workgroup per head: kk/k/a prep, wkv7, GroupNorm,
 // + v*sum(k*r*r_k), *g.  Writes fp32 y [C].
 struct Att7Dec {

@@ -193,7 +193,7 @@ __device__ __forceinline__ float tree_wave32(const float (&p)[32]) {
 // One row of the v6 decay LoRA tail by one thread: lanes 0..nl-1 of k_mm's row (nl <= NL <= 32,
 // one unit each); the first PF units were prefetched into wp[].  Partials of lanes >= NL are
 // compile-time zeros, so the tree folds to the nonzero part.
-template <int WF, int PF, int NL>
+template <int WF, int PF, int NL, bool NT = true>
 __device__ __forceinline__ float decay_row_thread(const DMat & W, int row, const ActBuf & act, int nl,
                                                   const WBlk (&wp)[PF > 0 ? PF : 1]) {
     float p[32], p2[32];
@@ -201,7 +201,7 @@ __device__ __forceinline__ float decay_row_thread(const DMat & W, int row, const
     for (int l = 0; l < 32; l++) {
         p[l] = p2[l] = 0.0f;
         if (l < NL && l < nl) {
-            const WBlk w = (l < PF) ? wp[l < PF ? l : 0] : load_unit<WF>(W, row, 0, l);
+            const WBlk w = (l < PF) ? wp[l < PF ? l : 0] : load_unit<WF, NT>(W, row, 0, l);
             const AUnit x = load_act_unit<WF, true>(act, 0, l);
             dot_unit<WF>(w, x, p[l], p2[l]);
         }
@@ -403,6 +403,64 @@ bool launch_att6_dec(hipStream_t st, const Att6Dec & a) {
             case W_Q5_1: hipLaunchKernelGGL((k_att6_dec<W_Q5_1, 4>), grid, block, lds, st, a); break;
             default: hipLaunchKernelGGL((k_att6_dec<W_Q8_0, 4>), grid, block, lds, st, a); break;
         }
+    }
+    HIP_OK(hipGetLastError());
+    return true;
+}
+
+// Sequence path, v6 decay LoRA tail: w[t][c] = exp(-exp(Wd2[c] . Q8(dl[t]) + decay[c])), one thread
+// per channel over DECAY_TT tokens with decay_row_thread -- k_att6_dec's arithmetic, so decode and
+// sequence agree bit for bit.  Replaces the f32->Q8 conversion + K = D GEMM launch pair (a 2-block
+// GEMM is all fixed cost on the MFMA path).  Workgroup = DECAY_TT tokens x 256 channels: the
+// tokens' Q8 images sit in LDS, the thread's Wd2 row units stay in registers across the tokens.
+constexpr int DECAY_TT = 16;
+
+template <int WF>
+__global__ __launch_bounds__(256) void k_v6_decay_seq(int T, int C, DMat wd2, const float * dl, const float * decay,
+                                                      float * w) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int t0 = blockIdx.x * DECAY_TT, D = wd2.K, tid = threadIdx.x, nb = D >> 5;
+    const int fmt = act_fmt_for(WF), abytes = (lds_bytes_for(fmt, D) + 15) & ~15;
+    const int row = min((int)blockIdx.y * 256 + tid, C - 1);
+    WBlk wp[4];
+#pragma unroll
+    for (int l = 0; l < 4; l++) wp[l] = load_wblk<WF>(wd2, (size_t)row * nb + min(l, nb - 1));  // re-read: cached
+    const float dec = decay[row];
+    // D % 32 == 0, so every 32 consecutive e are one quantization block of one token
+    for (int e = tid; e < DECAY_TT * D; e += 256) {
+        const int tt = e / D, k = e % D;
+        const ActBuf act = lds_act(smem + tt * abytes, fmt, D);
+        emit32(act, 0, k, dl[(size_t)min(t0 + tt, T - 1) * D + k]);
+    }
+    __syncthreads();
+    if ((int)blockIdx.y * 256 + tid >= C) return;
+    const int nt = min(DECAY_TT, T - t0);
+    for (int tt = 0; tt < nt; tt++) {
+        const ActBuf act = lds_act(smem + tt * abytes, fmt, D);
+        const float s = decay_row_thread<WF, 4, 4>(wd2, row, act, nb, wp);
+        w[(size_t)(t0 + tt) * C + row] = expf(-expf(s + dec));
+    }
+}
+
+bool v6_decay_seq_supported(int wd2_type, int D) {
+    return wd2_type >= W_Q4_0 && D % 32 == 0 && D >= 32 && D <= 128;
+}
+
+bool launch_v6_decay_seq(hipStream_t st, int T, int C, const DMat & wd2, const float * dl, const float * decay,
+                         float * w) {
+    if (!v6_decay_seq_supported(wd2.type, wd2.K) || wd2.M != C) {
+        fprintf(stderr, "rwkv: v6 decay tail: unsupported shape (%d x %d, type %d)\n", (int)wd2.M, (int)wd2.K,
+                (int)wd2.type);
+        return false;
+    }
+    const dim3 grid((T + DECAY_TT - 1) / DECAY_TT, (C + 255) / 256);
+    const int lds = DECAY_TT * ((lds_bytes_for(act_fmt_for(wd2.type), wd2.K) + 15) & ~15);
+    switch (wd2.type) {
+        case W_Q4_0: hipLaunchKernelGGL(k_v6_decay_seq<W_Q4_0>, grid, dim3(256), lds, st, T, C, wd2, dl, decay, w); break;
+        case W_Q4_1: hipLaunchKernelGGL(k_v6_decay_seq<W_Q4_1>, grid, dim3(256), lds, st, T, C, wd2, dl, decay, w); break;
+        case W_Q5_0: hipLaunchKernelGGL(k_v6_decay_seq<W_Q5_0>, grid, dim3(256), lds, st, T, C, wd2, dl, decay, w); break;
+        case W_Q5_1: hipLaunchKernelGGL(k_v6_decay_seq<W_Q5_1>, grid, dim3(256), lds, st, T, C, wd2, dl, decay, w); break;
+        default: hipLaunchKernelGGL(k_v6_decay_seq<W_Q8_0>, grid, dim3(256), lds, st, T, C, wd2, dl, decay, w); break;
     }
     HIP_OK(hipGetLastError());
     return true;

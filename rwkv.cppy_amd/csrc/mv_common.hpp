@@ -51,7 +51,7 @@ __device__ __forceinline__ ActBuf lds_act(char * smem, int fmt, int K) {
     return a;
 }
 
-inline int lds_bytes_for(int fmt, int K) {
+__host__ __device__ inline int lds_bytes_for(int fmt, int K) {
     if (fmt == A_F32) return K * 4;
     if (fmt == A_F16) return K * 2;
     const int nb = K / 32;

@@ -118,6 +118,8 @@ struct MMGroup {
     MMEntry e[MM_MAX_ENTRIES];
     int n;
     int T;
+    float * part;        // split-K partials (qgemm.hip, single small-M entries): QG_SPLIT x T x M floats
+    size_t part_floats;
 };
 
 #define HIP_OK(x)                                                                             \

@@ -300,6 +300,7 @@ Engine::~Engine() {
     if (stream_) (void)hipStreamSynchronize(stream_);
     drop_graphs();
     if (gy_) (void)hipFree(gy_);
+    if (part_) (void)hipFree(part_);
     for (void * p : ws_allocs_) (void)hipFree(p);
     if (htokens_) (void)hipHostFree(htokens_);
     collect_timing();
@@ -496,6 +497,19 @@ bool Engine::mm_dispatch(MMGroup & g, int wtype) {
         gy_ = nullptr;
         HIP_OK(hipMalloc(&gy_, need * 4 + 64));
         gy_cap_ = need;
+    }
+    // split-K partials for a single small-M entry (launch_qgemm decides)
+    if (g.n == 1 && g.e[0].W.M <= 256) {
+        const size_t pneed = (size_t)8 * g.T * g.e[0].W.M;
+        if (pneed > part_cap_) {
+            HIP_OK(hipStreamSynchronize(stream_));
+            if (part_) (void)hipFree(part_);
+            part_ = nullptr;
+            HIP_OK(hipMalloc(&part_, pneed * 4 + 64));
+            part_cap_ = pneed;
+        }
+        g.part = part_;
+        g.part_floats = part_cap_;
     }
     size_t off = 0;
     for (int i = 0; i < g.n; i++) {

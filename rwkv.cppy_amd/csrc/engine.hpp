@@ -149,6 +149,8 @@ class Engine {
     bool mm_dispatch(MMGroup & g, int wtype);
     float * gy_ = nullptr;     // scratch y of emit-only GEMM entries
     size_t gy_cap_ = 0;
+    float * part_ = nullptr;   // split-K partials (launch_qgemm)
+    size_t part_cap_ = 0;
     bool use_mm_ = false;
     bool tile_acts_ = false;  // Aview: Q8 activations in sequence-GEMM tiles (forward, T >= 2)
     void drop_graphs();

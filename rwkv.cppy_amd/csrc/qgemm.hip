@@ -275,12 +275,17 @@ __device__ __forceinline__ void qg_fold(float (&st)[6][TI][2][4], float (&st2)[6
 // as k_qgemm with the step bookkeeping resolved at compile time -- each 8-step chunk is
 // straight-line code (the class-pair folds after steps 1, 3, 5 close 1, 2, 1 levels; after step
 // 7, 3 + ctz(~chunk) levels), and the copy walk is blocks 8c + wave, 8c + wave + 4.
-template <int WF>
+// SPLIT > 1 (split-K for small M, _0 formats): workgroup s of a tile runs chunks
+// [s * NCHL, (s + 1) * NCHL) -- a complete subtree of the perfect binary tree over the 64 classes --
+// and stores that subtree sum to g.part; k_qg_combine adds the SPLIT subtrees with the tree's top
+// levels and applies the epilogue, so results equal the unsplit kernel bit for bit.
+template <int WF, int SPLIT = 1>
 __global__ __launch_bounds__(256) void k_qgemm_k64(MMGroup g) {
     using Lt = QGLayout<WF>;
     constexpr bool ONE = Lt::ONE;
     constexpr int TI = Lt::TI;
-    constexpr int NB = 64, NCH = NB / QG_STEPS;
+    constexpr int NB = 64, NCH = NB / QG_STEPS, NCHL = NCH / SPLIT;
+    static_assert(SPLIT == 1 || !ONE, "split-K: _0 formats only");
     __shared__ __attribute__((aligned(16))) char smem[2][Lt::BUF];
     int e = 0;
 #pragma unroll 1
@@ -288,7 +293,8 @@ __global__ __launch_bounds__(256) void k_qgemm_k64(MMGroup g) {
     const MMEntry & E = g.e[e];
     const int M = E.W.M, T = g.T;
     const int tilesT = (T + QG_TOK - 1) / QG_TOK;
-    const int local = (int)blockIdx.x - E.block0;
+    const int local0 = (int)blockIdx.x - E.block0;
+    const int sidx = local0 % SPLIT, local = local0 / SPLIT, ch0 = sidx * NCHL;
     const int mtile = local / tilesT, ttile = local % tilesT;
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int r16 = lane & 15, h = lane >> 4;
@@ -309,13 +315,13 @@ __global__ __launch_bounds__(256) void k_qgemm_k64(MMGroup g) {
     float st[6][TI][2][4], st2[6][TI][2][4];
     float tot[TI][2][4], tot2[TI][2][4];
     float c[TI][2][4], c2[TI][2][4];
-    load(0, lds0);
+    load(ch0, lds0);
     qg_chunk_done();
-    load(1, lds0 + Lt::BUF);
+    if (NCHL > 1) load(ch0 + 1, lds0 + Lt::BUF);
     QGOps<TI> cur;
     qg_read_ops<WF>(smem[0], cur, wr, wt, r16, h);
 #pragma unroll 1
-    for (int ch = 0; ch < NCH; ch++) {
+    for (int ch = 0; ch < NCHL; ch++) {  // local chunk index (the subtree's own tree)
         const char * buf = smem[ch & 1];
 #pragma unroll
         for (int k = 0; k < QG_STEPS; k++) {
@@ -340,13 +346,42 @@ __global__ __launch_bounds__(256) void k_qgemm_k64(MMGroup g) {
             }
             cur = nxt;
         }
-        if (ch + 1 < NCH) {
+        if (ch + 1 < NCHL) {
             qg_chunk_done();  // chunk ch+1 has landed and buffer ch&1 is free
-            if (ch + 2 < NCH) load(ch + 2, lds0 + (ch & 1) * Lt::BUF);
+            if (ch + 2 < NCHL) load(ch0 + ch + 2, lds0 + (ch & 1) * Lt::BUF);
             qg_read_ops<WF>(smem[(ch + 1) & 1], cur, wr, wt, r16, h);
         }
     }
-    qg_store<ONE, TI>(E, T, M, tok0, row0, wt, wr, r16, h, tot, tot2);
+    if constexpr (SPLIT == 1) {
+        qg_store<ONE, TI>(E, T, M, tok0, row0, wt, wr, r16, h, tot, tot2);
+    } else {
+        // the subtree over this split's 8 * NCHL classes sits at level 3 + log2(NCHL)
+        constexpr int LEV = NCHL == 1 ? 3 : NCHL == 2 ? 4 : 5;
+#pragma unroll
+        for (int i = 0; i < TI; i++)
+#pragma unroll
+            for (int j = 0; j < 2; j++) {
+                const int t = tok0 + wt + 16 * j + r16;
+                const int m0 = row0 + wr + 16 * i + 4 * h;
+                if (t >= T) continue;
+                float * pp = g.part + ((size_t)sidx * T + t) * M + m0;
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    if (m0 + q < M) pp[q] = st[LEV][i][j][q];
+            }
+    }
+}
+
+// Top of the class tree over SPLIT = 8 subtrees, then qg_store's total (+ 0.0f) and epilogue
+__global__ __launch_bounds__(256) void k_qg_combine(MMEntry E, int T, int M, const float * part) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (size_t)T * M) return;
+    const int t = (int)(i / M), m = (int)(i % M);
+    float p[8];
+#pragma unroll
+    for (int s = 0; s < 8; s++) p[s] = part[((size_t)s * T + t) * M + m];
+    const float tot = ((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7]));
+    E.y[(size_t)t * E.ldy + m] = apply_epi(E, t, m, tot + 0.0f);
 }
 
 template <int WF>
@@ -506,6 +541,23 @@ bool launch_qgemm(hipStream_t st, MMGroup & g, int wtype) {
     const dim3 grid(blocks), block(256);
     bool k64 = true;
     for (int i = 0; i < g.n; i++) k64 = k64 && g.e[i].W.K == 2048;
+    // split-K: one small-M entry (e.g. the v6 maa LoRA W1, 160 rows: 48 tiles for 256 CUs)
+    const bool split = k64 && !g_qgemm_generic && g.n == 1 && !qg_one(wtype) && g.T >= 2 && !g.e[0].emit &&
+                       blocks < 256 && g.part && g.part_floats >= (size_t)8 * g.T * g.e[0].W.M;
+    if (split) {
+        const dim3 sgrid(blocks * 8);
+        switch (wtype) {
+            case W_Q4_0: hipLaunchKernelGGL((k_qgemm_k64<W_Q4_0, 8>), sgrid, block, 0, st, g); break;
+            case W_Q5_0: hipLaunchKernelGGL((k_qgemm_k64<W_Q5_0, 8>), sgrid, block, 0, st, g); break;
+            default: hipLaunchKernelGGL((k_qgemm_k64<W_Q8_0, 8>), sgrid, block, 0, st, g); break;
+        }
+        HIP_OK(hipGetLastError());
+        const size_t n = (size_t)g.T * g.e[0].W.M;
+        hipLaunchKernelGGL(k_qg_combine, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, g.e[0], g.T, g.e[0].W.M,
+                           g.part);
+        HIP_OK(hipGetLastError());
+        return true;
+    }
     if (k64 && !g_qgemm_generic) {
         switch (wtype) {
             case W_Q4_0: hipLaunchKernelGGL(k_qgemm_k64<W_Q4_0>, grid, block, 0, st, g); break;

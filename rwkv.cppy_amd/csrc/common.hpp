@@ -110,6 +110,7 @@ struct MMEntry {
     int emit;
     int epi;
     int block0;         // first workgroup of this entry
+    int fuse_emit;      // qgemm: the epilogue emits `out` (Q8_0 tiles) itself; y is not written
 };
 
 constexpr int MM_MAX_ENTRIES = 8;

@@ -523,7 +523,8 @@ bool Engine::mm_dispatch(MMGroup & g, int wtype) {
     if (!launch_qgemm(stream_, g, wtype)) return false;
     for (int i = 0; i < g.n; i++) {
         const MMEntry & e = g.e[i];
-        if (e.emit && e.ldy == e.W.M && !launch_act_from_f32(stream_, e.y, g.T, e.W.M, e.out)) return false;
+        if (e.emit && !e.fuse_emit && e.ldy == e.W.M && !launch_act_from_f32(stream_, e.y, g.T, e.W.M, e.out))
+            return false;
         if (e.emit && e.ldy != e.W.M) {
             fprintf(stderr, "rwkv: emitting GEMM entry needs ldy == M\n");
             return false;

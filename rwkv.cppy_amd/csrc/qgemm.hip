@@ -215,6 +215,46 @@ __device__ __forceinline__ void qg_epi(const QGOps<TI> & cur, const v4i_t (&sv)[
 template <bool ONE, int TI>
 __device__ __forceinline__ void qg_store(const MMEntry & E, int T, int M, int tok0, int row0, int wt, int wr, int r16,
                                          int h, const float (&tot)[TI][2][4], const float (&tot2)[TI][2][4]) {
+    if constexpr (TI == 2 && !ONE) {
+        if (E.fuse_emit) {
+            // The wave's 32 rows (wr % 32 == 0) of a token are one quantization block of the next
+            // matmul's input: lanes r16 + 16 h hold rows 16 i + 4 h + q.  quant32 / store32's values:
+            // amax and sum over the block by xor-16/32 lane exchanges (order-free), ggml rounding.
+#pragma unroll
+            for (int j = 0; j < 2; j++) {
+                const int t = tok0 + wt + 16 * j + r16;
+                float v[2][4];
+                float am = 0.0f;
+#pragma unroll
+                for (int i = 0; i < 2; i++)
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        const int m = row0 + wr + 16 * i + 4 * h + q;
+                        v[i][q] = apply_epi_v(E, m, tot[i][j][q] + 0.0f, 0.0f, 0.0f);
+                        am = fmaxf(am, fabsf(v[i][q]));
+                    }
+                am = fmaxf(am, __shfl_xor(am, 16));
+                am = fmaxf(am, __shfl_xor(am, 32));
+                const float d = am / 127.f;
+                const float id = (am != 0.0f) ? 127.f / am : 0.0f;
+                uint32_t packed[2];
+#pragma unroll
+                for (int i = 0; i < 2; i++) {
+                    packed[i] = 0;
+#pragma unroll
+                    for (int q = 0; q < 4; q++) packed[i] |= ((uint32_t)(int)rintf(v[i][q] * id) & 0xffu) << (8 * q);
+                }
+                if (t < T) {
+                    uint8_t * rec = E.out.tq + ((size_t)(t / QG_TOK) * (M >> 5) + ((row0 + wr) >> 5)) * qg_a_bytes(false);
+                    const int tl = t % QG_TOK;
+#pragma unroll
+                    for (int i = 0; i < 2; i++) *(uint32_t *)(rec + i * QG_TOK * 16 + tl * 16 + 4 * h) = packed[i];
+                    if (h == 0) ((float *)(rec + QG_A_D))[tl] = f16_round(d);
+                }
+            }
+            return;
+        }
+    }
     const bool vec = ((E.ldy | M) & 3) == 0 && (((uintptr_t)E.y | (uintptr_t)E.aux) & 15) == 0;
 #pragma unroll
     for (int i = 0; i < TI; i++)
@@ -538,6 +578,13 @@ bool launch_qgemm(hipStream_t st, MMGroup & g, int wtype) {
         blocks += (e.W.M + rows - 1) / rows * tilesT;
     }
     if (!blocks) return true;
+    // Q8_0 emission fused into the epilogue (the Q4_0 / Q5_0 / Q8_0 GEMMs: a wave holds 32 rows)
+    for (int i = 0; i < g.n; i++) {
+        MMEntry & e = g.e[i];
+        e.fuse_emit = !qg_one(wtype) && e.emit && e.out.tiled && e.out.fmt == A_Q8_0 && e.out.tq && e.out.K == e.W.M &&
+                      e.W.M % 64 == 0 && e.ldy == e.W.M && e.epi != EPI_ADD && e.epi != EPI_SIGMUL_ADD &&
+                      e.epi != EPI_VMIX7 && e.epi != EPI_DECAY6 && e.epi != EPI_DECAY7 && e.epi != EPI_SIGMOID_BIAS;
+    }
     const dim3 grid(blocks), block(256);
     bool k64 = true;
     for (int i = 0; i < g.n; i++) k64 = k64 && g.e[i].W.K == 2048;

@@ -350,7 +350,7 @@ struct Mix5Args {
 // mixes in registers (read once per token tile instead of once per token) and the tile's lora rows
 // sit in LDS; per token the five D-long fp64 sums (k_v6_mix5_dec's order: sequential over i) run
 // side by side.
-constexpr int MIX_TT = 16;
+constexpr int MIX_TT = 8;
 
 // TQ > 0: all five outputs are Q8 sequence-GEMM token tiles (TQ = 2: Q8_1); each lane's record
 // address is formed once (a workgroup's MIX_TT tokens lie in one QG_TOK-token tile) and the

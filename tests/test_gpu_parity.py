@@ -271,7 +271,7 @@ def test_synthetic_real_width_matches_oracle(tmp_path, arch, fmt):
     m.free()
 
 
-@pytest.mark.parametrize('arch,fmt', [(6, 'Q4_0'), (5, 'Q4_1'), (7, 'Q5_1'), (6, 'Q8_0')])
+@pytest.mark.parametrize('arch,fmt', [(6, 'Q4_0'), (5, 'Q4_1'), (7, 'Q5_1'), (6, 'Q8_0'), (6, 'Q5_1'), (6, 'Q5_0')])
 def test_real_width_long_sequence_bit_exact(tmp_path, arch, fmt):
     """70 tokens through the sequence kernels (MFMA GEMM, chunk-staged wkv: 32+32+6) equal 70
     serial decode steps bit for bit, and chunked evaluation equals both."""

@@ -279,13 +279,27 @@ static int tile_q(const ActBuf * outs, int n, int K) {
 // rwkv_carry_x (rwkv_graph.inc:56-82) + the token-shift mixes of each version.
 template <int TQ>
 __global__ __launch_bounds__(1024) void k_ln_mix(LnMixArgs a) {
-    __shared__ double sh[8];
-    const int t = blockIdx.x * TOKS_PER_WG + (threadIdx.x >> 8), C = a.C, tid = threadIdx.x & 255;
+    // LayerNorm statistics of the workgroup's TOKS_PER_WG + 1 rows (its tokens and the one before),
+    // one wave per row (the canonical one-wave association), shared through LDS
+    __shared__ float s_mean[TOKS_PER_WG + 1], s_scale[TOKS_PER_WG + 1];
+    const int tg = threadIdx.x >> 8, t = blockIdx.x * TOKS_PER_WG + tg, C = a.C, tid = threadIdx.x & 255;
+    const int wave = threadIdx.x >> 6;
+    if (wave <= TOKS_PER_WG) {
+        const int rt = (int)blockIdx.x * TOKS_PER_WG - 1 + wave;
+        if (rt >= 0 && rt < a.T) {
+            float m, sc;
+            ln_stats_any(a.x + (size_t)rt * C, C, 1e-5f, m, sc);
+            if ((threadIdx.x & 63) == 0) {
+                s_mean[wave] = m;
+                s_scale[wave] = sc;
+            }
+        }
+    }
+    __syncthreads();
     if (t >= a.T) return;  // whole 256-thread token groups
     const float * xt = a.x + (size_t)t * C;
-    float mean, scale, pmean = 0.0f, pscale = 0.0f;
-    ln_stats(xt, C, 1e-5f, mean, scale, sh);
-    if (t > 0) ln_stats(xt - C, C, 1e-5f, pmean, pscale, sh);
+    const float mean = s_mean[tg + 1], scale = s_scale[tg + 1];
+    const float pmean = t > 0 ? s_mean[tg] : 0.0f, pscale = t > 0 ? s_scale[tg] : 0.0f;
     for (int c0 = 0; c0 < C; c0 += 256) {
         const int c = c0 + tid;
         if (c0 + (tid & ~63) >= C) continue;  // whole wave out of range (C % 64 == 0)

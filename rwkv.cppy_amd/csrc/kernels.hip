@@ -6,6 +6,7 @@
 // them (the quantized block accumulation).
 #include "kernels.hpp"
 
+#include <algorithm>
 #include <type_traits>
 #include "device_common.hpp"
 
@@ -120,7 +121,11 @@ __global__ __launch_bounds__(256) void k_mm(MMGroup g) {
     const int rowwg = ((int)blockIdx.x - E.block0) * RW;
     const int row0 = rowwg + wave * RPW;
     const int T = g.T;
-    for (int t0 = 0; t0 < T; t0 += NT) {
+    // grid.y splits the tokens into spans (a multiple of NT each): every output keeps its own
+    // arithmetic, the small-M groups (LoRA first stages, 18 row blocks) just get more workgroups
+    const int span = ((T + (int)gridDim.y - 1) / (int)gridDim.y + NT - 1) / NT * NT;
+    const int tb = (int)blockIdx.y * span, te = min(T, tb + span);
+    for (int t0 = tb; t0 < te; t0 += NT) {
         float acc[RPW][NT], acc2[RPW][NT];
 #pragma unroll
         for (int r = 0; r < RPW; r++)
@@ -187,8 +192,11 @@ static bool launch_mm_wf(hipStream_t st, MMGroup & g) {
         if (emit) hipLaunchKernelGGL((k_mm<WF, 8, 1>), grid, block, 0, st, g);
         else hipLaunchKernelGGL((k_mm<WF, 2, 1>), grid, block, 0, st, g);
     } else {
-        if (emit) hipLaunchKernelGGL((k_mm<WF, 8, 4>), grid, block, 0, st, g);
-        else hipLaunchKernelGGL((k_mm<WF, 2, 4>), grid, block, 0, st, g);
+        // token spans so that the grid has ~1024 workgroups (at most one span per 4 tokens)
+        const int gy = std::max(1, std::min((T + 3) / 4, 1024 / blocks));
+        const dim3 grid2(blocks, gy);
+        if (emit) hipLaunchKernelGGL((k_mm<WF, 8, 4>), grid2, block, 0, st, g);
+        else hipLaunchKernelGGL((k_mm<WF, 2, 4>), grid2, block, 0, st, g);
     }
     HIP_OK(hipGetLastError());
     return true;

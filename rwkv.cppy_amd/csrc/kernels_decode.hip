@@ -98,8 +98,7 @@ bool launch_mv_group(hipStream_t st, MVGroup & g) {
         g.stride = grid;
     }
     g.grid = grid;
-    int U = umax <= 1 ? 1 : umax <= 2 ? 2 : 4;
-    if (src != SRC_ACT && U == 2) U = 4;
+    const int U = umax <= 1 ? 1 : umax <= 2 ? 2 : 4;  // 2: K = 2560 (v7-2.9B) quantized rows
     int wfix = g.e[0].W.type;
     for (int i = 1; i < g.n; i++)
         if (g.e[i].W.type != wfix) wfix = -1;

@@ -628,9 +628,11 @@ bool launch_mv_shape(hipStream_t st, MVGroup & g, int U, int srck, int form, boo
         constexpr int Rv = (E) ? 8 : 2;                       \
         if (K <= 2048) {                                      \
             if (U == 1) MV_L(Rv, 1, S, F, E, 32);             \
+            else if (U == 2) MV_L(Rv, 2, S, F, E, 32);        \
             else MV_L(Rv, 4, S, F, E, 32);                    \
         } else {                                              \
             if (U == 1) MV_L(Rv, 1, S, F, E, 64);             \
+            else if (U == 2) MV_L(Rv, 2, S, F, E, 64);        \
             else MV_L(Rv, 4, S, F, E, 64);                    \
         }                                                     \
     } while (0)

@@ -1119,11 +1119,17 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits) {
             src_lnmix(b.add(L.att_r, r_, EPI_STORE), x_, si + C, L.ln1_w, L.ln1_b, mu, 1, so + C);
             src_lnmix(b.add(L.att_k, k_, EPI_STORE), x_, si + C, L.ln1_w, L.ln1_b, mu + 2 * (size_t)C, 1);
             src_lnmix(b.add(L.att_v, v_, EPI_STORE), x_, si + C, L.ln1_w, L.ln1_b, mu + 3 * (size_t)C, 1);
-            src_lnmix(b.add(L.w1, dsmall_[0], EPI_TANH), x_, si + C, L.ln1_w, L.ln1_b, mu + 1 * (size_t)C, 1);
-            src_lnmix(b.add(L.a1, dsmall_[1], EPI_STORE), x_, si + C, L.ln1_w, L.ln1_b, mu + 4 * (size_t)C, 1);
-            src_lnmix(b.add(L.g1, dsmall_[2], EPI_SIGMOID), x_, si + C, L.ln1_w, L.ln1_b, mu + 5 * (size_t)C, 1);
-            if (l != 0) src_lnmix(b.add(L.v1, dsmall_[3], EPI_STORE), x_, si + C, L.ln1_w, L.ln1_b, mu + 3 * (size_t)C, 1);
+            // the LoRA first stages (F16 in the released files) as their own launch when their type
+            // differs from r,k,v: one weight type per launch keeps the fixed-type kernels (fewer
+            // registers, no per-entry type switch, no padded units)
+            MV lb;
+            MV & bl = L.w1.type == L.att_r.type ? b : lb;
+            src_lnmix(bl.add(L.w1, dsmall_[0], EPI_TANH), x_, si + C, L.ln1_w, L.ln1_b, mu + 1 * (size_t)C, 1);
+            src_lnmix(bl.add(L.a1, dsmall_[1], EPI_STORE), x_, si + C, L.ln1_w, L.ln1_b, mu + 4 * (size_t)C, 1);
+            src_lnmix(bl.add(L.g1, dsmall_[2], EPI_SIGMOID), x_, si + C, L.ln1_w, L.ln1_b, mu + 5 * (size_t)C, 1);
+            if (l != 0) src_lnmix(bl.add(L.v1, dsmall_[3], EPI_STORE), x_, si + C, L.ln1_w, L.ln1_b, mu + 3 * (size_t)C, 1);
             if (!mv(b.g)) return false;
+            if (lb.g.n && !mv(lb.g)) return false;
             if (l == 0) HIP_OK(hipMemcpyAsync(vfirst_, v_, (size_t)C * 4, hipMemcpyDeviceToDevice, stream_));
             MV c;
             src_f32(c.add(L.w2, w_, EPI_DECAY7, nullptr, L.w0), dsmall_[0]);

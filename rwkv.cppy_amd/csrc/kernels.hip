@@ -192,8 +192,8 @@ static bool launch_mm_wf(hipStream_t st, MMGroup & g) {
         if (emit) hipLaunchKernelGGL((k_mm<WF, 8, 1>), grid, block, 0, st, g);
         else hipLaunchKernelGGL((k_mm<WF, 2, 1>), grid, block, 0, st, g);
     } else {
-        // token spans so that the grid has ~1024 workgroups (at most one span per 4 tokens)
-        const int gy = std::max(1, std::min((T + 3) / 4, 1024 / blocks));
+        // token spans so that the grid has ~4096 workgroups (at most one span per 4 tokens)
+        const int gy = std::max(1, std::min((T + 3) / 4, 4096 / blocks));
         const dim3 grid2(blocks, gy);
         if (emit) hipLaunchKernelGGL((k_mm<WF, 8, 4>), grid2, block, 0, st, g);
         else hipLaunchKernelGGL((k_mm<WF, 2, 4>), grid2, block, 0, st, g);

@@ -32,6 +32,7 @@ sys.path.insert(0, os.path.join(REPO, 'tests'))
 
 METRIC = 'tokens/sec RWKV-v6-World-1B6 Q4_0 decode + seq-eval @1/2/4/8 GPU; HBM GB/s vs peak'
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+INT8_MFMA_PEAK_TOPS = 5000.0  # dense int8 MFMA: 2x the ~2.5 PF dense bf16 rate (MI355X_MICROARCH.md, Matrix cores)
 
 CONFIGS = {
     # name: arch, n_vocab, n_embed, n_layer, ffn (0 = arch default), format, label
@@ -205,53 +206,101 @@ def main():
                 logits.ctypes.data_as(P_F))
     t2 = time.perf_counter()
     for i in range(args.abi_steps):
-        assert L.rwkv_eval(ctx.ptr, int(dec_tokens[i]), state.ctypes.data_as(P_F), state.ctypes.data_as(P_F),
+        assert L.rwkv_eval(ctx.ptr, int(dec_tokens[i % len(dec_tokens)]), state.ctypes.data_as(P_F), state.ctypes.data_as(P_F),
                            logits.ctypes.data_as(P_F))
     abi_tps = args.abi_steps / (time.perf_counter() - t2) if args.abi_steps > 0 else 0.0
     log(f'ABI decode (host state {state_len * 4 / 1e6:.1f} MB each way): {abi_tps:.1f} tok/s')
 
-    # ---------------- dominant-kernel roofline (HIP events on the context stream) ----------------
-    assert L.rwkv_mi355x_state_upload(ctx.ptr, None)
-    L.rwkv_mi355x_set_kernel_timing(ctx.ptr, True)
-    for i in range(args.timing_steps):
-        step(i)
-    L.rwkv_mi355x_sync(ctx.ptr)
-    n = L.rwkv_mi355x_kernel_stats(ctx.ptr, -1, None, 0, None, None, None, None)
-    kstats = []
-    for i in range(n):
-        name = ctypes.create_string_buffer(128)
-        la, ms, by, fl = ctypes.c_longlong(), ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
-        L.rwkv_mi355x_kernel_stats(ctx.ptr, i, name, 128, ctypes.byref(la), ctypes.byref(ms), ctypes.byref(by),
-                                   ctypes.byref(fl))
-        kstats.append(dict(name=name.value.decode(), launches=la.value, ms=ms.value, bytes=by.value, flops=fl.value))
-    L.rwkv_mi355x_set_kernel_timing(ctx.ptr, False)
-    kstats.sort(key=lambda k: -k['ms'])
-    for k in kstats:
-        log(f"  {k['name']:<18} launches {k['launches']:5d} avg {k['ms'] / k['launches'] * 1e3:8.2f} us "
-            f"{k['bytes'] / k['launches'] / 1e6:8.3f} MB/launch -> {k['bytes'] / k['ms'] / 1e6:8.1f} GB/s")
-    dom = kstats[0]
-    avg_us = dom['ms'] / dom['launches'] * 1e3
-    bytes_per_launch = dom['bytes'] / dom['launches']
-    achieved = bytes_per_launch / (avg_us * 1e-6) / 1e9
-    mm_ms = sum(k['ms'] for k in kstats) / args.timing_steps
-    mm_bytes = sum(k['bytes'] for k in kstats) / args.timing_steps
-    traffic = None
-    pmc = os.path.join(REPO, 'profiles', 'pmc_traffic.json')
-    if os.path.isfile(pmc):
-        t = json.load(open(pmc)).get(args.config, {}).get(dom['name'])
-        if t:
-            traffic = t['traffic_bytes_per_launch']
-    roofline = {
-        'kernel': dom['name'], 'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-        'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic,
-        'avg_launch_us': round(avg_us, 3), 'algorithmic_bytes_per_launch': round(bytes_per_launch),
-        'all_matmuls_GBps': round(mm_bytes / (mm_ms * 1e-3) / 1e9, 1),
-        'decode_bytes_per_token': round(L.rwkv_mi355x_decode_bytes(ctx.ptr, True)),
-        'decode_GBps_end_to_end': round(L.rwkv_mi355x_decode_bytes(ctx.ptr, True) / (ms_per_step * 1e-3) / 1e9, 1),
-    }
+    # ---------------- kernel timing (HIP events on the context stream) ----------------
+    def read_stats():
+        n = L.rwkv_mi355x_kernel_stats(ctx.ptr, -1, None, 0, None, None, None, None)
+        out = []
+        for i in range(n):
+            name = ctypes.create_string_buffer(128)
+            la, ms, by, fl = ctypes.c_longlong(), ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+            L.rwkv_mi355x_kernel_stats(ctx.ptr, i, name, 128, ctypes.byref(la), ctypes.byref(ms), ctypes.byref(by),
+                                       ctypes.byref(fl))
+            if la.value > 0:
+                out.append(dict(name=name.value.decode(), launches=la.value, ms=ms.value, bytes=by.value,
+                                flops=fl.value))
+        return sorted(out, key=lambda k: -k['ms'])
 
-    # ---------------- CPU baseline: oracle (CPU restatement of the reference arithmetic) ----------------
+    errors = []
+    roofline = None
+    timing_steps = max(1, args.timing_steps)
+    try:
+        assert L.rwkv_mi355x_state_upload(ctx.ptr, None)
+        L.rwkv_mi355x_set_kernel_timing(ctx.ptr, True)
+        for i in range(timing_steps):
+            step(i % len(arrs))
+        L.rwkv_mi355x_sync(ctx.ptr)
+        kstats = read_stats()
+        L.rwkv_mi355x_set_kernel_timing(ctx.ptr, False)
+        for k in kstats:
+            log(f"  {k['name']:<18} launches {k['launches']:5d} avg {k['ms'] / k['launches'] * 1e3:8.2f} us "
+                f"{k['bytes'] / k['launches'] / 1e6:8.3f} MB/launch -> {k['bytes'] / k['ms'] / 1e6:8.1f} GB/s")
+        # the decode matvec (all k_mv / k_mva launches, head included) is the dominant kernel class
+        dom = next((k for k in kstats if k['name'] == 'k_mv'), kstats[0] if kstats else None)
+        if dom is None:
+            raise RuntimeError('no decode kernel timings recorded')
+        avg_us = dom['ms'] / dom['launches'] * 1e3
+        bytes_per_launch = dom['bytes'] / dom['launches']
+        achieved = bytes_per_launch / (avg_us * 1e-6) / 1e9
+        traffic = None
+        pmc = os.path.join(REPO, 'profiles', 'pmc_traffic.json')
+        if os.path.isfile(pmc):
+            t = json.load(open(pmc)).get(args.config, {}).get(dom['name'])
+            if t:
+                traffic = t['traffic_bytes_per_launch']
+        dbytes = L.rwkv_mi355x_decode_bytes(ctx.ptr, True)
+        roofline = {
+            'kernel': dom['name'], 'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+            'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic,
+            'avg_launch_us': round(avg_us, 3), 'algorithmic_bytes_per_launch': round(bytes_per_launch),
+            'launches_per_token': round(dom['launches'] / timing_steps, 1),
+            'decode_bytes_per_token': round(dbytes),
+            'decode_GBps_end_to_end': round(dbytes / (ms_per_step * 1e-3) / 1e9, 1),
+            'decode_frac_end_to_end': round(dbytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+        }
+    except Exception as e:
+        errors.append(f'roofline: {e!r}')
+        log(f'roofline failed: {e!r}')
+        L.rwkv_mi355x_set_kernel_timing(ctx.ptr, False)
+
+    # ---------------- sequence GEMM MFMA utilisation (same run, HIP events) ----------------
+    seq_roofline = None
+    if args.seq_reps > 0:
+        try:
+            assert L.rwkv_mi355x_state_upload(ctx.ptr, None)
+            L.rwkv_mi355x_set_kernel_timing(ctx.ptr, True)
+            assert L.rwkv_mi355x_eval_device(ctx.ptr, sp, len(seq), True, None, True)
+            sstats = read_stats()
+            L.rwkv_mi355x_set_kernel_timing(ctx.ptr, False)
+            g = [k for k in sstats if k['name'].startswith('k_qgemm')]
+            if not g:
+                raise RuntimeError('no k_qgemm timings recorded')
+            ms = sum(k['ms'] for k in g)
+            flops = sum(k['flops'] for k in g)
+            tops = flops / (ms * 1e-3) / 1e12
+            other = [k for k in sstats if not k['name'].startswith('k_qgemm')]
+            seq_roofline = {
+                'kernel': 'k_qgemm (all int8-MFMA sequence GEMM launches)', 'bound': 'mfma',
+                'achieved': round(tops, 1), 'peak': INT8_MFMA_PEAK_TOPS, 'unit': 'TOP/s',
+                'frac': round(tops / INT8_MFMA_PEAK_TOPS, 4), 'launches': sum(k['launches'] for k in g),
+                'ms_per_sequence': round(ms, 3), 'algorithmic_ops': flops,
+                'share_of_seq_eval': round(ms / (seq_s * 1e3), 3) if ts else None,
+                'other_matmul_ms': round(sum(k['ms'] for k in other), 3),
+            }
+            log(f"seq GEMM: {ms:.2f} ms per sequence, {tops:.1f} TOP/s = {100 * tops / INT8_MFMA_PEAK_TOPS:.1f}% "
+                f"of the int8 MFMA peak")
+        except Exception as e:
+            errors.append(f'seq_roofline: {e!r}')
+            log(f'seq roofline failed: {e!r}')
+            L.rwkv_mi355x_set_kernel_timing(ctx.ptr, False)
+
+    # ---------------- CPU baseline + parity of this run's model (oracle = CPU restatement) ----------------
     cpu = None
+    parity = None
     if rank == 0 and world == 1 and not args.skip_cpu:
         try:
             from oracle_ctypes import OracleModel, lib as olib
@@ -260,13 +309,15 @@ def main():
             t3 = time.time()
             om = OracleModel(path)
             load_s = time.time() - t3
+            cpu_tokens = [int(t) for t in np.random.default_rng(99).integers(0, n_vocab, size=256)]
             st = None
+            olg = None
             ntok = 0
             t4 = time.perf_counter()
-            while True:
-                lg, st = om.eval_sequence([int(dec_tokens[ntok])], st)
+            while ntok < len(cpu_tokens):
+                olg, st = om.eval_sequence([cpu_tokens[ntok]], st)
                 ntok += 1
-                if time.perf_counter() - t4 >= args.cpu_seconds or ntok >= 256:
+                if time.perf_counter() - t4 >= args.cpu_seconds:
                     break
             cpu_s = time.perf_counter() - t4
             cpu = {'value': round(ntok / cpu_s, 3), 'unit': 'tokens/s', 'cores': olib().oracle_get_threads(),
@@ -275,9 +326,40 @@ def main():
                              f'{cpu_s:.1f}s; oracle/ C restatement of the reference CPU arithmetic '
                              f'(ggml Q8 activation quantization + int8 block dots), OpenMP over rows'}
             log(f'cpu baseline: {cpu["value"]} tok/s on {cpu["cores"]} threads (load {load_s:.1f}s)')
+            # parity: the same tokens through the GPU decode path from a fresh state
+            assert L.rwkv_mi355x_state_upload(ctx.ptr, None)
+            glg = np.zeros(n_vocab, np.float32)
+            for i in range(ntok):
+                a_, p_ = tok_arr([cpu_tokens[i]])
+                last = i == ntok - 1
+                assert L.rwkv_mi355x_eval_device(ctx.ptr, p_, 1, last, glg.ctypes.data_as(P_F) if last else None, last)
+            gst = np.zeros(state_len, np.float32)
+            assert L.rwkv_mi355x_state_download(ctx.ptr, gst.ctypes.data_as(P_F))
             om.close()
-        except Exception as e:  # the baseline is reported, never required
-            log(f'cpu baseline failed: {e}')
+            # bit-exactness gate: the oracle's GPU-association variant over the first tokens
+            from oracle_ctypes import gpu_variant
+            nbx = min(8, ntok)
+            blg, bst = gpu_variant(path, cpu_tokens[:nbx])
+            assert L.rwkv_mi355x_state_upload(ctx.ptr, None)
+            xlg = np.zeros(n_vocab, np.float32)
+            for i in range(nbx):
+                a_, p_ = tok_arr([cpu_tokens[i]])
+                last = i == nbx - 1
+                assert L.rwkv_mi355x_eval_device(ctx.ptr, p_, 1, last, xlg.ctypes.data_as(P_F) if last else None, last)
+            xst = np.zeros(state_len, np.float32)
+            assert L.rwkv_mi355x_state_download(ctx.ptr, xst.ctypes.data_as(P_F))
+            bit_exact = bool(np.array_equal(xlg.view(np.uint32), blg.view(np.uint32)) and
+                             np.array_equal(xst.view(np.uint32), bst.view(np.uint32)))
+            parity = {'bit_exact_vs_gpu_association_oracle': bit_exact, 'bit_exact_tokens': nbx,
+                      'tokens': ntok, 'vs': 'oracle variant 0 (ggml CPU numerics, ggml summation order)',
+                      'max_abs_dlogit': float(np.abs(glg - olg).max()),
+                      'max_abs_dstate': float(np.abs(gst - st).max()),
+                      'max_abs_logit': float(np.abs(olg).max())}
+            log(f"parity: bit-exact vs GPU-association oracle over {nbx} tokens: {bit_exact}; "
+                f"vs ggml-order oracle over {ntok} tokens: max|dlogit| {parity['max_abs_dlogit']:.3g}")
+        except Exception as e:
+            errors.append(f'cpu_baseline: {e!r}')
+            log(f'cpu baseline failed: {e!r}')
 
     L.rwkv_free(ctx.ptr)
     if rank == 0:
@@ -293,8 +375,16 @@ def main():
                          'pipeline': pipe},
             'abi_decode_tokens_per_s': round(abi_tps * world, 2),
             'roofline': roofline,
+            'seq_roofline': seq_roofline,
             'cpu_baseline': cpu,
+            'parity': parity,
         }
+        if rank == 0 and world == 1 and not args.skip_cpu and cpu is None:
+            errors.append('cpu_baseline missing')
+        if roofline is None:
+            errors.append('roofline missing')
+        if errors:
+            out['errors'] = errors
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

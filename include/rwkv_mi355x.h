@@ -29,6 +29,11 @@ RWKV_API bool rwkv_mi355x_eval_device(struct rwkv_context * ctx, const uint32_t 
                                       bool compute_logits, float * logits_out, bool sync);
 RWKV_API bool rwkv_mi355x_sync(struct rwkv_context * ctx);
 
+/* Debugging aid: copies `bytes` of the named workspace buffer of the last evaluation to host `out`
+ * (names: x xa sx r k v g w y a nb bb vfirst fr lora bonus logits, slot<i>.<q|d|s|qsum|h|f>).
+ * Returns the bytes copied, or -1 (unknown name / copy failure).  Not part of rwkv.h. */
+RWKV_API long long rwkv_mi355x_debug_buffer(struct rwkv_context * ctx, const char * name, void * out, size_t bytes);
+
 /* One stage of the layer pipeline (the reference has no such entry point -- it is
  * the unit the multi-GPU sequence evaluation is built from, rwkv.cppy_amd/python/rwkv_cpp/pipeline.py).
  * Runs layers [layer_begin, layer_end) over T tokens on the device-resident state; only those

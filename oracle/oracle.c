@@ -457,10 +457,206 @@ int oracle_get_threads(void) {
 #endif
 }
 
+/* ---------------------------------------------------- GPU-association variant
+ * Variant bit 8 (ORACLE_VARIANT_GPU) evaluates the same ggml semantics in the association the
+ * MI355X kernels use, so the GPU path can be held BIT-EXACT to a CPU restatement.
+ * Every op below is an IEEE-exact primitive (add, mul, fma, correctly rounded div/sqrt, rint,
+ * ldexp), evaluated in the order the kernels evaluate it:
+ *   - matmul: output (row, token) is a 64-lane wave; lane l owns the 16-byte units l, l+64, ...
+ *     (a quantized 32-block; 8 F16 or 4 F32 elements) and chains them in ascending order
+ *     (quantized: acc = fma(d_w*d_x, sumi, acc), _1 formats: acc2 += m_w*s_x; F16/F32: one fma
+ *     per element); the 64 lane partials are folded by wave_sum63's perfect binary tree over
+ *     adjacent lanes; _1 formats add the folded acc2, others add +0.0.
+ *   - LayerNorm (ggml_norm, fp64 sums): lane l owns x[l + 64 j], four fp64 partials by j % 4
+ *     combined as (p0 + p1) + (p2 + p3), then the same 64-lane tree in fp64.
+ *   - per-head sums (GroupNorm statistics, wkv7 row sums, l2norm, v7 bonus) fold with the
+ *     xor butterfly of __shfl_xor (stride S/2 first); wkv6 y sums over keys split in
+ *     G = min(256/S, S) groups of S/G keys (head size 64: four 4-key runs (p0+p1)+(p2+p3)),
+ *     groups folded as a stride-halving tree.
+ *   - exp / tanh: the kernels' own polynomial implementations (device_common.hpp rk_expf /
+ *     rk_tanhf), restated below with the same constants and operation order. */
+#define OV_GPU 8
+
+static float gpu_expf(float x) {
+    if (x != x) return x;
+    if (x > 0x1.62e43p+6f) return INFINITY;
+    if (x < -0x1.9fe36ap+6f) return 0.0f;
+    const float n = rintf(x * 0x1.715476p+0f);
+    float r = fmaf(n, -0x1.62e43p-1f, x);
+    r = fmaf(n, 0x1.05c61p-29f, r);
+    float q = 0x1.687c22p-10f;
+    q = fmaf(q, r, 0x1.123b8ep-7f);
+    q = fmaf(q, r, 0x1.555b58p-5f);
+    q = fmaf(q, r, 0x1.55548ep-3f);
+    q = fmaf(q, r, 0x1.fffff8p-2f);
+    const float r2 = r * r;
+    const float p = fmaf(r2, q, r) + 1.0f;
+    return ldexpf(p, (int)n);
+}
+
+static float gpu_tanhf(float x) {
+    const float ax = fabsf(x);
+    if (ax < 0.625f) {
+        const float x2 = x * x;
+        float p = -0x1.7507acp-8f;
+        p = fmaf(p, x2, 0x1.51f0f0p-6f);
+        p = fmaf(p, x2, -0x1.b83322p-5f);
+        p = fmaf(p, x2, 0x1.1106d6p-3f);
+        p = fmaf(p, x2, -0x1.555532p-2f);
+        return fmaf(x * x2, p, x);
+    }
+    const float t = ax > 9.0f ? 1.0f : 1.0f - 2.0f / (gpu_expf(ax + ax) + 1.0f);
+    return copysignf(t, x);
+}
+
+static inline float o_exp(float x) { return (g_variant & OV_GPU) ? gpu_expf(x) : expf(x); }
+static inline float o_tanh(float x) { return (g_variant & OV_GPU) ? gpu_tanhf(x) : tanhf(x); }
+
+float oracle_gpu_expf(float x) { return gpu_expf(x); }
+float oracle_gpu_tanhf(float x) { return gpu_tanhf(x); }
+
+/* wave_sum63 (device_common.hpp): perfect binary tree over adjacent lanes, n a power of two */
+static float tree_f(float * a, int n) {
+    for (; n > 1; n >>= 1)
+        for (int i = 0; i < n / 2; i++) a[i] = a[2 * i] + a[2 * i + 1];
+    return a[0];
+}
+static double tree_d(double * a, int n) {
+    for (; n > 1; n >>= 1)
+        for (int i = 0; i < n / 2; i++) a[i] = a[2 * i] + a[2 * i + 1];
+    return a[0];
+}
+/* group_sum (__shfl_xor butterfly, stride n/2 first): every lane ends with this value */
+static float bfly_f(float * a, int n) {
+    for (; n > 1; n >>= 1)
+        for (int i = 0; i < n / 2; i++) a[i] = a[i] + a[i + n / 2];
+    return a[0];
+}
+static double bfly_d(double * a, int n) {
+    for (; n > 1; n >>= 1)
+        for (int i = 0; i < n / 2; i++) a[i] = a[i] + a[i + n / 2];
+    return a[0];
+}
+
+/* ggml_norm statistics in the kernels' association (ln_stats_regs / ln_stats_wave) */
+static void ln_stats_gpu(const float * x, int64_t n, float eps, float * mean_out, float * scale_out) {
+    double lanes[64];
+    const int64_t P = n / 64;
+    for (int l = 0; l < 64; l++) {
+        double p[4] = {0.0, 0.0, 0.0, 0.0};
+        for (int64_t j = 0; j < P; j++) p[j & 3] += (double)x[l + 64 * j];
+        lanes[l] = (p[0] + p[1]) + (p[2] + p[3]);
+    }
+    const float mean = (float)(tree_d(lanes, 64) / (double)n);
+    for (int l = 0; l < 64; l++) {
+        double q[4] = {0.0, 0.0, 0.0, 0.0};
+        for (int64_t j = 0; j < P; j++) {
+            const float d = x[l + 64 * j] - mean;
+            q[j & 3] += (double)(d * d);
+        }
+        lanes[l] = (q[0] + q[1]) + (q[2] + q[3]);
+    }
+    const float var = (float)(tree_d(lanes, 64) / (double)n);
+    *mean_out = mean;
+    *scale_out = 1.0f / sqrtf(var + eps);
+}
+
+/* quantized matmul in the kernels' association; weights unpacked once per row */
+static void matmul_gpu(int wtype, const uint8_t * W, int64_t K, int64_t M, const float * x, int64_t T, float * y) {
+    const int nthr = oracle_get_threads();
+    (void)nthr;
+    if (wtype == OT_FP32 || wtype == OT_FP16) {
+        const int per = wtype == OT_FP32 ? 4 : 8;   /* elements per 16-byte unit */
+        float * xr = (float *)malloc((size_t)(T * K) * sizeof(float));
+        for (int64_t i = 0; i < T * K; i++)
+            xr[i] = wtype == OT_FP16 ? oracle_f16_to_f32(oracle_f32_to_f16(x[i])) : x[i];
+#pragma omp parallel num_threads(nthr)
+        {
+            float * wr = (float *)malloc((size_t)K * sizeof(float));
+#pragma omp for schedule(static)
+            for (int64_t m = 0; m < M; m++) {
+                if (wtype == OT_FP32) memcpy(wr, W + (size_t)m * K * 4, (size_t)K * 4);
+                else for (int64_t k = 0; k < K; k++) wr[k] = h2f(W + ((size_t)m * K + k) * 2);
+                for (int64_t t = 0; t < T; t++) {
+                    const float * xt = xr + t * K;
+                    float acc[64];
+                    for (int l = 0; l < 64; l++) acc[l] = 0.0f;
+                    for (int64_t c = 0; c * per < K; c++) {  /* unit c -> lane c % 64, ascending */
+                        float a = acc[c & 63];
+                        for (int e = 0; e < per; e++) a = fmaf(wr[c * per + e], xt[c * per + e], a);
+                        acc[c & 63] = a;
+                    }
+                    y[t * M + m] = tree_f(acc, 64) + 0.0f;
+                }
+            }
+            free(wr);
+        }
+        free(xr);
+        return;
+    }
+    const int atype = (wtype == OT_Q4_1 || wtype == OT_Q5_1) ? OT_Q8_1 : OT_Q8_0;
+    const int one = atype == OT_Q8_1;
+    const int abb = one ? 36 : 34, aqo = one ? 4 : 2;
+    const int64_t nb = K / QK;
+    const size_t wbb = oracle_block_bytes(wtype);
+    uint8_t * xq = (uint8_t *)malloc((size_t)(T * nb * abb));
+    for (int64_t t = 0; t < T; t++) oracle_quantize_act(atype, x + t * K, xq + t * nb * abb, K);
+    /* activations unpacked: int8 values, d, s per block */
+    int8_t * xi = (int8_t *)malloc((size_t)(T * K));
+    float * xd = (float *)malloc((size_t)(T * nb) * sizeof(float));
+    float * xs = (float *)malloc((size_t)(T * nb) * sizeof(float));
+    for (int64_t t = 0; t < T; t++)
+        for (int64_t b = 0; b < nb; b++) {
+            const uint8_t * xb = xq + (t * nb + b) * abb;
+            memcpy(xi + t * K + b * 32, xb + aqo, 32);
+            xd[t * nb + b] = h2f(xb);
+            xs[t * nb + b] = one ? h2f(xb + 2) : 0.0f;
+        }
+#pragma omp parallel num_threads(nthr)
+    {
+        int8_t * wi8 = (int8_t *)malloc((size_t)K);
+        float * dw = (float *)malloc((size_t)nb * sizeof(float));
+        float * mw = (float *)malloc((size_t)nb * sizeof(float));
+        int wi[32];
+#pragma omp for schedule(static)
+        for (int64_t m = 0; m < M; m++) {
+            const uint8_t * wrow = W + (size_t)m * nb * wbb;
+            for (int64_t b = 0; b < nb; b++) {
+                block_ints(wtype, wrow + b * wbb, wi, &dw[b], &mw[b]);
+                for (int j = 0; j < 32; j++) wi8[b * 32 + j] = (int8_t)wi[j];
+            }
+            for (int64_t t = 0; t < T; t++) {
+                float acc[64], acc2[64];
+                for (int l = 0; l < 64; l++) acc[l] = acc2[l] = 0.0f;
+                const int8_t * xt = xi + t * K;
+                for (int64_t b = 0; b < nb; b++) {  /* block b -> lane b % 64, ascending */
+                    int sumi = 0;
+                    for (int j = 0; j < 32; j++) sumi += (int)wi8[b * 32 + j] * (int)xt[b * 32 + j];
+                    acc[b & 63] = fmaf(dw[b] * xd[t * nb + b], (float)sumi, acc[b & 63]);
+                    if (one) acc2[b & 63] += mw[b] * xs[t * nb + b];
+                }
+                const float s = tree_f(acc, 64);
+                y[t * M + m] = one ? s + tree_f(acc2, 64) : s + 0.0f;
+            }
+        }
+        free(wi8);
+        free(dw);
+        free(mw);
+    }
+    free(xq);
+    free(xi);
+    free(xd);
+    free(xs);
+}
+
 /* ggml_mul_mat(W, x) with W ne=[K, M] (row m = K contiguous elements). */
 void oracle_matmul(int wtype, const void * Wv, int64_t K, int64_t M,
                    const float * x, int64_t T, float * y) {
     const uint8_t * W = (const uint8_t *)Wv;
+    if (g_variant & OV_GPU) {
+        matmul_gpu(wtype, W, K, M, x, T, y);
+        return;
+    }
     const int nthr = oracle_get_threads();
     (void)nthr;
     if (wtype == OT_FP32) {
@@ -843,6 +1039,17 @@ void oracle_init_state(const oracle_model * m, float * state) {
 
 /* ggml_norm (double accumulation) then *w +b, rwkv_operators.inc:93-97 */
 static void norm_row(const float * x, float * y, int64_t n, float eps, const float * w, const float * b) {
+    if ((g_variant & OV_GPU) && n % 64 == 0) {
+        float mean, scale;
+        ln_stats_gpu(x, n, eps, &mean, &scale);
+        for (int64_t i = 0; i < n; i++) {
+            float v = (x[i] - mean) * scale;
+            if (w) v = v * w[i];
+            if (b) v = v + b[i];
+            y[i] = v;
+        }
+        return;
+    }
     double sum = 0.0;
     float fs = 0.0f;
     for (int64_t ii = 0; ii < n; ii++) {
@@ -867,8 +1074,8 @@ static void norm_row(const float * x, float * y, int64_t n, float eps, const flo
     if (b) for (int64_t i = 0; i < n; i++) y[i] = y[i] + b[i];
 }
 
-static inline float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
-static inline float siluf_(float x) { return x / (1.0f + expf(-x)); }
+static inline float sigmoidf_(float x) { return 1.0f / (1.0f + o_exp(-x)); }
+static inline float siluf_(float x) { return x / (1.0f + o_exp(-x)); }
 
 static void mm(const otensor * W, const float * x, int64_t T, float * y) {
     oracle_matmul((int)W->type, W->data, W->ne[0], W->ne[1], x, T, y);
@@ -879,6 +1086,36 @@ static void mm(const otensor * W, const float * x, int64_t T, float * y) {
 static void wkv6(int64_t T, int64_t H, int64_t S, const float * k, const float * v, const float * r,
                  const float * u, const float * w, int w_per_token, float * state, float * y) {
     const int64_t C = H * S;
+    if (g_variant & OV_GPU) {
+        /* k_att6_dec / k_wkv6 / k_wkv6_s64: value column j, keys split in G groups of IPG */
+        const int64_t G = (256 / S) < S ? (256 / S) : S, IPG = S / G;
+        for (int64_t t = 0; t < T; t++) {
+            const float * wt = w + (w_per_token ? t * C : 0);
+            for (int64_t h = 0; h < H; h++) {
+                float * st = state + h * S * S;
+                const int64_t o = t * C + h * S;
+                for (int64_t j = 0; j < S; j++) {
+                    float part[64];
+                    for (int64_t g = 0; g < G; g++) {
+                        float acc = 0.0f, p4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+                        for (int64_t ii = 0; ii < IPG; ii++) {
+                            const int64_t i = g * IPG + ii;
+                            const float prev = st[i * S + j];
+                            const float kv = v[o + j] * k[o + i];
+                            const float temp = kv * u[h * S + i] + prev;
+                            const float tt = temp * r[o + i];
+                            acc += tt;
+                            p4[ii >> 2] += tt;
+                            st[i * S + j] = prev * wt[h * S + i] + kv;
+                        }
+                        part[g] = IPG == 16 ? (p4[0] + p4[1]) + (p4[2] + p4[3]) : acc;
+                    }
+                    y[o + j] = bfly_f(part, (int)G);
+                }
+            }
+        }
+        return;
+    }
     for (int64_t t = 0; t < T; t++) {
         const float * wt = w + (w_per_token ? t * C : 0);
         for (int64_t i = 0; i < C; i++) y[t * C + i] = 0.0f;
@@ -904,6 +1141,38 @@ static void wkv6(int64_t T, int64_t H, int64_t S, const float * k, const float *
 static void wkv7(int64_t T, int64_t H, int64_t S, const float * r, const float * w, const float * k,
                  const float * v, const float * a, const float * b, float * state, float * y) {
     const int64_t C = H * S;
+    if (g_variant & OV_GPU) {
+        /* k_att7_dec / k_wkv7 / k_wkv7_s64: value row i, keys split in G groups of JPG */
+        const int64_t G = (256 / S) < S ? (256 / S) : S, JPG = S / G;
+        for (int64_t t = 0; t < T; t++)
+            for (int64_t h = 0; h < H; h++) {
+                float * st = state + h * S * S;
+                const int64_t th = t * C + h * S;
+                for (int64_t i = 0; i < S; i++) {
+                    float sa[64], acc[64];
+                    for (int64_t g = 0; g < G; g++) {
+                        float s = 0.0f;
+                        for (int64_t jj = 0; jj < JPG; jj++) s += a[th + g * JPG + jj] * st[i * S + g * JPG + jj];
+                        sa[g] = s;
+                    }
+                    const float sat = bfly_f(sa, (int)G);
+                    const float vi = v[th + i];
+                    for (int64_t g = 0; g < G; g++) {
+                        float s = 0.0f;
+                        for (int64_t jj = 0; jj < JPG; jj++) {
+                            const int64_t j = g * JPG + jj;
+                            const float kv = vi * k[th + j];
+                            const float ns = st[i * S + j] * w[th + j] + kv + sat * b[th + j];
+                            st[i * S + j] = ns;
+                            s += ns * r[th + j];
+                        }
+                        acc[g] = s;
+                    }
+                    y[th + i] = bfly_f(acc, (int)G);
+                }
+            }
+        return;
+    }
     for (int64_t t = 0; t < T; t++) {
         for (int64_t h = 0; h < H; h++) {
             float * st = state + h * S * S;
@@ -949,6 +1218,28 @@ static void mix_v4(const float * xa, const float * xp, const float * mu, int64_t
 }
 
 static void group_norm(float * x, int64_t T, int64_t H, int64_t S, float eps, const float * w, const float * b) {
+    if (g_variant & OV_GPU) {
+        /* k_att6_dec / k_att7_dec / k_groupnorm: fp64 butterfly sums over the head's S lanes */
+        double buf[64];
+        for (int64_t t = 0; t < T; t++)
+            for (int64_t h = 0; h < H; h++) {
+                float * p = x + t * H * S + h * S;
+                for (int64_t i = 0; i < S; i++) buf[i] = (double)p[i];
+                const float mean = (float)(bfly_d(buf, (int)S) / (double)S);
+                for (int64_t i = 0; i < S; i++) {
+                    const float d = p[i] - mean;
+                    buf[i] = (double)(d * d);
+                }
+                const float var = (float)(bfly_d(buf, (int)S) / (double)S);
+                const float scale = 1.0f / sqrtf(var + eps);
+                for (int64_t i = 0; i < S; i++) {
+                    float o = (p[i] - mean) * scale;
+                    o = o * w[h * S + i];
+                    p[i] = o + b[h * S + i];
+                }
+            }
+        return;
+    }
     float * tmp = ALLOC(S);
     for (int64_t t = 0; t < T; t++)
         for (int64_t h = 0; h < H; h++) {
@@ -978,13 +1269,13 @@ static void layer_v4(const oracle_model * m, const olayer * L, float * x, int64_
             const float kt = k[t * C + c], vt = v[t * C + c];
             float ww = L->att_first[c] + kt;
             float qq = fmaxf(pp[c], ww);
-            float e1 = expf(pp[c] - qq), e2 = expf(ww - qq);
+            float e1 = o_exp(pp[c] - qq), e2 = o_exp(ww - qq);
             float a = e1 * aa[c] + e2 * vt;
             float bsum = e1 * bb[c] + e2;
             ww = pp[c] + L->att_decay[c];
             qq = fmaxf(ww, kt);
-            e1 = expf(ww - qq);
-            e2 = expf(kt - qq);
+            e1 = o_exp(ww - qq);
+            e2 = o_exp(kt - qq);
             aa[c] = e1 * aa[c] + e2 * vt;
             bb[c] = e1 * bb[c] + e2;
             pp[c] = qq;
@@ -1066,7 +1357,7 @@ static void layer_v6(const oracle_model * m, const olayer * L, float * x, int64_
         xxx[i] = sx[i] * L->maa_x[i % C] + xa[i];
     }
     mm(L->maa_w1, xxx, T, lora);
-    for (int64_t i = 0; i < T * D5; i++) lora[i] = tanhf(lora[i]);
+    for (int64_t i = 0; i < T * D5; i++) lora[i] = o_tanh(lora[i]);
     /* bmm with time_maa_w2 [5][C][D] (ne=[D,C,5]); order w,k,v,r,g */
     for (int n = 0; n < 5; n++)
         for (int64_t t = 0; t < T; t++)
@@ -1084,11 +1375,11 @@ static void layer_v6(const oracle_model * m, const olayer * L, float * x, int64_
     mm(L->att_g, xs[4], T, g);
     for (int64_t i = 0; i < T * C; i++) g[i] = siluf_(g[i]);
     mm(L->decay_w1, xs[0], T, dl);
-    for (int64_t i = 0; i < T * DW; i++) dl[i] = tanhf(dl[i]);
+    for (int64_t i = 0; i < T * DW; i++) dl[i] = o_tanh(dl[i]);
     mm(L->decay_w2, dl, T, w);
     for (int64_t i = 0; i < T * C; i++) {
         float ww = w[i] + L->att_decay[i % C];
-        w[i] = expf(-expf(ww));
+        w[i] = o_exp(-o_exp(ww));
     }
     wkv6(T, H, S, k, v, r, L->att_faaaa, w, 1, heads, y);
     group_norm(y, T, H, S, 64e-5f, L->att_lnx_w, L->att_lnx_b);
@@ -1152,9 +1443,9 @@ static void layer_v7(const oracle_model * m, const olayer * L, float * x, int64_
     mm(L->a2, tmp, T, a);
     for (int64_t i = 0; i < T * C; i++) a[i] = sigmoidf_(a[i] + L->a0[i % C]);
     mm(L->w1, xs[1], T, tmp);
-    for (int64_t i = 0; i < T * DW; i++) tmp[i] = tanhf(tmp[i]);
+    for (int64_t i = 0; i < T * DW; i++) tmp[i] = o_tanh(tmp[i]);
     mm(L->w2, tmp, T, w);
-    for (int64_t i = 0; i < T * C; i++) w[i] = expf(sigmoidf_(w[i] + L->w0[i % C]) * -0.606531f);
+    for (int64_t i = 0; i < T * C; i++) w[i] = o_exp(sigmoidf_(w[i] + L->w0[i % C]) * -0.606531f);
     mm(L->att_k, xs[2], T, k);
     for (int64_t i = 0; i < T * C; i++) kk[i] = k[i] * L->k_k[i % C];
     /* rwkv_l2norm per head, rwkv_operators.inc:40-82 */
@@ -1162,7 +1453,13 @@ static void layer_v7(const oracle_model * m, const olayer * L, float * x, int64_
         for (int64_t h = 0; h < H; h++) {
             float * p = kk + t * C + h * S;
             float sum = 0.0f;
-            for (int64_t i = 0; i < S; i++) sum += p[i] * p[i];
+            if (g_variant & OV_GPU) {
+                float sq[64];
+                for (int64_t i = 0; i < S; i++) sq[i] = p[i] * p[i];
+                sum = bfly_f(sq, (int)S);
+            } else {
+                for (int64_t i = 0; i < S; i++) sum += p[i] * p[i];
+            }
             const float scale = 1.0f / fmaxf(sqrtf(sum), 1e-12f);
             for (int64_t i = 0; i < S; i++) p[i] = p[i] * scale;
         }
@@ -1188,7 +1485,13 @@ static void layer_v7(const oracle_model * m, const olayer * L, float * x, int64_
         for (int64_t h = 0; h < H; h++) {
             const int64_t o0 = t * C + h * S;
             float sum = 0.0f;
-            for (int64_t i = 0; i < S; i++) sum += (k[o0 + i] * r[o0 + i]) * L->r_k[h * S + i];
+            if (g_variant & OV_GPU) {
+                float pr[64];
+                for (int64_t i = 0; i < S; i++) pr[i] = (k[o0 + i] * r[o0 + i]) * L->r_k[h * S + i];
+                sum = bfly_f(pr, (int)S);
+            } else {
+                for (int64_t i = 0; i < S; i++) sum += (k[o0 + i] * r[o0 + i]) * L->r_k[h * S + i];
+            }
             for (int64_t i = 0; i < S; i++) y[o0 + i] = y[o0 + i] + v[o0 + i] * sum;
         }
     for (int64_t i = 0; i < T * C; i++) y[i] = y[i] * g[i];

@@ -51,8 +51,15 @@ int oracle_eval_layers(const oracle_model * m, const uint32_t * tokens, size_t T
 /* rwkv_quantize_model_file semantics (rwkv_quantize.inc:16-171).  0 on success. */
 int oracle_quantize_file(const char * in_path, const char * out_path, const char * format);
 
-/* 0: ggml-mirror numerics (default).  1, 2: re-associated reductions (noise-floor probes). */
+/* 0: ggml-mirror numerics (default).  Bits 1, 2, 4: re-associated reductions (noise-floor
+ * probes).  Bit 8 (ORACLE_VARIANT_GPU): the MI355X kernels' association and their exp/tanh, which
+ * the GPU path reproduces bit for bit (oracle.c "GPU-association variant"). */
+#define ORACLE_VARIANT_GPU 8
 void oracle_set_variant(int v);
+
+/* The kernels' exp / tanh restated (device_common.hpp rk_expf / rk_tanhf). */
+float oracle_gpu_expf(float x);
+float oracle_gpu_tanhf(float x);
 
 /* Number of OpenMP threads used by the matmuls (<=0: library default). */
 void oracle_set_threads(int n);

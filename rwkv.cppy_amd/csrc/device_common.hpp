@@ -74,11 +74,56 @@ __device__ inline double block_sum_d(double v, double * sh) {
     return r;
 }
 
-__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
-__device__ __forceinline__ float siluf_(float x) { return x / (1.0f + expf(-x)); }
+// exp / tanh as fixed sequences of IEEE-exact operations (fma, mul, add, correctly rounded
+// division, rint, ldexp), so a CPU restatement reproduces every result bit for bit (the oracle's
+// GPU-association variant, oracle.c gpu_expf / gpu_tanhf).  The device libm (ocml) routes exp
+// through v_exp_f32, whose rounding is not specified.  Accuracy: <= 1 ulp over the float range.
+//   exp: x = n ln2 + r (Cody-Waite, |r| <= ln2/2), e^r = 1 + r + r^2 Q(r), degree-4 Q (fitted).
+//   tanh: |x| < 0.625: x + x^3 P(x^2), degree-4 P (fitted); else 1 - 2 / (e^{2|x|} + 1).
+__device__ __forceinline__ float rk_expf(float x) {
+    if (x != x) return x;
+    if (x > 0x1.62e43p+6f) return __int_as_float(0x7f800000);
+    if (x < -0x1.9fe36ap+6f) return 0.0f;
+    const float n = rintf(x * 0x1.715476p+0f);
+    float r = fmaf(n, -0x1.62e43p-1f, x);
+    r = fmaf(n, 0x1.05c61p-29f, r);
+    float q = 0x1.687c22p-10f;
+    q = fmaf(q, r, 0x1.123b8ep-7f);
+    q = fmaf(q, r, 0x1.555b58p-5f);
+    q = fmaf(q, r, 0x1.55548ep-3f);
+    q = fmaf(q, r, 0x1.fffff8p-2f);
+    const float r2 = r * r;
+    const float p = fmaf(r2, q, r) + 1.0f;
+    return ldexpf(p, (int)n);
+}
+__device__ __forceinline__ float rk_tanhf(float x) {
+    const float ax = fabsf(x);
+    if (ax < 0.625f) {
+        const float x2 = x * x;
+        float p = -0x1.7507acp-8f;
+        p = fmaf(p, x2, 0x1.51f0f0p-6f);
+        p = fmaf(p, x2, -0x1.b83322p-5f);
+        p = fmaf(p, x2, 0x1.1106d6p-3f);
+        p = fmaf(p, x2, -0x1.555532p-2f);
+        return fmaf(x * x2, p, x);
+    }
+    const float t = ax > 9.0f ? 1.0f : 1.0f - 2.0f / (rk_expf(ax + ax) + 1.0f);
+    return copysignf(t, x);
+}
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + rk_expf(-x)); }
+__device__ __forceinline__ float siluf_(float x) { return x / (1.0f + rk_expf(-x)); }
 
 __device__ __forceinline__ float h2f(uint16_t b) { return __half2float(__ushort_as_half(b)); }
-__device__ __forceinline__ float f16_round(float f) { return __half2float(__float2half(f)); }
+// f32 -> f16 of a value that was first rounded to f32 (ggml's GGML_FP32_TO_FP16(d * sum): two
+// roundings).  The empty asm pins f as an f32 register value: without it the backend folds
+// fptrunc(fmul(a, b)) into v_fma_mixlo_f16 a, b, 0 -- ONE rounding of the exact product, which
+// differs from the two-step result whenever the f32 product lands on an f16 midpoint
+// (tools/debug_stage.py found it in the Q8_1 s = d * sum of the activation quantizer).
+__device__ __forceinline__ __half to_half(float f) {
+    asm volatile("" : "+v"(f));
+    return __float2half(f);
+}
+__device__ __forceinline__ float f16_round(float f) { return __half2float(to_half(f)); }
 
 // Reductions across each 32-lane half-wave (all lanes get the result): DPP inside the 16-lane
 // rows, then v_permlane16_swap between the two rows of the half.  Max and integer sums are
@@ -155,7 +200,7 @@ __device__ __forceinline__ void emit32(const ActBuf & a, int t, int k, float v) 
         return;
     }
     if (a.fmt == A_F16) {
-        a.h[idx] = __float2half(v);
+        a.h[idx] = to_half(v);
         return;
     }
     store32(a, t, k, quant32(v));
@@ -278,12 +323,27 @@ __device__ __forceinline__ int block_dot(const DMat & W, int row, int b, int nb,
 
 typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
 
+// F16 dot of one 16-byte unit (8 halves of w and x): acc = fma(w[k], x[k], acc) for k = 0..7 in
+// order, the halves widened exactly to f32.  (v_dot2_f32_f16 is not used: its internal rounding
+// is unspecified -- tools/arith_probe.hip measured 11% of results off a single-rounding model --
+// so no CPU restatement could reproduce it.)
+__device__ __forceinline__ float dot8_f16(const int4 & w, const int4 & x, float acc) {
+    const int wv[4] = {w.x, w.y, w.z, w.w}, xv[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const half2_t a = __builtin_bit_cast(half2_t, wv[i]), b = __builtin_bit_cast(half2_t, xv[i]);
+        acc = fmaf((float)a.x, (float)b.x, acc);
+        acc = fmaf((float)a.y, (float)b.y, acc);
+    }
+    return acc;
+}
+
 // apply_epi with y[t][row] (yv) and aux[t][row] (av) already loaded (only read by the epilogues
 // that use them: ADD / SIGMUL_ADD / VMIX7)
 __device__ __forceinline__ float apply_epi_v(const MMEntry & E, int row, float acc, float yv, float av) {
     switch (E.epi) {
         case EPI_SIGMOID: return sigmoidf_(acc);
-        case EPI_TANH: return tanhf(acc);
+        case EPI_TANH: return rk_tanhf(acc);
         case EPI_SILU: return siluf_(acc);
         case EPI_RELU_SQ: {
             const float r = acc > 0.0f ? acc : 0.0f;
@@ -291,8 +351,8 @@ __device__ __forceinline__ float apply_epi_v(const MMEntry & E, int row, float a
         }
         case EPI_ADD: return yv + acc;
         case EPI_SIGMUL_ADD: return yv + sigmoidf_(av) * acc;
-        case EPI_DECAY6: return expf(-expf(acc + E.bias[row]));
-        case EPI_DECAY7: return expf(sigmoidf_(acc + E.bias[row]) * -0.606531f);
+        case EPI_DECAY6: return rk_expf(-rk_expf(acc + E.bias[row]));
+        case EPI_DECAY7: return rk_expf(sigmoidf_(acc + E.bias[row]) * -0.606531f);
         case EPI_SIGMOID_BIAS: return sigmoidf_(acc + E.bias[row]);
         case EPI_VMIX7: return yv + (av - yv) * sigmoidf_(acc + E.bias[row]);
         default: return acc;
@@ -305,7 +365,7 @@ __device__ __forceinline__ float apply_epi(const MMEntry & E, int t, int row, fl
     const size_t yi = (size_t)t * E.ldy + row;
     switch (E.epi) {
         case EPI_SIGMOID: return sigmoidf_(acc);
-        case EPI_TANH: return tanhf(acc);
+        case EPI_TANH: return rk_tanhf(acc);
         case EPI_SILU: return siluf_(acc);
         case EPI_RELU_SQ: {
             const float r = acc > 0.0f ? acc : 0.0f;
@@ -313,8 +373,8 @@ __device__ __forceinline__ float apply_epi(const MMEntry & E, int t, int row, fl
         }
         case EPI_ADD: return E.y[yi] + acc;
         case EPI_SIGMUL_ADD: return E.y[yi] + sigmoidf_(E.aux[yi]) * acc;
-        case EPI_DECAY6: return expf(-expf(acc + E.bias[row]));
-        case EPI_DECAY7: return expf(sigmoidf_(acc + E.bias[row]) * -0.606531f);
+        case EPI_DECAY6: return rk_expf(-rk_expf(acc + E.bias[row]));
+        case EPI_DECAY7: return rk_expf(sigmoidf_(acc + E.bias[row]) * -0.606531f);
         case EPI_SIGMOID_BIAS: return sigmoidf_(acc + E.bias[row]);
         case EPI_VMIX7: {
             const float v = E.y[yi];

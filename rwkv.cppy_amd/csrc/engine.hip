@@ -1314,6 +1314,31 @@ bool Engine::eval_layers(const uint32_t * tokens, size_t T, uint32_t l0, uint32_
     return true;
 }
 
+// Names: x xa sx r k v g w y a nb bb vfirst fr lora bonus logits, slot<i>.<q|d|s|qsum|h|f>.
+long long Engine::debug_copy(const char * name, void * out, size_t bytes) {
+    if (!name || !out) return -1;
+    const std::string n(name);
+    const void * src = nullptr;
+    const std::pair<const char *, float *> fb[] = {{"x", x_}, {"xa", xa_}, {"sx", sx_}, {"r", r_}, {"k", k_},
+        {"v", v_}, {"g", g_}, {"w", w_}, {"y", y_}, {"a", a_}, {"nb", nb_}, {"bb", bb_}, {"vfirst", vfirst_},
+        {"fr", fr_}, {"lora", lora_}, {"bonus", bonus_}, {"logits", logits_}};
+    for (const auto & p : fb)
+        if (n == p.first) src = p.second;
+    if (!src && n.rfind("slot", 0) == 0) {
+        const size_t dot = n.find('.');
+        const int i = atoi(n.c_str() + 4);
+        if (dot == std::string::npos || i < 0 || i >= kSlots) return -1;
+        const std::string f = n.substr(dot + 1);
+        const ActSlot & s = slots_[i];
+        src = f == "q" ? (const void *)s.q : f == "d" ? (const void *)s.d : f == "s" ? (const void *)s.s
+            : f == "qsum" ? (const void *)s.qsum : f == "h" ? (const void *)s.h : f == "f" ? (const void *)s.f : nullptr;
+    }
+    if (!src) return -1;
+    if (hipStreamSynchronize(stream_) != hipSuccess || hipMemcpy(out, src, bytes, hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
+    return (long long)bytes;
+}
+
 bool Engine::eval_device(const uint32_t * tokens, size_t T, bool want_logits, float * logits_out, bool sync_after) {
     HIP_OK(hipSetDevice(m_->device));
     if (!run_tokens(tokens, T, want_logits || logits_out != nullptr)) return false;

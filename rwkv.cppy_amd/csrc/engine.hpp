@@ -94,6 +94,8 @@ class Engine {
     bool mm_launch(MMGroup & g, int wtype);
     const std::vector<KernelStat> & stats();
     float * device_state() const { return dstate_[cur_]; }
+    // debugging aid (rwkv_mi355x_debug_buffer): copies a workspace buffer of the last evaluation
+    long long debug_copy(const char * name, void * out, size_t bytes);
 
   private:
     bool ensure_workspace(int T);

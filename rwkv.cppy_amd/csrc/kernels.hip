@@ -57,12 +57,7 @@ __device__ __forceinline__ void mm_accumulate(const MMEntry & E, int row0, int t
                     const int4 w = *(const int4 *)((const __half *)W.qs + (size_t)row * K + k);
 #pragma unroll
                     for (int n = 0; n < NT; n++) {
-                        float a = acc[r][n];
-                        a = __builtin_amdgcn_fdot2(__builtin_bit_cast(half2_t, w.x), __builtin_bit_cast(half2_t, x[n].x), a, false);
-                        a = __builtin_amdgcn_fdot2(__builtin_bit_cast(half2_t, w.y), __builtin_bit_cast(half2_t, x[n].y), a, false);
-                        a = __builtin_amdgcn_fdot2(__builtin_bit_cast(half2_t, w.z), __builtin_bit_cast(half2_t, x[n].z), a, false);
-                        a = __builtin_amdgcn_fdot2(__builtin_bit_cast(half2_t, w.w), __builtin_bit_cast(half2_t, x[n].w), a, false);
-                        acc[r][n] = a;
+                        acc[r][n] = dot8_f16(w, x[n], acc[r][n]);
                     }
                 }
             }
@@ -516,13 +511,13 @@ __global__ __launch_bounds__(256) void k_wkv4(int T, int C, const float * r, con
         const float kt = k[i], vt = v[i];
         float ww = fi + kt;
         float qq = fmaxf(pp, ww);
-        float e1 = expf(pp - qq), e2 = expf(ww - qq);
+        float e1 = rk_expf(pp - qq), e2 = rk_expf(ww - qq);
         const float an = e1 * aa + e2 * vt;
         const float bn = e1 * bb + e2;
         ww = pp + de;
         qq = fmaxf(ww, kt);
-        e1 = expf(ww - qq);
-        e2 = expf(kt - qq);
+        e1 = rk_expf(ww - qq);
+        e2 = rk_expf(kt - qq);
         aa = e1 * aa + e2 * vt;
         bb = e1 * bb + e2;
         pp = qq;

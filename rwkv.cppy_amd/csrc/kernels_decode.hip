@@ -238,13 +238,13 @@ __device__ __forceinline__ void decay_rows(const Att6Dec & a, const ActBuf & act
         const WBlk none[1] = {};
         if (tid < S) {
             const float s = decay_row_thread<WF, 0, 16>(a.wd2, c0 + tid, act, nl, none);
-            sw[tid] = expf(-expf(s + a.decay[c0 + tid]));
+            sw[tid] = rk_expf(-rk_expf(s + a.decay[c0 + tid]));
         }
     } else {
         const int lane = tid & 63, nw = blockDim.x >> 6;
         for (int j = tid >> 6; j < S; j += nw) {
             const float s = decay_row_wave<WF>(a.wd2, c0 + j, act, lane);
-            if (lane == 63) sw[j] = expf(-expf(s + a.decay[c0 + j]));
+            if (lane == 63) sw[j] = rk_expf(-rk_expf(s + a.decay[c0 + j]));
         }
     }
 }
@@ -303,7 +303,7 @@ __global__ __launch_bounds__(256) void k_att6_dec(Att6Dec a) {
         } else if constexpr (PF > 0) {
             if (tid < S) {
                 const float s = decay_row_thread<WF, PF, PF>(a.wd2, c0 + tid, act, a.wd2.K >> 5, wp);
-                sw[tid] = expf(-expf(s + dec_c));
+                sw[tid] = rk_expf(-rk_expf(s + dec_c));
             }
         } else {
             switch (a.wd2.type) {
@@ -437,7 +437,7 @@ __global__ __launch_bounds__(256) void k_v6_decay_seq(int T, int C, DMat wd2, co
     for (int tt = 0; tt < nt; tt++) {
         const ActBuf act = lds_act(smem + tt * abytes, fmt, D);
         const float s = decay_row_thread<WF, 4, 4>(wd2, row, act, nb, wp);
-        w[(size_t)(t0 + tt) * C + row] = expf(-expf(s + dec));
+        w[(size_t)(t0 + tt) * C + row] = rk_expf(-rk_expf(s + dec));
     }
 }
 

@@ -160,12 +160,7 @@ __device__ __forceinline__ void dot_unit(const WBlk & w, const AUnit & x, float 
         s = fmaf(__int_as_float(w.q0.w), __int_as_float(x.lo.w), s);
         acc = s;
     } else if constexpr (WF == W_F16) {
-        float s = acc;
-        s = __builtin_amdgcn_fdot2(__builtin_bit_cast(half2_t, w.q0.x), __builtin_bit_cast(half2_t, x.lo.x), s, false);
-        s = __builtin_amdgcn_fdot2(__builtin_bit_cast(half2_t, w.q0.y), __builtin_bit_cast(half2_t, x.lo.y), s, false);
-        s = __builtin_amdgcn_fdot2(__builtin_bit_cast(half2_t, w.q0.z), __builtin_bit_cast(half2_t, x.lo.z), s, false);
-        s = __builtin_amdgcn_fdot2(__builtin_bit_cast(half2_t, w.q0.w), __builtin_bit_cast(half2_t, x.lo.w), s, false);
-        acc = s;
+        acc = dot8_f16(w.q0, x.lo, acc);
     } else {
         float dw, mw;
         const int sumi = dot_wblk<WF>(w, x.lo, x.hi, x.qs, dw, mw);
@@ -247,7 +242,7 @@ __device__ __forceinline__ void chunk_store(const MVEntry & E, const ActBuf & a,
         int p[4];
 #pragma unroll
         for (int j = 0; j < 4; j++)
-            p[j] = __builtin_bit_cast(int, __halves2half2(__float2half(v[2 * j]), __float2half(v[2 * j + 1])));
+            p[j] = __builtin_bit_cast(int, __halves2half2(to_half(v[2 * j]), to_half(v[2 * j + 1])));
         if (valid) *(int4 *)(a.h + k0) = make_int4(p[0], p[1], p[2], p[3]);
     } else {
         // ggml quantize_row_q8_0 / q8_1 (x86): d = amax/127, q = rint(x*127/amax)
@@ -300,7 +295,7 @@ __device__ __forceinline__ EpiIn epi_load(const MVEntry & E, int row) {
 __device__ __forceinline__ float epi_apply(int epi, float acc, const EpiIn & p) {
     switch (epi) {
         case EPI_SIGMOID: return sigmoidf_(acc);
-        case EPI_TANH: return tanhf(acc);
+        case EPI_TANH: return rk_tanhf(acc);
         case EPI_SILU: return siluf_(acc);
         case EPI_RELU_SQ: {
             const float r = acc > 0.0f ? acc : 0.0f;
@@ -308,8 +303,8 @@ __device__ __forceinline__ float epi_apply(int epi, float acc, const EpiIn & p) 
         }
         case EPI_ADD: return p.y + acc;
         case EPI_SIGMUL_ADD: return p.y + sigmoidf_(p.aux) * acc;
-        case EPI_DECAY6: return expf(-expf(acc + p.bias));
-        case EPI_DECAY7: return expf(sigmoidf_(acc + p.bias) * -0.606531f);
+        case EPI_DECAY6: return rk_expf(-rk_expf(acc + p.bias));
+        case EPI_DECAY7: return rk_expf(sigmoidf_(acc + p.bias) * -0.606531f);
         case EPI_SIGMOID_BIAS: return sigmoidf_(acc + p.bias);
         case EPI_VMIX7: return p.y + (p.aux - p.y) * sigmoidf_(acc + p.bias);
         default: return acc;

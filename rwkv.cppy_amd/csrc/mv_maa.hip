@@ -89,7 +89,7 @@ __global__ __launch_bounds__(512) void k_v6_maa_dec(MaaDec a) {
 #pragma unroll
         for (int r = 0; r < R; r++) {
             const float s = one ? wave_sum63(acc[r]) + wave_sum63(acc2[r]) : wave_sum63(acc[r]) + 0.0f;
-            if (lane == 63 && wave * R + r < D) s_lora[wave * R + r] = tanhf(s);  // EPI_TANH
+            if (lane == 63 && wave * R + r < D) s_lora[wave * R + r] = rk_tanhf(s);  // EPI_TANH
         }
         __syncthreads();  // (2) lora_n ready
         // k_v6_mix5_dec's arithmetic: m = sum_i (double)(w2[i] * lora[i]) in order

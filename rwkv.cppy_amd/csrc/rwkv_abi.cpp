@@ -240,6 +240,9 @@ RWKV_API bool rwkv_mi355x_eval_layers(struct rwkv_context * ctx, const uint32_t 
 }
 
 RWKV_API bool rwkv_mi355x_sync(struct rwkv_context * ctx) { return ctx->engine->sync(); }
+RWKV_API long long rwkv_mi355x_debug_buffer(struct rwkv_context * ctx, const char * name, void * out, size_t bytes) {
+    return ctx && ctx->engine ? ctx->engine->debug_copy(name, out, bytes) : -1;
+}
 RWKV_API void * rwkv_mi355x_stream(struct rwkv_context * ctx) { return (void *)ctx->engine->stream(); }
 RWKV_API float * rwkv_mi355x_device_state(struct rwkv_context * ctx) { return ctx->engine->device_state(); }
 

@@ -149,6 +149,36 @@ def set_variant(v):
     L.oracle_set_variant(v)
 
 
+# Variant bit 8: the GPU kernels' association (oracle.c "GPU-association variant") -- the variant the
+# MI355X path must reproduce bit for bit.
+VARIANT_GPU = 8
+
+
+def gpu_variant(path, tokens, sequence=False, state_in=None):
+    """(logits, state) of the oracle's GPU-association variant: serial single-token evals, or one
+    eval_sequence call when sequence=True."""
+    set_variant(VARIANT_GPU)
+    try:
+        m = OracleModel(path)
+        out = m.eval_sequence(tokens, state_in) if sequence else m.eval_serial(tokens, state_in)
+        m.close()
+    finally:
+        set_variant(0)
+    return out
+
+
+def assert_bits_equal(a, b, what=''):
+    """Bit-for-bit equality of two float32 arrays (a -0.0 / +0.0 difference counts)."""
+    a = np.ascontiguousarray(a, np.float32)
+    b = np.ascontiguousarray(b, np.float32)
+    assert a.shape == b.shape, (what, a.shape, b.shape)
+    ne = np.flatnonzero(a.view(np.uint32) != b.view(np.uint32))
+    if ne.size:
+        i = int(ne[0])
+        raise AssertionError(f'{what}: {ne.size} of {a.size} values differ; first at {i}: {a[i]!r} vs {b[i]!r}, '
+                             f'max|d| {float(np.nanmax(np.abs(a - b))):.3g}')
+
+
 def noise_band(path, tokens, sequence=False):
     """Oracle logits/state (variant 0) plus the largest deviation any re-associated variant
     (1..7: reversed order / scalar ggml dot / fp32 accumulators) produces: how strongly this

@@ -4,7 +4,8 @@
 - activation quantizer (emit stage of every producer kernel) vs oracle_quantize_act:
   bit-exact int8 codes and fp16 scales (ggml quantize_row_q8_0/q8_1 x86 semantics).
 - matmul kernel (every weight format, decode T=1 and batched T>1, ragged M/K) vs
-  oracle_matmul: identical integer block dots, so only the fp32 summation order differs:
+  oracle_matmul: bit-exact against the oracle's GPU-association variant (same block dots, same
+  fp32 association); against the ggml-order oracle only the fp32 summation order differs:
   |y_gpu - y_oracle| <= 1e-5 * (|W| |x|) + 1e-6 elementwise.
 - int8-MFMA sequence GEMM vs the matvec/matmul kernel: bit-exact (same block dots, same fp32
   association), across formats, ragged M/T and K spanning 1..7 lane classes per row.
@@ -14,7 +15,8 @@ import ctypes
 import numpy as np
 import pytest
 
-from oracle_ctypes import TYPE_IDS, dequantize, matmul as oracle_matmul, quantize_act, quantize_rows
+from oracle_ctypes import (TYPE_IDS, VARIANT_GPU, assert_bits_equal, dequantize, matmul as oracle_matmul,
+                           quantize_act, quantize_rows, set_variant)
 from rwkv_lib import library
 
 pytestmark = pytest.mark.gpu
@@ -35,6 +37,23 @@ def lib():
     return L
 
 
+def double_rounding_blocks(n, seed=5):
+    """n 32-element blocks whose Q8_1 s = fp16(fp32(d * sum)) differs from a single rounding of the
+    exact product d * sum (the case a fused fp32->fp16 multiply gets wrong)."""
+    rng = np.random.default_rng(seed)
+    found = []
+    while len(found) < n:
+        x = (rng.standard_normal((200000, 32)) * rng.uniform(0.01, 4, (200000, 1))).astype(np.float32)
+        am = np.abs(x).max(1)
+        d = (am / np.float32(127)).astype(np.float32)
+        q = np.rint(x * (np.float32(127) / am)[:, None]).astype(np.int64)
+        exact = d.astype(np.float64) * q.sum(1)
+        two = exact.astype(np.float32).astype(np.float16)
+        one = exact.astype(np.float16)
+        found.extend(x[two != one][: n - len(found)])
+    return np.array(found, np.float32)
+
+
 @pytest.mark.parametrize('wfmt,afmt', [('Q4_0', 'Q8_0'), ('Q4_1', 'Q8_1')])
 def test_activation_quantizer_bit_exact(wfmt, afmt):
     rng = np.random.default_rng(1)
@@ -43,6 +62,9 @@ def test_activation_quantizer_bit_exact(wfmt, afmt):
     x[0, :32] = 0.0                              # all-zero block -> d = 0, q = 0
     x[1, :32] = np.arange(32, dtype=np.float32)  # ties: x*127/31 not integral -> rint path
     x[2, 64:96] = np.float32(0.5)                # every element exactly at amax
+    x[3, :32] *= np.float32(1e-5)                # d and d*sum in the fp16 subnormal range
+    x[3, 32:64] = np.float32(3e-7)               # amax/127 below the smallest fp16 subnormal
+    x[3, 64:64 + 8 * 32] = double_rounding_blocks(8).ravel()  # fp16(fp32(d*sum)) != fp16(d*sum)
     q = np.zeros((T, K), np.int8)
     d = np.zeros(T * K // 32, np.float32)
     s = np.zeros(T * K // 32, np.float32)
@@ -62,6 +84,7 @@ def test_matmul_kernel(fmt, M, K, T):
     rng = np.random.default_rng(M * 7 + K + T)
     w = (rng.standard_normal((M, K)) / np.sqrt(K)).astype(np.float32)
     x = rng.standard_normal((T, K)).astype(np.float32)
+    x[0, :64] *= np.float32(1e-5)  # Q8 scales (and Q8_1 sums) in the fp16 subnormal range
     if fmt == 'FP32':
         wb = w.view(np.uint8).ravel()
     elif fmt == 'FP16':
@@ -70,6 +93,12 @@ def test_matmul_kernel(fmt, M, K, T):
         wb = quantize_rows(fmt, w)
     y = np.zeros((T, M), np.float32)
     assert lib().rwkv_mi355x_selftest_matmul(TYPE_IDS[fmt], wb.ctypes.data, K, M, x.ctypes.data, T, y.ctypes.data)
+    set_variant(VARIANT_GPU)
+    try:
+        ref8 = oracle_matmul(fmt, wb, K, M, x)
+    finally:
+        set_variant(0)
+    assert_bits_equal(y, ref8, f'{fmt} matmul vs GPU-association oracle')
     ref = oracle_matmul(fmt, wb, K, M, x)
     bound = np.abs(x.astype(np.float64)) @ np.abs(dequantize(fmt, wb, K, M).astype(np.float64)).T
     err = np.abs(y.astype(np.float64) - ref)

@@ -350,7 +350,9 @@ bool Engine::ensure_workspace(int T) {
     if (T <= tcap_) return true;
     HIP_OK(hipStreamSynchronize(stream_));
     drop_graphs();
-    // keep state and logits, drop the rest
+    // keep state and logits, drop the rest; until every allocation below has succeeded the
+    // workspace counts as absent (tcap_ = 0, pointers null), so a failed grow can never leave a
+    // capacity that points at freed or missing buffers
     std::vector<void *> keep = {dstate_[0], dstate_[1], logits_};
     if (mv_scratch_) keep.push_back(mv_scratch_);
     for (void * p : ws_allocs_) {
@@ -359,6 +361,12 @@ bool Engine::ensure_workspace(int T) {
         if (!k) (void)hipFree(p);
     }
     ws_allocs_ = keep;
+    tcap_ = 0;
+    float ** fbufs[] = {&x_, &xa_, &sx_, &r_, &k_, &v_, &g_, &w_, &y_, &a_, &nb_, &bb_, &vfirst_, &fr_, &lora_, &bonus_};
+    for (float ** b : fbufs) *b = nullptr;
+    for (auto & p : dsmall_) p = nullptr;
+    dtokens_ = nullptr;
+    for (auto & s : slots_) s = ActSlot{};
     HIP_OK(hipEventSynchronize(tok_event_));
     if (htokens_) {
         (void)hipHostFree(htokens_);
@@ -366,37 +374,58 @@ bool Engine::ensure_workspace(int T) {
     }
     int cap = 1;
     while (cap < T) cap *= 2;
-    tcap_ = cap;
     const size_t C = m_->n_embed, TC = (size_t)cap * C;
+    bool ok = true;
     auto A = [&](size_t bytes) -> void * {
         void * p = nullptr;
-        if (hipMalloc(&p, bytes + 64) != hipSuccess) return nullptr;
+        if (!ok || hipMalloc(&p, bytes + 64) != hipSuccess) {
+            ok = false;
+            return nullptr;
+        }
         ws_allocs_.push_back(p);
         return p;
     };
-    float ** fbufs[] = {&x_, &xa_, &sx_, &r_, &k_, &v_, &g_, &w_, &y_, &a_, &nb_, &bb_, &vfirst_, &fr_};
-    for (float ** b : fbufs)
-        if (!(*b = (float *)A(TC * 4))) return false;
+    float *x = nullptr, *xa = nullptr, *sx = nullptr, *r = nullptr, *k = nullptr, *v = nullptr, *g = nullptr,
+          *w = nullptr, *y = nullptr, *a = nullptr, *nb = nullptr, *bb = nullptr, *vf = nullptr, *fr = nullptr;
+    float ** locals[] = {&x, &xa, &sx, &r, &k, &v, &g, &w, &y, &a, &nb, &bb, &vf, &fr};
+    for (float ** b : locals) *b = (float *)A(TC * 4);
     const size_t kmax = std::max<size_t>((size_t)m_->kmax, C);
-    if (!(lora_ = (float *)A((size_t)cap * kmax * 4))) return false;
-    if (!(bonus_ = (float *)A((size_t)cap * std::max<int64_t>(1, m_->H) * 4))) return false;
-    for (auto & p : dsmall_)
-        if (!(p = (float *)A(kmax * 4))) return false;
-    if (!(dtokens_ = (uint32_t *)A((size_t)cap * 4))) return false;
-    for (auto & s : slots_) {
-        const size_t n = (size_t)cap * kmax, nb = n / 32 + 1;
+    float * lora = (float *)A((size_t)cap * kmax * 4);
+    float * bonus = (float *)A((size_t)cap * std::max<int64_t>(1, m_->H) * 4);
+    float * dsmall[4];
+    for (auto & p : dsmall) p = (float *)A(kmax * 4);
+    uint32_t * dtok = (uint32_t *)A((size_t)cap * 4);
+    ActSlot slots[kSlots];
+    for (auto & s : slots) {
+        const size_t n = (size_t)cap * kmax, nbk = n / 32 + 1;
         s.q = (int8_t *)A(n);
-        s.d = (float *)A(nb * 4);
-        s.s = (float *)A(nb * 4);
-        s.qsum = (int *)A(nb * 4);
+        s.d = (float *)A(nbk * 4);
+        s.s = (float *)A(nbk * 4);
+        s.qsum = (int *)A(nbk * 4);
         s.h = (__half *)A(n * 2);
         s.f = (float *)A(n * 4);
         // sequence-GEMM token tiles: whole QG_TOK-token tiles, records of up to qg_a_bytes(true)
         const size_t ttiles = ((size_t)cap + QG_TOK - 1) / QG_TOK;
         s.tq = (uint8_t *)A(ttiles * (kmax / 32 + 1) * qg_a_bytes(true));
-        if (!s.q || !s.d || !s.s || !s.qsum || !s.h || !s.f || !s.tq) return false;
     }
-    HIP_OK(hipHostMalloc((void **)&htokens_, (size_t)cap * 4, hipHostMallocDefault));
+    uint32_t * htok = nullptr;
+    if (ok && hipHostMalloc((void **)&htok, (size_t)cap * 4, hipHostMallocDefault) != hipSuccess) {
+        htok = nullptr;
+        ok = false;
+    }
+    if (!ok) {
+        (void)hipGetLastError();  // clear the sticky out-of-memory status: later launches check it
+        fprintf(stderr, "rwkv: device workspace allocation for %d tokens failed\n", cap);
+        return false;  // tcap_ stays 0: the next call retries the allocation
+    }
+    for (size_t i = 0; i < sizeof(locals) / sizeof(*locals); i++) *fbufs[i] = *locals[i];
+    lora_ = lora;
+    bonus_ = bonus;
+    for (int i = 0; i < 4; i++) dsmall_[i] = dsmall[i];
+    dtokens_ = dtok;
+    for (int i = 0; i < kSlots; i++) slots_[i] = slots[i];
+    htokens_ = htok;
+    tcap_ = cap;
     return true;
 }
 
@@ -495,7 +524,12 @@ bool Engine::mm_dispatch(MMGroup & g, int wtype) {
         HIP_OK(hipStreamSynchronize(stream_));
         if (gy_) (void)hipFree(gy_);
         gy_ = nullptr;
-        HIP_OK(hipMalloc(&gy_, need * 4 + 64));
+        gy_cap_ = 0;
+        if (hipMalloc(&gy_, need * 4 + 64) != hipSuccess) {
+            gy_ = nullptr;
+            (void)hipGetLastError();
+            return false;
+        }
         gy_cap_ = need;
     }
     // split-K partials for a single small-M entry (launch_qgemm decides)
@@ -505,7 +539,12 @@ bool Engine::mm_dispatch(MMGroup & g, int wtype) {
             HIP_OK(hipStreamSynchronize(stream_));
             if (part_) (void)hipFree(part_);
             part_ = nullptr;
-            HIP_OK(hipMalloc(&part_, pneed * 4 + 64));
+            part_cap_ = 0;
+            if (hipMalloc(&part_, pneed * 4 + 64) != hipSuccess) {
+                part_ = nullptr;
+                (void)hipGetLastError();
+                return false;
+            }
             part_cap_ = pneed;
         }
         g.part = part_;
@@ -1201,6 +1240,19 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits) {
 
 // Runs T tokens from dstate_[cur_] (ping-pong), chunked by the workspace capacity.
 bool Engine::run_tokens(const uint32_t * tokens, size_t T, bool want_logits) {
+    // a failed call restores the ping-pong parity it started with, so the next state upload
+    // (every rwkv_eval with state_in, rwkv_mi355x_state_upload) lands where the next step reads;
+    // the device state's contents after a failure are unspecified (re-upload it)
+    const int cur0 = cur_;
+    if (!run_tokens_impl(tokens, T, want_logits)) {
+        (void)hipStreamSynchronize(stream_);
+        cur_ = cur0;
+        return false;
+    }
+    return true;
+}
+
+bool Engine::run_tokens_impl(const uint32_t * tokens, size_t T, bool want_logits) {
     const size_t kChunkMax = 1024;
     size_t done = 0;
     while (done < T) {

@@ -105,6 +105,7 @@ class Engine {
     bool forward_decode(const float * sin, float * sout, bool logits);
     bool mv(MVGroup & g);
     bool run_tokens(const uint32_t * tokens, size_t T, bool want_logits);
+    bool run_tokens_impl(const uint32_t * tokens, size_t T, bool want_logits);
     bool layer_v4(int l, int T, const float * si, float * so);
     bool layer_v5(int l, int T, const float * si, float * so);
     bool layer_v6(int l, int T, const float * si, float * so);

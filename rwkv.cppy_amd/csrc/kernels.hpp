@@ -129,6 +129,7 @@ struct MVGroup {
     int stride;              // set by launch_mv_group: >0 = workgroups walk row blocks
     int grid;                // set by launch_mv_group: workgroups launched
     int units_max;           // set by launch_mv_group: max 16-byte units per lane over entries
+    int rows;                // set by launch_mv_group: rows per wave of the launched shape
 };
 
 // Busy-waits about `us` microseconds on the device (kernel timing: lets the host queue a whole
@@ -138,6 +139,7 @@ bool launch_delay(hipStream_t st, int us);
 void set_mv_device_cus(int n);
 
 bool launch_mv_group(hipStream_t st, MVGroup & g);
+int mva_rows();
 
 // v6 token-shift mixes with the maa LoRA (rwkv_graph.inc:308-346); xa = LN(x) is the new
 // att_xx carry already written by the W1 matvec prologue; w2t is time_maa_w2 transposed to

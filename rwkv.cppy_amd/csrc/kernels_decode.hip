@@ -21,6 +21,19 @@ extern template bool launch_mv_shape<W_Q5_1>(hipStream_t, MVGroup &, int, int, i
 extern template bool launch_mv_shape<W_Q8_0>(hipStream_t, MVGroup &, int, int, int, bool, dim3);
 
 static int g_mv_cus = 256;
+
+// Rows per wave of k_mva (RWKV_MI355X_MVA_R = 2, 4 or 8; default 2).  More rows per wave put
+// more weight loads in flight per lane behind fewer workgroups; measured on the v6-1B6 decode
+// chain (128 tokens): 2 rows 853 us/token, 4 rows 883, 8 rows 876 -- the launch stays latency
+// bound and two rows keep the most waves issuing.
+int mva_rows() {
+    static const int v = [] {
+        const char * e = getenv("RWKV_MI355X_MVA_R");
+        const int r = e ? atoi(e) : 2;
+        return r == 4 || r == 8 ? r : 2;
+    }();
+    return v;
+}
 void set_mv_device_cus(int n) { g_mv_cus = n > 0 ? n : 256; }
 
 bool launch_mv_group(hipStream_t st, MVGroup & g) {
@@ -42,7 +55,16 @@ bool launch_mv_group(hipStream_t st, MVGroup & g) {
         fprintf(stderr, "rwkv: emitting matvec needs a prologue source\n");
         return false;
     }
-    const int R = emit ? 8 : 2, RW = 4 * R;
+    // rows per wave: 8 when emitting (a 32-row block per workgroup), else 2; the lean
+    // activation-input kernel k_mva (one weight type, <= 4 units per lane) takes mva_rows()
+    int wfix = g.e[0].W.type;
+    for (int i = 1; i < g.n; i++)
+        if (g.e[i].W.type != wfix) wfix = -1;
+    int umax0 = 1;
+    for (int i = 0; i < g.n; i++) umax0 = std::max(umax0, mv_units(g.e[i].W.type, g.e[i].W.K));
+    const bool mva = !prologue && !emit && wfix >= 0 && umax0 <= 4;
+    const int R = emit ? 8 : mva ? mva_rows() : 2, RW = 4 * R;
+    g.rows = R;
     int blocks = 0, umax = 1, lds = 0;
     for (int i = 0; i < g.n; i++) {
         MVEntry & e = g.e[i];
@@ -99,9 +121,6 @@ bool launch_mv_group(hipStream_t st, MVGroup & g) {
     }
     g.grid = grid;
     const int U = umax <= 1 ? 1 : umax <= 2 ? 2 : 4;  // 2: K = 2560 (v7-2.9B) quantized rows
-    int wfix = g.e[0].W.type;
-    for (int i = 1; i < g.n; i++)
-        if (g.e[i].W.type != wfix) wfix = -1;
     bool ok = false;
     switch (wfix) {
         case W_F16: ok = launch_mv_shape<W_F16>(st, g, U, srck, form, emit, dim3(grid)); break;

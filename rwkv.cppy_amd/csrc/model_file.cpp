@@ -102,6 +102,8 @@ bool read_file_header(FILE * f, FileHeader & h) {
 }
 
 // rwkv_fread_tensor_header (rwkv_file_format.inc:167-197)
+static constexpr uint32_t kMaxKeyLen = 4096;
+
 static bool read_tensor_header(FILE * f, HostTensor & t, uint32_t & key_len) {
     uint32_t h[3];
     RWKV_CHECK(RWKV_ERROR_FILE_READ, false, fread(h, 4, 3, f) == 3, "Failed to read tensor header");
@@ -113,6 +115,11 @@ static bool read_tensor_header(FILE * f, HostTensor & t, uint32_t & key_len) {
     RWKV_CHECK(RWKV_ERROR_DATA_TYPE, false, type_supported(t.type), "Tensor data type (%s) is not supported", type_name(t.type));
     t.ne[0] = t.ne[1] = t.ne[2] = 1;
     RWKV_CHECK(RWKV_ERROR_FILE_READ, false, fread(t.ne, 4, t.ndim, f) == t.ndim, "Failed to read tensor shape");
+    RWKV_CHECK(RWKV_ERROR_FILE_READ, false, key_len <= kMaxKeyLen, "Tensor name too long (%" PRIu32 " bytes)", key_len);
+    for (uint32_t i = 0; i < t.ndim; i++)
+        RWKV_CHECK(RWKV_ERROR_SHAPE, false, t.ne[i] >= 1 && t.ne[i] <= (1u << 30), "Tensor dimension %u out of range", t.ne[i]);
+    RWKV_CHECK(RWKV_ERROR_SHAPE, false, !type_quantized(t.type) || t.ne[0] % 32 == 0,
+               "Quantized tensor row length %" PRIu32 " is not a multiple of 32", t.ne[0]);
     return true;
 }
 
@@ -174,6 +181,99 @@ static bool check_params(const ModelFile & mf) {
     return need(mf, "ln_out.weight") && need(mf, "ln_out.bias") && need(mf, "head.weight");
 }
 
+// Every tensor against the dimensions the kernels derive from the header and the layer-0 tensors
+// (the checks ggml's op asserts make in the reference when the graph is built): C = n_embed,
+// V = n_vocab, H/S (rwkv_model_loading.inc:403-409), FFN width F, LoRA widths.  Vectors must be
+// FP32/FP16; matrices [K, M] any supported type (quantized K % 32 == 0, checked at read).
+static bool shape_is(const ModelFile & mf, const std::string & key, std::initializer_list<uint32_t> ne, bool vec) {
+    const HostTensor * t = mf.find(key);
+    if (!t) return true;  // optional (absent where the version has no such tensor); need() checks presence
+    uint64_t n = 1;
+    for (uint32_t v : ne) n *= v;
+    bool ok = t->nel() == n;
+    if (ok && !vec) {  // matrices: exactly [ne0, ne1]
+        const uint32_t * e = ne.begin();
+        ok = t->ndim == 2 && t->ne[0] == e[0] && t->ne[1] == e[1];
+    }
+    RWKV_CHECK(RWKV_ERROR_MODEL_PARAMS | RWKV_ERROR_SHAPE, false, ok, "Parameter %s has an unexpected shape (%u x %u x %u)",
+               key.c_str(), t->ne[0], t->ne[1], t->ne[2]);
+    RWKV_CHECK(RWKV_ERROR_MODEL_PARAMS | RWKV_ERROR_DATA_TYPE, false, !vec || t->type <= 1,
+               "Parameter %s must be FP32 or FP16", key.c_str());
+    return true;
+}
+
+static bool check_shapes(const ModelFile & mf) {
+    const uint32_t C = mf.header.n_embed, V = mf.header.n_vocab;
+    const uint32_t H = (uint32_t)mf.head_count, S = (uint32_t)mf.head_size;
+    RWKV_CHECK(RWKV_ERROR_MODEL_PARAMS | RWKV_ERROR_DIMENSION, false, C >= 1 && V >= 1 && mf.header.n_layer >= 1,
+               "Model dimensions out of range");
+    RWKV_CHECK(RWKV_ERROR_MODEL_PARAMS | RWKV_ERROR_DIMENSION, false, mf.arch_major < 5 || (H >= 1 && (uint64_t)H * S == C),
+               "n_embed %u is not head_count %u x head_size %u", C, H, S);
+    const HostTensor * fk = mf.find("blocks.0.ffn.key.weight");
+    const uint32_t F = fk->ne[1];
+    bool ok = shape_is(mf, "blocks.0.ln0.weight", {C}, true) && shape_is(mf, "blocks.0.ln0.bias", {C}, true) &&
+              shape_is(mf, "ln_out.weight", {C}, true) && shape_is(mf, "ln_out.bias", {C}, true) &&
+              shape_is(mf, "head.weight", {C, V}, false);
+    uint32_t D5 = 0, DW = 0, DW7 = 0, DA7 = 0, DG7 = 0, DV7 = 0;
+    if (mf.arch_major == 6) {
+        D5 = mf.find("blocks.0.att.time_maa_w1")->ne[1];
+        DW = mf.find("blocks.0.att.time_decay_w1")->ne[1];
+        RWKV_CHECK(RWKV_ERROR_MODEL_PARAMS | RWKV_ERROR_SHAPE, false, D5 % 5 == 0 && D5 / 5 <= 64 && DW >= 1,
+                   "Unsupported v6 LoRA widths (maa %u, decay %u)", D5, DW);
+    }
+    if (mf.arch_major == 7) {
+        DW7 = mf.find("blocks.0.att.w1")->ne[1];
+        DA7 = mf.find("blocks.0.att.a1")->ne[1];
+        DG7 = mf.find("blocks.0.att.g1")->ne[1];
+        const HostTensor * v1 = mf.header.n_layer > 1 ? mf.find("blocks.1.att.v1") : nullptr;
+        DV7 = v1 ? v1->ne[1] : 0;
+    }
+    for (uint32_t i = 0; ok && i < mf.header.n_layer; i++) {
+        const std::string p = "blocks." + std::to_string(i) + ".";
+        auto V1 = [&](const char * k) { return shape_is(mf, p + k, {C}, true); };
+        auto M2 = [&](const char * k, uint32_t K, uint32_t M) { return shape_is(mf, p + k, {K, M}, false); };
+        ok = V1("ln1.weight") && V1("ln1.bias") && V1("ln2.weight") && V1("ln2.bias") &&
+             M2("att.key.weight", C, C) && M2("att.value.weight", C, C) && M2("att.receptance.weight", C, C) &&
+             M2("att.output.weight", C, C) && M2("ffn.key.weight", C, F) && M2("ffn.value.weight", F, C);
+        if (ok && mf.arch_major != 7) ok = M2("ffn.receptance.weight", C, C);
+        if (ok && (mf.arch_major == 4 || mf.arch_major == 5))
+            ok = V1("att.time_mix_k") && V1("att.time_mix_v") && V1("att.time_mix_r") && V1("ffn.time_mix_k") &&
+                 V1("ffn.time_mix_r");
+        if (ok && mf.arch_major == 4) ok = V1("att.time_first") && V1("att.time_decay");
+        if (ok && mf.arch_major >= 5) ok = V1("att.ln_x.weight") && V1("att.ln_x.bias");
+        if (ok && mf.arch_major == 5) {
+            if (mf.arch_minor >= 2)
+                ok = shape_is(mf, p + "att.time_decay", {C}, true) && V1("att.time_faaaa") && V1("att.time_mix_g") &&
+                     M2("att.gate.weight", C, C);
+            else
+                ok = shape_is(mf, p + "att.time_decay", {H}, true) && shape_is(mf, p + "att.time_first", {H}, true);
+            for (const char * k : {"att.time_decay", "att.time_faaaa", "att.time_first"}) {
+                const HostTensor * t = mf.find(p + k);
+                RWKV_CHECK(RWKV_ERROR_MODEL_PARAMS | RWKV_ERROR_DATA_TYPE, false, !t || t->type == 0,
+                           "Parameter %s%s must be FP32", p.c_str(), k);
+            }
+        }
+        if (ok && mf.arch_major == 6) {
+            ok = V1("att.time_maa_x") && V1("att.time_maa_w") && V1("att.time_maa_k") && V1("att.time_maa_v") &&
+                 V1("att.time_maa_r") && V1("att.time_maa_g") && V1("att.time_faaaa") && V1("att.time_decay") &&
+                 V1("ffn.time_maa_k") && V1("ffn.time_maa_r") && M2("att.time_maa_w1", C, D5) &&
+                 shape_is(mf, p + "att.time_maa_w2", {D5 / 5, C, 5}, true) && M2("att.time_decay_w1", C, DW) &&
+                 M2("att.time_decay_w2", DW, C) && M2("att.gate.weight", C, C);
+            const HostTensor * w2 = mf.find(p + "att.time_maa_w2");
+            RWKV_CHECK(RWKV_ERROR_MODEL_PARAMS | RWKV_ERROR_SHAPE, false, !ok || (w2->type == 0 && w2->ndim == 3),
+                       "Parameter %satt.time_maa_w2 must be an FP32 [D, C, 5] tensor", p.c_str());
+        }
+        if (ok && mf.arch_major == 7) {
+            ok = shape_is(mf, p + "att.x_rwkvag", {C, 1, 6}, true) && V1("att.w0") && V1("att.a0") && V1("att.k_k") &&
+                 V1("att.k_a") && shape_is(mf, p + "att.r_k", {S, H}, true) && V1("ffn.x_k") &&
+                 M2("att.w1", C, DW7) && M2("att.w2", DW7, C) && M2("att.a1", C, DA7) && M2("att.a2", DA7, C) &&
+                 M2("att.g1", C, DG7) && M2("att.g2", DG7, C);
+            if (ok && i != 0) ok = V1("att.v0") && M2("att.v1", C, DV7) && M2("att.v2", DV7, C);
+        }
+    }
+    return ok;
+}
+
 bool load_model_file(const char * path, ModelFile & mf) {
     FILE * f = fopen(path, "rb");
     RWKV_CHECK(RWKV_ERROR_FILE | RWKV_ERROR_FILE_OPEN, false, f != nullptr, "Failed to open file %s", path);
@@ -190,9 +290,19 @@ bool load_model_file(const char * path, ModelFile & mf) {
         HostTensor t;
         uint32_t key_len = 0;
         bool ok = read_tensor_header(f, t, key_len);
+        const off_t left = (off_t)st.st_size - ftello(f);
+        if (ok) {
+            ok = (off_t)key_len <= left;
+            if (!ok) add_error(RWKV_ERROR_FILE_READ);
+        }
         if (ok) {
             t.name.resize(key_len);
             ok = key_len == 0 || fread(&t.name[0], 1, key_len, f) == key_len;
+            if (!ok) add_error(RWKV_ERROR_FILE_READ);
+        }
+        if (ok) {
+            const size_t nb = type_nbytes(t.type, t.nel());
+            ok = (off_t)nb <= (off_t)st.st_size - ftello(f);
             if (!ok) add_error(RWKV_ERROR_FILE_READ);
         }
         if (ok) {
@@ -234,11 +344,13 @@ bool load_model_file(const char * path, ModelFile & mf) {
         mf.head_count = mf.find("blocks.0.att.time_decay")->ne[2];
     }
     if (mf.head_count) mf.head_size = (int64_t)mf.find("blocks.0.ln1.weight")->ne[0] / mf.head_count;
+    if (!check_shapes(mf)) return false;
 
     const HostTensor * emb = mf.find("emb.weight");
     RWKV_CHECK(RWKV_ERROR_MODEL_PARAMS | RWKV_ERROR_SHAPE, false, emb->ndim == 2, "Unexpected dimension count of embedding matrix %u", emb->ndim);
     RWKV_CHECK(RWKV_ERROR_MODEL_PARAMS | RWKV_ERROR_DIMENSION, false, emb->ne[0] == mf.header.n_embed, "Unexpected dimension of embedding matrix %u", emb->ne[0]);
     RWKV_CHECK(RWKV_ERROR_MODEL_PARAMS | RWKV_ERROR_DIMENSION, false, emb->ne[1] == mf.header.n_vocab, "Unexpected dimension of embedding matrix %u", emb->ne[1]);
+    RWKV_CHECK(RWKV_ERROR_MODEL_PARAMS | RWKV_ERROR_DATA_TYPE, false, emb->type <= 1, "Embedding matrix must be FP32 or FP16");
     return true;
 }
 

@@ -275,6 +275,20 @@ __device__ __forceinline__ void chunk_store(const MVEntry & E, const ActBuf & a,
     }
 }
 
+// Row sums r = 0..R-1 (valid in lane 63 after wave_sum63) gathered so that lane r holds row r's
+// sum: the rows' epilogues (exp/tanh chains) then run side by side in R lanes instead of one
+// after another in lane 63.  Pure data movement: results are bit-identical.
+template <int R>
+__device__ __forceinline__ float lane_row_sum(const float (&s)[R], int lane) {
+    float mine = 0.0f;
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const float v = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, s[r]), 63));
+        mine = lane == r ? v : mine;
+    }
+    return mine;
+}
+
 // Epilogue operands of one output row, loaded at kernel start (not after the dots).
 struct EpiIn {
     float y, aux, bias;
@@ -372,13 +386,10 @@ __device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, int b0, in
     for (int u = 0; u < U; u++)
 #pragma unroll
         for (int r = 0; r < R; r++) w[r][u] = load_unit<WF>(W, rows[r], u, lane);
-    EpiIn ep[R];
-    if constexpr (!EMIT) {
-#pragma unroll
-        for (int r = 0; r < R; r++) ep[r] = epi_load(Ent, rows[r]);
-    } else {
-        ep[0] = epi_load(Ent, min(wgi * RW + (tid < RW ? tid : 0), M - 1));
-    }
+    // epilogue operands: !EMIT lane r < R runs row row0 + r's epilogue; EMIT thread tid < RW row tid
+    EpiIn ep;
+    if constexpr (!EMIT) ep = epi_load(Ent, min(row0 + min(lane, R - 1), M - 1));
+    else ep = epi_load(Ent, min(wgi * RW + (tid < RW ? tid : 0), M - 1));
     if constexpr (PRO) __syncthreads();  // activation image ready
     else a = Ent.act;
     PROBE(1);
@@ -417,11 +428,8 @@ __device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, int b0, in
             if (s[0] == 1.2345f) g_probe[0] = 0;  // orders the stamp after the dots
 #endif
             PROBE(2);
-#pragma unroll
-            for (int r = 0; r < R; r++) {
-                const int row = row0 + r;
-                if (lane == 63 && row < M) Ent.y[row] = epi_apply(Ent.epi, s[r], ep[r]);
-            }
+            const float v = epi_apply(Ent.epi, lane_row_sum<R>(s, lane), ep);
+            if (lane < R && row0 + lane < M) Ent.y[row0 + lane] = v;
         } else {
             // RW rows per block (a multiple of 32): apply the epilogue and emit each 32 rows as
             // one quantization block of the next matmul's input (ggml Q8 / fp16 / fp32)
@@ -434,7 +442,7 @@ __device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, int b0, in
                 const int row = wgi * RW + tid;
                 float vv = 0.0f;
                 if (row < M) {
-                    vv = epi_apply(Ent.epi, red[tid], ep[0]);
+                    vv = epi_apply(Ent.epi, red[tid], ep);
                     if (Ent.y) Ent.y[row] = vv;
                 }
                 if (Ent.act_out.fmt >= 0 && Ent.emit) emit32(Ent.act_out, 0, row, vv);
@@ -451,12 +459,8 @@ __device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, int b0, in
         for (int u = 0; u < U; u++)
 #pragma unroll
             for (int r = 0; r < R; r++) w[r][u] = load_unit<WF>(W, rows[r], u, lane);
-        if constexpr (!EMIT) {
-#pragma unroll
-            for (int r = 0; r < R; r++) ep[r] = epi_load(Ent, rows[r]);
-        } else {
-            ep[0] = epi_load(Ent, min(wgi * RW + (tid < RW ? tid : 0), M - 1));
-        }
+        if constexpr (!EMIT) ep = epi_load(Ent, min(row0 + min(lane, R - 1), M - 1));
+        else ep = epi_load(Ent, min(wgi * RW + (tid < RW ? tid : 0), M - 1));
     }
 }
 
@@ -540,13 +544,12 @@ __global__ __launch_bounds__(256) void k_mva(int b1, int b2, int b3, int b4, int
     AUnit x[U];
 #pragma unroll
     for (int u = 0; u < U; u++) x[u] = load_act_unit<WF, false>(a, u, lane);
-    EpiIn ep[R];
-#pragma unroll
-    for (int r = 0; r < R; r++) {
-        ep[r].y = h.y[rows[r]];
-        ep[r].aux = aux[rows[r] * astep];
-        ep[r].bias = bias[rows[r] * bstep];
-    }
+    // epilogue operands of row row0 + lane (lanes 0..R-1 run the rows' epilogues)
+    const int erow = min(row0 + min(lane, R - 1), M - 1);
+    EpiIn ep;
+    ep.y = h.y[erow];
+    ep.aux = aux[erow * astep];
+    ep.bias = bias[erow * bstep];
     // keep the machine scheduler from interleaving later rows' loads with earlier rows' dots
     __builtin_amdgcn_sched_barrier(0);
     float acc[R], acc2[R];
@@ -564,15 +567,13 @@ __global__ __launch_bounds__(256) void k_mva(int b1, int b2, int b3, int b4, int
         }
     }
     constexpr bool one = WF == W_Q4_1 || WF == W_Q5_1;
+    float sr[R];
 #pragma unroll
-    for (int r = 0; r < R; r++) {
-        const float sr = one ? wave_sum63(acc[r]) + wave_sum63(acc2[r]) : wave_sum63(acc[r]) + 0.0f;
-        const int row = row0 + r;
-        // epilogue on every lane: its operand loads then stay ahead of the dots instead of being
-        // sunk into the lane-63 store branch (a dependent round trip at the kernel's end)
-        const float v = epi_apply(h.epi, sr, ep[r]);
-        if (lane == 63 && row < M) h.y[row] = v;
-    }
+    for (int r = 0; r < R; r++) sr[r] = one ? wave_sum63(acc[r]) + wave_sum63(acc2[r]) : wave_sum63(acc[r]) + 0.0f;
+    // epilogue on lane r for row r, on every lane (the operand loads stay ahead of the dots
+    // instead of being sunk into the store branch: a dependent round trip at the kernel's end)
+    const float v = epi_apply(h.epi, lane_row_sum<R>(sr, lane), ep);
+    if (lane < R && row0 + lane < M) h.y[row0 + lane] = v;
 }
 
 // One weight-type translation unit (mv_*.hip) instantiates every launch shape for WFIX.
@@ -589,12 +590,19 @@ bool launch_mv_shape(hipStream_t st, MVGroup & g, int U, int srck, int form, boo
     const int K = g.e[0].W.K;
     if constexpr (WFIX >= 0) {
         if (srck == MVK_ACT && !emit && g.units_max <= U) {
-#define MVA_L(Uv) \
-    hipLaunchKernelGGL((k_mva<WFIX, 2, Uv>), grid, dim3(256), 0, st, b[1], b[2], b[3], b[4], b[5], b[6], b[7], g)
+#define MVA_R(Rv, Uv) \
+    hipLaunchKernelGGL((k_mva<WFIX, Rv, Uv>), grid, dim3(256), 0, st, b[1], b[2], b[3], b[4], b[5], b[6], b[7], g)
+#define MVA_L(Uv)                          \
+    do {                                   \
+        if (g.rows == 2) MVA_R(2, Uv);     \
+        else if (g.rows == 8) MVA_R(8, Uv); \
+        else MVA_R(4, Uv);                 \
+    } while (0)
             if (U == 1) MVA_L(1);
             else if (U == 2) MVA_L(2);
             else MVA_L(4);
 #undef MVA_L
+#undef MVA_R
             return true;
         }
     }

@@ -10,6 +10,8 @@
 // for v6-1B6 Q4_0, read from L2), which replaces one dependent launch per layer.
 #include "mv_common.hpp"
 
+#include <stdlib.h>
+
 namespace rwkvmi {
 
 struct MaaDec {
@@ -30,7 +32,7 @@ struct MaaDec {
 // (its W2 column prefetched with the weights).  Waves 4..7: the activation image (LayerNorm +
 // token shift + quantization, one 512-element chunk per wave per pass) and the fp32 xa image.
 // Each wave keeps well under 63 loads in flight, so none stalls on the vmcnt limit.
-template <int WF, int R, int U, int LNP, int DM>
+template <int WF, int R, int U, int LNP, int DM, int CPW>
 __global__ __launch_bounds__(512) void k_v6_maa_dec(MaaDec a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ float s_lora[64];
@@ -52,8 +54,8 @@ __global__ __launch_bounds__(512) void k_v6_maa_dec(MaaDec a) {
 #pragma unroll
             for (int r = 0; r < R; r++) w[r][u] = load_unit<WF, false>(W, rows[r], u, lane);
         // this thread's mix channel: W2 column, carry, maa
-        const int c = blockIdx.x * 256 + tid;
-        const bool cval = (int)(blockIdx.x * 256 + (tid & ~31)) < C;  // half-wave uniform
+        const int c = blockIdx.x * CPW + tid;
+        const bool cval = tid < CPW && (int)(blockIdx.x * CPW + (tid & ~31)) < C;  // half-wave uniform
         const int cc = min(c, C - 1);
         float w2v[DM];
         const float * w2 = a.w2t + (size_t)n * D * C + cc;
@@ -86,11 +88,11 @@ __global__ __launch_bounds__(512) void k_v6_maa_dec(MaaDec a) {
             }
         }
         constexpr bool one = WF == W_Q4_1 || WF == W_Q5_1;
+        float s[R];
 #pragma unroll
-        for (int r = 0; r < R; r++) {
-            const float s = one ? wave_sum63(acc[r]) + wave_sum63(acc2[r]) : wave_sum63(acc[r]) + 0.0f;
-            if (lane == 63 && wave * R + r < D) s_lora[wave * R + r] = rk_tanhf(s);  // EPI_TANH
-        }
+        for (int r = 0; r < R; r++) s[r] = one ? wave_sum63(acc[r]) + wave_sum63(acc2[r]) : wave_sum63(acc[r]) + 0.0f;
+        const float t = rk_tanhf(lane_row_sum<R>(s, lane));  // EPI_TANH, lane r for row r
+        if (lane < R && wave * R + lane < D) s_lora[wave * R + lane] = t;
         __syncthreads();  // (2) lora_n ready
         // k_v6_mix5_dec's arithmetic: m = sum_i (double)(w2[i] * lora[i]) in order
         const float xa = s_xa[cc];
@@ -135,10 +137,28 @@ __global__ __launch_bounds__(512) void k_v6_maa_dec(MaaDec a) {
     __syncthreads();  // (2)
 }
 
+// Channels mixed per workgroup (CPW): the workgroups of one mix each recompute its D rows of W1
+// (37 KB of L2 reads for v6-1B6) and stream CPW columns of W2 from HBM; 64 gives 32 x 5 = 160
+// workgroups for C = 2048 (256: 40), so the W2 stream is spread over more CUs.
+static int maa_cpw() {
+    static const int v = [] {
+        const char * e = getenv("RWKV_MI355X_MAA_CPW");
+        const int c = e ? atoi(e) : 64;
+        return c == 128 || c == 256 ? c : 64;
+    }();
+    return v;
+}
+
 template <int WF>
 static bool launch_maa_t(hipStream_t st, const MaaDec & a, int lds, int units) {
-    const dim3 grid((a.C + 255) / 256, 5);
-#define MAA_L(Rv, Uv, P) hipLaunchKernelGGL((k_v6_maa_dec<WF, Rv, Uv, P, (Rv) * 4>), grid, dim3(512), lds, st, a)
+    const int cpw = maa_cpw();
+    const dim3 grid((a.C + cpw - 1) / cpw, 5);
+#define MAA_L(Rv, Uv, P)                                                                                           \
+    do {                                                                                                           \
+        if (cpw == 64) hipLaunchKernelGGL((k_v6_maa_dec<WF, Rv, Uv, P, (Rv) * 4, 64>), grid, dim3(512), lds, st, a); \
+        else if (cpw == 128) hipLaunchKernelGGL((k_v6_maa_dec<WF, Rv, Uv, P, (Rv) * 4, 128>), grid, dim3(512), lds, st, a); \
+        else hipLaunchKernelGGL((k_v6_maa_dec<WF, Rv, Uv, P, (Rv) * 4, 256>), grid, dim3(512), lds, st, a);      \
+    } while (0)
 #define MAA_P(Rv, Uv) \
     do { if (a.C <= 2048) MAA_L(Rv, Uv, 32); else MAA_L(Rv, Uv, 64); } while (0)
     const bool u1 = units <= 1;

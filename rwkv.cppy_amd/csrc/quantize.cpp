@@ -5,6 +5,8 @@
 #include <math.h>
 #include <stdio.h>
 #include <string.h>
+
+#include <exception>
 #include <sys/stat.h>
 
 #include <algorithm>
@@ -416,7 +418,12 @@ static bool write_synthetic(const char * path, int arch, uint32_t V, uint32_t C,
 }  // namespace rwkvmi
 
 extern "C" RWKV_API bool rwkv_quantize_model_file(const char * in, const char * out, const char * fmt) {
-    return rwkvmi::quantize_model_file(in, out, fmt);
+    try {
+        return rwkvmi::quantize_model_file(in, out, fmt);
+    } catch (const std::exception &) {
+        rwkvmi::add_error(RWKV_ERROR_ALLOC);
+        return false;
+    }
 }
 
 extern "C" RWKV_API bool rwkv_mi355x_write_synthetic_model(const char * path, int arch, uint32_t n_vocab,

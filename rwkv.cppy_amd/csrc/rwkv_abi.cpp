@@ -7,6 +7,7 @@
 
 #include <atomic>
 #include <inttypes.h>
+#include <exception>
 #include <mutex>
 #include <string>
 
@@ -84,9 +85,7 @@ static struct rwkv_context * new_context(SharedModel * sm, uint32_t n_threads) {
     return ctx;
 }
 
-RWKV_API struct rwkv_context * rwkv_init_from_file(const char * path, const uint32_t n_threads, const uint32_t n_gpu_layers) {
-    (void)n_gpu_layers;
-    g_last_error = RWKV_ERROR_NONE;
+static struct rwkv_context * init_from_file(const char * path, const uint32_t n_threads) {
     int ndev = 0;
     const hipError_t de = hipGetDeviceCount(&ndev);
     RWKV_CHECK(RWKV_ERROR_CTX | RWKV_ERROR_UNSUPPORTED, nullptr, de == hipSuccess && ndev > 0,
@@ -109,6 +108,18 @@ RWKV_API struct rwkv_context * rwkv_init_from_file(const char * path, const uint
         delete sm;
     }
     return ctx;
+}
+
+// No C++ exception crosses the C ABI: a failed host allocation (std::bad_alloc from a corrupt
+// file's sizes, say) becomes RWKV_ERROR_ALLOC and a NULL context.
+RWKV_API struct rwkv_context * rwkv_init_from_file(const char * path, const uint32_t n_threads, const uint32_t n_gpu_layers) {
+    (void)n_gpu_layers;
+    g_last_error = RWKV_ERROR_NONE;
+    try {
+        return init_from_file(path, n_threads);
+    } catch (const std::exception & e) {
+        RWKV_CHECK(RWKV_ERROR_CTX | RWKV_ERROR_ALLOC, nullptr, false, "Failed to load %s: %s", path, e.what());
+    }
 }
 
 RWKV_API struct rwkv_context * rwkv_clone_context(struct rwkv_context * ctx, const uint32_t n_threads) {

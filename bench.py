@@ -167,9 +167,9 @@ def main():
     if world > 1 and args.seq_reps > 0:
         try:
             from rwkv_cpp.pipeline import LibraryStage, pipeline_eval_sequence, stage_layers
-            archv = (ctypes.c_int64 * 4)()
-            L.rwkv_mi355x_arch(ctx.ptr, archv)
-            stage = LibraryStage(lib, ctx, n_vocab, int(archv[0]))
+            # a stage context holding only this rank's layers (and the head on the last rank),
+            # computing on its own stream with no host wait between chunks
+            stage = LibraryStage.from_file(lib, path, rank, world, async_=True)
             chunk = args.pipe_chunk or max(64, args.seq_len // (2 * world))
             pseq = np.random.default_rng(4321).integers(0, n_vocab, size=args.seq_len)  # same on every rank
             dev = torch.device('cuda', gpu)
@@ -192,7 +192,10 @@ def main():
             l0, l1 = stage_layers(NL, world, rank)
             pipe = {'tokens_per_s': round(args.seq_len / min(pts), 1), 'ms_per_sequence': round(min(pts) * 1e3, 3),
                     'parallelism': f'layer pipeline x{world}', 'scaling': 'strong', 'chunk': chunk,
-                    'transport': f'torch.distributed {backend} isend/irecv of x [chunk, C] fp32'}
+                    'transport': f'torch.distributed {backend} isend/irecv of x [chunk, C] fp32',
+                    'stage_weight_gb_rank0': round(L.rwkv_mi355x_weight_bytes(stage.ctx.ptr, True) / 1e9, 4),
+                    'model_weight_gb': round(L.rwkv_mi355x_weight_bytes(ctx.ptr, True) / 1e9, 4)}
+            lib.rwkv_free(stage.ctx)
             log(f'pipeline seq-eval over {world} stages (rank {rank}: layers [{l0}, {l1})): '
                 f'{min(pts) * 1e3:.1f} ms, {args.seq_len / min(pts):.0f} tok/s, chunk {chunk}')
         except Exception as e:  # reported, never required for the decode line

@@ -47,6 +47,23 @@ RWKV_API bool rwkv_mi355x_eval_layers(struct rwkv_context * ctx, const uint32_t 
                                       uint32_t layer_begin, uint32_t layer_end, float * x_dev, float * vfirst_dev,
                                       bool compute_logits, float * logits_out);
 
+/* The same stage, enqueued on the context's stream (rwkv_mi355x_stream) without waiting for it:
+ * the caller orders its own work (e.g. an RCCL send of x_dev) on that stream.  Logits, when
+ * computed, stay on the device (rwkv_mi355x_logits_device). */
+RWKV_API bool rwkv_mi355x_eval_layers_async(struct rwkv_context * ctx, const uint32_t * tokens, size_t T,
+                                            uint32_t layer_begin, uint32_t layer_end, float * x_dev, float * vfirst_dev,
+                                            bool compute_logits);
+RWKV_API float * rwkv_mi355x_logits_device(struct rwkv_context * ctx);
+
+/* A pipeline stage's context: only layers [layer_begin, layer_end) are uploaded (plus the
+ * embedding when layer_begin == 0 and the head when layer_end == n_layer), so a stage's HBM holds
+ * ~1/P of the weights (reference placement by layer range: rwkv_model_loading.inc:128-142).  The
+ * state keeps the full layout.  Whole-model calls (rwkv_eval, ...) fail with
+ * RWKV_ERROR_CTX | RWKV_ERROR_UNSUPPORTED on such a context; rwkv_mi355x_eval_layers accepts
+ * ranges inside [layer_begin, layer_end). */
+RWKV_API struct rwkv_context * rwkv_mi355x_init_from_file_layers(const char * path, uint32_t n_threads,
+                                                                 uint32_t layer_begin, uint32_t layer_end);
+
 /* The context's HIP stream (hipStream_t), so callers can time kernels with events on it. */
 RWKV_API void * rwkv_mi355x_stream(struct rwkv_context * ctx);
 

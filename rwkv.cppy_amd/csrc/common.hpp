@@ -66,6 +66,11 @@ struct ActBuf {
 //   activations per (QG_TOK-token tile, block b), ordered [token tile][b]:
 //                 [2 halves x QG_TOK tokens x 16 B int8][QG_TOK x f32 d][Q8_1: QG_TOK x f32 s]
 constexpr int QG_TOK = 64;
+// Row r's 32 int8 weights sit at byte r * 32 of the weight record with their two 16-byte halves
+// swapped when bit 3 of r is set: the GEMM's 8-byte fragment reads (lane = row r16 of a 16-row
+// tile, 8-byte piece h) then hit 32 distinct LDS banks per 32-lane group instead of rows r and
+// r + 8 sharing banks (2-way conflicts on every read, 49% of LDS cycles in the PMC profile).
+__host__ __device__ constexpr int qg_w_off(int r, int byte) { return r * 32 + (byte ^ (((r >> 3) & 1) << 4)); }
 __host__ __device__ constexpr bool qg_one(int wt) { return wt == W_Q4_1 || wt == W_Q5_1; }
 __host__ __device__ constexpr int qg_rows(int wt) { return qg_one(wt) ? 32 : 64; }
 __host__ __device__ constexpr int qg_w_d(int wt) { return qg_rows(wt) * 32; }

@@ -130,7 +130,7 @@ bool upload_mat(DeviceModel & dm, const HostTensor * t, DMat & out, bool count_b
                     uint8_t * rec = &gt[(rt * nb + b) * rb];
                     for (int r = 0; r < R && rt * R + r < M; r++) {
                         const size_t i = (rt * R + r) * nb + b;
-                        int8_t * w8 = (int8_t *)rec + r * 32;
+                        int8_t * w8 = (int8_t *)rec;
                         for (int j = 0; j < 32; j++) {
                             int v;
                             if (wt == W_Q8_0) {
@@ -142,7 +142,7 @@ bool upload_mat(DeviceModel & dm, const HostTensor * t, DMat & out, bool count_b
                                 if (wt == W_Q4_0) v -= 8;
                                 if (wt == W_Q5_0) v -= 16;
                             }
-                            w8[j] = (int8_t)v;
+                            w8[qg_w_off(r, j)] = (int8_t)v;
                         }
                         const float d = f16_to_f32(one ? (uint16_t)(sc32[i] & 0xFFFFu) : sc16[i]);
                         memcpy(rec + qg_w_d(wt) + r * 4, &d, 4);
@@ -172,10 +172,17 @@ bool upload_mat(DeviceModel & dm, const HostTensor * t, DMat & out, bool count_b
     return true;
 }
 
-bool upload_model(const ModelFile & mf, DeviceModel & dm) {
+bool upload_model(const ModelFile & mf, DeviceModel & dm, uint32_t layer_begin, uint32_t layer_end) {
     dm.n_vocab = mf.header.n_vocab;
     dm.n_embed = mf.header.n_embed;
     dm.n_layer = mf.header.n_layer;
+    dm.layer_lo = std::min(layer_begin, dm.n_layer);
+    dm.layer_hi = std::min(layer_end, dm.n_layer);
+    if (dm.layer_lo >= dm.layer_hi) {
+        fprintf(stderr, "rwkv: empty layer range [%u, %u)\n", layer_begin, layer_end);
+        return false;
+    }
+    const bool first = dm.layer_lo == 0, last = dm.layer_hi == dm.n_layer;
     dm.major = mf.arch_major;
     dm.minor = mf.arch_minor;
     dm.H = mf.head_count;
@@ -187,13 +194,16 @@ bool upload_model(const ModelFile & mf, DeviceModel & dm) {
         return false;
     }
     auto T = [&](const std::string & n) { return mf.find(n); };
-    if (!upload_mat(dm, T("emb.weight"), dm.emb, false, false)) return false;
-    if (!upload_mat(dm, T("head.weight"), dm.head, true, true)) return false;
-    if (!(dm.ln0_w = upload_vec(dm, T("blocks.0.ln0.weight"))) || !(dm.ln0_b = upload_vec(dm, T("blocks.0.ln0.bias"))) ||
-        !(dm.lnout_w = upload_vec(dm, T("ln_out.weight"))) || !(dm.lnout_b = upload_vec(dm, T("ln_out.bias"))))
+    // a pipeline stage holds only its layers (+ embedding on the first, head on the last)
+    if (first && (!upload_mat(dm, T("emb.weight"), dm.emb, false, false) ||
+                  !(dm.ln0_w = upload_vec(dm, T("blocks.0.ln0.weight"))) ||
+                  !(dm.ln0_b = upload_vec(dm, T("blocks.0.ln0.bias")))))
+        return false;
+    if (last && (!upload_mat(dm, T("head.weight"), dm.head, true, true) ||
+                 !(dm.lnout_w = upload_vec(dm, T("ln_out.weight"))) || !(dm.lnout_b = upload_vec(dm, T("ln_out.bias")))))
         return false;
     dm.layers.resize(dm.n_layer);
-    for (uint32_t i = 0; i < dm.n_layer; i++) {
+    for (uint32_t i = dm.layer_lo; i < dm.layer_hi; i++) {
         DLayer & L = dm.layers[i];
         const std::string p = "blocks." + std::to_string(i) + ".";
         auto V = [&](const char * n) { return upload_vec(dm, T(p + n)); };
@@ -1338,7 +1348,7 @@ bool Engine::eval(const uint32_t * tokens, size_t T, const float * state_in, flo
 // are device buffers [T][C] on this engine's device carrying the residual stream (and v7's
 // layer-0 values) between stages.  Synchronous: on return x_io holds this stage's output.
 bool Engine::eval_layers(const uint32_t * tokens, size_t T, uint32_t l0, uint32_t l1, float * x_io, float * vfirst_io,
-                         bool want_logits, float * logits_out) {
+                         bool want_logits, float * logits_out, bool sync) {
     HIP_OK(hipSetDevice(m_->device));
     if (!ensure_workspace((int)T)) return false;
     const size_t bytes = T * (size_t)m_->n_embed * 4;
@@ -1362,7 +1372,7 @@ bool Engine::eval_layers(const uint32_t * tokens, size_t T, uint32_t l0, uint32_
     if (vfirst_io && m_->major == 7) HIP_OK(hipMemcpyAsync(vfirst_io, vfirst_, bytes, hipMemcpyDeviceToDevice, stream_));
     if (lg && logits_out)
         HIP_OK(hipMemcpyAsync(logits_out, logits_, (size_t)m_->n_vocab * 4, hipMemcpyDeviceToHost, stream_));
-    HIP_OK(hipStreamSynchronize(stream_));
+    if (sync) HIP_OK(hipStreamSynchronize(stream_));  // async: the caller orders on stream() (pipeline.py)
     return true;
 }
 

@@ -33,6 +33,8 @@ struct DLayer {
 struct DeviceModel {
     int refcount = 0;
     int device = 0;
+    uint32_t layer_lo = 0, layer_hi = 0;  // layers whose weights are resident: [layer_lo, layer_hi)
+    bool partial() const { return layer_lo != 0 || layer_hi != n_layer; }
     uint32_t n_vocab = 0, n_embed = 0, n_layer = 0;
     int major = 4, minor = 0;
     int64_t H = 0, S = 0;
@@ -50,7 +52,7 @@ struct DeviceModel {
     double small_param_bytes = 0;    // fp32 vectors read per token
 };
 
-bool upload_model(const ModelFile & mf, DeviceModel & dm);
+bool upload_model(const ModelFile & mf, DeviceModel & dm, uint32_t layer_begin = 0, uint32_t layer_end = UINT32_MAX);
 // repacks one ggml-order matrix into the device layout (allocations recorded in dm.allocs)
 bool upload_mat(DeviceModel & dm, const HostTensor * t, DMat & out, bool count_bytes, bool is_head);
 void free_model(DeviceModel & dm);
@@ -85,7 +87,8 @@ class Engine {
     // device-resident evaluation on the context's own state
     bool eval_device(const uint32_t * tokens, size_t T, bool want_logits, float * logits_out, bool sync);
     bool eval_layers(const uint32_t * tokens, size_t T, uint32_t l0, uint32_t l1, float * x_io, float * vfirst_io,
-                     bool want_logits, float * logits_out);
+                     bool want_logits, float * logits_out, bool sync = true);
+    float * device_logits() const { return logits_; }
     bool state_upload(const float * state);
     bool state_download(float * state);
     bool sync();

@@ -3,6 +3,7 @@
 #include "model_file.hpp"
 
 #include <inttypes.h>
+#include <stdlib.h>
 #include <string.h>
 #include <sys/stat.h>
 
@@ -274,7 +275,19 @@ static bool check_shapes(const ModelFile & mf) {
     return ok;
 }
 
-bool load_model_file(const char * path, ModelFile & mf) {
+// Is tensor `name`'s data needed by a context owning layers [l0, l1) of an n_layer model?
+static bool tensor_wanted(const std::string & name, uint32_t l0, uint32_t l1, uint32_t n_layer) {
+    if (name.rfind("blocks.", 0) == 0) {
+        const uint32_t i = (uint32_t)strtoul(name.c_str() + 7, nullptr, 10);
+        if (name.find(".ln0.") != std::string::npos) return l0 == 0;
+        return i >= l0 && i < l1;
+    }
+    if (name == "emb.weight") return l0 == 0;
+    if (name == "head.weight" || name.rfind("ln_out.", 0) == 0) return l1 >= n_layer;
+    return true;
+}
+
+bool load_model_file(const char * path, ModelFile & mf, uint32_t layer_begin, uint32_t layer_end) {
     FILE * f = fopen(path, "rb");
     RWKV_CHECK(RWKV_ERROR_FILE | RWKV_ERROR_FILE_OPEN, false, f != nullptr, "Failed to open file %s", path);
     struct stat st;
@@ -307,8 +320,12 @@ bool load_model_file(const char * path, ModelFile & mf) {
         }
         if (ok) {
             const size_t nb = type_nbytes(t.type, t.nel());
-            t.data.resize(nb);
-            ok = nb == 0 || fread(t.data.data(), 1, nb, f) == nb;
+            if (tensor_wanted(t.name, layer_begin, layer_end, mf.header.n_layer)) {
+                t.data.resize(nb);
+                ok = nb == 0 || fread(t.data.data(), 1, nb, f) == nb;
+            } else {
+                ok = fseeko(f, (off_t)nb, SEEK_CUR) == 0;  // another stage's tensor: shape only
+            }
             if (!ok) add_error(RWKV_ERROR_FILE_READ);
         }
         if (!ok) {

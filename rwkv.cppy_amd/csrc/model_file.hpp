@@ -52,7 +52,10 @@ bool read_file_header(FILE * f, FileHeader & h);
 
 // Loads the whole file and checks the per-version parameter table.  Sets global error flags
 // exactly like rwkv_load_model_from_file (rwkv_model_loading.inc:288-419).
-bool load_model_file(const char * path, ModelFile & mf);
+// layer_begin/layer_end: only the data of blocks.<i>.* with i in [layer_begin, layer_end) (plus
+// emb.weight / blocks.0.ln0 when layer_begin == 0, ln_out / head when layer_end == n_layer) is
+// read; every other tensor keeps its header (all shapes are still checked) and empty data.
+bool load_model_file(const char * path, ModelFile & mf, uint32_t layer_begin = 0, uint32_t layer_end = UINT32_MAX);
 
 // fp16 helpers (round-to-nearest-even, same as F16C)
 uint16_t f32_to_f16(float f);

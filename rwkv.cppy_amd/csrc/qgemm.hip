@@ -146,7 +146,7 @@ __device__ __forceinline__ void qg_read_ops(const char * sp, QGOps<QGLayout<WF>:
     using Lt = QGLayout<WF>;
 #pragma unroll
     for (int i = 0; i < Lt::TI; i++) {
-        o.af[i] = *(const long *)(sp + (wr + 16 * i + r16) * 32 + h * 8);  // int8 row, k = 8h..8h+7
+        o.af[i] = *(const long *)(sp + qg_w_off(wr + 16 * i + r16, h * 8));  // int8 row, k = 8h..8h+7
         const int ro = wr + 16 * i + 4 * h;
         o.sd[i] = *(const float4 *)(sp + qg_w_d(WF) + ro * 4);
         if constexpr (Lt::ONE) o.sm[i] = *(const float4 *)(sp + qg_w_m(WF) + ro * 4);

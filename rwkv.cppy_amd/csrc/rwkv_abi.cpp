@@ -85,18 +85,21 @@ static struct rwkv_context * new_context(SharedModel * sm, uint32_t n_threads) {
     return ctx;
 }
 
-static struct rwkv_context * init_from_file(const char * path, const uint32_t n_threads) {
+static struct rwkv_context * init_from_file(const char * path, const uint32_t n_threads, uint32_t layer_begin = 0,
+                                            uint32_t layer_end = UINT32_MAX) {
     int ndev = 0;
     const hipError_t de = hipGetDeviceCount(&ndev);
     RWKV_CHECK(RWKV_ERROR_CTX | RWKV_ERROR_UNSUPPORTED, nullptr, de == hipSuccess && ndev > 0,
                "No HIP device available: this library evaluates RWKV on an AMD Instinct MI355X (gfx950) only");
     ModelFile mf;
-    if (!load_model_file(path, mf)) return nullptr;
+    if (!load_model_file(path, mf, layer_begin, layer_end)) return nullptr;
+    RWKV_CHECK(RWKV_ERROR_ARGS, nullptr, layer_begin < layer_end && layer_begin < mf.header.n_layer,
+               "Bad layer range [%u, %u) for %u layers", layer_begin, layer_end, mf.header.n_layer);
     SharedModel * sm = new (std::nothrow) SharedModel();
     RWKV_CHECK(RWKV_ERROR_CTX | RWKV_ERROR_ALLOC, nullptr, sm != nullptr, "Failed to allocate model");
     sm->dm.device = pick_device();
     if (sm->dm.device >= ndev) sm->dm.device = 0;
-    if (hipSetDevice(sm->dm.device) != hipSuccess || !upload_model(mf, sm->dm)) {
+    if (hipSetDevice(sm->dm.device) != hipSuccess || !upload_model(mf, sm->dm, layer_begin, layer_end)) {
         free_model(sm->dm);
         delete sm;
         RWKV_CHECK(RWKV_ERROR_MODEL | RWKV_ERROR_ALLOC, nullptr, false, "Failed to upload the model to the GPU");
@@ -122,6 +125,16 @@ RWKV_API struct rwkv_context * rwkv_init_from_file(const char * path, const uint
     }
 }
 
+RWKV_API struct rwkv_context * rwkv_mi355x_init_from_file_layers(const char * path, const uint32_t n_threads,
+                                                                 const uint32_t layer_begin, const uint32_t layer_end) {
+    g_last_error = RWKV_ERROR_NONE;
+    try {
+        return init_from_file(path, n_threads, layer_begin, layer_end);
+    } catch (const std::exception & e) {
+        RWKV_CHECK(RWKV_ERROR_CTX | RWKV_ERROR_ALLOC, nullptr, false, "Failed to load %s: %s", path, e.what());
+    }
+}
+
 RWKV_API struct rwkv_context * rwkv_clone_context(struct rwkv_context * ctx, const uint32_t n_threads) {
     if (!ctx) return nullptr;
     rwkv_context * c = new_context(ctx->model, n_threads);
@@ -134,6 +147,9 @@ RWKV_API bool rwkv_eval(struct rwkv_context * ctx, const uint32_t token, const f
     ctx->last_error = RWKV_ERROR_NONE;
     const size_t n_vocab = ctx->model->dm.n_vocab;
     CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, token < n_vocab, "Token (%" PRIu32 ") is out of range (0 .. %zu)", token, n_vocab - 1);
+    CTX_CHECK(ctx, RWKV_ERROR_CTX | RWKV_ERROR_UNSUPPORTED, false, !ctx->model->dm.partial(),
+              "This context holds layers [%u, %u) only (a pipeline stage): use rwkv_mi355x_eval_layers",
+              ctx->model->dm.layer_lo, ctx->model->dm.layer_hi);
     CTX_CHECK(ctx, RWKV_ERROR_CTX, false, ctx->engine->eval(&token, 1, state_in, state_out, logits_out), "GPU evaluation failed");
     return true;
 }
@@ -144,6 +160,9 @@ RWKV_API bool rwkv_eval_sequence(struct rwkv_context * ctx, const uint32_t * tok
     CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, T > 0, "Sequence length is 0");
     if (!tokens) return true;  // build/cache only (rwkv_eval_inc:102,122): workspace is allocated lazily
     if (T == 1) return rwkv_eval(ctx, tokens[0], state_in, state_out, logits_out);
+    CTX_CHECK(ctx, RWKV_ERROR_CTX | RWKV_ERROR_UNSUPPORTED, false, !ctx->model->dm.partial(),
+              "This context holds layers [%u, %u) only (a pipeline stage): use rwkv_mi355x_eval_layers",
+              ctx->model->dm.layer_lo, ctx->model->dm.layer_hi);
     const size_t n_vocab = ctx->model->dm.n_vocab;
     for (size_t i = 0; i < T; i++) {
         CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, tokens[i] < n_vocab, "Token at index %zu (%" PRIu32 ") is out of range (0 .. %zu)",
@@ -224,19 +243,25 @@ RWKV_API bool rwkv_mi355x_eval_device(struct rwkv_context * ctx, const uint32_t 
                                       float * logits_out, bool sync) {
     ctx->last_error = RWKV_ERROR_NONE;
     CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, T > 0 && tokens != nullptr, "Sequence length is 0");
+    CTX_CHECK(ctx, RWKV_ERROR_CTX | RWKV_ERROR_UNSUPPORTED, false, !ctx->model->dm.partial(),
+              "This context holds layers [%u, %u) only (a pipeline stage)", ctx->model->dm.layer_lo, ctx->model->dm.layer_hi);
     for (size_t i = 0; i < T; i++)
         CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, tokens[i] < ctx->model->dm.n_vocab, "Token out of range");
     CTX_CHECK(ctx, RWKV_ERROR_CTX, false, ctx->engine->eval_device(tokens, T, compute_logits || logits_out, logits_out, sync), "GPU evaluation failed");
     return true;
 }
 
-RWKV_API bool rwkv_mi355x_eval_layers(struct rwkv_context * ctx, const uint32_t * tokens, size_t T,
-                                      uint32_t layer_begin, uint32_t layer_end, float * x_dev, float * vfirst_dev,
-                                      bool compute_logits, float * logits_out) {
+static bool eval_layers(struct rwkv_context * ctx, const uint32_t * tokens, size_t T, uint32_t layer_begin,
+                        uint32_t layer_end, float * x_dev, float * vfirst_dev, bool compute_logits, float * logits_out,
+                        bool sync) {
     ctx->last_error = RWKV_ERROR_NONE;
+    CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, sync || logits_out == nullptr, "Asynchronous stage: logits stay on the device");
     const DeviceModel & dm = ctx->model->dm;
     CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, T > 0, "Sequence length is 0");
     CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, layer_begin < layer_end && layer_end <= dm.n_layer, "Bad layer range");
+    CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, layer_begin >= dm.layer_lo && layer_end <= dm.layer_hi,
+              "Layers [%u, %u) are not resident in this context (it holds [%u, %u))", layer_begin, layer_end, dm.layer_lo,
+              dm.layer_hi);
     CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, layer_begin == 0 || x_dev != nullptr, "x_dev required after layer 0");
     CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, layer_begin == 0 || dm.major != 7 || vfirst_dev != nullptr,
               "vfirst_dev required after layer 0 (v7)");
@@ -245,10 +270,26 @@ RWKV_API bool rwkv_mi355x_eval_layers(struct rwkv_context * ctx, const uint32_t 
         for (size_t i = 0; i < T; i++) CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, tokens[i] < dm.n_vocab, "Token out of range");
     }
     CTX_CHECK(ctx, RWKV_ERROR_CTX, false,
-              ctx->engine->eval_layers(tokens, T, layer_begin, layer_end, x_dev, vfirst_dev, compute_logits, logits_out),
+              ctx->engine->eval_layers(tokens, T, layer_begin, layer_end, x_dev, vfirst_dev, compute_logits, logits_out,
+                                       sync),
               "GPU evaluation failed");
     return true;
 }
+
+RWKV_API bool rwkv_mi355x_eval_layers(struct rwkv_context * ctx, const uint32_t * tokens, size_t T,
+                                      uint32_t layer_begin, uint32_t layer_end, float * x_dev, float * vfirst_dev,
+                                      bool compute_logits, float * logits_out) {
+    return eval_layers(ctx, tokens, T, layer_begin, layer_end, x_dev, vfirst_dev, compute_logits, logits_out, true);
+}
+
+RWKV_API bool rwkv_mi355x_eval_layers_async(struct rwkv_context * ctx, const uint32_t * tokens, size_t T,
+                                            uint32_t layer_begin, uint32_t layer_end, float * x_dev, float * vfirst_dev,
+                                            bool compute_logits) {
+    return eval_layers(ctx, tokens, T, layer_begin, layer_end, x_dev, vfirst_dev, compute_logits, nullptr, false);
+}
+
+RWKV_API float * rwkv_mi355x_logits_device(struct rwkv_context * ctx) { return ctx->engine->device_logits(); }
+
 
 RWKV_API bool rwkv_mi355x_sync(struct rwkv_context * ctx) { return ctx->engine->sync(); }
 RWKV_API long long rwkv_mi355x_debug_buffer(struct rwkv_context * ctx, const char * name, void * out, size_t bytes) {

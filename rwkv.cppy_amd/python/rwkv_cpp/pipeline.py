@@ -13,6 +13,7 @@ this library: tests/test_gpu_parity.py).
 The per-stage computation is injected (`stage_fn`), so the same driver runs the library
 (LibraryStage, GPU) and, in the CPU tests, the oracle.
 """
+import contextlib
 from typing import Callable, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -36,26 +37,9 @@ def stage_layers(n_layer: int, world: int, rank: int) -> Tuple[int, int]:
 StageFn = Callable[[np.ndarray, int, int, torch.Tensor, bool], Optional[np.ndarray]]
 
 
-def pipeline_eval_sequence(stage_fn: StageFn, tokens: Sequence[int], chunk: int, n_layer: int, n_embed: int,
-                           planes: int, rank: int, world: int, device: torch.device,
-                           wire_device: Optional[torch.device] = None, group=None,
-                           want_logits: bool = True) -> Optional[np.ndarray]:
-    """Runs this rank's stage over every chunk of `tokens`; returns the logits of the last token on
-    the last stage (None elsewhere).  wire_device: where messages live for the backend (the GPU for
-    nccl, the CPU for gloo); defaults to `device`."""
-    if chunk <= 0 or len(tokens) == 0:
-        raise ValueError('empty sequence or chunk size 0')
-    wire = wire_device or device
-    toks = np.ascontiguousarray(np.asarray(tokens, dtype=np.uint32))
-    bounds = [(i, min(i + chunk, len(toks))) for i in range(0, len(toks), chunk)]
-    l0, l1 = stage_layers(n_layer, world, rank)
-    prev, nxt = rank - 1, rank + 1
-
-    def post_recv(c: int):
-        a, b = bounds[c]
-        buf = torch.empty((planes, b - a, n_embed), dtype=torch.float32, device=wire)
-        return dist.irecv(buf, src=prev, group=group), buf
-
+def _run_chunks(stage_fn, toks, bounds, l0, l1, post_recv, planes, n_embed, rank, world, device, wire, group,
+                want_logits, host_sync):
+    nxt = rank + 1
     pending = post_recv(0) if rank > 0 else None
     sends: List = []
     logits = None
@@ -63,8 +47,8 @@ def pipeline_eval_sequence(stage_fn: StageFn, tokens: Sequence[int], chunk: int,
         if rank > 0:
             work, buf = pending
             work.wait()
-            if wire.type == 'cuda':
-                torch.cuda.current_stream(wire).synchronize()  # the stage runs on its own stream
+            if host_sync and wire.type == 'cuda':
+                torch.cuda.current_stream(wire).synchronize()  # a synchronous stage runs on its own stream
             pending = post_recv(c + 1) if c + 1 < len(bounds) else None
             x = buf if buf.device == device else buf.to(device)
         else:
@@ -81,16 +65,83 @@ def pipeline_eval_sequence(stage_fn: StageFn, tokens: Sequence[int], chunk: int,
     return logits
 
 
+def pipeline_eval_sequence(stage_fn: StageFn, tokens: Sequence[int], chunk: int, n_layer: int, n_embed: int,
+                           planes: int, rank: int, world: int, device: torch.device,
+                           wire_device: Optional[torch.device] = None, group=None,
+                           want_logits: bool = True) -> Optional[np.ndarray]:
+    """Runs this rank's stage over every chunk of `tokens`; returns the logits of the last token on
+    the last stage (None elsewhere).  wire_device: where messages live for the backend (the GPU for
+    nccl, the CPU for gloo); defaults to `device`."""
+    if chunk <= 0 or len(tokens) == 0:
+        raise ValueError('empty sequence or chunk size 0')
+    wire = wire_device or device
+    toks = np.ascontiguousarray(np.asarray(tokens, dtype=np.uint32))
+    bounds = [(i, min(i + chunk, len(toks))) for i in range(0, len(toks), chunk)]
+    l0, l1 = stage_layers(n_layer, world, rank)
+    prev = rank - 1
+
+    def post_recv(c: int):
+        a, b = bounds[c]
+        buf = torch.empty((planes, b - a, n_embed), dtype=torch.float32, device=wire)
+        return dist.irecv(buf, src=prev, group=group), buf
+
+    # an asynchronous stage (LibraryStage(async_=True)) computes on its own HIP stream: make it
+    # current so the receive, the compute and the send of each chunk are stream-ordered with no
+    # host wait; a synchronous stage returns with its output complete
+    stream = getattr(stage_fn, 'stream', None)
+    ctx = torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
+    with ctx:
+        logits = _run_chunks(stage_fn, toks, bounds, l0, l1, post_recv, planes, n_embed, rank, world, device, wire,
+                             group, want_logits, host_sync=stream is None)
+        if stream is not None:
+            stream.synchronize()
+    return logits
+
+
+def model_n_layer(path: str) -> int:
+    """n_layer from an rwkv.cpp file header (docs/FILE_FORMAT.md: magic, version, n_vocab, n_embed,
+    n_layer, data_type as uint32)."""
+    hdr = np.fromfile(path, dtype=np.uint32, count=6)
+    if hdr.size != 6 or hdr[0] != 0x67676d66:
+        raise ValueError(f'{path}: not an rwkv.cpp model file')
+    return int(hdr[4])
+
+
 class LibraryStage:
     """stage_fn over librwkv.so's rwkv_mi355x_eval_layers on this process's GPU.  The context keeps
-    its stage's state slice resident in HBM across calls (reset with reset_state)."""
+    its stage's state slice resident in HBM across calls (reset with reset_state).
 
-    def __init__(self, library, ctx, n_vocab: int, arch_major: int):
+    async_=True enqueues each stage call on the context's HIP stream without a host wait
+    (rwkv_mi355x_eval_layers_async); `stream` is that stream as a torch ExternalStream, which
+    pipeline_eval_sequence makes current so the RCCL send of a chunk is ordered behind its compute
+    and the next chunk's compute overlaps the send."""
+
+    def __init__(self, library, ctx, n_vocab: int, arch_major: int, async_: bool = False):
         self.lib = library
         self.ctx = ctx
         self.n_vocab = n_vocab
         self.v7 = arch_major == 7
         self.planes = 2 if self.v7 else 1
+        self.async_ = async_
+        self.stream = None
+        if async_:
+            self.stream = torch.cuda.ExternalStream(int(library.library.rwkv_mi355x_stream(ctx.ptr)))
+
+    @classmethod
+    def from_file(cls, library, path: str, rank: int, world: int, async_: bool = False):
+        """The stage context of `rank`: only its layers' weights are uploaded
+        (rwkv_mi355x_init_from_file_layers), so a stage's HBM holds ~1/world of the model."""
+        import ctypes
+        from .rwkv_cpp_shared_library import RWKVContext
+        n_layer = model_n_layer(path)
+        l0, l1 = stage_layers(n_layer, world, rank)
+        ptr = library.library.rwkv_mi355x_init_from_file_layers(path.encode(), 1, l0, l1)
+        if not ptr:
+            raise ValueError(f'failed to load layers [{l0}, {l1}) of {path}')
+        ctx = RWKVContext(ptr)
+        arch = (ctypes.c_int64 * 4)()
+        library.library.rwkv_mi355x_arch(ctx.ptr, arch)
+        return cls(library, ctx, library.library.rwkv_get_n_vocab(ctx.ptr), int(arch[0]), async_=async_)
 
     def reset_state(self, state: Optional[np.ndarray] = None) -> None:
         ptr = None if state is None else state.ctypes.data
@@ -101,9 +152,16 @@ class LibraryStage:
         import ctypes
         if x.device.type != 'cuda' or not x.is_contiguous():
             raise ValueError('stage buffers must be contiguous device tensors')
-        logits = np.zeros(self.n_vocab, np.float32) if want_logits else None
         xp = x.data_ptr()
         vp = x[1].data_ptr() if self.v7 else None
+        if self.async_ and not want_logits:
+            # enqueued on the context stream; the caller's RCCL ops on the same stream follow it
+            ok = self.lib.library.rwkv_mi355x_eval_layers_async(self.ctx.ptr, tokens.ctypes.data, len(tokens), l0, l1,
+                                                                xp, vp, False)
+            if not ok:
+                raise ValueError(f'rwkv_mi355x_eval_layers_async failed on layers [{l0}, {l1})')
+            return None
+        logits = np.zeros(self.n_vocab, np.float32) if want_logits else None
         lg = logits.ctypes.data_as(ctypes.POINTER(ctypes.c_float)) if want_logits else None
         ok = self.lib.library.rwkv_mi355x_eval_layers(self.ctx.ptr, tokens.ctypes.data, len(tokens), l0, l1, xp, vp,
                                                       want_logits, lg)

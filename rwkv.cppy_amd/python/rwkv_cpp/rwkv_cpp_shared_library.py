@@ -74,6 +74,14 @@ class RWKVSharedLibrary:
         L.rwkv_mi355x_eval_device.restype = ctypes.c_bool
         L.rwkv_mi355x_eval_layers.argtypes = [vp, vp, sz, u32, u32, vp, vp, ctypes.c_bool, P_FLOAT]
         L.rwkv_mi355x_eval_layers.restype = ctypes.c_bool
+        L.rwkv_mi355x_eval_layers_async.argtypes = [vp, vp, sz, u32, u32, vp, vp, ctypes.c_bool]
+        L.rwkv_mi355x_eval_layers_async.restype = ctypes.c_bool
+        L.rwkv_mi355x_logits_device.argtypes = [vp]
+        L.rwkv_mi355x_logits_device.restype = vp
+        L.rwkv_mi355x_init_from_file_layers.argtypes = [ctypes.c_char_p, u32, u32, u32]
+        L.rwkv_mi355x_init_from_file_layers.restype = vp
+        L.rwkv_mi355x_debug_buffer.argtypes = [vp, ctypes.c_char_p, vp, sz]
+        L.rwkv_mi355x_debug_buffer.restype = ctypes.c_longlong
         L.rwkv_mi355x_sync.argtypes = [vp]
         L.rwkv_mi355x_sync.restype = ctypes.c_bool
         L.rwkv_mi355x_stream.argtypes = [vp]

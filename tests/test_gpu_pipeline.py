@@ -69,23 +69,21 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _rank_main(rank, world, port, path, toks, chunk, out_dir):
+def _rank_main(rank, world, port, path, toks, chunk, out_dir, async_):
     import ctypes
     import sys
     import torch.distributed as dist
     sys.path.insert(0, os.path.join(os.path.dirname(LIB_PATH), '..', 'python'))
     from rwkv_cpp import RWKVSharedLibrary
-    from rwkv_cpp.pipeline import LibraryStage, pipeline_eval_sequence, stage_layers
+    from rwkv_cpp.pipeline import LibraryStage, model_n_layer, pipeline_eval_sequence, stage_layers
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
     dist.init_process_group('gloo', rank=rank, world_size=world)
     try:
         L = RWKVSharedLibrary(LIB_PATH)
-        ctx = L.rwkv_init_from_file(path, 1, 99)
-        arch = (ctypes.c_int64 * 4)()
-        L.library.rwkv_mi355x_arch(ctx.ptr, arch)
-        stage = LibraryStage(L, ctx, L.rwkv_get_n_vocab(ctx), int(arch[0]))
+        stage = LibraryStage.from_file(L, path, rank, world, async_=async_)   # this stage's layers only
+        ctx = stage.ctx
         stage.reset_state()
-        n_layer, C = L.rwkv_get_n_layer(ctx), L.rwkv_get_n_embed(ctx)
+        n_layer, C = model_n_layer(path), L.rwkv_get_n_embed(ctx)
         lg = pipeline_eval_sequence(stage, toks, chunk, n_layer, C, stage.planes, rank, world,
                                     torch.device('cuda', 0), wire_device=torch.device('cpu'))
         st = np.zeros(L.rwkv_get_state_buffer_element_count(ctx), np.float32)
@@ -93,6 +91,9 @@ def _rank_main(rank, world, port, path, toks, chunk, out_dir):
         l0, l1 = stage_layers(n_layer, world, rank)
         per = len(st) // n_layer
         np.save(os.path.join(out_dir, f'state{rank}.npy'), st[l0 * per:l1 * per])
+        np.save(os.path.join(out_dir, f'bytes{rank}.npy'),
+                np.array([L.library.rwkv_mi355x_weight_bytes(ctx.ptr, False),
+                          L.library.rwkv_mi355x_weight_bytes(ctx.ptr, True)]))
         if lg is not None:
             np.save(os.path.join(out_dir, 'logits.npy'), lg)
         L.rwkv_free(ctx)
@@ -100,8 +101,12 @@ def _rank_main(rank, world, port, path, toks, chunk, out_dir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('arch,fmt,chunk', [(6, 'Q4_0', 16), (7, 'Q5_1', 33)])
-def test_two_process_pipeline_bit_exact(tmp_path, arch, fmt, chunk):
+@pytest.mark.parametrize('arch,fmt,chunk,world,async_', [(6, 'Q4_0', 16, 2, False), (7, 'Q5_1', 33, 2, True),
+                                                         (5, 'Q4_1', 20, 3, True)])
+def test_multi_process_pipeline_bit_exact(tmp_path, arch, fmt, chunk, world, async_):
+    """Stage contexts loaded with rwkv_mi355x_init_from_file_layers hold only their layers (HBM weight
+    bytes ~1/world of the model's; the head only on the last stage) and the pipelined result equals
+    one rwkv_eval_sequence bit for bit, synchronous and stream-ordered (async) stages alike."""
     import torch.multiprocessing as mp
     L = library()
     p = _synthetic(tmp_path, arch, fmt)
@@ -109,13 +114,51 @@ def test_two_process_pipeline_bit_exact(tmp_path, arch, fmt, chunk):
     m = RWKVModel(L, p)
     ref_lg, ref_st = m.eval_sequence(toks, None, use_numpy=True)
     n_layer = L.rwkv_get_n_layer(m._ctx)
+    full_layers = L.library.rwkv_mi355x_weight_bytes(m._ctx.ptr, False)
+    full_head = L.library.rwkv_mi355x_weight_bytes(m._ctx.ptr, True) - full_layers
     m.free()
-    mp.start_processes(_rank_main, args=(2, _free_port(), p, toks, chunk, str(tmp_path)), nprocs=2,
+    mp.start_processes(_rank_main, args=(world, _free_port(), p, toks, chunk, str(tmp_path), async_), nprocs=world,
                        start_method='spawn', join=True)
     assert np.array_equal(np.load(tmp_path / 'logits.npy').view(np.uint32), ref_lg.view(np.uint32))
     per = len(ref_st) // n_layer
     from rwkv_cpp.pipeline import stage_layers
-    for r in range(2):
-        l0, l1 = stage_layers(n_layer, 2, r)
+    total = 0.0
+    for r in range(world):
+        l0, l1 = stage_layers(n_layer, world, r)
         got = np.load(tmp_path / f'state{r}.npy')
         assert np.array_equal(got.view(np.uint32), ref_st[l0 * per:l1 * per].view(np.uint32)), r
+        lb, tb = np.load(tmp_path / f'bytes{r}.npy')
+        # layers are near-equal in size (v7's layer 0 lacks the value-residual LoRA)
+        assert lb <= full_layers * (l1 - l0) / n_layer * 1.05, (r, lb, full_layers)
+        assert (tb - lb) == pytest.approx(full_head if r == world - 1 else 0.0, rel=1e-6, abs=1.0), r
+        total += lb
+    assert total == pytest.approx(full_layers, rel=1e-9)   # the stages partition the layer weights
+
+
+def test_stage_context_rejects_whole_model_calls(tmp_path):
+    """A stage context (layers [l0, l1) only) refuses rwkv_eval / rwkv_eval_sequence and layer ranges it
+    does not hold, with the context's error flags set -- never a fault."""
+    import ctypes
+    L = library()
+    lib = L.library
+    p = _synthetic(tmp_path, 6, 'Q4_0')
+    ptr = lib.rwkv_mi355x_init_from_file_layers(p.encode(), 1, 1, 3)
+    assert ptr
+    lib.rwkv_set_print_errors(ptr, False)
+    C, n_vocab = lib.rwkv_get_n_embed(ptr), lib.rwkv_get_n_vocab(ptr)
+    st = np.zeros(lib.rwkv_get_state_buffer_element_count(ptr), np.float32)
+    lg = np.zeros(n_vocab, np.float32)
+    fp = ctypes.POINTER(ctypes.c_float)
+    assert not lib.rwkv_eval(ptr, 1, None, st.ctypes.data_as(fp), lg.ctypes.data_as(fp))
+    assert lib.rwkv_get_last_error(ptr) != 0
+    toks = (ctypes.c_int32 * 3)(1, 2, 3)
+    assert not lib.rwkv_eval_sequence(ptr, toks, 3, None, st.ctypes.data_as(fp), lg.ctypes.data_as(fp))
+    assert lib.rwkv_get_last_error(ptr) != 0
+    x = torch.zeros((1, 3, C), dtype=torch.float32, device='cuda')
+    t = np.array([1, 2, 3], np.uint32)
+    assert lib.rwkv_mi355x_state_upload(ptr, None)
+    assert not lib.rwkv_mi355x_eval_layers(ptr, t.ctypes.data, 3, 0, 2, x.data_ptr(), None, False, None)
+    assert lib.rwkv_get_last_error(ptr) != 0
+    assert lib.rwkv_mi355x_eval_layers(ptr, t.ctypes.data, 3, 1, 3, x.data_ptr(), None, False, None)
+    assert lib.rwkv_get_last_error(ptr) == 0
+    lib.rwkv_free(ptr)

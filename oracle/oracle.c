@@ -467,10 +467,11 @@ int oracle_get_threads(void) {
  *     (quantized: acc = fma(d_w*d_x, sumi, acc), _1 formats: acc2 += m_w*s_x; F16/F32: one fma
  *     per element); the 64 lane partials are folded by wave_sum63's perfect binary tree over
  *     adjacent lanes; _1 formats add the folded acc2, others add +0.0.
- *   - LayerNorm (ggml_norm, fp64 sums): lane l owns x[l + 64 j], four fp64 partials by j % 4
- *     combined as (p0 + p1) + (p2 + p3), then the same 64-lane tree in fp64.
- *   - per-head sums (GroupNorm statistics, wkv7 row sums, l2norm, v7 bonus) fold with the
- *     xor butterfly of __shfl_xor (stride S/2 first); wkv6 y sums over keys split in
+ *   - LayerNorm (ggml_norm, fp64 sums): 512-element chunks, lane l owning the chunk's elements
+ *     8l..8l+7 as an fp64 pairwise tree, the same 64-lane tree per chunk, chunks in order.
+ *   - GroupNorm statistics fold in wave_sum63's tree (adjacent lanes first); the other per-head
+ *     sums (wkv7 row sums, l2norm, v7 bonus) fold with the xor butterfly of __shfl_xor (stride
+ *     S/2 first); wkv6 y sums over keys split in
  *     G = min(256/S, S) groups of S/G keys (head size 64: four 4-key runs (p0+p1)+(p2+p3)),
  *     groups folded as a stride-halving tree.
  *   - exp / tanh: the kernels' own polynomial implementations (device_common.hpp rk_expf /
@@ -532,31 +533,46 @@ static float bfly_f(float * a, int n) {
         for (int i = 0; i < n / 2; i++) a[i] = a[i] + a[i + n / 2];
     return a[0];
 }
-static double bfly_d(double * a, int n) {
-    for (; n > 1; n >>= 1)
-        for (int i = 0; i < n / 2; i++) a[i] = a[i] + a[i + n / 2];
-    return a[0];
-}
 
-/* ggml_norm statistics in the kernels' association (ln_stats_regs / ln_stats_wave) */
+/* ggml_norm statistics in the kernels' chunk association (device_common.hpp ln_stats_wave and the
+ * decode prologues): 512-element chunks; lane l of a chunk owns elements 8l..8l+7, summed as the
+ * fp64 pairwise tree ((e0+e1)+(e2+e3))+((e4+e5)+(e6+e7)); the 64 lane sums fold by wave_sum63's
+ * tree; chunk sums are added in ascending order; elements past n count as zeros. */
+static double ln_tree8(const float * v) {
+    const double a = ((double)v[0] + (double)v[1]) + ((double)v[2] + (double)v[3]);
+    const double b = ((double)v[4] + (double)v[5]) + ((double)v[6] + (double)v[7]);
+    return a + b;
+}
 static void ln_stats_gpu(const float * x, int64_t n, float eps, float * mean_out, float * scale_out) {
     double lanes[64];
-    const int64_t P = n / 64;
-    for (int l = 0; l < 64; l++) {
-        double p[4] = {0.0, 0.0, 0.0, 0.0};
-        for (int64_t j = 0; j < P; j++) p[j & 3] += (double)x[l + 64 * j];
-        lanes[l] = (p[0] + p[1]) + (p[2] + p[3]);
-    }
-    const float mean = (float)(tree_d(lanes, 64) / (double)n);
-    for (int l = 0; l < 64; l++) {
-        double q[4] = {0.0, 0.0, 0.0, 0.0};
-        for (int64_t j = 0; j < P; j++) {
-            const float d = x[l + 64 * j] - mean;
-            q[j & 3] += (double)(d * d);
+    const int64_t nc = (n + 511) / 512;
+    double s = 0.0;
+    for (int64_t c = 0; c < nc; c++) {
+        for (int l = 0; l < 64; l++) {
+            float v[8];
+            for (int j = 0; j < 8; j++) {
+                const int64_t k = c * 512 + 8 * l + j;
+                v[j] = k < n ? x[k] : 0.0f;
+            }
+            lanes[l] = ln_tree8(v);
         }
-        lanes[l] = (q[0] + q[1]) + (q[2] + q[3]);
+        s += tree_d(lanes, 64);
     }
-    const float var = (float)(tree_d(lanes, 64) / (double)n);
+    const float mean = (float)(s / (double)n);
+    double q = 0.0;
+    for (int64_t c = 0; c < nc; c++) {
+        for (int l = 0; l < 64; l++) {
+            float v[8];
+            for (int j = 0; j < 8; j++) {
+                const int64_t k = c * 512 + 8 * l + j;
+                const float d = (k < n ? x[k] : 0.0f) - mean;
+                v[j] = k < n ? d * d : 0.0f;
+            }
+            lanes[l] = ln_tree8(v);
+        }
+        q += tree_d(lanes, 64);
+    }
+    const float var = (float)(q / (double)n);
     *mean_out = mean;
     *scale_out = 1.0f / sqrtf(var + eps);
 }
@@ -1219,18 +1235,19 @@ static void mix_v4(const float * xa, const float * xp, const float * mu, int64_t
 
 static void group_norm(float * x, int64_t T, int64_t H, int64_t S, float eps, const float * w, const float * b) {
     if (g_variant & OV_GPU) {
-        /* k_att6_dec / k_att7_dec / k_groupnorm: fp64 butterfly sums over the head's S lanes */
+        /* k_att6_dec / k_att7_dec / k_groupnorm: fp64 sums over the head's S lanes in wave_sum63's
+         * tree (group_tree_sum_d: adjacent lanes first) */
         double buf[64];
         for (int64_t t = 0; t < T; t++)
             for (int64_t h = 0; h < H; h++) {
                 float * p = x + t * H * S + h * S;
                 for (int64_t i = 0; i < S; i++) buf[i] = (double)p[i];
-                const float mean = (float)(bfly_d(buf, (int)S) / (double)S);
+                const float mean = (float)(tree_d(buf, (int)S) / (double)S);
                 for (int64_t i = 0; i < S; i++) {
                     const float d = p[i] - mean;
                     buf[i] = (double)(d * d);
                 }
-                const float var = (float)(bfly_d(buf, (int)S) / (double)S);
+                const float var = (float)(tree_d(buf, (int)S) / (double)S);
                 const float scale = 1.0f / sqrtf(var + eps);
                 for (int64_t i = 0; i < S; i++) {
                     float o = (p[i] - mean) * scale;

@@ -2,6 +2,7 @@
 #pragma once
 
 #include "common.hpp"
+#include "stamp.hpp"
 
 namespace rwkvmi {
 
@@ -395,83 +396,118 @@ __device__ __forceinline__ double wave_allsum_d(double v) {
     return __builtin_bit_cast(double, ((long long)hi << 32) | (long long)(unsigned)lo);
 }
 
-// LayerNorm statistics of x[0..K) by ONE wave, no LDS and no barrier (ggml_norm semantics:
-// fp64 sums, two passes, population variance).  Lane l owns x[l + 64 j] (coalesced loads),
-// summed into four fp64 partials (j % 4) combined as (p0+p1)+(p2+p3), then wave_sum63_d.
-// Every LayerNorm on the device (decode prologues, sequence kernels) uses this one
-// association, so decode and sequence agree bit for bit.  Requires K % 64 == 0,
-// K <= 64*PMAX, all lanes active.
-// Register form of ln_stats_wave for K <= 64*PC: load phase and compute phase separate, so a
-// caller can put other loads in flight between them.
-template <int PC>
-__device__ __forceinline__ void ln_load_regs(const float * x, int K, float (&v)[PC]) {
-    const int lane = threadIdx.x & 63, P = K >> 6;
-#pragma unroll
-    for (int j = 0; j < PC; j++) v[j] = x[lane + 64 * min(j, P - 1)];
-}
-template <int PC>
-__device__ __forceinline__ void ln_stats_regs(const float (&v)[PC], int K, float eps, float & mean, float & scale) {
-    const int P = K >> 6;
-    double p[4] = {0.0, 0.0, 0.0, 0.0}, q[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int j = 0; j < PC; j++)
-        if (j < P) p[j & 3] += (double)v[j];
-    const double s = wave_allsum_d((p[0] + p[1]) + (p[2] + p[3]));
-    mean = (float)(s / (double)K);
-#pragma unroll
-    for (int j = 0; j < PC; j++)
-        if (j < P) {
-            const float d = v[j] - mean;
-            q[j & 3] += (double)(d * d);
-        }
-    const double s2 = wave_allsum_d((q[0] + q[1]) + (q[2] + q[3]));
-    const float var = (float)(s2 / (double)K);
-    scale = 1.0f / sqrtf(var + eps);
+// s / n for the statistics' means: a power-of-two n divides by scaling (v_ldexp, exact and
+// bit-identical to the correctly rounded division), other n take the fp64 division.
+__device__ __forceinline__ double div_count(double s, int n) {
+    return (n & (n - 1)) == 0 ? ldexp(s, -__builtin_ctz((unsigned)n)) : s / (double)n;
 }
 
-template <int PC>
-__device__ __forceinline__ void ln_stats_wave(const float * x, int K, float eps, float & mean, float & scale) {
-    const int lane = threadIdx.x & 63, P = K >> 6;
-    double p[4] = {0.0, 0.0, 0.0, 0.0}, q[4] = {0.0, 0.0, 0.0, 0.0};
-    if (P <= PC) {
-        // one chunk: the second pass reuses the registers
-        float v[PC];
-        ln_load_regs<PC>(x, K, v);
-        ln_stats_regs<PC>(v, K, eps, mean, scale);
-        return;
-    } else {
-        // chunks of PC elements per lane, reloaded for the second pass (same association)
-        for (int j0 = 0; j0 < P; j0 += PC) {
-            float v[PC];
+// Per-head fp64 sum (GroupNorm statistics) in wave_sum63's association -- adjacent lanes
+// paired first -- with the result on every lane of the group.  Width 64: the DPP tree plus a
+// lane-63 broadcast (no LDS round trips); narrower groups: the xor butterfly with the stride
+// doubling (1, 2, 4, ...), which folds in the same order.
+__device__ __forceinline__ double group_tree_sum_d(double v, int width) {
+    if (width == 64) return wave_allsum_d(v);
+    for (int o = 1; o < width; o <<= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// LayerNorm statistics (ggml_norm semantics: fp64 sums, two passes, population variance) in
+// the CHUNK association that every LayerNorm on the device and the oracle's GPU variant share:
+// x is cut into 512-element chunks; lane l of a chunk owns its 8 consecutive elements 8l..8l+7
+// (two 16-byte loads), summed as an fp64 pairwise tree; the chunk's 64 lane sums fold by
+// wave_sum63's tree; chunk sums are added in ascending chunk order.  Elements past K count as
+// zeros (K % 8 == 0).  The decode prologues spread the chunks over several waves and exchange
+// the chunk sums through LDS; the sequence kernels walk the chunks in one wave -- same bits.
+constexpr int LN_CHUNK = 512;
+
+__device__ __forceinline__ double ln_tree8(const float (&v)[8]) {
+    const double a = ((double)v[0] + (double)v[1]) + ((double)v[2] + (double)v[3]);
+    const double b = ((double)v[4] + (double)v[5]) + ((double)v[6] + (double)v[7]);
+    return a + b;
+}
+// sum of one chunk's elements (every lane gets it); x = this lane's 8 elements
+__device__ __forceinline__ double ln_chunk_sum(const float (&x)[8], bool valid) {
+    float v[8];
 #pragma unroll
-            for (int j = 0; j < PC; j++) v[j] = x[lane + 64 * min(j0 + j, P - 1)];
+    for (int j = 0; j < 8; j++) v[j] = valid ? x[j] : 0.0f;
+    return wave_allsum_d(ln_tree8(v));
+}
+// sum of one chunk's (x - mean)^2
+__device__ __forceinline__ double ln_chunk_sq(const float (&x)[8], bool valid, float mean) {
+    float v[8];
 #pragma unroll
-            for (int j = 0; j < PC; j++)
-                if (j0 + j < P) p[j & 3] += (double)v[j];
-        }
-        const double s = wave_allsum_d((p[0] + p[1]) + (p[2] + p[3]));
-        mean = (float)(s / (double)K);
-        for (int j0 = 0; j0 < P; j0 += PC) {
-            float v[PC];
-#pragma unroll
-            for (int j = 0; j < PC; j++) v[j] = x[lane + 64 * min(j0 + j, P - 1)];
-#pragma unroll
-            for (int j = 0; j < PC; j++)
-                if (j0 + j < P) {
-                    const float d = v[j] - mean;
-                    q[j & 3] += (double)(d * d);
-                }
-        }
+    for (int j = 0; j < 8; j++) {
+        const float d = x[j] - mean;
+        v[j] = valid ? d * d : 0.0f;
     }
-    const double s2 = wave_allsum_d((q[0] + q[1]) + (q[2] + q[3]));
-    const float var = (float)(s2 / (double)K);
-    scale = 1.0f / sqrtf(var + eps);
+    return wave_allsum_d(ln_tree8(v));
+}
+__device__ __forceinline__ float ln_scale(double sq, int K, float eps) {
+    const float var = (float)div_count(sq, K);
+    return 1.0f / sqrtf(var + eps);
 }
 
-// PC (elements per lane held at once) is a multiple of 4, so chunking keeps the j % 4
-// association of the partials.
+__device__ __forceinline__ void ln_load8(float (&v)[8], const float * x, int k, int K) {
+    const float * p = x + min(k, K - 8);
+    const float4 a = *(const float4 *)p, b = *(const float4 *)(p + 4);
+    v[0] = a.x, v[1] = a.y, v[2] = a.z, v[3] = a.w, v[4] = b.x, v[5] = b.y, v[6] = b.z, v[7] = b.w;
+}
+
+// One wave, the chunks already in registers (nc <= NC): x[c] = this lane's 8 elements of chunk c.
+// The chunk sums are independent DPP chains, so their latencies overlap.
+template <int NC>
+__device__ __forceinline__ void ln_stats_regs(const float (&x)[NC][8], int nc, int K, float eps, float & mean,
+                                              float & scale) {
+    const int lane = threadIdx.x & 63;
+    double cs[NC];
+#pragma unroll
+    for (int c = 0; c < NC; c++) cs[c] = c < nc ? ln_chunk_sum(x[c], c * LN_CHUNK + lane * 8 < K) : 0.0;
+    double s = 0.0;
+#pragma unroll
+    for (int c = 0; c < NC; c++)
+        if (c < nc) s += cs[c];
+    mean = (float)div_count(s, K);
+#pragma unroll
+    for (int c = 0; c < NC; c++) cs[c] = c < nc ? ln_chunk_sq(x[c], c * LN_CHUNK + lane * 8 < K, mean) : 0.0;
+    double q = 0.0;
+#pragma unroll
+    for (int c = 0; c < NC; c++)
+        if (c < nc) q += cs[c];
+    scale = ln_scale(q, K, eps);
+}
+
+// One wave, any K (x 16-byte aligned): the chunks in order, kept in registers for the second
+// pass up to 4 chunks (K <= 2048), reloaded beyond.
+__device__ inline void ln_stats_wave(const float * x, int K, float eps, float & mean, float & scale) {
+    const int lane = threadIdx.x & 63, nc = (K + LN_CHUNK - 1) / LN_CHUNK;
+    float v[4][8];
+#pragma unroll
+    for (int c = 0; c < 4; c++) ln_load8(v[c], x, min(c, nc - 1) * LN_CHUNK + lane * 8, K);
+    double s = 0.0;
+#pragma unroll
+    for (int c = 0; c < 4; c++)
+        if (c < nc) s += ln_chunk_sum(v[c], c * LN_CHUNK + lane * 8 < K);
+    for (int c = 4; c < nc; c++) {
+        float t[8];
+        ln_load8(t, x, c * LN_CHUNK + lane * 8, K);
+        s += ln_chunk_sum(t, c * LN_CHUNK + lane * 8 < K);
+    }
+    mean = (float)div_count(s, K);
+    double q = 0.0;
+#pragma unroll
+    for (int c = 0; c < 4; c++)
+        if (c < nc) q += ln_chunk_sq(v[c], c * LN_CHUNK + lane * 8 < K, mean);
+    for (int c = 4; c < nc; c++) {
+        float t[8];
+        ln_load8(t, x, c * LN_CHUNK + lane * 8, K);
+        q += ln_chunk_sq(t, c * LN_CHUNK + lane * 8 < K, mean);
+    }
+    scale = ln_scale(q, K, eps);
+}
+
 __device__ __forceinline__ void ln_stats_any(const float * x, int K, float eps, float & mean, float & scale) {
-    ln_stats_wave<32>(x, K, eps, mean, scale);
+    ln_stats_wave(x, K, eps, mean, scale);
 }
 
 // Block-level entry point kept for the sequence kernels: every wave computes the same

@@ -14,8 +14,49 @@
 #include <string>
 
 #include "kernels.hpp"
+#include "stamp.hpp"
 
 namespace rwkvmi {
+
+#ifdef RWKV_STAMP
+// Diagnostic builds (stamp.hpp): every kernel translation unit registers a setter for its copy
+// of the device-side control block; the rings are dumped to $RWKV_STAMP_OUT when an engine dies.
+static std::vector<void (*)(const StampCtl &)> & stamp_setters() {
+    static std::vector<void (*)(const StampCtl &)> v;
+    return v;
+}
+int stamp_register(void (*f)(const StampCtl &)) {
+    stamp_setters().push_back(f);
+    return 0;
+}
+static StampCtl g_host_stamp = {nullptr, nullptr};
+static void stamp_init() {
+    if (g_host_stamp.buf) return;
+    const size_t bytes = (size_t)kStampCUs * kStampRing * 64;
+    if (hipMalloc(&g_host_stamp.buf, bytes) != hipSuccess || hipMalloc(&g_host_stamp.ctr, kStampCUs * 4) != hipSuccess)
+        return;
+    (void)hipMemset(g_host_stamp.buf, 0, bytes);
+    (void)hipMemset(g_host_stamp.ctr, 0, kStampCUs * 4);
+    for (auto f : stamp_setters()) f(g_host_stamp);
+    (void)hipDeviceSynchronize();
+}
+static void stamp_dump() {
+    const char * out = getenv("RWKV_STAMP_OUT");
+    if (!out || !g_host_stamp.buf) return;
+    const size_t bytes = (size_t)kStampCUs * kStampRing * 64;
+    std::vector<unsigned long long> h(bytes / 8);
+    if (hipMemcpy(h.data(), g_host_stamp.buf, bytes, hipMemcpyDeviceToHost) != hipSuccess) return;
+    FILE * f = fopen(out, "wb");
+    if (!f) return;
+    // only the non-empty records: {t0, t1, t2, tag, x0..x3}
+    for (size_t i = 0; i < h.size(); i += 8)
+        if (h[i]) fwrite(&h[i], 8, 8, f);
+    fclose(f);
+}
+#else
+static void stamp_init() {}
+static void stamp_dump() {}
+#endif
 
 // ------------------------------------------------------------------------- upload
 
@@ -308,6 +349,7 @@ __global__ void k_init_state(float * st, size_t n, int C, int v4) {
 
 Engine::~Engine() {
     if (stream_) (void)hipStreamSynchronize(stream_);
+    stamp_dump();
     drop_graphs();
     if (gy_) (void)hipFree(gy_);
     if (part_) (void)hipFree(part_);
@@ -321,6 +363,7 @@ Engine::~Engine() {
 
 bool Engine::init() {
     HIP_OK(hipSetDevice(m_->device));
+    stamp_init();
     {
         int cus = 0;
         HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, m_->device));

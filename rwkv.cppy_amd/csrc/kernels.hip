@@ -229,6 +229,7 @@ bool launch_delay(hipStream_t st, int us) {
 __global__ __launch_bounds__(256) void k_embed_ln(const uint32_t * tokens, DMat emb, const float * w,
                                                   const float * b, float * x) {
     __shared__ double sh[8];
+    STAMP_BEGIN();
     const int t = blockIdx.x, C = emb.K;
     const size_t tok = tokens[t];
     float * xr = x + (size_t)t * C;
@@ -240,6 +241,7 @@ __global__ __launch_bounds__(256) void k_embed_ln(const uint32_t * tokens, DMat 
     float mean, scale;
     ln_stats(xr, C, 1e-5f, mean, scale, sh);
     for (int c = threadIdx.x; c < C; c += blockDim.x) xr[c] = ln_apply(xr[c], mean, scale, w[c], b[c]);
+    STAMP_END(5);
 }
 
 bool launch_embed_ln(hipStream_t st, const uint32_t * tokens, int T, const DMat & emb, const float * w,
@@ -1019,11 +1021,11 @@ __global__ __launch_bounds__(1024) void k_groupnorm(int T, int H, int S, float e
         if (c0 + (tid & ~63) >= C) continue;
         const size_t i = (size_t)t * C + c;
         const float x = y[i];
-        const double s = group_sum((double)x, S);
-        const float mean = (float)(s / (double)S);
+        const double s = group_tree_sum_d((double)x, S);
+        const float mean = (float)div_count(s, S);
         const float d = x - mean;
-        const double s2 = group_sum((double)(d * d), S);
-        const float var = (float)(s2 / (double)S);
+        const double s2 = group_tree_sum_d((double)(d * d), S);
+        const float var = (float)div_count(s2, S);
         const float scale = 1.0f / sqrtf(var + eps);
         float o = d * scale;
         o = o * w[c];

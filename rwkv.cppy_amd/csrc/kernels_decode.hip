@@ -276,12 +276,13 @@ __device__ __forceinline__ void decay_rows(const Att6Dec & a, const ActBuf & act
 template <int WF, int PF>
 __global__ __launch_bounds__(256) void k_att6_dec(Att6Dec a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    __shared__ float sr[64], sk[64], sv[64], sw[64], su[64];
+    __shared__ __attribute__((aligned(16))) float sr[64], sk[64], sv[64], sw[64], su[64];
     __shared__ float part[16][64];
     const int h = blockIdx.x, S = a.S, G = min(256 / S, S), IPG = S / G;
     const int tid = threadIdx.x, j = tid % S, g = min(tid / S, G - 1), c0 = h * S;
     const bool active = tid < S * G;
     const size_t hb = (size_t)h * S * S;
+    STAMP_BEGIN();
     float st[16];
 #pragma unroll
     for (int ii = 0; ii < 16; ii++)
@@ -317,6 +318,7 @@ __global__ __launch_bounds__(256) void k_att6_dec(Att6Dec a) {
         }
     }
     __syncthreads();
+    STAMP_MID();
     if (WF != -2 && !a.w) {
         if constexpr (WF == -2) {
         } else if constexpr (PF > 0) {
@@ -338,28 +340,50 @@ __global__ __launch_bounds__(256) void k_att6_dec(Att6Dec a) {
         }
         __syncthreads();
     }
+    STAMP_X(0);
     // wkv6 for one token (ggml_rwkv_wkv6 semantics, same arithmetic as the sequence kernels).
     // Head size 64 (IPG 16): the group's sum is (p0 + p1) + (p2 + p3) over its four 4-key runs,
     // k_wkv6_s64's association; other head sizes: one sequential run (k_wkv6's).
     if (active) {
         const float vj = sv[j];
+        // the group's key operands into registers first (all LDS reads in flight at once; head
+        // size 64: 16-byte reads), then the arithmetic -- same operations, same order
+        float kq[16], uq[16], rq[16], wq[16];
+        if (IPG == 16) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const float4 k4 = *(const float4 *)(sk + g * 16 + 4 * q), u4 = *(const float4 *)(su + g * 16 + 4 * q);
+                const float4 r4 = *(const float4 *)(sr + g * 16 + 4 * q), w4 = *(const float4 *)(sw + g * 16 + 4 * q);
+                kq[4 * q] = k4.x, kq[4 * q + 1] = k4.y, kq[4 * q + 2] = k4.z, kq[4 * q + 3] = k4.w;
+                uq[4 * q] = u4.x, uq[4 * q + 1] = u4.y, uq[4 * q + 2] = u4.z, uq[4 * q + 3] = u4.w;
+                rq[4 * q] = r4.x, rq[4 * q + 1] = r4.y, rq[4 * q + 2] = r4.z, rq[4 * q + 3] = r4.w;
+                wq[4 * q] = w4.x, wq[4 * q + 1] = w4.y, wq[4 * q + 2] = w4.z, wq[4 * q + 3] = w4.w;
+            }
+        } else {
+#pragma unroll
+            for (int ii = 0; ii < 16; ii++) {
+                const int i = g * IPG + min(ii, IPG - 1);
+                kq[ii] = sk[i], uq[ii] = su[i], rq[ii] = sr[i], wq[ii] = sw[i];
+            }
+        }
         float acc = 0.0f, p4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
         for (int ii = 0; ii < 16; ii++) {
             if (ii < IPG) {
                 const int i = g * IPG + ii;
                 const float prev = st[ii];
-                const float kv = vj * sk[i];
-                const float temp = kv * su[i] + prev;
-                const float t = temp * sr[i];
+                const float kv = vj * kq[ii];
+                const float temp = kv * uq[ii] + prev;
+                const float t = temp * rq[ii];
                 acc += t;
                 p4[ii >> 2] += t;
-                a.sout[hb + (size_t)i * S + j] = prev * sw[i] + kv;
+                a.sout[hb + (size_t)i * S + j] = prev * wq[ii] + kv;
             }
         }
         part[g][j] = IPG == 16 ? (p4[0] + p4[1]) + (p4[2] + p4[3]) : acc;
     }
     __syncthreads();
+    STAMP_X(1);
     // GroupNorm over the head (ggml_norm, fp64 sums) * ln_x (+ b) (* g)
     if (tid < S) {
         float p[16];
@@ -371,11 +395,11 @@ __global__ __launch_bounds__(256) void k_att6_dec(Att6Dec a) {
 #pragma unroll
                 for (int q = 0; q < o; q++) p[q] = p[q] + p[q + o];
         const float x = p[0];
-        const double s = group_sum((double)x, S);
-        const float mean = (float)(s / (double)S);
+        const double s = group_tree_sum_d((double)x, S);
+        const float mean = (float)div_count(s, S);
         const float d = x - mean;
-        const double s2 = group_sum((double)(d * d), S);
-        const float var = (float)(s2 / (double)S);
+        const double s2 = group_tree_sum_d((double)(d * d), S);
+        const float var = (float)div_count(s2, S);
         const float scale = 1.0f / sqrtf(var + a.eps);
         float o = d * scale;
         o = o * lnw_c;
@@ -384,6 +408,7 @@ __global__ __launch_bounds__(256) void k_att6_dec(Att6Dec a) {
         if (a.yq.fmt >= 0) emit32(a.yq, 0, c0 + tid, o);  // S >= 32: whole half-wave blocks
         else a.y[c0 + tid] = o;
     }
+    STAMP_END(3);
 }
 
 bool launch_att6_dec(hipStream_t st, const Att6Dec & a) {
@@ -548,11 +573,11 @@ __global__ __launch_bounds__(256) void k_att7_dec(Att7Dec a) {
     if (tid < S) {
         const int c = c0 + tid;
         const float x = sy[tid];
-        const double s = group_sum((double)x, S);
-        const float mean = (float)(s / (double)S);
+        const double s = group_tree_sum_d((double)x, S);
+        const float mean = (float)div_count(s, S);
         const float d = x - mean;
-        const double s2 = group_sum((double)(d * d), S);
-        const float var = (float)(s2 / (double)S);
+        const double s2 = group_tree_sum_d((double)(d * d), S);
+        const float var = (float)div_count(s2, S);
         const float scale = 1.0f / sqrtf(var + 64e-5f);
         float o = d * scale;
         o = o * lnw_c;

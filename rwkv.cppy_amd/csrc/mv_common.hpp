@@ -335,9 +335,12 @@ __device__ __forceinline__ float epi_apply(int epi, float acc, const EpiIn & p) 
 // vmcnt is in order per wave, so a prologue wave never waits behind the weight stream and a
 // dot wave's weights are in flight from its first instruction.
 template <int WF, int R, int U, int SRCK, int FORM, bool EMIT, int NW, int LNP>
-__device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, int b0, int stride, char * smem, float * red) {
+__device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, int b0, int stride, char * smem, float * red,
+                                        unsigned long long * stamp_mid = nullptr,
+                                        unsigned long long * stamp_x = nullptr) {
     constexpr bool PRO = SRCK != MVK_ACT;
-    constexpr int LNR = LNP > 0 ? LNP : 1;
+    // LayerNorm chunks per prologue wave held in registers: LNP 32 -> K <= 2048, 64 -> K <= 4096
+    constexpr int LCW = LNP > 32 ? 2 : 1;
     constexpr int RW = NW * R;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const DMat & W = Ent.W;
@@ -349,22 +352,73 @@ __device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, int b0, in
     if constexpr (PRO) {
         a = lds_act(smem, act_fmt_for(WF), K);
         if (wave >= NW) {
-            // ---- prologue wave
-            const int pw = wave - NW;
-            float lv[LNR];
-            ChunkIn ci;
-            const int k0 = pw * 512 + lane * 8;
-            if constexpr (SRCK == MVK_LN) ln_load_regs<LNR>(Ent.x, K, lv);
-            chunk_load<SRCK, FORM>(Ent, min(k0, K - 8), ci);
-            float mean = 0.0f, scale = 0.0f;
-            if constexpr (SRCK == MVK_LN) ln_stats_regs<LNR>(lv, K, 1e-5f, mean, scale);
+            // ---- prologue wave: chunks pw, pw + NW (512 elements each, 8 per lane)
+            const int pw = wave - NW, nch = (K + LN_CHUNK - 1) / LN_CHUNK;
             const bool write_carry = Ent.carry_out && wgi == (int)blockIdx.x - b0;
-            chunk_store<WF, SRCK, FORM>(Ent, a, ci, mean, scale, write_carry, k0, k0 < K, lane);
-            for (int c = pw + NW; c * 512 < K; c += NW) {
-                const int kk = c * 512 + lane * 8;
-                chunk_load<SRCK, FORM>(Ent, min(kk, K - 8), ci);
-                chunk_store<WF, SRCK, FORM>(Ent, a, ci, mean, scale, write_carry, kk, kk < K, lane);
+            ChunkIn ci[LCW];
+            int kc[LCW];
+#pragma unroll
+            for (int q = 0; q < LCW; q++) {
+                kc[q] = (pw + q * NW) * LN_CHUNK + lane * 8;
+                chunk_load<SRCK, FORM>(Ent, min(kc[q], K - 8), ci[q]);
             }
+
+            // issue order: the input loads above go out before the dot waves start the weight
+            // stream (they wait at this barrier), so they are not queued behind megabytes of
+            // weights in the memory system; no wait on the loads themselves here
+            asm volatile("s_barrier" ::: "memory");
+#ifdef RWKV_STAMP
+            if (pw == 0 && stamp_x) {
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                if (lane == 0) stamp_x[0] = __builtin_amdgcn_s_memrealtime();
+            }
+#endif
+            float mean = 0.0f, scale = 0.0f;
+            if constexpr (SRCK == MVK_LN) {
+                // LayerNorm statistics in the chunk association (device_common.hpp): each wave
+                // sums its chunks, the chunk sums meet in LDS (two barriers the dot waves join)
+                __shared__ double ln_part[2][8];
+#pragma unroll
+                for (int q = 0; q < LCW; q++)
+                    if (pw + q * NW < nch) {
+                        const double cs = ln_chunk_sum(ci[q].x, kc[q] < K);
+                        if (lane == 0) ln_part[0][pw + q * NW] = cs;
+                    }
+                asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+                double sm = 0.0;
+                for (int c = 0; c < nch; c++) sm += ln_part[0][c];
+                mean = (float)div_count(sm, K);
+#pragma unroll
+                for (int q = 0; q < LCW; q++)
+                    if (pw + q * NW < nch) {
+                        const double cs = ln_chunk_sq(ci[q].x, kc[q] < K, mean);
+                        if (lane == 0) ln_part[1][pw + q * NW] = cs;
+                    }
+                asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+                double sq = 0.0;
+                for (int c = 0; c < nch; c++) sq += ln_part[1][c];
+                scale = ln_scale(sq, K, 1e-5f);
+            }
+#ifdef RWKV_STAMP
+            if (pw == 0 && stamp_x && lane == 0) stamp_x[1] = __builtin_amdgcn_s_memrealtime() + (scale == 1.2345f);
+#endif
+#pragma unroll
+            for (int q = 0; q < LCW; q++)
+                if (pw + q * NW < nch) chunk_store<WF, SRCK, FORM>(Ent, a, ci[q], mean, scale, write_carry, kc[q], kc[q] < K, lane);
+            if constexpr (SRCK == MVK_F32) {
+                // plain fp32 input: any K, further chunks streamed
+                for (int c = pw + LCW * NW; c < nch; c += NW) {
+                    const int kk = c * LN_CHUNK + lane * 8;
+                    chunk_load<SRCK, FORM>(Ent, min(kk, K - 8), ci[0]);
+                    chunk_store<WF, SRCK, FORM>(Ent, a, ci[0], mean, scale, write_carry, kk, kk < K, lane);
+                }
+            }
+#ifdef RWKV_STAMP
+            if (pw == 0 && stamp_x) {
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                if (lane == 0) stamp_x[2] = __builtin_amdgcn_s_memrealtime();
+            }
+#endif
             __syncthreads();
             // take part in the dot waves' barriers, then leave (to the kernel's common end)
             for (;;) {
@@ -377,6 +431,12 @@ __device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, int b0, in
         }
     }
     // ---- dot wave: this wave's weight units (HBM) and the epilogue operands
+    if constexpr (PRO) {
+        // the weight pointers reach SGPRs before the issue-order barrier, so the stream starts
+        // right after it (a kernarg scalar load behind the barrier is a round trip in the path)
+        asm volatile("" ::"s"(W.qs), "s"(W.sc), "s"(W.qh));
+        asm volatile("s_barrier" ::: "memory");  // after the prologue's input loads
+    }
     int row0 = wgi * RW + wave * R;
     int rows[R];
 #pragma unroll
@@ -386,6 +446,12 @@ __device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, int b0, in
     for (int u = 0; u < U; u++)
 #pragma unroll
         for (int r = 0; r < R; r++) w[r][u] = load_unit<WF>(W, rows[r], u, lane);
+    if constexpr (SRCK == MVK_LN) {
+        // the prologue's two statistics barriers, right after the weight issue (no wait on
+        // this wave's loads; the epilogue operands are fetched after them)
+        asm volatile("s_barrier" ::: "memory");
+        asm volatile("s_barrier" ::: "memory");
+    }
     // epilogue operands: !EMIT lane r < R runs row row0 + r's epilogue; EMIT thread tid < RW row tid
     EpiIn ep;
     if constexpr (!EMIT) ep = epi_load(Ent, min(row0 + min(lane, R - 1), M - 1));
@@ -393,6 +459,12 @@ __device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, int b0, in
     if constexpr (PRO) __syncthreads();  // activation image ready
     else a = Ent.act;
     PROBE(1);
+#ifdef RWKV_STAMP
+    if (stamp_mid && wgi == (int)blockIdx.x - b0) {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        *stamp_mid = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
 
     for (;;) {
         // dots
@@ -483,8 +555,16 @@ __global__ __launch_bounds__(512) void k_mv(int b1, int b2, int b3, int b4, int 
     const int b0 = e == 0 ? 0 : e == 1 ? b1 : e == 2 ? b2 : e == 3 ? b3 : e == 4 ? b4 : e == 5 ? b5 : e == 6 ? b6 : b7;
     const MVEntry & Ent = g.e[e];
     const int wgi = bx - b0;
+    STAMP_BEGIN();
+#ifdef RWKV_STAMP
+    unsigned long long * smid = &stamp_t1_;
+    unsigned long long * sx = stamp_x_;
+#else
+    unsigned long long * smid = nullptr;
+    unsigned long long * sx = nullptr;
+#endif
     if constexpr (WFIX >= 0) {
-        mv_body<WFIX, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red);
+        mv_body<WFIX, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red, smid, sx);
     } else {
         switch (Ent.W.type) {
             case W_F32: mv_body<W_F32, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red); break;
@@ -497,6 +577,9 @@ __global__ __launch_bounds__(512) void k_mv(int b1, int b2, int b3, int b4, int 
             default: break;
         }
     }
+    (void)smid;
+    (void)sx;
+    STAMP_END(2);
 }
 
 // Activation-input matvec (SRC_ACT, no emission, one weight type): the lean form of mv_body's
@@ -531,6 +614,7 @@ __global__ __launch_bounds__(256) void k_mva(int b1, int b2, int b3, int b4, int
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int M = h.M, K = h.K;
+    STAMP_BEGIN();
     const int row0 = (bx - b0) * (4 * R) + wave * R;
     int rows[R];
 #pragma unroll
@@ -552,6 +636,7 @@ __global__ __launch_bounds__(256) void k_mva(int b1, int b2, int b3, int b4, int
     ep.bias = bias[erow * bstep];
     // keep the machine scheduler from interleaving later rows' loads with earlier rows' dots
     __builtin_amdgcn_sched_barrier(0);
+    STAMP_MID();
     float acc[R], acc2[R];
 #pragma unroll
     for (int r = 0; r < R; r++) acc[r] = acc2[r] = 0.0f;
@@ -574,6 +659,7 @@ __global__ __launch_bounds__(256) void k_mva(int b1, int b2, int b3, int b4, int
     // instead of being sunk into the store branch: a dependent round trip at the kernel's end)
     const float v = epi_apply(h.epi, lane_row_sum<R>(sr, lane), ep);
     if (lane < R && row0 + lane < M) h.y[row0 + lane] = v;
+    STAMP_END(1);
 }
 
 // One weight-type translation unit (mv_*.hip) instantiates every launch shape for WFIX.

@@ -40,8 +40,11 @@ __global__ __launch_bounds__(512) void k_v6_maa_dec(MaaDec a) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const ActBuf act = lds_act(smem, act_fmt_for(WF), K);
     float * s_xa = (float *)(smem + a.xa_off);
+    STAMP_BEGIN();
     if (wave < 4) {
         // ---- dot wave: rows n*D + wave*R + r of W1
+        asm volatile("" ::"s"(a.w1.qs), "s"(a.w1.sc), "s"(a.w1.qh));  // pointers before the barrier
+        asm volatile("s_barrier" ::: "memory");  // after the prologue waves' input loads
         const DMat & W = a.w1;
         const int units = mv_units(WF, K);
         const int row0 = n * D + wave * R, rlast = n * D + D - 1;
@@ -53,6 +56,9 @@ __global__ __launch_bounds__(512) void k_v6_maa_dec(MaaDec a) {
         for (int u = 0; u < U; u++)
 #pragma unroll
             for (int r = 0; r < R; r++) w[r][u] = load_unit<WF, false>(W, rows[r], u, lane);
+        // the prologue's two LayerNorm statistics barriers, right after the weight issue
+        asm volatile("s_barrier" ::: "memory");
+        asm volatile("s_barrier" ::: "memory");
         // this thread's mix channel: W2 column, carry, maa
         const int c = blockIdx.x * CPW + tid;
         const bool cval = tid < CPW && (int)(blockIdx.x * CPW + (tid & ~31)) < C;  // half-wave uniform
@@ -66,6 +72,7 @@ __global__ __launch_bounds__(512) void k_v6_maa_dec(MaaDec a) {
         }
         const float carry_c = a.carry[cc], mu_c = a.maa[n][cc];
         __syncthreads();  // (1) activation image ready
+        STAMP_MID();
         float acc[R], acc2[R];
 #pragma unroll
         for (int r = 0; r < R; r++) acc[r] = acc2[r] = 0.0f;
@@ -94,6 +101,7 @@ __global__ __launch_bounds__(512) void k_v6_maa_dec(MaaDec a) {
         const float t = rk_tanhf(lane_row_sum<R>(s, lane));  // EPI_TANH, lane r for row r
         if (lane < R && wave * R + lane < D) s_lora[wave * R + lane] = t;
         __syncthreads();  // (2) lora_n ready
+        if (wave == 0) STAMP_X(3);
         // k_v6_mix5_dec's arithmetic: m = sum_i (double)(w2[i] * lora[i]) in order
         const float xa = s_xa[cc];
         const float sx = carry_c - xa;
@@ -103,6 +111,7 @@ __global__ __launch_bounds__(512) void k_v6_maa_dec(MaaDec a) {
             if (i < D) accd += (double)(w2v[i] * s_lora[i]);
         const float m = (float)accd;
         if (cval) emit32(a.out[n], 0, c, (m + mu_c) * sx + xa);
+        STAMP_END_NS(4 + 16 * blockIdx.y);
         return;
     }
     // ---- prologue wave
@@ -115,24 +124,55 @@ __global__ __launch_bounds__(512) void k_v6_maa_dec(MaaDec a) {
     E.mu = a.maa_x;
     E.carry_out = a.carry_out;
     E.f = nullptr;
-    float lv[LNP];
-    ln_load_regs<LNP>(a.x, K, lv);
-    ChunkIn ci;
-    int k0 = pw * 512 + lane * 8;
-    chunk_load<MVK_LN, 1>(E, min(k0, K - 8), ci);
-    float mean = 0.0f, scale = 0.0f;
-    ln_stats_regs<LNP>(lv, K, 1e-5f, mean, scale);
-    const bool write_carry = blockIdx.x == 0 && n == 0;
-    for (;;) {
-        if (k0 < K) {
+    // chunks pw, pw + 4 of the LayerNorm input (512 elements each, 8 per lane)
+    constexpr int LCW = LNP > 32 ? 2 : 1;
+    const int nch = (K + LN_CHUNK - 1) / LN_CHUNK;
+    ChunkIn ci[LCW];
+    int kc[LCW];
 #pragma unroll
-            for (int j = 0; j < 8; j++) s_xa[k0 + j] = ln_apply(ci.x[j], mean, scale, ci.w[j], ci.b[j]);
-        }
-        chunk_store<WF, MVK_LN, 1>(E, act, ci, mean, scale, write_carry, k0, k0 < K, lane);
-        k0 += 4 * 512;
-        if (k0 - lane * 8 >= K) break;
-        chunk_load<MVK_LN, 1>(E, min(k0, K - 8), ci);
+    for (int q = 0; q < LCW; q++) {
+        kc[q] = (pw + 4 * q) * LN_CHUNK + lane * 8;
+        chunk_load<MVK_LN, 1>(E, min(kc[q], K - 8), ci[q]);
     }
+    asm volatile("s_barrier" ::: "memory");  // input loads issued ahead of the weight stream
+    if (pw == 0) STAMP_X(0);
+    // LayerNorm statistics, chunk association (device_common.hpp); the dot waves join the two
+    // exchange barriers
+    __shared__ double ln_part[2][8];
+#pragma unroll
+    for (int q = 0; q < LCW; q++)
+        if (pw + 4 * q < nch) {
+            const double cs = ln_chunk_sum(ci[q].x, kc[q] < K);
+            if (lane == 0) ln_part[0][pw + 4 * q] = cs;
+        }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    double sm = 0.0;
+    for (int c = 0; c < nch; c++) sm += ln_part[0][c];
+    const float mean = (float)div_count(sm, K);
+#pragma unroll
+    for (int q = 0; q < LCW; q++)
+        if (pw + 4 * q < nch) {
+            const double cs = ln_chunk_sq(ci[q].x, kc[q] < K, mean);
+            if (lane == 0) ln_part[1][pw + 4 * q] = cs;
+        }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    double sq = 0.0;
+    for (int c = 0; c < nch; c++) sq += ln_part[1][c];
+    const float scale = ln_scale(sq, K, 1e-5f);
+#ifdef RWKV_STAMP
+    if (pw == 0 && lane == 0) stamp_x_[1] = __builtin_amdgcn_s_memrealtime() + (scale == 1.2345f);
+#endif
+    const bool write_carry = blockIdx.x == 0 && n == 0;
+#pragma unroll
+    for (int q = 0; q < LCW; q++) {
+        if (pw + 4 * q >= nch) continue;
+        if (kc[q] < K) {
+#pragma unroll
+            for (int j = 0; j < 8; j++) s_xa[kc[q] + j] = ln_apply(ci[q].x[j], mean, scale, ci[q].w[j], ci[q].b[j]);
+        }
+        chunk_store<WF, MVK_LN, 1>(E, act, ci[q], mean, scale, write_carry, kc[q], kc[q] < K, lane);
+    }
+    if (pw == 0) STAMP_X(2);
     __syncthreads();  // (1)
     __syncthreads();  // (2)
 }

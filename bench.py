@@ -60,6 +60,8 @@ def main():
     ap.add_argument('--timing-steps', type=int, default=8)
     ap.add_argument('--cpu-seconds', type=float, default=12.0)
     ap.add_argument('--skip-cpu', action='store_true')
+    ap.add_argument('--batch', default='8,32,64', help='batched decode sizes (contexts per step; "" = none)')
+    ap.add_argument('--batch-steps', type=int, default=32)
     ap.add_argument('--model-dir', default=os.environ.get('RWKV_BENCH_DIR', '/tmp/rwkv_bench'))
     args = ap.parse_args()
 
@@ -145,6 +147,47 @@ def main():
     ms_per_step = elapsed * 1e3 / args.steps
     value = world * args.steps / elapsed
     log(f'decode: {ms_per_step * 1e3:.1f} us/token, {value:.1f} tok/s aggregate over {world} GPU(s)')
+
+    # ---------------- batched multi-context decode ----------------
+    # B independent contexts advance one token each per step (rwkv_mi355x_eval_batch_device: states
+    # and logits in HBM, two state buffers alternating); tokens/s = B * steps / time
+    batch = []
+    for B in [int(b) for b in args.batch.split(',') if b.strip()]:
+        try:
+            dev = torch.device('cuda', gpu)
+            sbuf = [torch.zeros((B, state_len), dtype=torch.float32, device=dev) for _ in range(2)]
+            lbuf = torch.zeros((B, n_vocab), dtype=torch.float32, device=dev)
+            btoks = rng.integers(0, n_vocab, size=(args.batch_steps + 4, B)).astype(np.uint32)
+
+            def bstep(i, fresh=False):
+                sin = None if fresh else sbuf[i & 1].data_ptr()
+                if not L.rwkv_mi355x_eval_batch_device(ctx.ptr, btoks[i].ctypes.data, B, sin,
+                                                       sbuf[(i & 1) ^ 1].data_ptr(), lbuf.data_ptr()):
+                    raise RuntimeError('eval_batch_device failed')
+
+            torch.cuda.synchronize()
+            bstep(0, fresh=True)
+            for i in range(1, 4):
+                bstep(i)
+            L.rwkv_mi355x_sync(ctx.ptr)
+            barrier()
+            tb = time.perf_counter()
+            for i in range(4, 4 + args.batch_steps):
+                bstep(i)
+            L.rwkv_mi355x_sync(ctx.ptr)
+            barrier()
+            eb = time.perf_counter() - tb
+            if world > 1:
+                eb = allmax(eb)
+            batch.append({'contexts': B, 'tokens_per_s': round(world * B * args.batch_steps / eb, 1),
+                          'ms_per_step': round(eb * 1e3 / args.batch_steps, 4),
+                          'tokens_per_s_per_context': round(args.batch_steps / eb, 1)})
+            log(f'batched decode B={B}: {eb * 1e3 / args.batch_steps:.3f} ms/step, '
+                f'{world * B * args.batch_steps / eb:.0f} tok/s aggregate')
+            del sbuf, lbuf
+        except Exception as e:
+            log(f'batched decode B={B} failed: {e!r}')
+            batch.append({'contexts': B, 'error': repr(e)})
 
     # ---------------- sequence eval ----------------
     seq = rng.integers(0, n_vocab, size=args.seq_len)
@@ -377,6 +420,9 @@ def main():
                          'ms_per_sequence': round(seq_s * 1e3, 3), 'parallelism': f'replicas x{world}',
                          'pipeline': pipe},
             'abi_decode_tokens_per_s': round(abi_tps * world, 2),
+            'batched_decode': {'what': 'B independent contexts, one token each per step, weights read once per '
+                                       'step (rwkv_mi355x_eval_batch_device; bit-exact to per-context rwkv_eval)',
+                               'parallelism': f'replicas x{world}', 'runs': batch},
             'roofline': roofline,
             'seq_roofline': seq_roofline,
             'cpu_baseline': cpu,

@@ -64,6 +64,22 @@ RWKV_API float * rwkv_mi355x_logits_device(struct rwkv_context * ctx);
 RWKV_API struct rwkv_context * rwkv_mi355x_init_from_file_layers(const char * path, uint32_t n_threads,
                                                                  uint32_t layer_begin, uint32_t layer_end);
 
+/* Batched decode (multi-context serving): n_contexts independent sequences of this
+ * model advance ONE token each in one pass -- the rwkv_eval of each context, with every weight byte
+ * read once per step for all of them (the reference runs clones side by side instead:
+ * rwkv_clone_context, rwkv.h:93-99, rwkv.cpp:123-139).  Results are bit-identical to
+ * rwkv_eval(ctx, tokens[i], state_in + i * state_len, ...) for every i.
+ * tokens: host [n_contexts]; state_in / state_out: [n_contexts][state_len] (state_in NULL = fresh
+ * states, state_out NULL = not returned); logits_out: [n_contexts][logits_len] or NULL.
+ * n_contexts <= 256.  Host buffers; synchronous. */
+RWKV_API bool rwkv_mi355x_eval_batch(struct rwkv_context * ctx, const uint32_t * tokens, size_t n_contexts,
+                                     const float * state_in, float * state_out, float * logits_out);
+/* The same with state_in / state_out / logits_out in device memory of the context's GPU (no PCIe
+ * traffic; state_in != state_out; NULL state_out / logits_out: kept in library buffers).
+ * Enqueued on the context's stream (rwkv_mi355x_stream); returns without waiting. */
+RWKV_API bool rwkv_mi355x_eval_batch_device(struct rwkv_context * ctx, const uint32_t * tokens, size_t n_contexts,
+                                            const float * state_in, float * state_out, float * logits_out);
+
 /* The context's HIP stream (hipStream_t), so callers can time kernels with events on it. */
 RWKV_API void * rwkv_mi355x_stream(struct rwkv_context * ctx);
 

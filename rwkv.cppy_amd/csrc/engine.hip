@@ -351,6 +351,10 @@ Engine::~Engine() {
     if (stream_) (void)hipStreamSynchronize(stream_);
     stamp_dump();
     drop_graphs();
+    drop_batch_graphs();
+    for (float * p : bstate_)
+        if (p) (void)hipFree(p);
+    if (blogits_) (void)hipFree(blogits_);
     if (gy_) (void)hipFree(gy_);
     if (part_) (void)hipFree(part_);
     for (void * p : ws_allocs_) (void)hipFree(p);
@@ -403,6 +407,7 @@ bool Engine::ensure_workspace(int T) {
     if (T <= tcap_) return true;
     HIP_OK(hipStreamSynchronize(stream_));
     drop_graphs();
+    drop_batch_graphs();
     // keep state and logits, drop the rest; until every allocation below has succeeded the
     // workspace counts as absent (tcap_ = 0, pointers null), so a failed grow can never leave a
     // capacity that points at freed or missing buffers
@@ -569,6 +574,14 @@ void Engine::set_timing(bool on) {
 // Sequence matmuls on quantized weights go to the int8-MFMA GEMM; entries that only emit get
 // a scratch y, and emission is a separate quantization pass (same bits as k_mm's epilogue).
 bool Engine::mm_dispatch(MMGroup & g, int wtype) {
+    // batched decode (bs_ > 0): the decode matvec over the contexts (k_mvb; k_mm for shapes it
+    // does not cover -- the same bits)
+    if (bs_) {
+        bool launched = false;
+        if (!launch_mvb_group(stream_, g, wtype, &launched)) return false;
+        if (launched) return true;
+        return launch_mm_group(stream_, g, wtype);
+    }
     if (g.T < 2 || !wtype_quantized(wtype) || use_mm_) return launch_mm_group(stream_, g, wtype);
     size_t need = 0;
     for (int i = 0; i < g.n; i++)
@@ -638,8 +651,9 @@ bool Engine::mm_launch(MMGroup & g, int wtype) {
         flops += 2.0 * e.W.M * e.W.K * g.T;
     }
     // kernel class = the template instantiation rocprofv3 reports: k_mm<WF, RPW, NT>
-    const bool mfma = g.T >= 2 && wtype_quantized(wtype) && !use_mm_;
-    const std::string name = mfma ? "k_qgemm<" + std::to_string(wtype) + ">"
+    const bool mfma = g.T >= 2 && wtype_quantized(wtype) && !use_mm_ && !bs_;
+    const std::string name = bs_ ? "k_mvb<" + std::to_string(wtype) + ">"
+                           : mfma ? "k_qgemm<" + std::to_string(wtype) + ">"
                                   : "k_mm<" + std::to_string(wtype) + ", " + (emit ? "8" : "2") + ", " + (g.T == 1 ? "1" : "4") + ">";
     const int si = add_stat(name);
     hipEvent_t a, b;
@@ -698,6 +712,7 @@ bool Engine::ffn(int l, int T, const float * si, float * so) {
     a.x = x_;
     a.carry_in = si;        // ffn_xx at layer offset 0
     a.carry_out = so;
+    a.bs = bs_;
     a.lnw = L.ln2_w;
     a.lnb = L.ln2_b;
     MMBatch b;
@@ -730,6 +745,18 @@ bool Engine::ffn(int l, int T, const float * si, float * so) {
     return b.run(*this, T);
 }
 
+// Batched decode (bs_ > 0): the attention core of every context is the decode kernel itself (one
+// workgroup per head and context, k_att6_dec / k_att7_dec); its output goes to Wo's input `o`
+// (emitted by the kernel when heads are whole quantization blocks, else fp32 y_ converted).
+template <class Att>
+static void batch_att(Att & a, int T, size_t bs, float * y, const ActBuf & o, int S) {
+    a.nb = T;
+    a.bs = bs;
+    a.y = y;
+    a.yq.fmt = -1;
+    if (S >= 32) a.yq = o;
+}
+
 bool Engine::layer_v4(int l, int T, const float * si, float * so) {
     const DLayer & L = m_->layers[l];
     const int C = (int)m_->n_embed;
@@ -740,6 +767,7 @@ bool Engine::layer_v4(int l, int T, const float * si, float * so) {
     a.x = x_;
     a.carry_in = si + C;
     a.carry_out = so + C;
+    a.bs = bs_;
     a.lnw = L.ln1_w;
     a.lnb = L.ln1_b;
     a.form = 0;
@@ -757,7 +785,7 @@ bool Engine::layer_v4(int l, int T, const float * si, float * so) {
     b.add(L.att_v, A(1, L.att_v), v_, C, EPI_STORE);
     if (!b.run(*this, T)) return false;
     ActBuf o = A(3, L.att_o);
-    if (!launch_wkv4(stream_, T, C, r_, k_, v_, L.att_first, L.att_decay, si, so, o)) return false;
+    if (!launch_wkv4(stream_, T, C, r_, k_, v_, L.att_first, L.att_decay, si, so, o, (int)bs_)) return false;
     b.add(L.att_o, o, x_, C, EPI_ADD);
     if (!b.run(*this, T)) return false;
     return ffn(l, T, si, so);
@@ -774,6 +802,7 @@ bool Engine::layer_v5(int l, int T, const float * si, float * so) {
     a.x = x_;
     a.carry_in = si + C;
     a.carry_out = so + C;
+    a.bs = bs_;
     a.lnw = L.ln1_w;
     a.lnb = L.ln1_b;
     a.form = 0;
@@ -795,7 +824,31 @@ bool Engine::layer_v5(int l, int T, const float * si, float * so) {
     b.add(L.att_v, A(1, L.att_v), v_, C, EPI_STORE);
     if (v52) b.add(L.att_g, A(3, L.att_g), g_, C, EPI_SILU);
     if (!b.run(*this, T)) return false;
-    if (!launch_wkv6(stream_, T, H, S, k_, v_, r_, L.att_u, L.att_w, 0, si + 2 * C, so + 2 * C, y_)) return false;
+    if (bs_) {
+        Att6Dec d;
+        memset(&d, 0, sizeof(d));
+        d.H = H;
+        d.S = S;
+        d.r = r_;
+        d.k = k_;
+        d.v = v_;
+        d.g = v52 ? g_ : nullptr;
+        d.u = L.att_u;
+        d.w = L.att_w;
+        d.sin = si + 2 * C;
+        d.sout = so + 2 * C;
+        d.lnx_w = L.att_lnx_w;
+        d.lnx_b = L.att_lnx_b;
+        d.eps = 1e-5f;
+        ActBuf o = A(4, L.att_o);
+        batch_att(d, T, bs_, y_, o, S);
+        if (!launch_att6_dec(stream_, d)) return false;
+        if (S < 32 && !launch_act_from_f32(stream_, y_, T, C, o)) return false;
+        b.add(L.att_o, o, x_, C, EPI_ADD);
+        if (!b.run(*this, T)) return false;
+        return ffn(l, T, si, so);
+    }
+    if (!launch_wkv6(stream_, T, H, S, k_, v_, r_, L.att_u, L.att_w, 0, si + 2 * C, so + 2 * C, y_, (int)bs_)) return false;
     ActBuf o = A(4, L.att_o);
     if (!launch_groupnorm(stream_, T, H, S, 1e-5f, y_, L.att_lnx_w, L.att_lnx_b, v52 ? 1 : 0, g_, nullptr, nullptr, o))
         return false;
@@ -814,6 +867,7 @@ bool Engine::layer_v6(int l, int T, const float * si, float * so) {
     a.x = x_;
     a.carry_in = si + C;
     a.carry_out = so + C;
+    a.bs = bs_;
     a.lnw = L.ln1_w;
     a.lnb = L.ln1_b;
     a.form = 1;
@@ -834,6 +888,40 @@ bool Engine::layer_v6(int l, int T, const float * si, float * so) {
     // (consumed by mix5 above)
     const int DD = L.decay_w2.K;  // decay LoRA width (64 for the released checkpoints)
     const bool dseq = v6_decay_seq_supported(L.decay_w2.type, DD) && L.decay_w1.M == DD;
+    if (bs_) {
+        // decode's split: decay W1 (tanh) with r,k,v,g; the LoRA tail, wkv and GroupNorm per head
+        b.add(L.att_r, outs[3], r_, C, EPI_STORE);
+        b.add(L.att_k, outs[1], k_, C, EPI_STORE);
+        b.add(L.att_v, outs[2], v_, C, EPI_STORE);
+        b.add(L.att_g, outs[4], g_, C, EPI_SILU);
+        b.add(L.decay_w1, outs[0], lora_, L.decay_w1.M, EPI_TANH);
+        if (!b.run(*this, T)) return false;
+        Att6Dec d;
+        memset(&d, 0, sizeof(d));
+        d.H = H;
+        d.S = S;
+        d.r = r_;
+        d.k = k_;
+        d.v = v_;
+        d.g = g_;
+        d.u = L.att_u;
+        d.wd2 = L.decay_w2;
+        d.dl = lora_;
+        d.ldd = L.decay_w1.M;
+        d.decay = L.decay6;
+        d.sin = si + 2 * C;
+        d.sout = so + 2 * C;
+        d.lnx_w = L.att_lnx_w;
+        d.lnx_b = L.att_lnx_b;
+        d.eps = 64e-5f;
+        ActBuf o = A(7, L.att_o);
+        batch_att(d, T, bs_, y_, o, S);
+        if (!launch_att6_dec(stream_, d)) return false;
+        if (S < 32 && !launch_act_from_f32(stream_, y_, T, C, o)) return false;
+        b.add(L.att_o, o, x_, C, EPI_ADD);
+        if (!b.run(*this, T)) return false;
+        return ffn(l, T, si, so);
+    }
     b.add(L.att_r, outs[3], r_, C, EPI_STORE);
     b.add(L.att_k, outs[1], k_, C, EPI_STORE);
     b.add(L.att_v, outs[2], v_, C, EPI_STORE);
@@ -847,7 +935,7 @@ bool Engine::layer_v6(int l, int T, const float * si, float * so) {
         b.add(L.decay_w2, dl, w_, C, EPI_DECAY6, nullptr, L.decay6);
         if (!b.run(*this, T)) return false;
     }
-    if (!launch_wkv6(stream_, T, H, S, k_, v_, r_, L.att_u, w_, 1, si + 2 * C, so + 2 * C, y_)) return false;
+    if (!launch_wkv6(stream_, T, H, S, k_, v_, r_, L.att_u, w_, 1, si + 2 * C, so + 2 * C, y_, (int)bs_)) return false;
     ActBuf o = A(7, L.att_o);
     if (!launch_groupnorm(stream_, T, H, S, 64e-5f, y_, L.att_lnx_w, L.att_lnx_b, 1, g_, nullptr, nullptr, o)) return false;
     b.add(L.att_o, o, x_, C, EPI_ADD);
@@ -865,6 +953,7 @@ bool Engine::layer_v7(int l, int T, const float * si, float * so) {
     a.x = x_;
     a.carry_in = si + C;
     a.carry_out = so + C;
+    a.bs = bs_;
     a.lnw = L.ln1_w;
     a.lnb = L.ln1_b;
     a.form = 1;
@@ -916,8 +1005,34 @@ bool Engine::layer_v7(int l, int T, const float * si, float * so) {
     b.add(L.g2, lg, g_, C, EPI_STORE);
     if (vlora) b.add(L.v2, lvv, v_, C, EPI_VMIX7, vfirst_, L.v0);
     if (!b.run(*this, T)) return false;
+    if (bs_) {
+        Att7Dec d;
+        memset(&d, 0, sizeof(d));
+        d.H = H;
+        d.S = S;
+        d.r = r_;
+        d.w = w_;
+        d.k = k_;
+        d.v = v_;
+        d.a = a_;
+        d.g = g_;
+        d.k_k = L.k_k;
+        d.k_a = L.k_a;
+        d.r_k = L.r_k;
+        d.sin = si + 2 * C;
+        d.sout = so + 2 * C;
+        d.lnx_w = L.att_lnx_w;
+        d.lnx_b = L.att_lnx_b;
+        ActBuf o = A(0, L.att_o);
+        batch_att(d, T, bs_, y_, o, S);
+        if (!launch_att7_dec(stream_, d)) return false;
+        if (S < 32 && !launch_act_from_f32(stream_, y_, T, C, o)) return false;
+        b.add(L.att_o, o, x_, C, EPI_ADD);
+        if (!b.run(*this, T)) return false;
+        return ffn(l, T, si, so);
+    }
     if (!launch_v7_prep(stream_, T, H, S, k_, a_, r_, L.k_k, L.k_a, L.r_k, nb_, bb_, bonus_)) return false;
-    if (!launch_wkv7(stream_, T, H, S, r_, w_, k_, v_, nb_, bb_, si + 2 * C, so + 2 * C, y_)) return false;
+    if (!launch_wkv7(stream_, T, H, S, r_, w_, k_, v_, nb_, bb_, si + 2 * C, so + 2 * C, y_, (int)bs_)) return false;
     ActBuf o = A(0, L.att_o);
     if (!launch_groupnorm(stream_, T, H, S, 64e-5f, y_, L.att_lnx_w, L.att_lnx_b, 2, g_, v_, bonus_, o)) return false;
     b.add(L.att_o, o, x_, C, EPI_ADD);
@@ -937,7 +1052,7 @@ bool Engine::forward_range(int T, const float * sin, float * sout, uint32_t l0, 
     if (l0 == 0 && !launch_embed_ln(stream_, dtokens_, T, m_->emb, m_->ln0_w, m_->ln0_b, x_)) return false;
     const size_t per_layer = m_->major >= 5 ? C * (2 + (size_t)m_->S) : 5 * C;
     // layer matmuls run over all T tokens: Q8 activations go straight into GEMM tiles
-    tile_acts_ = T >= 2 && !use_mm_;
+    tile_acts_ = T >= 2 && !use_mm_ && !bs_;
     for (uint32_t l = l0; l < l1; l++) {
         const float * si = sin + l * per_layer;
         float * so = sout + l * per_layer;
@@ -954,14 +1069,16 @@ bool Engine::forward_range(int T, const float * sin, float * sout, uint32_t l0, 
             return false;
         }
     }
-    tile_acts_ = false;  // the head runs on the last token only
+    tile_acts_ = false;  // the head runs on the last token only (batched decode: on every context)
     if (logits && l1 == m_->n_layer) {
         // rwkv_graph.inc:704-708 / :850-854
+        const int rows = bs_ ? T : 1;
         ActBuf hin = A(0, m_->head);
-        if (!launch_ln_emit(stream_, (int)C, x_ + (size_t)(T - 1) * C, m_->lnout_w, m_->lnout_b, hin)) return false;
+        if (!launch_ln_emit(stream_, (int)C, x_ + (size_t)(T - rows) * C, m_->lnout_w, m_->lnout_b, hin, rows))
+            return false;
         MMBatch b;
-        b.add(m_->head, hin, logits_, (int)m_->n_vocab, EPI_STORE);
-        if (!b.run(*this, 1)) return false;
+        b.add(m_->head, hin, head_out_ ? head_out_ : logits_, (int)m_->n_vocab, EPI_STORE);
+        if (!b.run(*this, rows)) return false;
     }
     return true;
 }
@@ -1442,6 +1559,121 @@ long long Engine::debug_copy(const char * name, void * out, size_t bytes) {
     if (hipStreamSynchronize(stream_) != hipSuccess || hipMemcpy(out, src, bytes, hipMemcpyDeviceToHost) != hipSuccess)
         return -1;
     return (long long)bytes;
+}
+
+// ---------------------------------------------------------------- batched decode
+// B independent contexts of this model advance one token each in one pass: the layer matmuls
+// run the decode matvec kernel (k_mm) over the B activation rows, so every weight byte is read
+// once per step for all B contexts, and each context's arithmetic is exactly its single-token
+// decode (same lane/block association, same kernels' per-token math); token shift and the wkv
+// recurrences take context t's state at t * state_len (LnMixArgs::bs, launch_wkv* bs).
+// states: [B][state_len] contiguous.  dev: pointers are device memory (else host).
+bool Engine::eval_batch(const uint32_t * tokens, size_t B, const float * state_in, float * state_out,
+                        float * logits_out, bool dev) {
+    HIP_OK(hipSetDevice(m_->device));
+    if (B == 0) return true;
+    if (B > (size_t)kBatchMax) {
+        fprintf(stderr, "rwkv: batched decode takes at most %d contexts (got %zu)\n", kBatchMax, B);
+        return false;
+    }
+    if (!ensure_workspace((int)B)) return false;
+    const size_t n = m_->state_len, V = m_->n_vocab;
+    if (B > bcap_) {
+        HIP_OK(hipStreamSynchronize(stream_));
+        drop_batch_graphs();
+        for (float *& p : bstate_) {
+            if (p) (void)hipFree(p);
+            p = nullptr;
+        }
+        if (blogits_) (void)hipFree(blogits_);
+        blogits_ = nullptr;
+        bcap_ = 0;
+        size_t cap = 1;
+        while (cap < B) cap *= 2;
+        bool ok = true;
+        for (float *& p : bstate_) ok = ok && hipMalloc(&p, cap * n * 4 + 64) == hipSuccess;
+        ok = ok && hipMalloc(&blogits_, cap * V * 4 + 64) == hipSuccess;
+        if (!ok) {
+            (void)hipGetLastError();
+            for (float *& p : bstate_) {
+                if (p) (void)hipFree(p);
+                p = nullptr;
+            }
+            if (blogits_) (void)hipFree(blogits_);
+            blogits_ = nullptr;
+            fprintf(stderr, "rwkv: batched decode state allocation for %zu contexts failed\n", B);
+            return false;
+        }
+        bcap_ = cap;
+    }
+    // tokens: pinned copy in stream order (the previous call's copy may still read it)
+    HIP_OK(hipEventSynchronize(tok_event_));
+    memcpy(htokens_, tokens, B * 4);
+    HIP_OK(hipMemcpyAsync(dtokens_, htokens_, B * 4, hipMemcpyHostToDevice, stream_));
+    HIP_OK(hipEventRecord(tok_event_, stream_));
+    // input states: device pointer as given, else staged into bstate_[0] (NULL = fresh states)
+    const float * sin = state_in;
+    if (!state_in) {
+        hipLaunchKernelGGL(k_init_state, dim3((unsigned)((B * n + 255) / 256)), dim3(256), 0, stream_, bstate_[0],
+                           B * n, (int)m_->n_embed, m_->major == 4 ? 1 : 0);
+        HIP_OK(hipGetLastError());
+        sin = bstate_[0];
+    } else if (!dev) {
+        HIP_OK(hipMemcpyAsync(bstate_[0], state_in, B * n * 4, hipMemcpyHostToDevice, stream_));
+        sin = bstate_[0];
+    }
+    float * sout = (dev && state_out) ? state_out : bstate_[1];
+    float * lout = (dev && logits_out) ? logits_out : blogits_;
+    const bool lg = logits_out != nullptr;
+    bool ok;
+    if (use_graphs_ && !timing_) {
+        // one graph per (B, state pointers, logits pointer): a decode loop alternating two state
+        // buffers replays two graphs
+        hipGraphExec_t ge = nullptr;
+        for (const BatchGraph & g : bgraphs_)
+            if (g.B == B && g.sin == sin && g.sout == sout && g.lout == (lg ? lout : nullptr)) ge = g.ge;
+        if (!ge) {
+            if (bgraphs_.size() >= 8) drop_batch_graphs();
+            hipGraph_t g = nullptr;
+            HIP_OK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
+            bs_ = n;
+            head_out_ = lout;
+            ok = forward_range((int)B, sin, sout, 0, m_->n_layer, lg);
+            bs_ = 0;
+            head_out_ = nullptr;
+            HIP_OK(hipStreamEndCapture(stream_, &g));
+            if (!ok) {
+                (void)hipGraphDestroy(g);
+                return false;
+            }
+            HIP_OK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+            (void)hipGraphDestroy(g);
+            bgraphs_.push_back(BatchGraph{B, sin, sout, lg ? lout : nullptr, ge});
+        }
+        HIP_OK(hipGraphLaunch(ge, stream_));
+        ok = true;
+    } else {
+        bs_ = n;
+        head_out_ = lout;
+        ok = forward_range((int)B, sin, sout, 0, m_->n_layer, lg);
+        bs_ = 0;
+        head_out_ = nullptr;
+    }
+    if (!ok) {
+        (void)hipStreamSynchronize(stream_);
+        return false;
+    }
+    if (!dev) {
+        if (logits_out) HIP_OK(hipMemcpyAsync(logits_out, lout, B * V * 4, hipMemcpyDeviceToHost, stream_));
+        if (state_out) HIP_OK(hipMemcpyAsync(state_out, sout, B * n * 4, hipMemcpyDeviceToHost, stream_));
+        HIP_OK(hipStreamSynchronize(stream_));
+    }
+    return true;
+}
+
+void Engine::drop_batch_graphs() {
+    for (BatchGraph & g : bgraphs_) (void)hipGraphExecDestroy(g.ge);
+    bgraphs_.clear();
 }
 
 bool Engine::eval_device(const uint32_t * tokens, size_t T, bool want_logits, float * logits_out, bool sync_after) {

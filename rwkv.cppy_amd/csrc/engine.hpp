@@ -88,6 +88,10 @@ class Engine {
     bool eval_device(const uint32_t * tokens, size_t T, bool want_logits, float * logits_out, bool sync);
     bool eval_layers(const uint32_t * tokens, size_t T, uint32_t l0, uint32_t l1, float * x_io, float * vfirst_io,
                      bool want_logits, float * logits_out, bool sync = true);
+    // batched decode: B contexts, one token each; states [B][state_len] (host or device, see dev)
+    bool eval_batch(const uint32_t * tokens, size_t B, const float * state_in, float * state_out, float * logits_out,
+                    bool dev);
+    static constexpr int kBatchMax = 256;
     float * device_logits() const { return logits_; }
     bool state_upload(const float * state);
     bool state_download(float * state);
@@ -159,6 +163,22 @@ class Engine {
     size_t part_cap_ = 0;
     bool use_mm_ = false;
     bool tile_acts_ = false;  // Aview: Q8 activations in sequence-GEMM tiles (forward, T >= 2)
+    // batched decode (eval_batch): state floats per context while a batched forward is built
+    // (0 otherwise), the head's output rows, and the engine-owned staging buffers / graphs
+    size_t bs_ = 0;
+    float * head_out_ = nullptr;
+    float * bstate_[2] = {nullptr, nullptr};
+    float * blogits_ = nullptr;
+    size_t bcap_ = 0;
+    struct BatchGraph {
+        size_t B;
+        const float * sin;
+        float * sout;
+        float * lout;
+        hipGraphExec_t ge;
+    };
+    std::vector<BatchGraph> bgraphs_;
+    void drop_batch_graphs();
     void drop_graphs();
     std::vector<Pending> pending_;
     std::vector<hipEvent_t> event_pool_;

@@ -188,7 +188,8 @@ static bool launch_mm_wf(hipStream_t st, MMGroup & g) {
         else hipLaunchKernelGGL((k_mm<WF, 2, 1>), grid, block, 0, st, g);
     } else {
         // token spans so that the grid has ~4096 workgroups (at most one span per 4 tokens)
-        const int gy = std::max(1, std::min((T + 3) / 4, 4096 / blocks));
+        // (batched decode, T <= 16 over >= 256 row blocks: one span, every weight read once)
+        const int gy = (T <= 16 && blocks >= 256) ? 1 : std::max(1, std::min((T + 3) / 4, 4096 / blocks));
         const dim3 grid2(blocks, gy);
         if (emit) hipLaunchKernelGGL((k_mm<WF, 8, 4>), grid2, block, 0, st, g);
         else hipLaunchKernelGGL((k_mm<WF, 2, 4>), grid2, block, 0, st, g);
@@ -305,12 +306,16 @@ __global__ __launch_bounds__(1024) void k_ln_mix(LnMixArgs a) {
     const float * xt = a.x + (size_t)t * C;
     const float mean = s_mean[tg + 1], scale = s_scale[tg + 1];
     const float pmean = t > 0 ? s_mean[tg] : 0.0f, pscale = t > 0 ? s_scale[tg] : 0.0f;
-    for (int c0 = 0; c0 < C; c0 += 256) {
+    // channel blocks of 256 split over grid.y (short sequences / batched decode: more workgroups)
+    for (int c0 = (int)blockIdx.y * 256; c0 < C; c0 += (int)gridDim.y * 256) {
         const int c = c0 + tid;
         if (c0 + (tid & ~63) >= C) continue;  // whole wave out of range (C % 64 == 0)
         const float xa = ln_apply(xt[c], mean, scale, a.lnw[c], a.lnb[c]);
-        const float xp = (t > 0) ? ln_apply(xt[c - C], pmean, pscale, a.lnw[c], a.lnb[c]) : a.carry_in[c];
-        if (t == a.T - 1 && a.carry_out) a.carry_out[c] = xa;
+        // batch (a.bs > 0): every token is its own context, shifted against its own carry
+        const float xp = a.bs ? a.carry_in[(size_t)t * a.bs + c]
+                              : (t > 0) ? ln_apply(xt[c - C], pmean, pscale, a.lnw[c], a.lnb[c]) : a.carry_in[c];
+        if (a.bs && a.carry_out) a.carry_out[(size_t)t * a.bs + c] = xa;
+        else if (t == a.T - 1 && a.carry_out) a.carry_out[c] = xa;
         if (a.out_xa) a.out_xa[(size_t)t * C + c] = xa;
         if (a.out_sx) a.out_sx[(size_t)t * C + c] = xp - xa;
         for (int n = 0; n < a.n_out; n++) {
@@ -328,7 +333,8 @@ __global__ __launch_bounds__(1024) void k_ln_mix(LnMixArgs a) {
 }
 
 bool launch_ln_mix(hipStream_t st, const LnMixArgs & a) {
-    const dim3 grid((a.T + TOKS_PER_WG - 1) / TOKS_PER_WG), block(256 * TOKS_PER_WG);
+    const dim3 grid((a.T + TOKS_PER_WG - 1) / TOKS_PER_WG, a.T <= 64 ? (a.C + 255) / 256 : 1),
+        block(256 * TOKS_PER_WG);
     const int tq = tile_q(a.out, a.n_out, a.C);
     if (tq == 1) hipLaunchKernelGGL(k_ln_mix<1>, grid, block, 0, st, a);
     else if (tq == 2) hipLaunchKernelGGL(k_ln_mix<2>, grid, block, 0, st, a);
@@ -339,17 +345,20 @@ bool launch_ln_mix(hipStream_t st, const LnMixArgs & a) {
 
 __global__ __launch_bounds__(256) void k_ln_emit(int C, const float * x, const float * w, const float * b, ActBuf out) {
     __shared__ double sh[8];
+    const int t = blockIdx.x;  // row t of x -> row t of out
+    x += (size_t)t * C;
     float mean, scale;
     ln_stats(x, C, 1e-5f, mean, scale, sh);
     for (int c0 = 0; c0 < C; c0 += blockDim.x) {
         const int c = c0 + threadIdx.x;
         if (c0 + (int)(threadIdx.x & ~63) >= C) continue;
-        emit32(out, 0, c, ln_apply(x[c], mean, scale, w[c], b[c]));
+        emit32(out, t, c, ln_apply(x[c], mean, scale, w[c], b[c]));
     }
 }
 
-bool launch_ln_emit(hipStream_t st, int C, const float * x, const float * w, const float * b, const ActBuf & out) {
-    hipLaunchKernelGGL(k_ln_emit, dim3(1), dim3(256), 0, st, C, x, w, b, out);
+bool launch_ln_emit(hipStream_t st, int C, const float * x, const float * w, const float * b, const ActBuf & out,
+                    int rows) {
+    hipLaunchKernelGGL(k_ln_emit, dim3(rows), dim3(256), 0, st, C, x, w, b, out);
     HIP_OK(hipGetLastError());
     return true;
 }
@@ -369,12 +378,12 @@ struct Mix5Args {
 // mixes in registers (read once per token tile instead of once per token) and the tile's lora rows
 // sit in LDS; per token the five D-long fp64 sums (k_v6_mix5_dec's order: sequential over i) run
 // side by side.
-constexpr int MIX_TT = 8;
+constexpr int MIX_TT8 = 8;  // token tile of long sequences (1 for short ones: more workgroups)
 
 // TQ > 0: all five outputs are Q8 sequence-GEMM token tiles (TQ = 2: Q8_1); each lane's record
 // address is formed once (a workgroup's MIX_TT tokens lie in one QG_TOK-token tile) and the
 // per-output emission is quant32 + store (store32's tiled values), no runtime format dispatch.
-template <int DM, int TQ>
+template <int DM, int TQ, int MIX_TT>
 __global__ __launch_bounds__(256) void k_v6_mix5(Mix5Args a) {
     __shared__ __attribute__((aligned(16))) float sl[MIX_TT][5 * DM];
     const int C = a.C, D = a.D, T = a.T;
@@ -476,16 +485,21 @@ bool launch_v6_mix5(hipStream_t st, int T, int C, int D, const float * lora, con
         fprintf(stderr, "rwkv: v6 maa LoRA width %d / n_embed %d unsupported\n", D, C);
         return false;
     }
-    const dim3 grid((C + 255) / 256, (T + MIX_TT - 1) / MIX_TT);
+    const int tt = T <= 64 ? 1 : MIX_TT8;
+    const dim3 grid((C + 255) / 256, (T + tt - 1) / tt);
     int tq = 0;
-    if (QG_TOK % MIX_TT == 0) {
+    {
         bool all = true;
         for (int n = 0; n < 5; n++)
             all = all && outs[n].tiled && outs[n].fmt == outs[0].fmt && outs[n].K == C &&
                   (outs[n].fmt == A_Q8_0 || outs[n].fmt == A_Q8_1);
         if (all) tq = outs[0].fmt == A_Q8_1 ? 2 : 1;
     }
-#define MIX5_L(DMv, TQv) hipLaunchKernelGGL((k_v6_mix5<DMv, TQv>), grid, dim3(256), 0, st, a)
+#define MIX5_L(DMv, TQv)                                                                    \
+    do {                                                                                    \
+        if (tt == 1) hipLaunchKernelGGL((k_v6_mix5<DMv, TQv, 1>), grid, dim3(256), 0, st, a); \
+        else hipLaunchKernelGGL((k_v6_mix5<DMv, TQv, MIX_TT8>), grid, dim3(256), 0, st, a); \
+    } while (0)
     if (D <= 32) {
         if (tq == 1) MIX5_L(32, 1);
         else if (tq == 2) MIX5_L(32, 2);
@@ -503,12 +517,16 @@ bool launch_v6_mix5(hipStream_t st, int T, int C, int D, const float * lora, con
 // --------------------------------------------------------------------------- v4 wkv
 __global__ __launch_bounds__(256) void k_wkv4(int T, int C, const float * r, const float * k, const float * v,
                                               const float * first, const float * decay, const float * sin,
-                                              float * sout, ActBuf out) {
+                                              float * sout, ActBuf out, int bs) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if ((int)(blockIdx.x * blockDim.x + (threadIdx.x & ~63)) >= C) return;
+    // batch (bs > 0): token blockIdx.y is its own context with its state at blockIdx.y * bs
+    const int t0 = bs ? (int)blockIdx.y : 0, t1 = bs ? t0 + 1 : T;
+    sin += (size_t)t0 * bs;
+    sout += (size_t)t0 * bs;
     float aa = sin[2 * C + c], bb = sin[3 * C + c], pp = sin[4 * C + c];
     const float fi = first[c], de = decay[c];
-    for (int t = 0; t < T; t++) {
+    for (int t = t0; t < t1; t++) {
         const size_t i = (size_t)t * C + c;
         const float kt = k[i], vt = v[i];
         float ww = fi + kt;
@@ -532,9 +550,9 @@ __global__ __launch_bounds__(256) void k_wkv4(int T, int C, const float * r, con
 
 bool launch_wkv4(hipStream_t st, int T, int C, const float * r, const float * k, const float * v,
                  const float * first, const float * decay, const float * state_in, float * state_out,
-                 const ActBuf & out) {
-    hipLaunchKernelGGL(k_wkv4, dim3((C + 255) / 256), dim3(256), 0, st, T, C, r, k, v, first, decay, state_in,
-                       state_out, out);
+                 const ActBuf & out, int bs) {
+    hipLaunchKernelGGL(k_wkv4, dim3((C + 255) / 256, bs ? T : 1), dim3(256), 0, st, T, C, r, k, v, first, decay,
+                       state_in, state_out, out, bs);
     HIP_OK(hipGetLastError());
     return true;
 }
@@ -545,10 +563,18 @@ bool launch_wkv4(hipStream_t st, int T, int C, const float * r, const float * k,
 template <int IPG>
 __global__ void k_wkv6(int T, int H, int S, int G, const float * k, const float * v, const float * r,
                        const float * u, const float * w, int w_per_token, const float * sin, float * sout,
-                       float * y) {
+                       float * y, int bs) {
     const int h = blockIdx.x;
     const int j = threadIdx.x / G, g = threadIdx.x % G;
     const int C = H * S;
+    if (bs) {  // batch: context blockIdx.z, one token
+        const size_t o = (size_t)blockIdx.z * C;
+        k += o, v += o, r += o, y += o;
+        if (w_per_token) w += o;
+        sin += (size_t)blockIdx.z * bs;
+        sout += (size_t)blockIdx.z * bs;
+        T = 1;
+    }
     float st[IPG];
     const size_t hb = (size_t)h * S * S;
 #pragma unroll
@@ -631,8 +657,16 @@ constexpr int WKV6_PAD = 8;  // >= 2 * the token group
 template <bool WPT, int NWV>
 __global__ __launch_bounds__(64 * NWV) void k_wkv6_s64(int T, int H, const float * k, const float * v, const float * r,
                                                        const float * u, const float * w, const float * sin, float * sout,
-                                                       float * y) {
+                                                       float * y, int bs) {
     constexpr int S = 64;
+    if (bs) {  // batch: context blockIdx.z, one token
+        const size_t o = (size_t)blockIdx.z * H * S;
+        k += o, v += o, r += o, y += o;
+        if (WPT) w += o;
+        sin += (size_t)blockIdx.z * bs;
+        sout += (size_t)blockIdx.z * bs;
+        T = 1;
+    }
     constexpr int CW = 4 * NWV, NT = 64 * NWV, QQ = WKV6_TC * 16 / NT;
     // WKV6_PAD rows past the chunk: a full chunk's look-ahead reads need no clamp (their tokens
     // are never used)
@@ -792,9 +826,10 @@ int g_wkv6_nwv = 4;  // waves per workgroup of k_wkv6_s64 (tools/wkv_probe.hip v
 
 bool launch_wkv6(hipStream_t st, int T, int H, int S, const float * k, const float * v, const float * r,
                  const float * u, const float * w, int w_per_token, const float * state_in, float * state_out,
-                 float * y) {
+                 float * y, int bs) {
+    const int nz = bs ? T : 1;
     if (S == 64) {
-#define WKV6_L(P, N) hipLaunchKernelGGL((k_wkv6_s64<P, N>), dim3(H, 16 / (N)), dim3(64 * (N)), 0, st, T, H, k, v, r, u, w, state_in, state_out, y)
+#define WKV6_L(P, N) hipLaunchKernelGGL((k_wkv6_s64<P, N>), dim3(H, 16 / (N), nz), dim3(64 * (N)), 0, st, T, H, k, v, r, u, w, state_in, state_out, y, bs)
         const int nwv = g_wkv6_nwv;
         if (w_per_token) {
             if (nwv == 1) WKV6_L(true, 1);
@@ -810,14 +845,14 @@ bool launch_wkv6(hipStream_t st, int T, int H, int S, const float * k, const flo
         return true;
     }
     const int G = pick_groups(S), IPG = S / G;
-    dim3 grid(H), block(S * G);
+    dim3 grid(H, 1, nz), block(S * G);
     switch (IPG) {
-        case 1: hipLaunchKernelGGL(k_wkv6<1>, grid, block, 0, st, T, H, S, G, k, v, r, u, w, w_per_token, state_in, state_out, y); break;
-        case 2: hipLaunchKernelGGL(k_wkv6<2>, grid, block, 0, st, T, H, S, G, k, v, r, u, w, w_per_token, state_in, state_out, y); break;
-        case 4: hipLaunchKernelGGL(k_wkv6<4>, grid, block, 0, st, T, H, S, G, k, v, r, u, w, w_per_token, state_in, state_out, y); break;
-        case 8: hipLaunchKernelGGL(k_wkv6<8>, grid, block, 0, st, T, H, S, G, k, v, r, u, w, w_per_token, state_in, state_out, y); break;
-        case 16: hipLaunchKernelGGL(k_wkv6<16>, grid, block, 0, st, T, H, S, G, k, v, r, u, w, w_per_token, state_in, state_out, y); break;
-        case 32: hipLaunchKernelGGL(k_wkv6<32>, grid, block, 0, st, T, H, S, G, k, v, r, u, w, w_per_token, state_in, state_out, y); break;
+        case 1: hipLaunchKernelGGL(k_wkv6<1>, grid, block, 0, st, T, H, S, G, k, v, r, u, w, w_per_token, state_in, state_out, y, bs); break;
+        case 2: hipLaunchKernelGGL(k_wkv6<2>, grid, block, 0, st, T, H, S, G, k, v, r, u, w, w_per_token, state_in, state_out, y, bs); break;
+        case 4: hipLaunchKernelGGL(k_wkv6<4>, grid, block, 0, st, T, H, S, G, k, v, r, u, w, w_per_token, state_in, state_out, y, bs); break;
+        case 8: hipLaunchKernelGGL(k_wkv6<8>, grid, block, 0, st, T, H, S, G, k, v, r, u, w, w_per_token, state_in, state_out, y, bs); break;
+        case 16: hipLaunchKernelGGL(k_wkv6<16>, grid, block, 0, st, T, H, S, G, k, v, r, u, w, w_per_token, state_in, state_out, y, bs); break;
+        case 32: hipLaunchKernelGGL(k_wkv6<32>, grid, block, 0, st, T, H, S, G, k, v, r, u, w, w_per_token, state_in, state_out, y, bs); break;
         default: fprintf(stderr, "rwkv: unsupported head size %d\n", S); return false;
     }
     HIP_OK(hipGetLastError());
@@ -865,10 +900,17 @@ bool launch_v7_prep(hipStream_t st, int T, int H, int S, float * k, const float 
 template <int JPG>
 __global__ void k_wkv7(int T, int H, int S, int G, const float * r, const float * w, const float * k,
                        const float * v, const float * a, const float * b, const float * sin, float * sout,
-                       float * y) {
+                       float * y, int bs) {
     const int h = blockIdx.x;
     const int i = threadIdx.x / G, g = threadIdx.x % G;
     const int C = H * S;
+    if (bs) {  // batch: context blockIdx.z, one token
+        const size_t o = (size_t)blockIdx.z * C;
+        r += o, w += o, k += o, v += o, a += o, b += o, y += o;
+        sin += (size_t)blockIdx.z * bs;
+        sout += (size_t)blockIdx.z * bs;
+        T = 1;
+    }
     const size_t hb = (size_t)h * S * S + (size_t)i * S + g * JPG;
     float st[JPG];
 #pragma unroll
@@ -901,8 +943,15 @@ __global__ void k_wkv7(int T, int H, int S, int G, const float * r, const float 
 // (and v) staged in LDS, the next chunk's loads in flight.
 __global__ __launch_bounds__(64) void k_wkv7_s64(int T, int H, const float * r, const float * w, const float * k,
                                                  const float * v, const float * a, const float * b,
-                                                 const float * sin, float * sout, float * y) {
+                                                 const float * sin, float * sout, float * y, int bs) {
     constexpr int S = 64;
+    if (bs) {  // batch: context blockIdx.z, one token
+        const size_t o = (size_t)blockIdx.z * H * S;
+        r += o, w += o, k += o, v += o, a += o, b += o, y += o;
+        sin += (size_t)blockIdx.z * bs;
+        sout += (size_t)blockIdx.z * bs;
+        T = 1;
+    }
     __shared__ __attribute__((aligned(16))) float sr[WKV_TC][S], sw[WKV_TC][S], sk[WKV_TC][S], sa_[WKV_TC][S],
         sb[WKV_TC][S], sv[WKV_TC][16];
     const int h = blockIdx.x, ib = blockIdx.y, lane = threadIdx.x;
@@ -988,21 +1037,23 @@ __global__ __launch_bounds__(64) void k_wkv7_s64(int T, int H, const float * r, 
 
 bool launch_wkv7(hipStream_t st, int T, int H, int S, const float * r, const float * w, const float * k,
                  const float * v, const float * a, const float * b, const float * state_in, float * state_out,
-                 float * y) {
+                 float * y, int bs) {
+    const int nz = bs ? T : 1;
     if (S == 64) {
-        hipLaunchKernelGGL(k_wkv7_s64, dim3(H, 4), dim3(64), 0, st, T, H, r, w, k, v, a, b, state_in, state_out, y);
+        hipLaunchKernelGGL(k_wkv7_s64, dim3(H, 4, nz), dim3(64), 0, st, T, H, r, w, k, v, a, b, state_in, state_out, y,
+                           bs);
         HIP_OK(hipGetLastError());
         return true;
     }
     const int G = pick_groups(S), JPG = S / G;
-    dim3 grid(H), block(S * G);
+    dim3 grid(H, 1, nz), block(S * G);
     switch (JPG) {
-        case 1: hipLaunchKernelGGL(k_wkv7<1>, grid, block, 0, st, T, H, S, G, r, w, k, v, a, b, state_in, state_out, y); break;
-        case 2: hipLaunchKernelGGL(k_wkv7<2>, grid, block, 0, st, T, H, S, G, r, w, k, v, a, b, state_in, state_out, y); break;
-        case 4: hipLaunchKernelGGL(k_wkv7<4>, grid, block, 0, st, T, H, S, G, r, w, k, v, a, b, state_in, state_out, y); break;
-        case 8: hipLaunchKernelGGL(k_wkv7<8>, grid, block, 0, st, T, H, S, G, r, w, k, v, a, b, state_in, state_out, y); break;
-        case 16: hipLaunchKernelGGL(k_wkv7<16>, grid, block, 0, st, T, H, S, G, r, w, k, v, a, b, state_in, state_out, y); break;
-        case 32: hipLaunchKernelGGL(k_wkv7<32>, grid, block, 0, st, T, H, S, G, r, w, k, v, a, b, state_in, state_out, y); break;
+        case 1: hipLaunchKernelGGL(k_wkv7<1>, grid, block, 0, st, T, H, S, G, r, w, k, v, a, b, state_in, state_out, y, bs); break;
+        case 2: hipLaunchKernelGGL(k_wkv7<2>, grid, block, 0, st, T, H, S, G, r, w, k, v, a, b, state_in, state_out, y, bs); break;
+        case 4: hipLaunchKernelGGL(k_wkv7<4>, grid, block, 0, st, T, H, S, G, r, w, k, v, a, b, state_in, state_out, y, bs); break;
+        case 8: hipLaunchKernelGGL(k_wkv7<8>, grid, block, 0, st, T, H, S, G, r, w, k, v, a, b, state_in, state_out, y, bs); break;
+        case 16: hipLaunchKernelGGL(k_wkv7<16>, grid, block, 0, st, T, H, S, G, r, w, k, v, a, b, state_in, state_out, y, bs); break;
+        case 32: hipLaunchKernelGGL(k_wkv7<32>, grid, block, 0, st, T, H, S, G, r, w, k, v, a, b, state_in, state_out, y, bs); break;
         default: fprintf(stderr, "rwkv: unsupported head size %d\n", S); return false;
     }
     HIP_OK(hipGetLastError());

@@ -11,6 +11,9 @@ bool launch_mm_group(hipStream_t st, MMGroup & g, int wtype);
 // int8-MFMA sequence GEMM for quantized weights (qgemm.hip); same results as launch_mm_group.
 // Every entry needs y; emission is left to the caller (launch_act_from_f32).
 bool launch_qgemm(hipStream_t st, MMGroup & g, int wtype);
+// Batched decode matvec (mv_batch.hip): the T rows are T independent contexts; same results as
+// launch_mm_group.  *launched = false (and nothing enqueued) for shapes it does not cover.
+bool launch_mvb_group(hipStream_t st, MMGroup & g, int wtype, bool * launched);
 
 // ---- elementwise / recurrence kernels -----------------------------------------------------
 // x[t] = LN(emb[tokens[t]]; w, b)   (rwkv_graph.inc:654-658)
@@ -29,6 +32,8 @@ struct LnMixArgs {
     ActBuf out[6];
     float * out_xa;             // optional fp32 [T][C]
     float * out_sx;             // optional fp32 [T][C] (xp - xa)
+    size_t bs;                  // 0: one sequence; > 0: batched decode -- token t is context t, its
+                                // carries at carry_in/out + t * bs (state floats per context)
 };
 bool launch_ln_mix(hipStream_t st, const LnMixArgs & a);
 
@@ -39,12 +44,14 @@ bool launch_v6_mix5(hipStream_t st, int T, int C, int D, const float * lora, con
 // v4 wkv with aa/bb/pp state (rwkv_graph.inc:119-161); emits r*wkv into `out`.
 bool launch_wkv4(hipStream_t st, int T, int C, const float * r, const float * k, const float * v,
                  const float * first, const float * decay, const float * state_in, float * state_out,
-                 const ActBuf & out);
+                 const ActBuf & out, int bs = 0);
 
 // ggml_rwkv_wkv6 semantics (v5/v6): y[T][C]; w_per_token selects v6 (w [T][C]) vs v5 (w [C]).
+// bs > 0 (every wkv launcher): batched decode -- the T tokens are T contexts, one token each,
+// context t's state at state_in/out + t * bs.
 bool launch_wkv6(hipStream_t st, int T, int H, int S, const float * k, const float * v, const float * r,
                  const float * u, const float * w, int w_per_token, const float * state_in,
-                 float * state_out, float * y);
+                 float * state_out, float * y, int bs = 0);
 
 // v7 per-head prep: kk = l2norm(k*k_k); k += a*ka - ka; nb = -kk; bb = kk*a; bonus = sum(k*r*r_k)
 bool launch_v7_prep(hipStream_t st, int T, int H, int S, float * k, const float * a, const float * r,
@@ -54,7 +61,7 @@ bool launch_v7_prep(hipStream_t st, int T, int H, int S, float * k, const float 
 // rwkv_operators_wkv_v7.inc:37-107
 bool launch_wkv7(hipStream_t st, int T, int H, int S, const float * r, const float * w, const float * k,
                  const float * v, const float * a, const float * b, const float * state_in,
-                 float * state_out, float * y);
+                 float * state_out, float * y, int bs = 0);
 
 // GroupNorm over heads + ln_x (+ v7 bonus) (+ gate), emitted as the output projection's input.
 // mode 0: none, 1: *g, 2: + v*bonus then *g
@@ -62,8 +69,9 @@ bool launch_groupnorm(hipStream_t st, int T, int H, int S, float eps, const floa
                       const float * b, int mode, const float * g, const float * v, const float * bonus,
                       const ActBuf & out);
 
-// LN of one row (x[row]) emitted into a 1-row ActBuf (head input).
-bool launch_ln_emit(hipStream_t st, int C, const float * x, const float * w, const float * b, const ActBuf & out);
+// LN of rows x[0..rows) emitted into rows 0..rows of an ActBuf (head input).
+bool launch_ln_emit(hipStream_t st, int C, const float * x, const float * w, const float * b, const ActBuf & out,
+                    int rows = 1);
 
 // v4 state init value helper: fills n floats with value
 bool launch_fill(hipStream_t st, float * p, size_t n, float value);
@@ -170,6 +178,10 @@ struct Att6Dec {
     float eps;
     float * y;
     ActBuf yq;               // fmt >= 0 (needs S >= 32): emit y in the Wo input format instead
+    // batched decode (nb > 1 contexts, grid.y): context b's r/k/v/g/y at + b*C, dl at + b*ldd,
+    // state at sin/sout + b*bs, yq row b
+    int nb, ldd;
+    size_t bs;
 };
 bool launch_att6_dec(hipStream_t st, const Att6Dec & a);
 
@@ -190,6 +202,8 @@ struct Att7Dec {
     const float * lnx_w, * lnx_b;
     float * y;
     ActBuf yq;               // fmt >= 0 (needs S >= 32): emit y in the Wo input format instead
+    int nb;                  // batched decode: contexts (grid.y), as Att6Dec
+    size_t bs;
 };
 bool launch_att7_dec(hipStream_t st, const Att7Dec & a);
 

@@ -282,11 +282,19 @@ __global__ __launch_bounds__(256) void k_att6_dec(Att6Dec a) {
     const int tid = threadIdx.x, j = tid % S, g = min(tid / S, G - 1), c0 = h * S;
     const bool active = tid < S * G;
     const size_t hb = (size_t)h * S * S;
+    // batched decode: context blockIdx.y (its [C] vectors, decay LoRA row and state); 0 in decode
+    const int bz = blockIdx.y;
+    const size_t cb = (size_t)bz * a.H * S;
+    const float * ar = a.r + cb, * ak = a.k + cb, * av = a.v + cb;
+    const float * ag = a.g ? a.g + cb : nullptr;
+    const float * adl = a.dl ? a.dl + (size_t)bz * a.ldd : nullptr;
+    const float * asin = a.sin + (size_t)bz * a.bs;
+    float * asout = a.sout + (size_t)bz * a.bs;
     STAMP_BEGIN();
     float st[16];
 #pragma unroll
     for (int ii = 0; ii < 16; ii++)
-        st[ii] = ii < IPG && active ? a.sin[hb + (size_t)(g * IPG + ii) * S + j] : 0.0f;
+        st[ii] = ii < IPG && active ? asin[hb + (size_t)(g * IPG + ii) * S + j] : 0.0f;
     WBlk wp[PF > 0 ? PF : 1];
     if constexpr (PF > 0) {
         const int nb = a.wd2.K >> 5;
@@ -298,12 +306,12 @@ __global__ __launch_bounds__(256) void k_att6_dec(Att6Dec a) {
     // are not a dependent round trip behind the barriers
     const int cme = c0 + min(tid, S - 1);
     const float lnw_c = a.lnx_w[cme], lnb_c = a.lnx_b[cme];
-    const float g_c = a.g ? a.g[cme] : 1.0f;
+    const float g_c = ag ? ag[cme] : 1.0f;
     const float dec_c = a.w ? 0.0f : a.decay[cme];
     if (tid < S) {
-        sr[tid] = a.r[c0 + tid];
-        sk[tid] = a.k[c0 + tid];
-        sv[tid] = a.v[c0 + tid];
+        sr[tid] = ar[c0 + tid];
+        sk[tid] = ak[c0 + tid];
+        sv[tid] = av[c0 + tid];
         su[tid] = a.u[c0 + tid];
         if (a.w) sw[tid] = a.w[c0 + tid];
     }
@@ -314,7 +322,7 @@ __global__ __launch_bounds__(256) void k_att6_dec(Att6Dec a) {
         act = lds_act(smem, act_fmt_for(a.wd2.type), D);
         for (int k0 = 0; k0 < D; k0 += blockDim.x) {
             if (k0 + (tid & ~31) >= D) continue;
-            emit32(act, 0, k0 + tid, a.dl[k0 + tid]);
+            emit32(act, 0, k0 + tid, adl[k0 + tid]);
         }
     }
     __syncthreads();
@@ -377,7 +385,7 @@ __global__ __launch_bounds__(256) void k_att6_dec(Att6Dec a) {
                 const float t = temp * rq[ii];
                 acc += t;
                 p4[ii >> 2] += t;
-                a.sout[hb + (size_t)i * S + j] = prev * wq[ii] + kv;
+                asout[hb + (size_t)i * S + j] = prev * wq[ii] + kv;
             }
         }
         part[g][j] = IPG == 16 ? (p4[0] + p4[1]) + (p4[2] + p4[3]) : acc;
@@ -404,9 +412,9 @@ __global__ __launch_bounds__(256) void k_att6_dec(Att6Dec a) {
         float o = d * scale;
         o = o * lnw_c;
         o = o + lnb_c;
-        if (a.g) o = o * g_c;
-        if (a.yq.fmt >= 0) emit32(a.yq, 0, c0 + tid, o);  // S >= 32: whole half-wave blocks
-        else a.y[c0 + tid] = o;
+        if (ag) o = o * g_c;
+        if (a.yq.fmt >= 0) emit32(a.yq, bz, c0 + tid, o);  // S >= 32: whole half-wave blocks
+        else a.y[cb + c0 + tid] = o;
     }
     STAMP_END(3);
 }
@@ -432,7 +440,7 @@ bool launch_att6_dec(hipStream_t st, const Att6Dec & a) {
         fprintf(stderr, "rwkv: quantized attention output needs head size >= 32\n");
         return false;
     }
-    dim3 grid(a.H), block(std::max(threads, 64));
+    dim3 grid(a.H, a.nb > 1 ? a.nb : 1), block(std::max(threads, 64));
     const bool pf = !a.w && a.wd2.type >= W_Q4_0 && (a.wd2.K >> 5) <= 4;
     if (a.w) {
         hipLaunchKernelGGL((k_att6_dec<-2, 0>), grid, block, lds, st, a);  // v5: no decay LoRA
@@ -516,6 +524,11 @@ __global__ __launch_bounds__(256) void k_att7_dec(Att7Dec a) {
     __shared__ float sbonus;
     const int h = blockIdx.x, S = a.S, G = S / JPG;
     const int tid = threadIdx.x, c0 = h * S;
+    // batched decode: context blockIdx.y (0 in decode)
+    const int bz = blockIdx.y;
+    const size_t cb = (size_t)bz * a.H * S;
+    const float * asin = a.sin + (size_t)bz * a.bs;
+    float * asout = a.sout + (size_t)bz * a.bs;
     // state rows and the GroupNorm epilogue operands are loaded first: no dependent round trip
     // behind the barriers
     const bool wact = tid < S * G;
@@ -523,25 +536,25 @@ __global__ __launch_bounds__(256) void k_att7_dec(Att7Dec a) {
     const size_t wbase = (size_t)h * S * S + (size_t)wi * S + wg * JPG;
     float st[JPG];
 #pragma unroll
-    for (int jj = 0; jj < JPG; jj++) st[jj] = a.sin[wbase + jj];
+    for (int jj = 0; jj < JPG; jj++) st[jj] = asin[wbase + jj];
     const int cme = c0 + min(tid, S - 1);
-    const float lnw_c = a.lnx_w[cme], lnb_c = a.lnx_b[cme], g_c = a.g[cme];
+    const float lnw_c = a.lnx_w[cme], lnb_c = a.lnx_b[cme], g_c = a.g[cb + cme];
     if (tid < S) {
         // prep (rwkv_graph.inc:432-437 + rwkv_operators.inc:40-82)
         const int c = c0 + tid;
-        const float kv = a.k[c];
+        const float kv = a.k[cb + c];
         const float kkr = kv * a.k_k[c];
         const float sum = group_sum(kkr * kkr, S);
         const float scale = 1.0f / fmaxf(sqrtf(sum), 1e-12f);
         const float kk = kkr * scale;
-        const float av = a.a[c];
+        const float av = a.a[cb + c];
         const float ka = kv * a.k_a[c];
         const float kadj = kv + (av * ka - ka);
-        const float rv = a.r[c];
+        const float rv = a.r[cb + c];
         sr[tid] = rv;
-        sw[tid] = a.w[c];
+        sw[tid] = a.w[cb + c];
         sk[tid] = kadj;
-        sv[tid] = a.v[c];
+        sv[tid] = a.v[cb + c];
         snb[tid] = -kk;
         sbb[tid] = kk * av;
         const float bs = group_sum((kadj * rv) * a.r_k[c], S);
@@ -563,7 +576,7 @@ __global__ __launch_bounds__(256) void k_att7_dec(Att7Dec a) {
             const int j = g * JPG + jj;
             const float kv = vi * sk[j];
             const float ns = st[jj] * sw[j] + kv + sa * sbb[j];
-            a.sout[base + jj] = ns;
+            asout[base + jj] = ns;
             acc += ns * sr[j];
         }
         acc = group_sum(acc, G);
@@ -584,8 +597,8 @@ __global__ __launch_bounds__(256) void k_att7_dec(Att7Dec a) {
         o = o + lnb_c;
         o = o + sv[tid] * sbonus;
         o = o * g_c;
-        if (a.yq.fmt >= 0) emit32(a.yq, 0, c, o);  // S >= 32: whole half-wave blocks
-        else a.y[c] = o;
+        if (a.yq.fmt >= 0) emit32(a.yq, bz, c, o);  // S >= 32: whole half-wave blocks
+        else a.y[cb + c] = o;
     }
 }
 
@@ -602,7 +615,7 @@ bool launch_att7_dec(hipStream_t st, const Att7Dec & a) {
         fprintf(stderr, "rwkv: quantized attention output needs head size >= 32\n");
         return false;
     }
-    dim3 grid(a.H), block(threads);
+    dim3 grid(a.H, a.nb > 1 ? a.nb : 1), block(threads);
     switch (JPG) {
         case 1: hipLaunchKernelGGL(k_att7_dec<1>, grid, block, 0, st, a); break;
         case 2: hipLaunchKernelGGL(k_att7_dec<2>, grid, block, 0, st, a); break;

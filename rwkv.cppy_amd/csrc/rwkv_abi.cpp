@@ -290,6 +290,35 @@ RWKV_API bool rwkv_mi355x_eval_layers_async(struct rwkv_context * ctx, const uin
 
 RWKV_API float * rwkv_mi355x_logits_device(struct rwkv_context * ctx) { return ctx->engine->device_logits(); }
 
+static bool eval_batch(struct rwkv_context * ctx, const uint32_t * tokens, size_t n, const float * state_in,
+                       float * state_out, float * logits_out, bool dev) {
+    ctx->last_error = RWKV_ERROR_NONE;
+    const DeviceModel & dm = ctx->model->dm;
+    CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, n > 0 && tokens != nullptr, "Batch is empty");
+    CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, n <= (size_t)Engine::kBatchMax, "Batch of %zu contexts (at most %d)", n,
+              Engine::kBatchMax);
+    CTX_CHECK(ctx, RWKV_ERROR_CTX | RWKV_ERROR_UNSUPPORTED, false, !dm.partial(),
+              "This context holds layers [%u, %u) only (a pipeline stage)", dm.layer_lo, dm.layer_hi);
+    CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, !dev || state_in == nullptr || state_in != state_out,
+              "Device batch: state_in and state_out must be different buffers");
+    for (size_t i = 0; i < n; i++)
+        CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, tokens[i] < dm.n_vocab, "Token at index %zu (%" PRIu32 ") is out of range",
+                  i, tokens[i]);
+    CTX_CHECK(ctx, RWKV_ERROR_CTX, false, ctx->engine->eval_batch(tokens, n, state_in, state_out, logits_out, dev),
+              "GPU evaluation failed");
+    return true;
+}
+
+RWKV_API bool rwkv_mi355x_eval_batch(struct rwkv_context * ctx, const uint32_t * tokens, size_t n_contexts,
+                                     const float * state_in, float * state_out, float * logits_out) {
+    return eval_batch(ctx, tokens, n_contexts, state_in, state_out, logits_out, false);
+}
+
+RWKV_API bool rwkv_mi355x_eval_batch_device(struct rwkv_context * ctx, const uint32_t * tokens, size_t n_contexts,
+                                            const float * state_in, float * state_out, float * logits_out) {
+    return eval_batch(ctx, tokens, n_contexts, state_in, state_out, logits_out, true);
+}
+
 
 RWKV_API bool rwkv_mi355x_sync(struct rwkv_context * ctx) { return ctx->engine->sync(); }
 RWKV_API long long rwkv_mi355x_debug_buffer(struct rwkv_context * ctx, const char * name, void * out, size_t bytes) {

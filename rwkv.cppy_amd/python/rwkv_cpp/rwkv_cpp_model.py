@@ -129,6 +129,25 @@ class RWKVModel:
                                                    self._ptr(logits_out))
         return logits_out, state_out
 
+    def eval_batch(self, tokens: List[int], states_in=None):
+        """MI355X extension (rwkv_mi355x_eval_batch): len(tokens) independent contexts advance one token
+        each in one pass over the weights.  states_in: float32 [n, state_len] numpy array, or None for
+        fresh states.  Returns (logits [n, n_vocab], states [n, state_len]); row i equals
+        eval(tokens[i], states_in[i]) bit for bit."""
+        import numpy as np
+        if not self._valid:
+            raise ValueError('Model was freed')
+        n = len(tokens)
+        if states_in is not None:
+            states_in = np.ascontiguousarray(states_in, dtype=np.float32)
+            if states_in.shape != (n, self._state_buffer_element_count):
+                raise ValueError(f'states_in must be [{n}, {self._state_buffer_element_count}]')
+        states = np.zeros((n, self._state_buffer_element_count), np.float32)
+        logits = np.zeros((n, self._logits_buffer_element_count), np.float32)
+        self._library.rwkv_mi355x_eval_batch(self._ctx, list(tokens), None if states_in is None else states_in.ctypes.data,
+                                             states.ctypes.data, logits.ctypes.data)
+        return logits, states
+
     def free(self) -> None:
         if not self._valid:
             raise ValueError('Already freed')

@@ -99,6 +99,10 @@ class RWKVSharedLibrary:
         L.rwkv_mi355x_write_synthetic_model.argtypes = [ctypes.c_char_p, ctypes.c_int, u32, u32, u32, u32,
                                                         ctypes.c_char_p, ctypes.c_uint64]
         L.rwkv_mi355x_write_synthetic_model.restype = ctypes.c_bool
+        L.rwkv_mi355x_eval_batch.argtypes = [vp, vp, sz, vp, vp, vp]
+        L.rwkv_mi355x_eval_batch.restype = ctypes.c_bool
+        L.rwkv_mi355x_eval_batch_device.argtypes = [vp, vp, sz, vp, vp, vp]
+        L.rwkv_mi355x_eval_batch_device.restype = ctypes.c_bool
         L.rwkv_mi355x_set_kernel_timing.argtypes = [vp, ctypes.c_bool]
         L.rwkv_mi355x_set_kernel_timing.restype = None
         L.rwkv_mi355x_kernel_stats.argtypes = [vp, ctypes.c_int, ctypes.c_char_p, sz, ctypes.POINTER(ctypes.c_longlong),
@@ -169,6 +173,16 @@ class RWKVSharedLibrary:
                                                      model_file_path_out.encode('utf-8'),
                                                      format_name.encode('utf-8')):
             raise ValueError('rwkv_quantize_model_file failed, check stderr')
+
+    # ---- additive: batched decode (include/rwkv_mi355x.h) ------------------------------------
+    def rwkv_mi355x_eval_batch(self, ctx: RWKVContext, tokens: List[int], state_in_address: Optional[int],
+                               state_out_address: Optional[int], logits_out_address: Optional[int]) -> None:
+        """len(tokens) contexts advance one token each; states [n][state_len], logits [n][n_vocab]
+        (host addresses, None = fresh states / not returned).  Bit-identical to rwkv_eval per context."""
+        arr = (ctypes.c_uint32 * len(tokens))(*tokens)
+        if not self.library.rwkv_mi355x_eval_batch(ctx.ptr, ctypes.cast(arr, ctypes.c_void_p), len(tokens),
+                                                   state_in_address, state_out_address, logits_out_address):
+            raise ValueError('rwkv_mi355x_eval_batch failed, check stderr')
 
     def rwkv_get_system_info_string(self) -> str:
         return self.library.rwkv_get_system_info_string().decode('utf-8')

@@ -882,7 +882,10 @@ bool Engine::layer_v6(int l, int T, const float * si, float * so) {
     if (!b.run(*this, T)) return false;
     // order w, k, v, r, g (rwkv_graph.inc:336-346)
     ActBuf outs[5] = {A(1, L.decay_w1), A(2, L.att_k), A(3, L.att_v), A(4, L.att_r), A(5, L.att_g)};
-    if (!launch_v6_mix5(stream_, T, C, D, lora_, L.maa_w2t, L.maa, xa_, sx_, outs)) return false;
+    // batched decode: the decode kernel's per-(mix, channel) arithmetic over the contexts
+    if (bs_ ? !launch_v6_mix5_dec(stream_, C, D, xa_, nullptr, lora_, L.maa_w2t, L.maa, outs, T, sx_)
+            : !launch_v6_mix5(stream_, T, C, D, lora_, L.maa_w2t, L.maa, xa_, sx_, outs))
+        return false;
     ActBuf dl = A(6, L.decay_w2);
     // decay tail by threads (k_att6_dec's rows) when Wd2 is quantized; dl fp32 then reuses lora_
     // (consumed by mix5 above)

@@ -152,8 +152,10 @@ int mva_rows();
 // v6 token-shift mixes with the maa LoRA (rwkv_graph.inc:308-346); xa = LN(x) is the new
 // att_xx carry already written by the W1 matvec prologue; w2t is time_maa_w2 transposed to
 // [5][D][C]; emits the five mixed vectors w,k,v,r,g.
+// Batched decode: nb > 1 contexts (grid.z), xa / sx [nb][C] (sx = xp - xa), lora [nb][5D].
 bool launch_v6_mix5_dec(hipStream_t st, int C, int D, const float * xa, const float * carry, const float * lora,
-                        const float * w2t, const float * const * maa, const ActBuf * outs);
+                        const float * w2t, const float * const * maa, const ActBuf * outs, int nb = 1,
+                        const float * sx = nullptr);
 
 // v6 maa LoRA in one launch (mv_maa.hip): LN(x) + token shift -> lora_n = tanh(W1[n] . xxx) ->
 // the five mixed vectors w,k,v,r,g, emitted in their matmuls' input formats; writes the new

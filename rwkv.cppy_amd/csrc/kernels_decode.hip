@@ -142,14 +142,17 @@ struct Mix5Dec {
     const float * xa, * carry, * lora, * w2t;
     const float * maa[5];
     ActBuf out[5];
+    // batched decode (grid.z = contexts): context b's xa / sx (xp - xa) rows at + b*C, lora at
+    // + b*5D, output row b; carry is then unused
+    const float * sx;
 };
 
-// grid (C/256, 5): block (cx, n) computes mixed vector n for 256 channels from xa = LN(x),
+// grid (C/256, 5[, B]): block (cx, n[, b]) computes mixed vector n for 256 channels from xa = LN(x),
 // which the preceding W1 matvec already wrote as the new att_xx carry.  w2t [5][D][C] makes
 // the per-channel D-long dots coalesced across lanes; accumulation order matches the oracle
 // (sequential over i, fp64).
 __global__ __launch_bounds__(256) void k_v6_mix5_dec(Mix5Dec a) {
-    const int n = blockIdx.y, C = a.C, D = a.D;
+    const int n = blockIdx.y, C = a.C, D = a.D, b = blockIdx.z;
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if ((int)(blockIdx.x * blockDim.x + (threadIdx.x & ~31)) >= C) return;  // half-wave uniform
     float w2v[64];
@@ -159,19 +162,20 @@ __global__ __launch_bounds__(256) void k_v6_mix5_dec(Mix5Dec a) {
         const float t = w2[(size_t)min(i, D - 1) * C];
         w2v[i] = (i < D) ? t : 0.0f;
     }
-    const float xa = a.xa[c], cc = a.carry[c], mu = a.maa[n][c];
-    const float sx = cc - xa;
-    const float * lv = a.lora + n * D;
+    const size_t cb = (size_t)b * C;
+    const float xa = a.xa[cb + c], mu = a.maa[n][c];
+    const float sx = a.sx ? a.sx[cb + c] : a.carry[c] - xa;
+    const float * lv = a.lora + (size_t)b * 5 * D + n * D;
     double acc = 0.0;
 #pragma unroll
     for (int i = 0; i < 64; i++)
         if (i < D) acc += (double)(w2v[i] * lv[i]);
     const float m = (float)acc;
-    emit32(a.out[n], 0, c, (m + mu) * sx + xa);
+    emit32(a.out[n], b, c, (m + mu) * sx + xa);
 }
 
 bool launch_v6_mix5_dec(hipStream_t st, int C, int D, const float * xa, const float * carry, const float * lora,
-                        const float * w2t, const float * const * maa, const ActBuf * outs) {
+                        const float * w2t, const float * const * maa, const ActBuf * outs, int nb, const float * sx) {
     Mix5Dec a;
     a.C = C;
     a.D = D;
@@ -179,15 +183,16 @@ bool launch_v6_mix5_dec(hipStream_t st, int C, int D, const float * xa, const fl
     a.carry = carry;
     a.lora = lora;
     a.w2t = w2t;
+    a.sx = sx;
     for (int n = 0; n < 5; n++) {
         a.maa[n] = maa[n];
         a.out[n] = outs[n];
     }
-    if (D > 64 || C % 32) {
+    if (D > 64 || C % 32 || (nb > 1 && !sx)) {
         fprintf(stderr, "rwkv: v6 maa LoRA width %d / n_embed %d unsupported\n", D, C);
         return false;
     }
-    dim3 grid((C + 255) / 256, 5);
+    dim3 grid((C + 255) / 256, 5, nb > 1 ? nb : 1);
     hipLaunchKernelGGL(k_v6_mix5_dec, grid, dim3(256), 0, st, a);
     HIP_OK(hipGetLastError());
     return true;

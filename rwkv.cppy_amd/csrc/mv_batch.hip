@@ -48,41 +48,50 @@ __global__ __launch_bounds__(256) void k_mvb(MMGroup g) {
         a.f = E.in.f + (size_t)t * K;
         return a;
     };
-    AUnit xn[U];
-    {
-        const ActBuf a = act_row(0);
+    // activation ring: the rows of the next PD contexts are in flight while one is computed
+    // (an L2 round trip is several contexts' worth of dots)
+    constexpr int PD = U == 1 ? 8 : U == 2 ? 4 : 2;
+    AUnit xb[PD][U];
 #pragma unroll
-        for (int u = 0; u < U; u++) xn[u] = load_act_unit<WF, false>(a, u, lane);
+    for (int p = 0; p < PD; p++) {
+        const ActBuf a = act_row(min(p, T - 1));
+#pragma unroll
+        for (int u = 0; u < U; u++) xb[p][u] = load_act_unit<WF, false>(a, u, lane);
     }
     constexpr bool one = WF == W_Q4_1 || WF == W_Q5_1;
 #pragma unroll 1
-    for (int t = 0; t < T; t++) {
-        AUnit x[U];
+    for (int t0 = 0; t0 < T; t0 += PD) {
 #pragma unroll
-        for (int u = 0; u < U; u++) x[u] = xn[u];
-        if (t + 1 < T) {
-            const ActBuf a = act_row(t + 1);
+        for (int p = 0; p < PD; p++) {
+            const int t = t0 + p;
+            if (t >= T) break;  // uniform
+            AUnit x[U];
 #pragma unroll
-            for (int u = 0; u < U; u++) xn[u] = load_act_unit<WF, false>(a, u, lane);
-        }
-        float acc[R], acc2[R];
+            for (int u = 0; u < U; u++) x[u] = xb[p][u];
+            if (t + PD < T) {
+                const ActBuf a = act_row(t + PD);
 #pragma unroll
-        for (int r = 0; r < R; r++) acc[r] = acc2[r] = 0.0f;
+                for (int u = 0; u < U; u++) xb[p][u] = load_act_unit<WF, false>(a, u, lane);
+            }
+            float acc[R], acc2[R];
 #pragma unroll
-        for (int u = 0; u < U; u++) {
-            const bool valid = unit_valid<WF>(K, u, lane);
+            for (int r = 0; r < R; r++) acc[r] = acc2[r] = 0.0f;
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const bool valid = unit_valid<WF>(K, u, lane);
+#pragma unroll
+                for (int r = 0; r < R; r++) {
+                    float s = acc[r], s2 = acc2[r];
+                    dot_unit<WF>(w[r][u], x[u], s, s2);
+                    acc[r] = valid ? s : acc[r];
+                    acc2[r] = valid ? s2 : acc2[r];
+                }
+            }
 #pragma unroll
             for (int r = 0; r < R; r++) {
-                float s = acc[r], s2 = acc2[r];
-                dot_unit<WF>(w[r][u], x[u], s, s2);
-                acc[r] = valid ? s : acc[r];
-                acc2[r] = valid ? s2 : acc2[r];
+                const float s = one ? wave_sum63(acc[r]) + wave_sum63(acc2[r]) : wave_sum63(acc[r]) + 0.0f;
+                if (lane == 63) red[t * RW + wave * R + r] = s;
             }
-        }
-#pragma unroll
-        for (int r = 0; r < R; r++) {
-            const float s = one ? wave_sum63(acc[r]) + wave_sum63(acc2[r]) : wave_sum63(acc[r]) + 0.0f;
-            if (lane == 63) red[t * RW + wave * R + r] = s;
         }
     }
     __syncthreads();
@@ -104,7 +113,9 @@ __global__ __launch_bounds__(256) void k_mvb(MMGroup g) {
 // Shapes: U = 16-byte units per lane (K), R rows per wave; emitting groups need R = 8.
 template <int WF>
 static bool launch_mvb_wf(hipStream_t st, MMGroup & g, bool emit, int U) {
-    const int R = emit ? 8 : U <= 4 ? 4 : 2;
+    // rows per wave: emitting groups need a 32-row block per workgroup; long rows (U >= 4: the
+    // FFN value matrix, the head) take fewer rows per wave so the grid still covers the chip
+    const int R = emit ? 8 : U <= 2 ? 4 : U <= 4 ? 2 : 1;
     const int RW = 4 * R;
     int blocks = 0;
     for (int i = 0; i < g.n; i++) {
@@ -123,9 +134,9 @@ static bool launch_mvb_wf(hipStream_t st, MMGroup & g, bool emit, int U) {
     } else if (U == 2) {
         MVB(4, 2, false);
     } else if (U <= 4) {
-        MVB(4, 4, false);
+        MVB(2, 4, false);
     } else {
-        MVB(2, 8, false);
+        MVB(1, 8, false);
     }
 #undef MVB
     HIP_OK(hipGetLastError());

@@ -55,7 +55,7 @@ def main():
     ap.add_argument('--config', default='v6-1b6-q4_0', choices=sorted(CONFIGS))
     ap.add_argument('--seq-len', type=int, default=1024)
     ap.add_argument('--seq-reps', type=int, default=3)
-    ap.add_argument('--abi-steps', type=int, default=16)
+    ap.add_argument('--abi-steps', type=int, default=32)
     ap.add_argument('--pipe-chunk', type=int, default=0, help='pipeline chunk (0: max(64, T / (2 N)))')
     ap.add_argument('--timing-steps', type=int, default=8)
     ap.add_argument('--cpu-seconds', type=float, default=12.0)
@@ -256,6 +256,24 @@ def main():
                            logits.ctypes.data_as(P_F))
     abi_tps = args.abi_steps / (time.perf_counter() - t2) if args.abi_steps > 0 else 0.0
     log(f'ABI decode (host state {state_len * 4 / 1e6:.1f} MB each way): {abi_tps:.1f} tok/s')
+    # the same calls with page-locked state / logits buffers (torch pin_memory): the library then
+    # streams the state per layer beside the decode chain (engine.hip eval_host_pipelined)
+    abi_pinned_tps = 0.0
+    if args.abi_steps > 0:
+        try:
+            pst = torch.zeros(state_len, dtype=torch.float32).pin_memory()
+            plg = torch.zeros(n_vocab, dtype=torch.float32).pin_memory()
+            pp, pl = ctypes.cast(pst.data_ptr(), P_F), ctypes.cast(plg.data_ptr(), P_F)
+            L.rwkv_init_state(ctx.ptr, pp)
+            for i in range(2):
+                assert L.rwkv_eval(ctx.ptr, int(dec_tokens[i]), pp, pp, pl)
+            t2 = time.perf_counter()
+            for i in range(args.abi_steps):
+                assert L.rwkv_eval(ctx.ptr, int(dec_tokens[i % len(dec_tokens)]), pp, pp, pl)
+            abi_pinned_tps = args.abi_steps / (time.perf_counter() - t2)
+            log(f'ABI decode, page-locked host state: {abi_pinned_tps:.1f} tok/s')
+        except Exception as e:
+            log(f'ABI decode (page-locked) failed: {e!r}')
 
     # ---------------- kernel timing (HIP events on the context stream) ----------------
     def read_stats():
@@ -420,6 +438,7 @@ def main():
                          'ms_per_sequence': round(seq_s * 1e3, 3), 'parallelism': f'replicas x{world}',
                          'pipeline': pipe},
             'abi_decode_tokens_per_s': round(abi_tps * world, 2),
+            'abi_decode_pinned_tokens_per_s': round(abi_pinned_tps * world, 2),
             'batched_decode': {'what': 'B independent contexts, one token each per step, weights read once per '
                                        'step (rwkv_mi355x_eval_batch_device; bit-exact to per-context rwkv_eval)',
                                'parallelism': f'replicas x{world}', 'runs': batch},

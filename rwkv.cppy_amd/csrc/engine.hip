@@ -351,6 +351,10 @@ Engine::~Engine() {
     if (stream_) (void)hipStreamSynchronize(stream_);
     stamp_dump();
     drop_graphs();
+    drop_io_graphs();
+    for (hipStream_t s : io_stream_)
+        if (s) (void)hipStreamDestroy(s);
+    for (hipEvent_t e : io_ev_) (void)hipEventDestroy(e);
     drop_batch_graphs();
     for (float * p : bstate_)
         if (p) (void)hipFree(p);
@@ -388,6 +392,10 @@ bool Engine::init() {
     generic_decode_ = gd && gd[0] == '1';
     const char * um = getenv("RWKV_MI355X_SEQ_MATVEC");  // sequence matmuls on k_mm (comparison)
     use_mm_ = um && um[0] == '1';
+    const char * io = getenv("RWKV_MI355X_STATE_PIPELINE");  // 0: host state copied whole (comparison)
+    io_pipeline_ = !(io && io[0] == '0');
+    const char * ic = getenv("RWKV_MI355X_IO_CHUNK");  // layers per chunk graph (host-state decode)
+    io_chunk_ = ic ? std::max(1, atoi(ic)) : 4;
     const char * sm = getenv("RWKV_MI355X_SPLIT_MAA");  // v6 decode: W1 and mix as two launches (comparison)
     split_maa_ = sm && sm[0] == '1';
     // the fused decode prologues hold LayerNorm inputs in registers up to n_embed 4096
@@ -408,6 +416,7 @@ bool Engine::ensure_workspace(int T) {
     HIP_OK(hipStreamSynchronize(stream_));
     drop_graphs();
     drop_batch_graphs();
+    drop_io_graphs();
     // keep state and logits, drop the rest; until every allocation below has succeeded the
     // workspace counts as absent (tcap_ = 0, pointers null), so a failed grow can never leave a
     // capacity that points at freed or missing buffers
@@ -1213,11 +1222,13 @@ static void src_f32(MVEntry & e, const float * f) {
 //   v6: W1+LN (1) -> mix5 (1) -> r,k,v,g,Wd1 (1) -> decay tail+wkv+GN (1) -> Wo (1) -> FFN k,r+LN (1) -> FFN v (1)
 //   v5: r,k,v,g+LN (1) -> wkv+GN (1) -> Wo (1) -> FFN (2)      v4: r,k,v+LN (1) -> wkv4 (1) -> Wo (1) -> FFN (2)
 //   v7: r,k,v,LoRA-in+LN (1) -> LoRA-out (1) -> prep+wkv7+GN (1) -> Wo (1) -> FFN (2)
-bool Engine::forward_decode(const float * sin, float * sout, bool logits) {
+// Layers [l0, l1) (embedding when l0 == 0, head when l1 == n_layer and logits).
+bool Engine::forward_decode(const float * sin, float * sout, bool logits, uint32_t l0, uint32_t l1) {
     const int C = (int)m_->n_embed, H = (int)m_->H, S = (int)m_->S;
-    if (!launch_embed_ln(stream_, dtokens_, 1, m_->emb, m_->ln0_w, m_->ln0_b, x_)) return false;
+    l1 = std::min(l1, m_->n_layer);
+    if (l0 == 0 && !launch_embed_ln(stream_, dtokens_, 1, m_->emb, m_->ln0_w, m_->ln0_b, x_)) return false;
     const size_t per_layer = m_->major >= 5 ? (size_t)C * (2 + (size_t)S) : 5 * (size_t)C;
-    for (uint32_t l = 0; l < m_->n_layer; l++) {
+    for (uint32_t l = l0; l < l1; l++) {
         const DLayer & L = m_->layers[l];
         const float * si = sin + l * per_layer;
         float * so = sout + l * per_layer;
@@ -1403,7 +1414,7 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits) {
             if (!mv(c.g)) return false;
         }
     }
-    if (logits) {
+    if (logits && l1 == m_->n_layer) {
         MV h;
         src_lnmix(h.add(m_->head, logits_, EPI_STORE), x_, nullptr, m_->lnout_w, m_->lnout_b, nullptr, 2);
         if (!mv(h.g)) return false;
@@ -1495,8 +1506,112 @@ bool Engine::sync() {
     return true;
 }
 
+// ---------------------------------------------------------------- ABI decode with host state
+// rwkv_eval's contract hands the whole recurrent state over as host buffers on every call
+// (rwkv_eval.inc:2-22): 13 MB each way for v6-1B6, ~0.5 ms of PCIe against a 0.82 ms decode.
+// The decode runs as io_chunk_-layer graphs instead of one, so the copies of one chunk's state
+// slice overlap the other chunks' kernels: the host uploads chunk c+1 (copy stream 0) while the
+// GPU runs chunk c, and downloads chunk c-1 (copy stream 1) while the GPU runs chunk c.  This
+// works for ordinary pageable buffers too: a pageable hipMemcpyAsync holds the HOST until its
+// bytes are staged, but the chunk graphs are already queued, so the GPU keeps computing.  The
+// bytes moved and every result are exactly those of the one-graph path.
+bool Engine::eval_host_chunked(uint32_t token, const float * state_in, float * state_out, float * logits_out) {
+    const uint32_t NL = m_->n_layer, K = (uint32_t)io_chunk_, NC = (NL + K - 1) / K;
+    const size_t C = m_->n_embed, per_layer = m_->major >= 5 ? C * (2 + (size_t)m_->S) : 5 * C;
+    if (!ensure_workspace(1)) return false;
+    if (!io_stream_[0]) {
+        for (auto & st : io_stream_) HIP_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    }
+    if (io_ev_.size() < 2 * (size_t)NC) {
+        for (hipEvent_t e : io_ev_) (void)hipEventDestroy(e);
+        io_ev_.assign(2 * NC, nullptr);
+        for (auto & e : io_ev_) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    const bool lg = logits_out != nullptr;
+    std::vector<hipGraphExec_t> & gs = io_graphs_[cur_][lg ? 1 : 0];
+    if (gs.size() != NC) {
+        for (hipGraphExec_t g : gs)
+            if (g) (void)hipGraphExecDestroy(g);
+        gs.assign(NC, nullptr);
+    }
+    float * din = dstate_[cur_], * dout = dstate_[cur_ ^ 1];
+    for (uint32_t c = 0; c < NC; c++) {
+        if (gs[c]) continue;
+        hipGraph_t g = nullptr;
+        HIP_OK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
+        const bool ok = forward_decode(din, dout, lg, c * K, (c + 1) * K);
+        HIP_OK(hipStreamEndCapture(stream_, &g));
+        if (!ok) {
+            (void)hipGraphDestroy(g);
+            return false;
+        }
+        HIP_OK(hipGraphInstantiate(&gs[c], g, nullptr, nullptr, 0));
+        (void)hipGraphDestroy(g);
+    }
+    auto slice = [&](uint32_t c, size_t & off, size_t & bytes) {
+        const uint32_t l0 = c * K, l1 = std::min(NL, l0 + K);
+        off = l0 * per_layer;
+        bytes = (l1 - l0) * per_layer * 4;
+    };
+    hipEvent_t * in_ev = io_ev_.data(), * done_ev = io_ev_.data() + NC;
+    size_t off, bytes;
+    HIP_OK(hipStreamWriteValue32(stream_, dtokens_, token, 0));
+    if (state_in) {
+        slice(0, off, bytes);
+        HIP_OK(hipMemcpyAsync(din + off, state_in + off, bytes, hipMemcpyHostToDevice, io_stream_[0]));
+        HIP_OK(hipEventRecord(in_ev[0], io_stream_[0]));
+    } else if (!init_state(din)) {
+        return false;
+    }
+    for (uint32_t c = 0; c < NC; c++) {
+        if (state_in) HIP_OK(hipStreamWaitEvent(stream_, in_ev[c], 0));
+        HIP_OK(hipGraphLaunch(gs[c], stream_));
+        HIP_OK(hipEventRecord(done_ev[c], stream_));
+        if (state_in && c + 1 < NC) {
+            slice(c + 1, off, bytes);
+            HIP_OK(hipMemcpyAsync(din + off, state_in + off, bytes, hipMemcpyHostToDevice, io_stream_[0]));
+            HIP_OK(hipEventRecord(in_ev[c + 1], io_stream_[0]));
+        }
+        if (state_out && c >= 1) {
+            slice(c - 1, off, bytes);
+            HIP_OK(hipStreamWaitEvent(io_stream_[1], done_ev[c - 1], 0));
+            HIP_OK(hipMemcpyAsync(state_out + off, dout + off, bytes, hipMemcpyDeviceToHost, io_stream_[1]));
+        }
+    }
+    if (state_out) {
+        slice(NC - 1, off, bytes);
+        HIP_OK(hipStreamWaitEvent(io_stream_[1], done_ev[NC - 1], 0));
+        HIP_OK(hipMemcpyAsync(state_out + off, dout + off, bytes, hipMemcpyDeviceToHost, io_stream_[1]));
+    }
+    if (logits_out)
+        HIP_OK(hipMemcpyAsync(logits_out, logits_, (size_t)m_->n_vocab * 4, hipMemcpyDeviceToHost, stream_));
+    HIP_OK(hipStreamSynchronize(io_stream_[1]));
+    HIP_OK(hipStreamSynchronize(io_stream_[0]));
+    HIP_OK(hipStreamSynchronize(stream_));
+    cur_ ^= 1;
+    return true;
+}
+
+void Engine::drop_io_graphs() {
+    for (auto & p : io_graphs_)
+        for (auto & v : p) {
+            for (hipGraphExec_t g : v)
+                if (g) (void)hipGraphExecDestroy(g);
+            v.clear();
+        }
+}
+
 bool Engine::eval(const uint32_t * tokens, size_t T, const float * state_in, float * state_out, float * logits_out) {
     HIP_OK(hipSetDevice(m_->device));
+    // one token with host state: chunked decode, copies overlapped (needs graphs; timing and the
+    // generic decode path keep the whole-state copies)
+    if (T == 1 && io_pipeline_ && use_graphs_ && !timing_ && !generic_decode_ && (state_in || state_out)) {
+        const int cur0 = cur_;
+        if (eval_host_chunked(tokens[0], state_in, state_out, logits_out)) return true;
+        (void)hipStreamSynchronize(stream_);
+        cur_ = cur0;
+        return false;
+    }
     if (!state_upload(state_in)) return false;
     if (!run_tokens(tokens, T, logits_out != nullptr)) return false;
     if (logits_out)

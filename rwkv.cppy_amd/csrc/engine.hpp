@@ -109,7 +109,7 @@ class Engine {
     bool init_state(float * st);
     bool forward(int T, const float * sin, float * sout, bool logits);
     bool forward_range(int T, const float * sin, float * sout, uint32_t l0, uint32_t l1, bool logits);
-    bool forward_decode(const float * sin, float * sout, bool logits);
+    bool forward_decode(const float * sin, float * sout, bool logits, uint32_t l0 = 0, uint32_t l1 = UINT32_MAX);
     bool mv(MVGroup & g);
     bool run_tokens(const uint32_t * tokens, size_t T, bool want_logits);
     bool run_tokens_impl(const uint32_t * tokens, size_t T, bool want_logits);
@@ -179,6 +179,15 @@ class Engine {
     };
     std::vector<BatchGraph> bgraphs_;
     void drop_batch_graphs();
+    // rwkv_eval with host state buffers: the decode as io_chunk_-layer graphs with the state
+    // copies of other chunks overlapped (eval_host_chunked)
+    bool io_pipeline_ = true;
+    int io_chunk_ = 4;
+    hipStream_t io_stream_[2] = {nullptr, nullptr};
+    std::vector<hipEvent_t> io_ev_;
+    std::vector<hipGraphExec_t> io_graphs_[2][2];  // [cur][logits] per chunk
+    bool eval_host_chunked(uint32_t token, const float * state_in, float * state_out, float * logits_out);
+    void drop_io_graphs();
     void drop_graphs();
     std::vector<Pending> pending_;
     std::vector<hipEvent_t> event_pool_;

@@ -60,7 +60,7 @@ def main():
     ap.add_argument('--timing-steps', type=int, default=8)
     ap.add_argument('--cpu-seconds', type=float, default=12.0)
     ap.add_argument('--skip-cpu', action='store_true')
-    ap.add_argument('--batch', default='8,32,64', help='batched decode sizes (contexts per step; "" = none)')
+    ap.add_argument('--batch', default='8,32,64,128', help='batched decode sizes (contexts per step; "" = none)')
     ap.add_argument('--batch-steps', type=int, default=32)
     ap.add_argument('--model-dir', default=os.environ.get('RWKV_BENCH_DIR', '/tmp/rwkv_bench'))
     args = ap.parse_args()

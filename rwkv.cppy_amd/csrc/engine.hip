@@ -394,6 +394,8 @@ bool Engine::init() {
     use_mm_ = um && um[0] == '1';
     const char * io = getenv("RWKV_MI355X_STATE_PIPELINE");  // 0: host state copied whole (comparison)
     io_pipeline_ = !(io && io[0] == '0');
+    const char * bg = getenv("RWKV_MI355X_BATCH_GEMM_MIN");  // contexts from which batches use the GEMM
+    batch_gemm_min_ = bg ? std::max(2, atoi(bg)) : 48;
     const char * ic = getenv("RWKV_MI355X_IO_CHUNK");  // layers per chunk graph (host-state decode)
     io_chunk_ = ic ? std::max(1, atoi(ic)) : 4;
     const char * sm = getenv("RWKV_MI355X_SPLIT_MAA");  // v6 decode: W1 and mix as two launches (comparison)
@@ -584,8 +586,9 @@ void Engine::set_timing(bool on) {
 // a scratch y, and emission is a separate quantization pass (same bits as k_mm's epilogue).
 bool Engine::mm_dispatch(MMGroup & g, int wtype) {
     // batched decode (bs_ > 0): the decode matvec over the contexts (k_mvb; k_mm for shapes it
-    // does not cover -- the same bits)
-    if (bs_) {
+    // does not cover -- the same bits); from batch_gemm_min_ contexts on, the quantized matmuls
+    // take the int8-MFMA sequence GEMM on token tiles instead (tile_acts_; also the same bits)
+    if (bs_ && !(tile_acts_ && wtype_quantized(wtype))) {
         bool launched = false;
         if (!launch_mvb_group(stream_, g, wtype, &launched)) return false;
         if (launched) return true;
@@ -597,6 +600,7 @@ bool Engine::mm_dispatch(MMGroup & g, int wtype) {
         if (!g.e[i].y) need += (size_t)g.T * g.e[i].W.M;
     if (need > gy_cap_) {
         HIP_OK(hipStreamSynchronize(stream_));
+        drop_batch_graphs();  // captured batched steps point at the old scratch
         if (gy_) (void)hipFree(gy_);
         gy_ = nullptr;
         gy_cap_ = 0;
@@ -612,6 +616,7 @@ bool Engine::mm_dispatch(MMGroup & g, int wtype) {
         const size_t pneed = (size_t)8 * g.T * g.e[0].W.M;
         if (pneed > part_cap_) {
             HIP_OK(hipStreamSynchronize(stream_));
+            drop_batch_graphs();
             if (part_) (void)hipFree(part_);
             part_ = nullptr;
             part_cap_ = 0;
@@ -660,9 +665,9 @@ bool Engine::mm_launch(MMGroup & g, int wtype) {
         flops += 2.0 * e.W.M * e.W.K * g.T;
     }
     // kernel class = the template instantiation rocprofv3 reports: k_mm<WF, RPW, NT>
-    const bool mfma = g.T >= 2 && wtype_quantized(wtype) && !use_mm_ && !bs_;
-    const std::string name = bs_ ? "k_mvb<" + std::to_string(wtype) + ">"
-                           : mfma ? "k_qgemm<" + std::to_string(wtype) + ">"
+    const bool mfma = g.T >= 2 && wtype_quantized(wtype) && !use_mm_ && (!bs_ || tile_acts_);
+    const std::string name = mfma ? "k_qgemm<" + std::to_string(wtype) + ">"
+                           : bs_ ? "k_mvb<" + std::to_string(wtype) + ">"
                                   : "k_mm<" + std::to_string(wtype) + ", " + (emit ? "8" : "2") + ", " + (g.T == 1 ? "1" : "4") + ">";
     const int si = add_stat(name);
     hipEvent_t a, b;
@@ -1064,7 +1069,7 @@ bool Engine::forward_range(int T, const float * sin, float * sout, uint32_t l0, 
     if (l0 == 0 && !launch_embed_ln(stream_, dtokens_, T, m_->emb, m_->ln0_w, m_->ln0_b, x_)) return false;
     const size_t per_layer = m_->major >= 5 ? C * (2 + (size_t)m_->S) : 5 * C;
     // layer matmuls run over all T tokens: Q8 activations go straight into GEMM tiles
-    tile_acts_ = T >= 2 && !use_mm_ && !bs_;
+    tile_acts_ = T >= 2 && !use_mm_ && (!bs_ || T >= batch_gemm_min_);
     for (uint32_t l = l0; l < l1; l++) {
         const float * si = sin + l * per_layer;
         float * so = sout + l * per_layer;
@@ -1751,6 +1756,17 @@ bool Engine::eval_batch(const uint32_t * tokens, size_t B, const float * state_i
         for (const BatchGraph & g : bgraphs_)
             if (g.B == B && g.sin == sin && g.sout == sout && g.lout == (lg ? lout : nullptr)) ge = g.ge;
         if (!ge) {
+            // first step with these buffers: run it eagerly (lazy GEMM scratch allocations happen
+            // here, outside any capture), then capture the graph the next steps replay
+            bs_ = n;
+            head_out_ = lout;
+            ok = forward_range((int)B, sin, sout, 0, m_->n_layer, lg);
+            bs_ = 0;
+            head_out_ = nullptr;
+            if (!ok) {
+                (void)hipStreamSynchronize(stream_);
+                return false;
+            }
             if (bgraphs_.size() >= 8) drop_batch_graphs();
             hipGraph_t g = nullptr;
             HIP_OK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
@@ -1767,8 +1783,9 @@ bool Engine::eval_batch(const uint32_t * tokens, size_t B, const float * state_i
             HIP_OK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
             (void)hipGraphDestroy(g);
             bgraphs_.push_back(BatchGraph{B, sin, sout, lg ? lout : nullptr, ge});
+        } else {
+            HIP_OK(hipGraphLaunch(ge, stream_));
         }
-        HIP_OK(hipGraphLaunch(ge, stream_));
         ok = true;
     } else {
         bs_ = n;

@@ -119,10 +119,10 @@ def cfg_dir(tmp_path_factory):
 
 
 @pytest.mark.parametrize('name', sorted(CONFIGS))
-@pytest.mark.parametrize('B', [8, 40])
+@pytest.mark.parametrize('B', [8, 56])
 def test_batch_real_width_bit_exact(cfg_dir, name, B):
     """BASELINE widths (2 layers, 4096-token vocabulary); B = 8 (decode matvec over the contexts)
-    and B = 40 (past batch_gemm_min_: the int8-MFMA GEMM on token tiles)."""
+    and B = 56 (past batch_gemm_min_ = 48: the int8-MFMA GEMM on token tiles)."""
     arch, C, F, fmt = CONFIGS[name]
     p = os.path.join(str(cfg_dir), f'{name}.bin')
     if not os.path.isfile(p):

@@ -198,7 +198,141 @@ static bool launch_mm_wf(hipStream_t st, MMGroup & g) {
     return true;
 }
 
+// --------------------------------------------------------------------------- small-K matmul
+// F16 / F32 weights whose rows fit one unit per lane of k_mm (K <= 512 halves / 256 floats: the v7
+// LoRA second stages, K = 64..480), T >= 2.  k_mm gives each output a whole wave, most of whose
+// lanes hold no unit (K = 96: 12 of 64) and then a 6-step DPP reduction.  Here one THREAD computes
+// one output: the lane partials p[l] = dot over unit l (k_mm's per-lane arithmetic, from 0) and
+// wave_sum63's perfect binary tree over them.  Lanes without a unit contribute +0, and a partial
+// is never -0 (every chain starts from +0), so the zero leaves change no bit and the tree is
+// folded only over the NL leading leaves (NL = the next power of two): results equal k_mm's.
+// Workgroup = 64 rows (one per lane) x MMS_TB tokens (waves take every 4th token); the rows'
+// weights and the tokens' activations are staged in LDS.
+constexpr int MMS_TB = 32;
+
+template <int WF>
+__device__ __forceinline__ float small_leaf(const char * wrow, const char * xrow, int l, int nl) {
+    float p = 0.0f;
+    if (l < nl) {
+        const int4 w = *(const int4 *)(wrow + 16 * l), x = *(const int4 *)(xrow + 16 * l);
+        if constexpr (WF == W_F16) {
+            p = dot8_f16(w, x, 0.0f);
+        } else {
+            p = fmaf(__int_as_float(w.x), __int_as_float(x.x), p);
+            p = fmaf(__int_as_float(w.y), __int_as_float(x.y), p);
+            p = fmaf(__int_as_float(w.z), __int_as_float(x.z), p);
+            p = fmaf(__int_as_float(w.w), __int_as_float(x.w), p);
+        }
+    }
+    return p;
+}
+
+// Leaves in groups of 8 (a perfect 8-leaf tree each), the groups folded as they are produced (a
+// binary counter: lv[k] holds the pending left subtree of 8 * 2^k leaves) -- the same perfect
+// binary tree over NL leaves with few live registers.
+template <int WF, int NL>
+__device__ __forceinline__ float small_row_dot(const char * wrow, const char * xrow, int nl) {
+    float lv[3];
+    float v = 0.0f;
+#pragma unroll 1
+    for (int g = 0; g < NL / 8; g++) {
+        float p[8];
+#pragma unroll
+        for (int l = 0; l < 8; l++) p[l] = small_leaf<WF>(wrow, xrow, 8 * g + l, nl);
+        v = ((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7]));
+#pragma unroll
+        for (int k = 0; (8 << k) < NL; k++) {
+            if (g & (1 << k)) {
+                v = lv[k] + v;
+            } else {
+                lv[k] = v;
+                break;
+            }
+        }
+    }
+    return v;  // the last group closed every level: the root
+}
+
+template <int WF>
+__global__ __launch_bounds__(256) void k_mm_small(MMGroup g, int wstride) {
+    extern __shared__ __attribute__((aligned(16))) char sm[];
+    int e = 0;
+#pragma unroll 1
+    while (e + 1 < g.n && (int)blockIdx.x >= g.e[e + 1].block0) e++;
+    const MMEntry & E = g.e[e];
+    const int M = E.W.M, K = E.W.K, T = g.T;
+    constexpr int ES = WF == W_F16 ? 2 : 4;       // element bytes
+    const int rowb = K * ES, nl = rowb / 16;       // bytes per row, units (lanes of k_mm)
+    const int row0 = ((int)blockIdx.x - E.block0) * 64, t0 = (int)blockIdx.y * MMS_TB;
+    char * ws = sm;                                // [64][wstride]
+    char * xs = sm + 64 * wstride;                 // [MMS_TB][rowb]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const char * wg = (const char *)E.W.qs;
+    const char * xg = (const char *)(WF == W_F16 ? (const void *)E.in.h : (const void *)E.in.f);
+    for (int i = tid; i < 64 * nl; i += 256) {
+        const int r = i / nl, u = i % nl;
+        const int row = min(row0 + r, M - 1);
+        *(int4 *)(ws + r * wstride + 16 * u) = *(const int4 *)(wg + (size_t)row * rowb + 16 * u);
+    }
+    for (int i = tid; i < MMS_TB * nl; i += 256) {
+        const int t = i / nl, u = i % nl;
+        const int tt = min(t0 + t, T - 1);
+        *(int4 *)(xs + t * rowb + 16 * u) = *(const int4 *)(xg + (size_t)tt * rowb + 16 * u);
+    }
+    __syncthreads();
+    const int row = row0 + lane;
+    const char * wrow = ws + lane * wstride;
+    for (int tl = wave; tl < MMS_TB; tl += 4) {
+        const int t = t0 + tl;
+        if (t >= T) break;  // wave-uniform
+        const char * xrow = xs + tl * rowb;
+        float s;
+        if (nl <= 8) s = small_row_dot<WF, 8>(wrow, xrow, nl);
+        else if (nl <= 16) s = small_row_dot<WF, 16>(wrow, xrow, nl);
+        else if (nl <= 32) s = small_row_dot<WF, 32>(wrow, xrow, nl);
+        else s = small_row_dot<WF, 64>(wrow, xrow, nl);
+        // k_mm: red + red2 (red2 = 0 for float weights)
+        const float acc = s + 0.0f;
+        float v = 0.0f;
+        if (row < M) {
+            v = apply_epi(E, t, row, acc);
+            if (E.y) E.y[(size_t)t * E.ldy + row] = v;
+        }
+        // a half-wave = 32 consecutive rows of token t (M % 32 == 0 when emitting)
+        if (E.emit && row0 + (lane & 32) < M) emit32(E.out, t, row, v);
+    }
+}
+
+// true (and launched) when every entry is an F16 / F32 matrix with one unit per k_mm lane
+static bool launch_mm_small(hipStream_t st, MMGroup & g, int wtype) {
+    if (g.T < 2 || (wtype != W_F16 && wtype != W_F32)) return false;
+    const int ES = wtype == W_F16 ? 2 : 4;
+    int blocks = 0, kmax = 0;
+    for (int i = 0; i < g.n; i++) {
+        const MMEntry & e = g.e[i];
+        if (e.W.type != wtype || e.W.K * ES > 1024 || (e.W.K * ES) % 16 || e.in.fmt != act_fmt_for(wtype) ||
+            (e.emit && e.W.M % 32))
+            return false;
+        kmax = std::max(kmax, e.W.K);
+    }
+    for (int i = 0; i < g.n; i++) {
+        g.e[i].block0 = blocks;
+        blocks += (g.e[i].W.M + 63) / 64;
+    }
+    const int wstride = kmax * ES + 16;  // padded row: 16-byte reads of 16 lanes spread over banks
+    const size_t lds = (size_t)64 * wstride + (size_t)MMS_TB * kmax * ES;
+    const dim3 grid(blocks, (g.T + MMS_TB - 1) / MMS_TB);
+    if (wtype == W_F16) hipLaunchKernelGGL(k_mm_small<W_F16>, grid, dim3(256), lds, st, g, wstride);
+    else hipLaunchKernelGGL(k_mm_small<W_F32>, grid, dim3(256), lds, st, g, wstride);
+    return hipGetLastError() == hipSuccess;
+}
+
 bool launch_mm_group(hipStream_t st, MMGroup & g, int wtype) {
+    static const bool small_on = [] {
+        const char * v = getenv("RWKV_MI355X_MM_SMALL");  // 0: small-K float matmuls on k_mm too
+        return !(v && v[0] == '0');
+    }();
+    if (small_on && launch_mm_small(st, g, wtype)) return true;
     switch (wtype) {
         case W_F32: return launch_mm_wf<W_F32>(st, g);
         case W_F16: return launch_mm_wf<W_F16>(st, g);

@@ -278,14 +278,16 @@ __device__ __forceinline__ void decay_rows(const Att6Dec & a, const ActBuf & act
 // each state load/store instruction covers S consecutive floats.  The per-thread partial y
 // sums meet in LDS and are folded with group_sum's butterfly tree, so decode and sequence
 // agree bit for bit.  PF > 0: quantized decay LoRA with <= PF units per row, prefetched.
-template <int WF, int PF>
+// SS = 64: head size 64 at compile time (straight-line state loop, constant store offsets);
+// SS = 0: any head size from a.S.
+template <int WF, int PF, int SS>
 __global__ __launch_bounds__(256) void k_att6_dec(Att6Dec a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ __attribute__((aligned(16))) float sr[64], sk[64], sv[64], sw[64], su[64];
     __shared__ float part[16][64];
-    const int h = blockIdx.x, S = a.S, G = min(256 / S, S), IPG = S / G;
+    const int h = blockIdx.x, S = SS ? SS : a.S, G = SS ? 256 / SS : min(256 / S, S), IPG = S / G;
     const int tid = threadIdx.x, j = tid % S, g = min(tid / S, G - 1), c0 = h * S;
-    const bool active = tid < S * G;
+    const bool active = SS ? true : tid < S * G;  // SS: the block is exactly S * G threads
     const size_t hb = (size_t)h * S * S;
     // batched decode: context blockIdx.y (its [C] vectors, decay LoRA row and state); 0 in decode
     const int bz = blockIdx.y;
@@ -296,10 +298,6 @@ __global__ __launch_bounds__(256) void k_att6_dec(Att6Dec a) {
     const float * asin = a.sin + (size_t)bz * a.bs;
     float * asout = a.sout + (size_t)bz * a.bs;
     STAMP_BEGIN();
-    float st[16];
-#pragma unroll
-    for (int ii = 0; ii < 16; ii++)
-        st[ii] = ii < IPG && active ? asin[hb + (size_t)(g * IPG + ii) * S + j] : 0.0f;
     WBlk wp[PF > 0 ? PF : 1];
     if constexpr (PF > 0) {
         const int nb = a.wd2.K >> 5;
@@ -313,21 +311,36 @@ __global__ __launch_bounds__(256) void k_att6_dec(Att6Dec a) {
     const float lnw_c = a.lnx_w[cme], lnb_c = a.lnx_b[cme];
     const float g_c = ag ? ag[cme] : 1.0f;
     const float dec_c = a.w ? 0.0f : a.decay[cme];
+    const float r_c = ar[cme], k_c = ak[cme], v_c = av[cme], u_c = a.u[cme];
+    const float w_c = a.w ? a.w[cme] : 0.0f;
+    const bool dlo = WF != -2 && !a.w;
+    float dl_c = 0.0f;
+    if (dlo && tid < a.wd2.K) dl_c = adl[tid];
+    // the state columns last: the operand loads above retire first (in-order vmcnt), so the
+    // decay tail below runs while the state is still in flight
+    float st[16];
+#pragma unroll
+    for (int ii = 0; ii < 16; ii++)
+        st[ii] = ii < IPG && active ? asin[hb + (size_t)(g * IPG + ii) * S + j] : 0.0f;
     if (tid < S) {
-        sr[tid] = ar[c0 + tid];
-        sk[tid] = ak[c0 + tid];
-        sv[tid] = av[c0 + tid];
-        su[tid] = a.u[c0 + tid];
-        if (a.w) sw[tid] = a.w[c0 + tid];
+        sr[tid] = r_c;
+        sk[tid] = k_c;
+        sv[tid] = v_c;
+        su[tid] = u_c;
+        if (a.w) sw[tid] = w_c;
     }
     ActBuf act;
-    if (WF != -2 && !a.w) {
+    if (dlo) {
         // v6 decay LoRA tail: w = exp(-exp(Wd2 . dl + decay)), rwkv_graph.inc:357-367
         const int D = a.wd2.K;
         act = lds_act(smem, act_fmt_for(a.wd2.type), D);
-        for (int k0 = 0; k0 < D; k0 += blockDim.x) {
-            if (k0 + (tid & ~31) >= D) continue;
-            emit32(act, 0, k0 + tid, adl[k0 + tid]);
+        if (PF > 0 || D <= (int)blockDim.x) {  // PF > 0: D <= 32 * PF
+            if ((tid & ~31) < D) emit32(act, 0, tid, dl_c);
+        } else {
+            for (int k0 = 0; k0 < D; k0 += blockDim.x) {
+                if (k0 + (tid & ~31) >= D) continue;
+                emit32(act, 0, k0 + tid, adl[k0 + tid]);
+            }
         }
     }
     __syncthreads();
@@ -447,19 +460,26 @@ bool launch_att6_dec(hipStream_t st, const Att6Dec & a) {
     }
     dim3 grid(a.H, a.nb > 1 ? a.nb : 1), block(std::max(threads, 64));
     const bool pf = !a.w && a.wd2.type >= W_Q4_0 && (a.wd2.K >> 5) <= 4;
+    const bool s64 = a.S == 64;
+#define ATT6(WFv, PFv)                                                                         \
+    do {                                                                                       \
+        if (s64) hipLaunchKernelGGL((k_att6_dec<WFv, PFv, 64>), grid, block, lds, st, a);      \
+        else hipLaunchKernelGGL((k_att6_dec<WFv, PFv, 0>), grid, block, lds, st, a);           \
+    } while (0)
     if (a.w) {
-        hipLaunchKernelGGL((k_att6_dec<-2, 0>), grid, block, lds, st, a);  // v5: no decay LoRA
+        ATT6(-2, 0);  // v5: no decay LoRA
     } else if (!pf) {
-        hipLaunchKernelGGL((k_att6_dec<-1, 0>), grid, block, lds, st, a);
+        ATT6(-1, 0);
     } else {
         switch (a.wd2.type) {
-            case W_Q4_0: hipLaunchKernelGGL((k_att6_dec<W_Q4_0, 4>), grid, block, lds, st, a); break;
-            case W_Q4_1: hipLaunchKernelGGL((k_att6_dec<W_Q4_1, 4>), grid, block, lds, st, a); break;
-            case W_Q5_0: hipLaunchKernelGGL((k_att6_dec<W_Q5_0, 4>), grid, block, lds, st, a); break;
-            case W_Q5_1: hipLaunchKernelGGL((k_att6_dec<W_Q5_1, 4>), grid, block, lds, st, a); break;
-            default: hipLaunchKernelGGL((k_att6_dec<W_Q8_0, 4>), grid, block, lds, st, a); break;
+            case W_Q4_0: ATT6(W_Q4_0, 4); break;
+            case W_Q4_1: ATT6(W_Q4_1, 4); break;
+            case W_Q5_0: ATT6(W_Q5_0, 4); break;
+            case W_Q5_1: ATT6(W_Q5_1, 4); break;
+            default: ATT6(W_Q8_0, 4); break;
         }
     }
+#undef ATT6
     HIP_OK(hipGetLastError());
     return true;
 }

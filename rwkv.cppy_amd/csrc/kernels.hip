@@ -682,9 +682,76 @@ __global__ __launch_bounds__(256) void k_wkv4(int T, int C, const float * r, con
     sout[4 * C + c] = pp;
 }
 
+// Sequence form (T > 1, one context): the same per-channel recurrence, one wave per 64 channels.
+// The k / v / r rows of the next WKV4_TT tokens are loaded while the current ones are computed
+// (the recurrence's dependent chain no longer waits on a load round trip per token), and the
+// outputs of a chunk are emitted after its recurrence steps, off the chain.  Per channel and
+// token the operations are k_wkv4's, in its order, so decode and sequence stay bit-identical.
+constexpr int WKV4_TT = 16;
+__global__ __launch_bounds__(64) void k_wkv4_seq(int T, int C, const float * r, const float * k, const float * v,
+                                                 const float * first, const float * decay, const float * sin,
+                                                 float * sout, ActBuf out) {
+    const int c = blockIdx.x * 64 + threadIdx.x;
+    const int cl = min(c, C - 1);
+    float aa = sin[2 * C + cl], bb = sin[3 * C + cl], pp = sin[4 * C + cl];
+    const float fi = first[cl], de = decay[cl];
+    float kn[WKV4_TT], vn[WKV4_TT], rn[WKV4_TT];
+    auto load = [&](int t0) {
+#pragma unroll
+        for (int tt = 0; tt < WKV4_TT; tt++) {
+            const size_t i = (size_t)min(t0 + tt, T - 1) * C + cl;
+            kn[tt] = k[i];
+            vn[tt] = v[i];
+            rn[tt] = r[i];
+        }
+    };
+    load(0);
+#pragma unroll 1
+    for (int t0 = 0; t0 < T; t0 += WKV4_TT) {
+        float kc[WKV4_TT], vc[WKV4_TT], rc[WKV4_TT], y[WKV4_TT];
+#pragma unroll
+        for (int tt = 0; tt < WKV4_TT; tt++) kc[tt] = kn[tt], vc[tt] = vn[tt], rc[tt] = rn[tt];
+        if (t0 + WKV4_TT < T) load(t0 + WKV4_TT);
+        const int n = min(WKV4_TT, T - t0);
+#pragma unroll
+        for (int tt = 0; tt < WKV4_TT; tt++) {
+            if (tt < n) {  // uniform
+                const float kt = kc[tt], vt = vc[tt];
+                float ww = fi + kt;
+                float qq = fmaxf(pp, ww);
+                float e1 = rk_expf(pp - qq), e2 = rk_expf(ww - qq);
+                const float an = e1 * aa + e2 * vt;
+                const float bn = e1 * bb + e2;
+                ww = pp + de;
+                qq = fmaxf(ww, kt);
+                e1 = rk_expf(ww - qq);
+                e2 = rk_expf(kt - qq);
+                aa = e1 * aa + e2 * vt;
+                bb = e1 * bb + e2;
+                pp = qq;
+                y[tt] = rc[tt] * (an / bn);
+            }
+        }
+#pragma unroll
+        for (int tt = 0; tt < WKV4_TT; tt++)
+            if (tt < n) emit32(out, t0 + tt, c, y[tt]);
+    }
+    if (c < C) {
+        sout[2 * C + c] = aa;
+        sout[3 * C + c] = bb;
+        sout[4 * C + c] = pp;
+    }
+}
+
 bool launch_wkv4(hipStream_t st, int T, int C, const float * r, const float * k, const float * v,
                  const float * first, const float * decay, const float * state_in, float * state_out,
                  const ActBuf & out, int bs) {
+    if (T > 1 && !bs && C % 64 == 0) {  // whole waves of channels
+        hipLaunchKernelGGL(k_wkv4_seq, dim3((C + 63) / 64), dim3(64), 0, st, T, C, r, k, v, first, decay, state_in,
+                           state_out, out);
+        HIP_OK(hipGetLastError());
+        return true;
+    }
     hipLaunchKernelGGL(k_wkv4, dim3((C + 255) / 256, bs ? T : 1), dim3(256), 0, st, T, C, r, k, v, first, decay,
                        state_in, state_out, out, bs);
     HIP_OK(hipGetLastError());

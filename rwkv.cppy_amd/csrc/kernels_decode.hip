@@ -554,35 +554,38 @@ __global__ __launch_bounds__(256) void k_att7_dec(Att7Dec a) {
     const size_t cb = (size_t)bz * a.H * S;
     const float * asin = a.sin + (size_t)bz * a.bs;
     float * asout = a.sout + (size_t)bz * a.bs;
-    // state rows and the GroupNorm epilogue operands are loaded first: no dependent round trip
-    // behind the barriers
+    // the per-channel operands (prep and GroupNorm epilogue) are loaded first and the state rows
+    // after them: the prep below waits only for the operands (in-order vmcnt) while the state is
+    // still in flight, and nothing is a dependent round trip behind the barriers
     const bool wact = tid < S * G;
     const int wi = min(tid / G, S - 1), wg = tid % G;
     const size_t wbase = (size_t)h * S * S + (size_t)wi * S + wg * JPG;
+    const int cme = c0 + min(tid, S - 1);
+    const float lnw_c = a.lnx_w[cme], lnb_c = a.lnx_b[cme], g_c = a.g[cb + cme];
+    const float k_c = a.k[cb + cme], kk_c = a.k_k[cme], a_c = a.a[cb + cme], ka_c = a.k_a[cme];
+    const float r_c = a.r[cb + cme], w_c = a.w[cb + cme], v_c = a.v[cb + cme], rk_c = a.r_k[cme];
+    __builtin_amdgcn_sched_barrier(0);  // keep the state loads behind the operand loads
     float st[JPG];
 #pragma unroll
     for (int jj = 0; jj < JPG; jj++) st[jj] = asin[wbase + jj];
-    const int cme = c0 + min(tid, S - 1);
-    const float lnw_c = a.lnx_w[cme], lnb_c = a.lnx_b[cme], g_c = a.g[cb + cme];
     if (tid < S) {
         // prep (rwkv_graph.inc:432-437 + rwkv_operators.inc:40-82)
-        const int c = c0 + tid;
-        const float kv = a.k[cb + c];
-        const float kkr = kv * a.k_k[c];
+        const float kv = k_c;
+        const float kkr = kv * kk_c;
         const float sum = group_sum(kkr * kkr, S);
         const float scale = 1.0f / fmaxf(sqrtf(sum), 1e-12f);
         const float kk = kkr * scale;
-        const float av = a.a[cb + c];
-        const float ka = kv * a.k_a[c];
+        const float av = a_c;
+        const float ka = kv * ka_c;
         const float kadj = kv + (av * ka - ka);
-        const float rv = a.r[cb + c];
+        const float rv = r_c;
         sr[tid] = rv;
-        sw[tid] = a.w[cb + c];
+        sw[tid] = w_c;
         sk[tid] = kadj;
-        sv[tid] = a.v[cb + c];
+        sv[tid] = v_c;
         snb[tid] = -kk;
         sbb[tid] = kk * av;
-        const float bs = group_sum((kadj * rv) * a.r_k[c], S);
+        const float bs = group_sum((kadj * rv) * rk_c, S);
         if (tid == 0) sbonus = bs;
     }
     __syncthreads();

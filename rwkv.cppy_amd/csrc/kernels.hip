@@ -891,7 +891,7 @@ __global__ __launch_bounds__(64 * NWV) void k_wkv6_s64(int T, int H, const float
     // #(tid & 15) of tokens (tid >> 4) + (NT/16) qq, qq < QQ; v: CW columns = NWV float4 per
     // token, threads < WKV6_TC*NWV move float4 #(tid % NWV) of token tid / NWV
     float4 pk[QQ], pr[QQ], pw[WPT ? QQ : 1], pv;
-    auto load_chunk = [&](int t0) {
+    auto load_chunk = [&](int t0) __attribute__((always_inline)) {
 #pragma unroll
         for (int qq = 0; qq < QQ; qq++) {
             const int t = min(t0 + (tid >> 4) + (NT / 16) * qq, T - 1);
@@ -904,7 +904,7 @@ __global__ __launch_bounds__(64 * NWV) void k_wkv6_s64(int T, int H, const float
         const int t = min(t0 + tv / NWV, T - 1);
         pv = *(const float4 *)(v + (size_t)t * C + (size_t)h * S + jb * CW + 4 * (tv % NWV));
     };
-    auto store_chunk = [&]() {
+    auto store_chunk = [&]() __attribute__((always_inline)) {
 #pragma unroll
         for (int qq = 0; qq < QQ; qq++) {
             const int tt = (tid >> 4) + (NT / 16) * qq;
@@ -918,7 +918,7 @@ __global__ __launch_bounds__(64 * NWV) void k_wkv6_s64(int T, int H, const float
         f2_t k[2], r[2], w[2];
         float v;
     };
-    auto read_tok = [&](Tok & o, int tt) {
+    auto read_tok = [&](Tok & o, int tt) __attribute__((always_inline)) {
         const float4 a = *(const float4 *)&sk[tt][i0];
         const float4 b = *(const float4 *)&sr[tt][i0];
         o.k[0] = f2_t{a.x, a.y}, o.k[1] = f2_t{a.z, a.w};
@@ -940,7 +940,7 @@ __global__ __launch_bounds__(64 * NWV) void k_wkv6_s64(int T, int H, const float
         constexpr int TG = 4;
         static_assert(2 * TG <= WKV6_PAD, "look-ahead rows");
         // FULL: a whole chunk (n == WKV6_TC), every token valid
-        auto group = [&](const Tok (&o)[TG], int tt0, auto full) {
+        auto group = [&](const Tok (&o)[TG], int tt0, auto full) __attribute__((always_inline)) {
             constexpr bool FULL = decltype(full)::value;
             f2_t x[TG][2];
 #pragma unroll
@@ -1140,8 +1140,13 @@ __global__ void k_wkv7(int T, int H, int S, int G, const float * r, const float 
 
 // Head size 64: one wave per (head, 16 value rows i), grid (H, 4); lane (g = lane >> 4, il =
 // lane & 15) owns row i = 16*blockIdx.y + il, keys j in [16g, 16g+16) -- k_wkv7's / k_att7_dec's
-// split and arithmetic with the same 4-group folds -- with 32-token chunks of r, w, k, a, b
-// (and v) staged in LDS, the next chunk's loads in flight.
+// split and arithmetic with the same 4-group folds.  r, w, k, a, b (and v) come in 16-token chunks
+// staged in a double-buffered LDS tile: the next chunk moves in two 8-token pieces, each loaded
+// into registers at the start of an 8-token block of the current chunk and stored to the other
+// buffer at its end (44 registers in flight instead of a whole chunk, which spilled to scratch),
+// and the 8 tokens of a block are unrolled so the compiler overlaps one token's output chain with
+// the next token's operand reads and state chain.
+constexpr int WKV7_TC = 16, WKV7_PB = 8;
 __global__ __launch_bounds__(64) void k_wkv7_s64(int T, int H, const float * r, const float * w, const float * k,
                                                  const float * v, const float * a, const float * b,
                                                  const float * sin, float * sout, float * y, int bs) {
@@ -1153,8 +1158,8 @@ __global__ __launch_bounds__(64) void k_wkv7_s64(int T, int H, const float * r, 
         sout += (size_t)blockIdx.z * bs;
         T = 1;
     }
-    __shared__ __attribute__((aligned(16))) float sr[WKV_TC][S], sw[WKV_TC][S], sk[WKV_TC][S], sa_[WKV_TC][S],
-        sb[WKV_TC][S], sv[WKV_TC][16];
+    __shared__ __attribute__((aligned(16))) float sr[2][WKV7_TC][S], sw[2][WKV7_TC][S], sk[2][WKV7_TC][S],
+        sa_[2][WKV7_TC][S], sb[2][WKV7_TC][S], sv[2][WKV7_TC][16];
     const int h = blockIdx.x, ib = blockIdx.y, lane = threadIdx.x;
     const int il = lane & 15, g = lane >> 4, i = ib * 16 + il;
     const int C = H * S;
@@ -1162,76 +1167,100 @@ __global__ __launch_bounds__(64) void k_wkv7_s64(int T, int H, const float * r, 
     float st[16];
 #pragma unroll
     for (int jj = 0; jj < 16; jj++) st[jj] = sin[hb + jj];
-    float4 p[5][8], pv[2];
-    const float * src[5] = {r, w, k, a, b};
-    auto load_chunk = [&](int t0) {
+    // piece PC (tokens 8 PC .. 8 PC + 7) of the chunk at T0: lane moves float4 #(lane & 15) of
+    // tokens (lane >> 4) + 4 e of the five key-indexed rows, lanes < 32 one float4 of v
+    float4 q00, q01, q10, q11, q20, q21, q30, q31, q40, q41, qv;  // scalars: arrays went to scratch
+    const int c4 = 4 * (lane & 15);
+#define WKV7_LD(T0, PC, E, A0, A1, A2, A3, A4)                                                            \
+    do {                                                                                                  \
+        const int t = min((T0) + WKV7_PB * (PC) + (lane >> 4) + 4 * (E), T - 1);                          \
+        const size_t base = (size_t)t * C + (size_t)h * S + c4;                                           \
+        A0 = *(const float4 *)(r + base);                                                                 \
+        A1 = *(const float4 *)(w + base);                                                                 \
+        A2 = *(const float4 *)(k + base);                                                                 \
+        A3 = *(const float4 *)(a + base);                                                                 \
+        A4 = *(const float4 *)(b + base);                                                                 \
+    } while (0)
+#define WKV7_LOADP(T0, PC)                                                                                \
+    do {                                                                                                  \
+        WKV7_LD(T0, PC, 0, q00, q10, q20, q30, q40);                                                      \
+        WKV7_LD(T0, PC, 1, q01, q11, q21, q31, q41);                                                      \
+        const int tv = min((T0) + WKV7_PB * (PC) + ((lane & 31) >> 2), T - 1);                            \
+        qv = *(const float4 *)(v + (size_t)tv * C + (size_t)h * S + ib * 16 + 4 * (lane & 3));            \
+    } while (0)
+#define WKV7_ST(BUF, PC, E, A0, A1, A2, A3, A4)                                                           \
+    do {                                                                                                  \
+        const int tt = WKV7_PB * (PC) + (lane >> 4) + 4 * (E);                                            \
+        *(float4 *)&sr[BUF][tt][c4] = A0;                                                                 \
+        *(float4 *)&sw[BUF][tt][c4] = A1;                                                                 \
+        *(float4 *)&sk[BUF][tt][c4] = A2;                                                                 \
+        *(float4 *)&sa_[BUF][tt][c4] = A3;                                                                \
+        *(float4 *)&sb[BUF][tt][c4] = A4;                                                                 \
+    } while (0)
+#define WKV7_STOREP(BUF, PC)                                                                              \
+    do {                                                                                                  \
+        WKV7_ST(BUF, PC, 0, q00, q10, q20, q30, q40);                                                     \
+        WKV7_ST(BUF, PC, 1, q01, q11, q21, q31, q41);                                                     \
+        if (lane < 32) *(float4 *)&sv[BUF][WKV7_PB * (PC) + (lane >> 2)][4 * (lane & 3)] = qv;            \
+    } while (0)
+    WKV7_LOADP(0, 0);
+    WKV7_STOREP(0, 0);
+    WKV7_LOADP(0, 1);
+    WKV7_STOREP(0, 1);
+    __syncthreads();
+    int buf = 0;
+    for (int t0 = 0; t0 < T; t0 += WKV7_TC) {
+        const int n = min(WKV7_TC, T - t0);
+        const bool nx = t0 + WKV7_TC < T;
 #pragma unroll
-        for (int q = 0; q < 8; q++) {
-            const int t = min(t0 + (lane >> 4) + 4 * q, T - 1);
-            const size_t base = (size_t)t * C + (size_t)h * S + 4 * (lane & 15);
+        for (int pc = 0; pc < WKV7_TC / WKV7_PB; pc++) {
+            if (nx) WKV7_LOADP(t0 + WKV7_TC, pc);
 #pragma unroll
-            for (int s = 0; s < 5; s++) p[s][q] = *(const float4 *)(src[s] + base);
-        }
+            for (int e = 0; e < WKV7_PB; e++) {
+                const int tt = WKV7_PB * pc + e;
+                if (tt < n) {  // uniform
+                    float aa[16];
 #pragma unroll
-        for (int q = 0; q < 2; q++) {
-            const int t = min(t0 + (lane >> 2) + 16 * q, T - 1);
-            pv[q] = *(const float4 *)(v + (size_t)t * C + (size_t)h * S + ib * 16 + 4 * (lane & 3));
-        }
-    };
-    auto store_chunk = [&]() {
+                    for (int q = 0; q < 4; q++) {
+                        const float4 x = *(const float4 *)&sa_[buf][tt][g * 16 + 4 * q];
+                        aa[4 * q] = x.x, aa[4 * q + 1] = x.y, aa[4 * q + 2] = x.z, aa[4 * q + 3] = x.w;
+                    }
+                    float sa = 0.0f;
 #pragma unroll
-        for (int q = 0; q < 8; q++) {
-            const int tt = (lane >> 4) + 4 * q, c4 = 4 * (lane & 15);
-            *(float4 *)&sr[tt][c4] = p[0][q];
-            *(float4 *)&sw[tt][c4] = p[1][q];
-            *(float4 *)&sk[tt][c4] = p[2][q];
-            *(float4 *)&sa_[tt][c4] = p[3][q];
-            *(float4 *)&sb[tt][c4] = p[4][q];
-        }
+                    for (int jj = 0; jj < 16; jj++) sa += aa[jj] * st[jj];
+                    sa = fold_g4(sa);
+                    const float vi = sv[buf][tt][il];
+                    float acc = 0.0f;
 #pragma unroll
-        for (int q = 0; q < 2; q++) *(float4 *)&sv[(lane >> 2) + 16 * q][4 * (lane & 3)] = pv[q];
-    };
-    load_chunk(0);
-    for (int t0 = 0; t0 < T; t0 += WKV_TC) {
-        store_chunk();
-        __syncthreads();
-        if (t0 + WKV_TC < T) load_chunk(t0 + WKV_TC);
-        const int n = min(WKV_TC, T - t0);
-        for (int tt = 0; tt < n; tt++) {
-            float aa[16];
+                    for (int q = 0; q < 4; q++) {
+                        const float4 kq = *(const float4 *)&sk[buf][tt][g * 16 + 4 * q];
+                        const float4 wq = *(const float4 *)&sw[buf][tt][g * 16 + 4 * q];
+                        const float4 bq = *(const float4 *)&sb[buf][tt][g * 16 + 4 * q];
+                        const float4 rq = *(const float4 *)&sr[buf][tt][g * 16 + 4 * q];
+                        const float kk[4] = {kq.x, kq.y, kq.z, kq.w}, ww[4] = {wq.x, wq.y, wq.z, wq.w};
+                        const float bb[4] = {bq.x, bq.y, bq.z, bq.w}, rr[4] = {rq.x, rq.y, rq.z, rq.w};
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const float4 x = *(const float4 *)&sa_[tt][g * 16 + 4 * q];
-                aa[4 * q] = x.x, aa[4 * q + 1] = x.y, aa[4 * q + 2] = x.z, aa[4 * q + 3] = x.w;
-            }
-            float sa = 0.0f;
-#pragma unroll
-            for (int jj = 0; jj < 16; jj++) sa += aa[jj] * st[jj];
-            sa = fold_g4(sa);
-            const float vi = sv[tt][il];
-            float acc = 0.0f;
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const float4 kq = *(const float4 *)&sk[tt][g * 16 + 4 * q];
-                const float4 wq = *(const float4 *)&sw[tt][g * 16 + 4 * q];
-                const float4 bq = *(const float4 *)&sb[tt][g * 16 + 4 * q];
-                const float4 rq = *(const float4 *)&sr[tt][g * 16 + 4 * q];
-                const float kk[4] = {kq.x, kq.y, kq.z, kq.w}, ww[4] = {wq.x, wq.y, wq.z, wq.w};
-                const float bb[4] = {bq.x, bq.y, bq.z, bq.w}, rr[4] = {rq.x, rq.y, rq.z, rq.w};
-#pragma unroll
-                for (int e = 0; e < 4; e++) {
-                    const int jj = 4 * q + e;
-                    const float kv = vi * kk[e];
-                    const float ns = st[jj] * ww[e] + kv + sa * bb[e];
-                    st[jj] = ns;
-                    acc += ns * rr[e];
+                        for (int e2 = 0; e2 < 4; e2++) {
+                            const int jj = 4 * q + e2;
+                            const float kv = vi * kk[e2];
+                            const float ns = st[jj] * ww[e2] + kv + sa * bb[e2];
+                            st[jj] = ns;
+                            acc += ns * rr[e2];
+                        }
+                    }
+                    acc = fold_g4(acc);
+                    if (g == 0) y[(size_t)(t0 + tt) * C + (size_t)h * S + i] = acc;
                 }
             }
-            acc = fold_g4(acc);
-            if (g == 0) y[(size_t)(t0 + tt) * C + (size_t)h * S + i] = acc;
+            if (nx) WKV7_STOREP(buf ^ 1, pc);
         }
         __syncthreads();
+        buf ^= 1;
     }
+#undef WKV7_LD
+#undef WKV7_ST
+#undef WKV7_LOADP
+#undef WKV7_STOREP
 #pragma unroll
     for (int jj = 0; jj < 16; jj++) sout[hb + jj] = st[jj];
 }

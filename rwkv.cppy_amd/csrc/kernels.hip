@@ -890,30 +890,53 @@ __global__ __launch_bounds__(64 * NWV) void k_wkv6_s64(int T, int H, const float
     // chunk staging: k/r/w rows of 64 floats = 16 float4 per token; thread moves float4
     // #(tid & 15) of tokens (tid >> 4) + (NT/16) qq, qq < QQ; v: CW columns = NWV float4 per
     // token, threads < WKV6_TC*NWV move float4 #(tid % NWV) of token tid / NWV
-    float4 pk[QQ], pr[QQ], pw[WPT ? QQ : 1], pv;
+    // QQ == 4 (4 waves, the default): the chunk's rows in named registers -- as arrays they are
+    // kept in scratch
+    float4 pk[QQ == 4 ? 1 : QQ], pr[QQ == 4 ? 1 : QQ], pw[WPT && QQ != 4 ? QQ : 1], pv;
+    float4 k0, k1, k2, k3, r0, r1, r2, r3, w0, w1, w2, w3;
+#define WKV6_LD(QI, KV, RV, WV)                                                                           \
+    do {                                                                                                  \
+        const int t = min(t0 + (tid >> 4) + (NT / 16) * (QI), T - 1);                                     \
+        const size_t base = (size_t)t * C + (size_t)h * S + 4 * (tid & 15);                               \
+        KV = *(const float4 *)(k + base);                                                                 \
+        RV = *(const float4 *)(r + base);                                                                 \
+        if constexpr (WPT) WV = *(const float4 *)(w + base);                                              \
+    } while (0)
+#define WKV6_ST(QI, KV, RV, WV)                                                                           \
+    do {                                                                                                  \
+        const int tt = (tid >> 4) + (NT / 16) * (QI);                                                     \
+        *(float4 *)&sk[tt][4 * (tid & 15)] = KV;                                                          \
+        *(float4 *)&sr[tt][4 * (tid & 15)] = RV;                                                          \
+        if constexpr (WPT) *(float4 *)&sw[tt][4 * (tid & 15)] = WV;                                       \
+    } while (0)
     auto load_chunk = [&](int t0) __attribute__((always_inline)) {
+        if constexpr (QQ == 4) {
+            WKV6_LD(0, k0, r0, w0);
+            WKV6_LD(1, k1, r1, w1);
+            WKV6_LD(2, k2, r2, w2);
+            WKV6_LD(3, k3, r3, w3);
+        } else {
 #pragma unroll
-        for (int qq = 0; qq < QQ; qq++) {
-            const int t = min(t0 + (tid >> 4) + (NT / 16) * qq, T - 1);
-            const size_t base = (size_t)t * C + (size_t)h * S + 4 * (tid & 15);
-            pk[qq] = *(const float4 *)(k + base);
-            pr[qq] = *(const float4 *)(r + base);
-            if constexpr (WPT) pw[qq] = *(const float4 *)(w + base);
+            for (int qq = 0; qq < QQ; qq++) WKV6_LD(qq, pk[qq], pr[qq], pw[qq]);
         }
         const int tv = min(tid, WKV6_TC * NWV - 1);
         const int t = min(t0 + tv / NWV, T - 1);
         pv = *(const float4 *)(v + (size_t)t * C + (size_t)h * S + jb * CW + 4 * (tv % NWV));
     };
     auto store_chunk = [&]() __attribute__((always_inline)) {
+        if constexpr (QQ == 4) {
+            WKV6_ST(0, k0, r0, w0);
+            WKV6_ST(1, k1, r1, w1);
+            WKV6_ST(2, k2, r2, w2);
+            WKV6_ST(3, k3, r3, w3);
+        } else {
 #pragma unroll
-        for (int qq = 0; qq < QQ; qq++) {
-            const int tt = (tid >> 4) + (NT / 16) * qq;
-            *(float4 *)&sk[tt][4 * (tid & 15)] = pk[qq];
-            *(float4 *)&sr[tt][4 * (tid & 15)] = pr[qq];
-            if constexpr (WPT) *(float4 *)&sw[tt][4 * (tid & 15)] = pw[qq];
+            for (int qq = 0; qq < QQ; qq++) WKV6_ST(qq, pk[qq], pr[qq], pw[qq]);
         }
         if (tid < WKV6_TC * NWV) *(float4 *)&sv[tid / NWV][4 * (tid % NWV)] = pv;
     };
+#undef WKV6_LD
+#undef WKV6_ST
     struct Tok {
         f2_t k[2], r[2], w[2];
         float v;

@@ -208,7 +208,7 @@ static bool launch_mm_wf(hipStream_t st, MMGroup & g) {
 // folded only over the NL leading leaves (NL = the next power of two): results equal k_mm's.
 // Workgroup = 64 rows (one per lane) x MMS_TB tokens (waves take every 4th token); the rows'
 // weights and the tokens' activations are staged in LDS.
-constexpr int MMS_TB = 32;
+constexpr int MMS_TB = 16;
 
 template <int WF>
 __device__ __forceinline__ float small_leaf(const char * wrow, const char * xrow, int l, int nl) {
@@ -269,13 +269,15 @@ __global__ __launch_bounds__(256) void k_mm_small(MMGroup g, int wstride) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const char * wg = (const char *)E.W.qs;
     const char * xg = (const char *)(WF == W_F16 ? (const void *)E.in.h : (const void *)E.in.f);
+    // (row, unit) of flat index i: i / nl through a float reciprocal (exact: i < 2^12, nl <= 64)
+    const float rnl = 1.0f / (float)nl;
     for (int i = tid; i < 64 * nl; i += 256) {
-        const int r = i / nl, u = i % nl;
+        const int r = (int)(((float)i + 0.5f) * rnl), u = i - r * nl;
         const int row = min(row0 + r, M - 1);
         *(int4 *)(ws + r * wstride + 16 * u) = *(const int4 *)(wg + (size_t)row * rowb + 16 * u);
     }
     for (int i = tid; i < MMS_TB * nl; i += 256) {
-        const int t = i / nl, u = i % nl;
+        const int t = (int)(((float)i + 0.5f) * rnl), u = i - t * nl;
         const int tt = min(t0 + t, T - 1);
         *(int4 *)(xs + t * rowb + 16 * u) = *(const int4 *)(xg + (size_t)tt * rowb + 16 * u);
     }

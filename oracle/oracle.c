@@ -1381,9 +1381,18 @@ static void layer_v6(const oracle_model * m, const olayer * L, float * x, int64_
             for (int64_t c = 0; c < C; c++) {
                 const float * w2 = L->maa_w2 + ((size_t)n * C + c) * D;
                 const float * lv = lora + t * D5 + n * D;
-                double acc = 0.0;
-                for (int64_t i = 0; i < D; i++) acc += (double)(w2[i] * lv[i]);
-                const float mval = (float)acc;
+                float mval;
+                if (g_variant & OV_GPU) {
+                    /* GPU association (k_v6_mix5 / k_v6_mix5_dec / k_v6_maa_dec): one fp32 fma
+                       chain over i in order, like ggml's SIMD vec_dot_f32 lanes (fp32 fma) */
+                    float a = 0.0f;
+                    for (int64_t i = 0; i < D; i++) a = fmaf(w2[i], lv[i], a);
+                    mval = a;
+                } else {
+                    double acc = 0.0;
+                    for (int64_t i = 0; i < D; i++) acc += (double)(w2[i] * lv[i]);
+                    mval = (float)acc;
+                }
                 xs[n][t * C + c] = (mval + L->maa[n][c]) * sx[t * C + c] + xa[t * C + c];
             }
     mm(L->att_r, xs[3], T, r);

@@ -442,28 +442,47 @@ __global__ __launch_bounds__(1024) void k_ln_mix(LnMixArgs a) {
     const float * xt = a.x + (size_t)t * C;
     const float mean = s_mean[tg + 1], scale = s_scale[tg + 1];
     const float pmean = t > 0 ? s_mean[tg] : 0.0f, pscale = t > 0 ? s_scale[tg] : 0.0f;
-    // channel blocks of 256 split over grid.y (short sequences / batched decode: more workgroups)
-    for (int c0 = (int)blockIdx.y * 256; c0 < C; c0 += (int)gridDim.y * 256) {
-        const int c = c0 + tid;
-        if (c0 + (tid & ~63) >= C) continue;  // whole wave out of range (C % 64 == 0)
-        const float xa = ln_apply(xt[c], mean, scale, a.lnw[c], a.lnb[c]);
-        // batch (a.bs > 0): every token is its own context, shifted against its own carry
-        const float xp = a.bs ? a.carry_in[(size_t)t * a.bs + c]
-                              : (t > 0) ? ln_apply(xt[c - C], pmean, pscale, a.lnw[c], a.lnb[c]) : a.carry_in[c];
-        if (a.bs && a.carry_out) a.carry_out[(size_t)t * a.bs + c] = xa;
-        else if (t == a.T - 1 && a.carry_out) a.carry_out[c] = xa;
-        if (a.out_xa) a.out_xa[(size_t)t * C + c] = xa;
-        if (a.out_sx) a.out_sx[(size_t)t * C + c] = xp - xa;
-        for (int n = 0; n < a.n_out; n++) {
-            const float mu = a.mu[n][c];
-            float v;
-            if (a.form == 0) {
-                v = xa * mu + (xp - xp * mu);
-            } else {
-                v = (xp - xa) * mu + xa;
+    // channel blocks of 256 split over grid.y (short sequences / batched decode: more workgroups);
+    // LNM_CB blocks at a time: all their loads are issued before the first store
+    constexpr int LNM_CB = TQ > 0 ? 4 : 2;  // (4 spills in the runtime-format emit)
+    const int cstride = (int)gridDim.y * 256;
+    const int nmu = min(a.n_out, 6);
+    for (int cb0 = (int)blockIdx.y * 256; cb0 < C; cb0 += LNM_CB * cstride) {
+        float xv[LNM_CB], pv[LNM_CB], wv[LNM_CB], bv[LNM_CB], muv[LNM_CB][6];
+#pragma unroll
+        for (int j = 0; j < LNM_CB; j++) {
+            const int c = min(cb0 + j * cstride + tid, C - 1);
+            xv[j] = xt[c];
+            wv[j] = a.lnw[c];
+            bv[j] = a.lnb[c];
+            // batch (a.bs > 0): every token is its own context, shifted against its own carry
+            pv[j] = a.bs ? a.carry_in[(size_t)t * a.bs + c] : (t > 0) ? xt[c - C] : a.carry_in[c];
+#pragma unroll
+            for (int n = 0; n < 6; n++) muv[j][n] = n < nmu ? a.mu[n][c] : 0.0f;
+        }
+#pragma unroll
+        for (int j = 0; j < LNM_CB; j++) {
+            const int c0 = cb0 + j * cstride, c = c0 + tid;
+            if (c0 + (tid & ~63) >= C) continue;  // whole wave out of range (C % 64 == 0)
+            const float xa = ln_apply(xv[j], mean, scale, wv[j], bv[j]);
+            const float xp = (a.bs || t == 0) ? pv[j] : ln_apply(pv[j], pmean, pscale, wv[j], bv[j]);
+            if (a.bs && a.carry_out) a.carry_out[(size_t)t * a.bs + c] = xa;
+            else if (t == a.T - 1 && a.carry_out) a.carry_out[c] = xa;
+            if (a.out_xa) a.out_xa[(size_t)t * C + c] = xa;
+            if (a.out_sx) a.out_sx[(size_t)t * C + c] = xp - xa;
+#pragma unroll
+            for (int n = 0; n < 6; n++) {
+                if (n >= nmu) break;
+                const float mu = muv[j][n];
+                float v;
+                if (a.form == 0) {
+                    v = xa * mu + (xp - xp * mu);
+                } else {
+                    v = (xp - xa) * mu + xa;
+                }
+                if constexpr (TQ > 0) emit32_tile<TQ>(a.out[n].tq, C, t, c, v);
+                else emit32(a.out[n], t, c, v);
             }
-            if constexpr (TQ > 0) emit32_tile<TQ>(a.out[n].tq, C, t, c, v);
-            else emit32(a.out[n], t, c, v);
         }
     }
 }
@@ -510,94 +529,89 @@ struct Mix5Args {
     ActBuf out[5];
 };
 
-// Workgroup = 256 channels x MIX_TT tokens: each thread holds its channel's W2 column for all five
-// mixes in registers (read once per token tile instead of once per token) and the tile's lora rows
-// sit in LDS; per token the five D-long fp64 sums (k_v6_mix5_dec's order: sequential over i) run
-// side by side.
-constexpr int MIX_TT8 = 8;  // token tile of long sequences (1 for short ones: more workgroups)
+// Workgroup = 64 channels x 5 mixes x MIX_TT tokens, wave n = mixed vector n (w, k, v, r, g):
+// each lane holds its channel's W2 column of that mix in registers (D floats, read once per token
+// tile); the tile's lora rows sit in LDS as [mix][i][token], so one 16-byte broadcast read gives
+// the i-th lora value of 4 tokens.  Per token the D-long fp32 fma chain runs in k_v6_mix5_dec's
+// order (sequential over i); 4 tokens' chains run side by side.  ~70 VGPRs: 6+ waves per SIMD.
+constexpr int MIX_TT = 16;
 
 // TQ > 0: all five outputs are Q8 sequence-GEMM token tiles (TQ = 2: Q8_1); each lane's record
 // address is formed once (a workgroup's MIX_TT tokens lie in one QG_TOK-token tile) and the
 // per-output emission is quant32 + store (store32's tiled values), no runtime format dispatch.
-template <int DM, int TQ, int MIX_TT>
-__global__ __launch_bounds__(256) void k_v6_mix5(Mix5Args a) {
-    __shared__ __attribute__((aligned(16))) float sl[MIX_TT][5 * DM];
-    const int C = a.C, D = a.D, T = a.T;
-    const int tid = threadIdx.x, c = blockIdx.x * blockDim.x + tid;
-    const bool cval = (int)(blockIdx.x * blockDim.x + (tid & ~31)) < C;  // half-wave uniform
+template <int DM, int TQ, bool EXACT>
+__global__ __launch_bounds__(320) void k_v6_mix5(Mix5Args a) {
+    static_assert(QG_TOK % MIX_TT == 0 && MIX_TT % 4 == 0, "mix5 token tile");
+    __shared__ __attribute__((aligned(16))) float sl[5][DM][MIX_TT];
+    const int C = a.C, D = EXACT ? DM : a.D, T = a.T;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int n = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // this wave's mix: operands selected with compile-time indices (no dynamic kernarg indexing)
+    const float * maa_n = a.maa[0];
+    ActBuf out_n = a.out[0];
+#pragma unroll
+    for (int m = 1; m < 5; m++)
+        if (n == m) {
+            maa_n = a.maa[m];
+            out_n = a.out[m];
+        }
+    const int c = blockIdx.x * 64 + lane;
+    const bool cval = (int)(blockIdx.x * 64 + (lane & ~31)) < C;  // half-wave uniform
     const int cc = min(c, C - 1);
     const int t0 = blockIdx.y * MIX_TT, nt = min(MIX_TT, T - t0);
-    for (int e = tid; e < MIX_TT * 5 * DM; e += 256) {
-        const int tt = e / (5 * DM), f = e % (5 * DM), n = f / DM, i = f % DM;
-        sl[tt][f] = (tt < nt && i < D) ? a.lora[(size_t)(t0 + tt) * 5 * D + n * D + i] : 0.0f;
+    for (int e = tid; e < 5 * DM * MIX_TT; e += 320) {
+        const int tt = e / (5 * DM), f = e % (5 * DM), m = f / DM, i = f % DM;  // coalesced reads
+        sl[m][i][tt] = (tt < nt && i < D) ? a.lora[(size_t)(t0 + tt) * 5 * D + m * D + i] : 0.0f;
     }
-    float w2v[5][DM], mu[5];
+    float w2v[DM];
+    const float mu = maa_n[cc];
 #pragma unroll
-    for (int n = 0; n < 5; n++) {
-        mu[n] = a.maa[n][cc];
-#pragma unroll
-        for (int i = 0; i < DM; i++) {
-            const float t = a.w2[((size_t)n * D + min(i, D - 1)) * C + cc];   // transposed [5][D][C]
-            w2v[n][i] = i < D ? t : 0.0f;
-        }
+    for (int i = 0; i < DM; i++) {
+        const float t = a.w2[((size_t)n * D + min(i, D - 1)) * C + cc];  // transposed [5][D][C]
+        w2v[i] = i < D ? t : 0.0f;
     }
-    uint8_t * rec[5];
+    uint8_t * rec = nullptr;
     int qoff = 0;
     if constexpr (TQ > 0) {
         // record of (token tile t0 / QG_TOK, block c / 32); byte of element c in half (c >> 4) & 1
         const size_t ri = (size_t)(t0 / QG_TOK) * (C >> 5) + (cc >> 5);
-#pragma unroll
-        for (int n = 0; n < 5; n++) rec[n] = a.out[n].tq + ri * qg_a_bytes(TQ == 2);
+        rec = out_n.tq + ri * qg_a_bytes(TQ == 2);
         qoff = ((cc >> 4) & 1) * QG_TOK * 16 + (cc & 15);
     }
     __syncthreads();
-    // two tokens at a time: ten independent fp64 chains side by side
-    for (int tt = 0; tt < nt; tt += 2) {
-        const int t1 = min(tt + 1, nt - 1);
-        const size_t ti0 = (size_t)(t0 + tt) * C + cc, ti1 = (size_t)(t0 + t1) * C + cc;
-        const float xa0 = a.xa[ti0], sx0 = a.sx[ti0], xa1 = a.xa[ti1], sx1 = a.sx[ti1];
-        double acc0[5] = {0.0, 0.0, 0.0, 0.0, 0.0}, acc1[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+    for (int tt = 0; tt < nt; tt += 4) {
+        float xa[4], sx[4], acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const size_t ti = (size_t)(t0 + min(tt + j, nt - 1)) * C + cc;
+            xa[j] = a.xa[ti];
+            sx[j] = a.sx[ti];
+        }
 #pragma unroll
         for (int i = 0; i < DM; i++) {
-            if (i < D) {
-#pragma unroll
-                for (int n = 0; n < 5; n++) {
-                    acc0[n] += (double)(w2v[n][i] * sl[tt][n * DM + i]);
-                    acc1[n] += (double)(w2v[n][i] * sl[t1][n * DM + i]);
-                }
+            if (EXACT || i < D) {
+                const float4 l = *(const float4 *)&sl[n][i][tt];
+                acc[0] = fmaf(w2v[i], l.x, acc[0]);
+                acc[1] = fmaf(w2v[i], l.y, acc[1]);
+                acc[2] = fmaf(w2v[i], l.z, acc[2]);
+                acc[3] = fmaf(w2v[i], l.w, acc[3]);
             }
         }
-        if constexpr (TQ > 0) {
-            if (cval) {
-                Q32 q0[5], q1[5];
+        if (!cval) continue;
 #pragma unroll
-                for (int n = 0; n < 5; n++) {
-                    q0[n] = quant32(((float)acc0[n] + mu[n]) * sx0 + xa0);
-                    q1[n] = quant32(((float)acc1[n] + mu[n]) * sx1 + xa1);
+        for (int j = 0; j < 4; j++) {
+            if (tt + j >= nt) break;
+            const float v = (acc[j] + mu) * sx[j] + xa[j];
+            if constexpr (TQ > 0) {
+                const Q32 q = quant32(v);
+                const int tl = (t0 + tt + j) % QG_TOK;
+                rec[qoff + tl * 16] = (uint8_t)(int8_t)q.q;
+                if ((c & 31) == 0) {
+                    ((float *)(rec + QG_A_D))[tl] = f16_round(q.d);
+                    if constexpr (TQ == 2) ((float *)(rec + QG_A_S))[tl] = f16_round(q.d * (float)q.sum);
                 }
-                const int tl0 = (t0 + tt) % QG_TOK, tl1 = (t0 + t1) % QG_TOK;
-#pragma unroll
-                for (int n = 0; n < 5; n++) {
-                    rec[n][qoff + tl0 * 16] = (uint8_t)(int8_t)q0[n].q;
-                    if (tt + 1 < nt) rec[n][qoff + tl1 * 16] = (uint8_t)(int8_t)q1[n].q;
-                    if ((c & 31) == 0) {
-                        float * dp = (float *)(rec[n] + QG_A_D);
-                        dp[tl0] = f16_round(q0[n].d);
-                        if (tt + 1 < nt) dp[tl1] = f16_round(q1[n].d);
-                        if constexpr (TQ == 2) {
-                            float * sp = (float *)(rec[n] + QG_A_S);
-                            sp[tl0] = f16_round(q0[n].d * (float)q0[n].sum);
-                            if (tt + 1 < nt) sp[tl1] = f16_round(q1[n].d * (float)q1[n].sum);
-                        }
-                    }
-                }
-            }
-        } else if (cval) {
-#pragma unroll
-            for (int n = 0; n < 5; n++) emit32(a.out[n], t0 + tt, c, ((float)acc0[n] + mu[n]) * sx0 + xa0);
-            if (tt + 1 < nt) {
-#pragma unroll
-                for (int n = 0; n < 5; n++) emit32(a.out[n], t0 + tt + 1, c, ((float)acc1[n] + mu[n]) * sx1 + xa1);
+            } else {
+                emit32(out_n, t0 + tt + j, c, v);
             }
         }
     }
@@ -621,8 +635,7 @@ bool launch_v6_mix5(hipStream_t st, int T, int C, int D, const float * lora, con
         fprintf(stderr, "rwkv: v6 maa LoRA width %d / n_embed %d unsupported\n", D, C);
         return false;
     }
-    const int tt = T <= 64 ? 1 : MIX_TT8;
-    const dim3 grid((C + 255) / 256, (T + tt - 1) / tt);
+    const dim3 grid((C + 63) / 64, (T + MIX_TT - 1) / MIX_TT);
     int tq = 0;
     {
         bool all = true;
@@ -631,10 +644,10 @@ bool launch_v6_mix5(hipStream_t st, int T, int C, int D, const float * lora, con
                   (outs[n].fmt == A_Q8_0 || outs[n].fmt == A_Q8_1);
         if (all) tq = outs[0].fmt == A_Q8_1 ? 2 : 1;
     }
-#define MIX5_L(DMv, TQv)                                                                    \
-    do {                                                                                    \
-        if (tt == 1) hipLaunchKernelGGL((k_v6_mix5<DMv, TQv, 1>), grid, dim3(256), 0, st, a); \
-        else hipLaunchKernelGGL((k_v6_mix5<DMv, TQv, MIX_TT8>), grid, dim3(256), 0, st, a); \
+#define MIX5_L(DMv, TQv)                                                                  \
+    do {                                                                                  \
+        if (D == DMv) hipLaunchKernelGGL((k_v6_mix5<DMv, TQv, true>), grid, dim3(320), 0, st, a); \
+        else hipLaunchKernelGGL((k_v6_mix5<DMv, TQv, false>), grid, dim3(320), 0, st, a);         \
     } while (0)
     if (D <= 32) {
         if (tq == 1) MIX5_L(32, 1);
@@ -1322,9 +1335,10 @@ __global__ __launch_bounds__(1024) void k_groupnorm(int T, int H, int S, float e
                                                     const float * bonus, ActBuf out) {
     const int t = blockIdx.x * TOKS_PER_WG + (threadIdx.x >> 8), C = H * S, tid = threadIdx.x & 255;
     if (t >= T) return;
-    for (int c0 = 0; c0 < C; c0 += 256) {
-        const int c = c0 + tid;
-        if (c0 + (tid & ~63) >= C) continue;
+    // channel block of 256 (4 heads of 64) per grid.y: one channel per thread
+    {
+        const int c0 = (int)blockIdx.y * 256, c = c0 + tid;
+        if (c0 + (tid & ~63) >= C) return;  // whole wave out of range
         const size_t i = (size_t)t * C + c;
         const float x = y[i];
         const double s = group_tree_sum_d((double)x, S);
@@ -1350,7 +1364,7 @@ bool launch_groupnorm(hipStream_t st, int T, int H, int S, float eps, const floa
         fprintf(stderr, "rwkv: head size %d unsupported by groupnorm\n", S);
         return false;
     }
-    const dim3 grid((T + TOKS_PER_WG - 1) / TOKS_PER_WG), block(256 * TOKS_PER_WG);
+    const dim3 grid((T + TOKS_PER_WG - 1) / TOKS_PER_WG, (H * S + 255) / 256), block(256 * TOKS_PER_WG);
     const int tq = tile_q(&out, 1, H * S);
     if (tq == 1) hipLaunchKernelGGL(k_groupnorm<1>, grid, block, 0, st, T, H, S, eps, y, w, b, mode, g, v, bonus, out);
     else if (tq == 2) hipLaunchKernelGGL(k_groupnorm<2>, grid, block, 0, st, T, H, S, eps, y, w, b, mode, g, v, bonus, out);

@@ -150,7 +150,7 @@ struct Mix5Dec {
 // grid (C/256, 5[, B]): block (cx, n[, b]) computes mixed vector n for 256 channels from xa = LN(x),
 // which the preceding W1 matvec already wrote as the new att_xx carry.  w2t [5][D][C] makes
 // the per-channel D-long dots coalesced across lanes; accumulation order matches the oracle
-// (sequential over i, fp64).
+// (one fp32 fma chain, sequential over i).
 __global__ __launch_bounds__(256) void k_v6_mix5_dec(Mix5Dec a) {
     const int n = blockIdx.y, C = a.C, D = a.D, b = blockIdx.z;
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -166,11 +166,10 @@ __global__ __launch_bounds__(256) void k_v6_mix5_dec(Mix5Dec a) {
     const float xa = a.xa[cb + c], mu = a.maa[n][c];
     const float sx = a.sx ? a.sx[cb + c] : a.carry[c] - xa;
     const float * lv = a.lora + (size_t)b * 5 * D + n * D;
-    double acc = 0.0;
+    float m = 0.0f;
 #pragma unroll
     for (int i = 0; i < 64; i++)
-        if (i < D) acc += (double)(w2v[i] * lv[i]);
-    const float m = (float)acc;
+        if (i < D) m = fmaf(w2v[i], lv[i], m);
     emit32(a.out[n], b, c, (m + mu) * sx + xa);
 }
 
@@ -489,7 +488,7 @@ bool launch_att6_dec(hipStream_t st, const Att6Dec & a) {
 // sequence agree bit for bit.  Replaces the f32->Q8 conversion + K = D GEMM launch pair (a 2-block
 // GEMM is all fixed cost on the MFMA path).  Workgroup = DECAY_TT tokens x 256 channels: the
 // tokens' Q8 images sit in LDS, the thread's Wd2 row units stay in registers across the tokens.
-constexpr int DECAY_TT = 16;
+constexpr int DECAY_TT = 4;  // 4: 2048 workgroups at T = 1024 (16: 512, 14.4 us)
 
 template <int WF>
 __global__ __launch_bounds__(256) void k_v6_decay_seq(int T, int C, DMat wd2, const float * dl, const float * decay,

@@ -102,14 +102,13 @@ __global__ __launch_bounds__(512) void k_v6_maa_dec(MaaDec a) {
         if (lane < R && wave * R + lane < D) s_lora[wave * R + lane] = t;
         __syncthreads();  // (2) lora_n ready
         if (wave == 0) STAMP_X(3);
-        // k_v6_mix5_dec's arithmetic: m = sum_i (double)(w2[i] * lora[i]) in order
+        // k_v6_mix5_dec's arithmetic: m = fma chain over i in order
         const float xa = s_xa[cc];
         const float sx = carry_c - xa;
-        double accd = 0.0;
+        float m = 0.0f;
 #pragma unroll
         for (int i = 0; i < DM; i++)
-            if (i < D) accd += (double)(w2v[i] * s_lora[i]);
-        const float m = (float)accd;
+            if (i < D) m = fmaf(w2v[i], s_lora[i], m);
         if (cval) emit32(a.out[n], 0, c, (m + mu_c) * sx + xa);
         STAMP_END_NS(4 + 16 * blockIdx.y);
         return;

@@ -1158,8 +1158,9 @@ static void wkv7(int64_t T, int64_t H, int64_t S, const float * r, const float *
                  const float * v, const float * a, const float * b, float * state, float * y) {
     const int64_t C = H * S;
     if (g_variant & OV_GPU) {
-        /* k_att7_dec / k_wkv7 / k_wkv7_s64: value row i, keys split in G groups of JPG */
-        const int64_t G = (256 / S) < S ? (256 / S) : S, JPG = S / G;
+        /* k_att7_dec / k_wkv7 / k_wkv7_s64: value row i, keys split in G groups of JPG (head size
+           64: 16 groups of 4, k_wkv7_s64 / k_att7_dec; others: k_wkv7's min(256 / S, S) groups) */
+        const int64_t G = S == 64 ? 16 : (256 / S) < S ? (256 / S) : S, JPG = S / G;
         for (int64_t t = 0; t < T; t++)
             for (int64_t h = 0; h < H; h++) {
                 float * st = state + h * S * S;

@@ -1176,18 +1176,27 @@ __global__ void k_wkv7(int T, int H, int S, int G, const float * r, const float 
     for (int jj = 0; jj < JPG; jj++) sout[hb + jj] = st[jj];
 }
 
-// Head size 64: one wave per (head, 16 value rows i), grid (H, 4); lane (g = lane >> 4, il =
-// lane & 15) owns row i = 16*blockIdx.y + il, keys j in [16g, 16g+16) -- k_wkv7's / k_att7_dec's
-// split and arithmetic with the same 4-group folds.  r, w, k, a, b (and v) come in 16-token chunks
-// staged in a double-buffered LDS tile: the next chunk moves in two 8-token pieces, each loaded
-// into registers at the start of an 8-token block of the current chunk and stored to the other
-// buffer at its end (44 registers in flight instead of a whole chunk, which spilled to scratch),
-// and the 8 tokens of a block are unrolled so the compiler overlaps one token's output chain with
-// the next token's operand reads and state chain.
-constexpr int WKV7_TC = 16, WKV7_PB = 8;
-__global__ __launch_bounds__(64) void k_wkv7_s64(int T, int H, const float * r, const float * w, const float * k,
-                                                 const float * v, const float * a, const float * b,
-                                                 const float * sin, float * sout, float * y, int bs) {
+// Head size 64: keys in 16 groups of 4 (k_att7_dec's split for S = 64, G = 16).  Workgroup = 4
+// waves over 16 value rows of one head, grid (H, 4); lane (g = lane & 15, il = 4 wv + (lane >> 4))
+// owns row i = 16 blockIdx.y + il, keys j = 4g .. 4g + 3.  Per token: sa = sum_j a_j s_ij (4 terms
+// in order from 0, then the 16 groups folded by the butterfly xor 8, 4, 2, 1 -- DPP row rotations,
+// every lane of the row ends with the same bits), the state update, and the output sum the same
+// way.  r, w, k, a, b (and v) come in 16-token chunks staged in a double-buffered LDS tile (the next
+// chunk in registers while the current one runs); y goes through an LDS tile, one store per chunk.
+constexpr int WKV7_TC = 16;
+
+// v + v(lane + 8 mod 16) + ... over a 16-lane DPP row: the butterfly of group_sum(., 16)
+__device__ __forceinline__ float row_bfly16(float v) {
+    v = v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xF, 0xF, false));
+    v = v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xF, 0xF, false));
+    v = v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x122, 0xF, 0xF, false));
+    v = v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x121, 0xF, 0xF, false));
+    return v;
+}
+
+__global__ __launch_bounds__(256) void k_wkv7_s64(int T, int H, const float * r, const float * w, const float * k,
+                                                  const float * v, const float * a, const float * b,
+                                                  const float * sin, float * sout, float * y, int bs) {
     constexpr int S = 64;
     if (bs) {  // batch: context blockIdx.z, one token
         const size_t o = (size_t)blockIdx.z * H * S;
@@ -1197,110 +1206,84 @@ __global__ __launch_bounds__(64) void k_wkv7_s64(int T, int H, const float * r, 
         T = 1;
     }
     __shared__ __attribute__((aligned(16))) float sr[2][WKV7_TC][S], sw[2][WKV7_TC][S], sk[2][WKV7_TC][S],
-        sa_[2][WKV7_TC][S], sb[2][WKV7_TC][S], sv[2][WKV7_TC][16];
-    const int h = blockIdx.x, ib = blockIdx.y, lane = threadIdx.x;
-    const int il = lane & 15, g = lane >> 4, i = ib * 16 + il;
+        sa_[2][WKV7_TC][S], sb[2][WKV7_TC][S], sv[2][WKV7_TC][16], sy[2][WKV7_TC][16];
+    const int h = blockIdx.x, ib = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int g = lane & 15, il = 4 * wv + (lane >> 4), i = ib * 16 + il;
     const int C = H * S;
-    const size_t hb = (size_t)h * S * S + (size_t)i * S + g * 16;
-    float st[16];
+    const size_t hb = (size_t)h * S * S + (size_t)i * S + 4 * g;
+    float st[4];
 #pragma unroll
-    for (int jj = 0; jj < 16; jj++) st[jj] = sin[hb + jj];
-    // piece PC (tokens 8 PC .. 8 PC + 7) of the chunk at T0: lane moves float4 #(lane & 15) of
-    // tokens (lane >> 4) + 4 e of the five key-indexed rows, lanes < 32 one float4 of v
-    float4 q00, q01, q10, q11, q20, q21, q30, q31, q40, q41, qv;  // scalars: arrays went to scratch
-    const int c4 = 4 * (lane & 15);
-#define WKV7_LD(T0, PC, E, A0, A1, A2, A3, A4)                                                            \
-    do {                                                                                                  \
-        const int t = min((T0) + WKV7_PB * (PC) + (lane >> 4) + 4 * (E), T - 1);                          \
-        const size_t base = (size_t)t * C + (size_t)h * S + c4;                                           \
-        A0 = *(const float4 *)(r + base);                                                                 \
-        A1 = *(const float4 *)(w + base);                                                                 \
-        A2 = *(const float4 *)(k + base);                                                                 \
-        A3 = *(const float4 *)(a + base);                                                                 \
-        A4 = *(const float4 *)(b + base);                                                                 \
-    } while (0)
-#define WKV7_LOADP(T0, PC)                                                                                \
-    do {                                                                                                  \
-        WKV7_LD(T0, PC, 0, q00, q10, q20, q30, q40);                                                      \
-        WKV7_LD(T0, PC, 1, q01, q11, q21, q31, q41);                                                      \
-        const int tv = min((T0) + WKV7_PB * (PC) + ((lane & 31) >> 2), T - 1);                            \
-        qv = *(const float4 *)(v + (size_t)tv * C + (size_t)h * S + ib * 16 + 4 * (lane & 3));            \
-    } while (0)
-#define WKV7_ST(BUF, PC, E, A0, A1, A2, A3, A4)                                                           \
-    do {                                                                                                  \
-        const int tt = WKV7_PB * (PC) + (lane >> 4) + 4 * (E);                                            \
-        *(float4 *)&sr[BUF][tt][c4] = A0;                                                                 \
-        *(float4 *)&sw[BUF][tt][c4] = A1;                                                                 \
-        *(float4 *)&sk[BUF][tt][c4] = A2;                                                                 \
-        *(float4 *)&sa_[BUF][tt][c4] = A3;                                                                \
-        *(float4 *)&sb[BUF][tt][c4] = A4;                                                                 \
-    } while (0)
-#define WKV7_STOREP(BUF, PC)                                                                              \
-    do {                                                                                                  \
-        WKV7_ST(BUF, PC, 0, q00, q10, q20, q30, q40);                                                     \
-        WKV7_ST(BUF, PC, 1, q01, q11, q21, q31, q41);                                                     \
-        if (lane < 32) *(float4 *)&sv[BUF][WKV7_PB * (PC) + (lane >> 2)][4 * (lane & 3)] = qv;            \
-    } while (0)
-    WKV7_LOADP(0, 0);
-    WKV7_STOREP(0, 0);
-    WKV7_LOADP(0, 1);
-    WKV7_STOREP(0, 1);
+    for (int e = 0; e < 4; e++) st[e] = sin[hb + e];  // (state slices need not be 16-byte aligned)
+    // staging: thread moves float4 #(tid & 15) of token (tid >> 4) of the five key-indexed rows;
+    // threads < 64 one float4 of v (token tid >> 2, rows 4 (tid & 3) ..)
+    float4 q0, q1, q2, q3, q4, qv;
+    const int c4 = 4 * (tid & 15), tl = tid >> 4;
+    auto load = [&](int t0) __attribute__((always_inline)) {
+        const int t = min(t0 + tl, T - 1);
+        const size_t base = (size_t)t * C + (size_t)h * S + c4;
+        q0 = *(const float4 *)(r + base);
+        q1 = *(const float4 *)(w + base);
+        q2 = *(const float4 *)(k + base);
+        q3 = *(const float4 *)(a + base);
+        q4 = *(const float4 *)(b + base);
+        if (tid < 64) {
+            const int tv = min(t0 + (tid >> 2), T - 1);
+            qv = *(const float4 *)(v + (size_t)tv * C + (size_t)h * S + ib * 16 + 4 * (tid & 3));
+        }
+    };
+    auto store = [&](int bf) __attribute__((always_inline)) {
+        *(float4 *)&sr[bf][tl][c4] = q0;
+        *(float4 *)&sw[bf][tl][c4] = q1;
+        *(float4 *)&sk[bf][tl][c4] = q2;
+        *(float4 *)&sa_[bf][tl][c4] = q3;
+        *(float4 *)&sb[bf][tl][c4] = q4;
+        if (tid < 64) *(float4 *)&sv[bf][tid >> 2][4 * (tid & 3)] = qv;
+    };
+    load(0);
+    store(0);
     __syncthreads();
     int buf = 0;
     for (int t0 = 0; t0 < T; t0 += WKV7_TC) {
         const int n = min(WKV7_TC, T - t0);
         const bool nx = t0 + WKV7_TC < T;
+        if (nx) load(t0 + WKV7_TC);  // in flight during this chunk
+#pragma unroll 4
+        for (int tt = 0; tt < n; tt++) {
+            const float4 av = *(const float4 *)&sa_[buf][tt][4 * g];
+            const float4 kq = *(const float4 *)&sk[buf][tt][4 * g];
+            const float4 wq = *(const float4 *)&sw[buf][tt][4 * g];
+            const float4 bq = *(const float4 *)&sb[buf][tt][4 * g];
+            const float4 rq = *(const float4 *)&sr[buf][tt][4 * g];
+            const float vi = sv[buf][tt][il];
+            float sa = 0.0f;
+            sa += av.x * st[0];
+            sa += av.y * st[1];
+            sa += av.z * st[2];
+            sa += av.w * st[3];
+            sa = row_bfly16(sa);
+            const float kk[4] = {kq.x, kq.y, kq.z, kq.w}, ww[4] = {wq.x, wq.y, wq.z, wq.w};
+            const float bb[4] = {bq.x, bq.y, bq.z, bq.w}, rr[4] = {rq.x, rq.y, rq.z, rq.w};
+            float acc = 0.0f;
 #pragma unroll
-        for (int pc = 0; pc < WKV7_TC / WKV7_PB; pc++) {
-            if (nx) WKV7_LOADP(t0 + WKV7_TC, pc);
-#pragma unroll
-            for (int e = 0; e < WKV7_PB; e++) {
-                const int tt = WKV7_PB * pc + e;
-                if (tt < n) {  // uniform
-                    float aa[16];
-#pragma unroll
-                    for (int q = 0; q < 4; q++) {
-                        const float4 x = *(const float4 *)&sa_[buf][tt][g * 16 + 4 * q];
-                        aa[4 * q] = x.x, aa[4 * q + 1] = x.y, aa[4 * q + 2] = x.z, aa[4 * q + 3] = x.w;
-                    }
-                    float sa = 0.0f;
-#pragma unroll
-                    for (int jj = 0; jj < 16; jj++) sa += aa[jj] * st[jj];
-                    sa = fold_g4(sa);
-                    const float vi = sv[buf][tt][il];
-                    float acc = 0.0f;
-#pragma unroll
-                    for (int q = 0; q < 4; q++) {
-                        const float4 kq = *(const float4 *)&sk[buf][tt][g * 16 + 4 * q];
-                        const float4 wq = *(const float4 *)&sw[buf][tt][g * 16 + 4 * q];
-                        const float4 bq = *(const float4 *)&sb[buf][tt][g * 16 + 4 * q];
-                        const float4 rq = *(const float4 *)&sr[buf][tt][g * 16 + 4 * q];
-                        const float kk[4] = {kq.x, kq.y, kq.z, kq.w}, ww[4] = {wq.x, wq.y, wq.z, wq.w};
-                        const float bb[4] = {bq.x, bq.y, bq.z, bq.w}, rr[4] = {rq.x, rq.y, rq.z, rq.w};
-#pragma unroll
-                        for (int e2 = 0; e2 < 4; e2++) {
-                            const int jj = 4 * q + e2;
-                            const float kv = vi * kk[e2];
-                            const float ns = st[jj] * ww[e2] + kv + sa * bb[e2];
-                            st[jj] = ns;
-                            acc += ns * rr[e2];
-                        }
-                    }
-                    acc = fold_g4(acc);
-                    if (g == 0) y[(size_t)(t0 + tt) * C + (size_t)h * S + i] = acc;
-                }
+            for (int e = 0; e < 4; e++) {
+                const float kv = vi * kk[e];
+                const float ns = st[e] * ww[e] + kv + sa * bb[e];
+                st[e] = ns;
+                acc += ns * rr[e];
             }
-            if (nx) WKV7_STOREP(buf ^ 1, pc);
+            acc = row_bfly16(acc);
+            if (g == 0) sy[buf][tt][il] = acc;
         }
+        if (nx) store(buf ^ 1);
         __syncthreads();
+        // the chunk's y tile [n tokens][16 rows]: threads < 64 one float4
+        if (tid < 64 && (tid >> 2) < n)
+            *(float4 *)(y + (size_t)(t0 + (tid >> 2)) * C + (size_t)h * S + ib * 16 + 4 * (tid & 3)) =
+                *(const float4 *)&sy[buf][tid >> 2][4 * (tid & 3)];
         buf ^= 1;
     }
-#undef WKV7_LD
-#undef WKV7_ST
-#undef WKV7_LOADP
-#undef WKV7_STOREP
 #pragma unroll
-    for (int jj = 0; jj < 16; jj++) sout[hb + jj] = st[jj];
+    for (int e = 0; e < 4; e++) sout[hb + e] = st[e];
 }
 
 bool launch_wkv7(hipStream_t st, int T, int H, int S, const float * r, const float * w, const float * k,
@@ -1308,7 +1291,7 @@ bool launch_wkv7(hipStream_t st, int T, int H, int S, const float * r, const flo
                  float * y, int bs) {
     const int nz = bs ? T : 1;
     if (S == 64) {
-        hipLaunchKernelGGL(k_wkv7_s64, dim3(H, 4, nz), dim3(64), 0, st, T, H, r, w, k, v, a, b, state_in, state_out, y,
+        hipLaunchKernelGGL(k_wkv7_s64, dim3(H, 4, nz), dim3(256), 0, st, T, H, r, w, k, v, a, b, state_in, state_out, y,
                            bs);
         HIP_OK(hipGetLastError());
         return true;

@@ -543,7 +543,7 @@ bool launch_v6_decay_seq(hipStream_t st, int T, int C, const DMat & wd2, const f
 
 // --------------------------------------------------------------------------- v7 attention (decode)
 template <int JPG>
-__global__ __launch_bounds__(256) void k_att7_dec(Att7Dec a) {
+__global__ __launch_bounds__(1024) void k_att7_dec(Att7Dec a) {
     __shared__ float sr[64], sw[64], sk[64], sv[64], snb[64], sbb[64], sy[64];
     __shared__ float sbonus;
     const int h = blockIdx.x, S = a.S, G = S / JPG;
@@ -634,7 +634,8 @@ bool launch_att7_dec(hipStream_t st, const Att7Dec & a) {
         fprintf(stderr, "rwkv: head size %d unsupported\n", a.S);
         return false;
     }
-    int G = 256 / a.S;
+    // keys per lane: 4 at head size 64 (16 groups, k_wkv7_s64's split), else pick_groups' split
+    int G = a.S == 64 ? 16 : 256 / a.S;
     if (G > a.S) G = a.S;
     const int JPG = a.S / G;
     const int threads = std::max(64, a.S * G);

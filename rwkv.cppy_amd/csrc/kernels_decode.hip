@@ -63,7 +63,18 @@ bool launch_mv_group(hipStream_t st, MVGroup & g) {
     int umax0 = 1;
     for (int i = 0; i < g.n; i++) umax0 = std::max(umax0, mv_units(g.e[i].W.type, g.e[i].W.K));
     const bool mva = !prologue && !emit && wfix >= 0 && umax0 <= 4;
-    const int R = emit ? 8 : mva ? mva_rows() : 2, RW = 4 * R;
+    // LayerNorm-prologue groups (not emitting) with more than two workgroups per CU at 2 rows per
+    // wave (v7 r,k,v: 960; v5 r,k,v,g: 2048) take 4 rows per wave: one round of workgroups fewer
+    // (v7-2.9B decode 469 -> 490 tok/s alone, with U = 1 above 513; v5-7B 517 -> 573)
+    static const int ln_r4 = [] {
+        const char * e = getenv("RWKV_MI355X_LN_R4");  // default on (0: off, A/B)
+        return e ? atoi(e) : 1;
+    }();
+    int rows2 = 0;
+    for (int i = 0; i < g.n; i++) rows2 += (g.e[i].W.M + 7) / 8;
+    const bool r4 = ln_r4 && prologue && !emit && srck == MVK_LN && (g.n > 1 || rows2 <= 8 * g_mv_cus) &&
+                    rows2 > 2 * g_mv_cus;
+    const int R = emit ? 8 : mva ? mva_rows() : r4 ? 4 : 2, RW = 4 * R;
     g.rows = R;
     int blocks = 0, umax = 1, lds = 0;
     for (int i = 0; i < g.n; i++) {
@@ -120,7 +131,15 @@ bool launch_mv_group(hipStream_t st, MVGroup & g) {
         g.stride = grid;
     }
     g.grid = grid;
-    const int U = umax <= 1 ? 1 : umax <= 2 ? 2 : 4;  // 2: K = 2560 (v7-2.9B) quantized rows
+    int U = umax <= 1 ? 1 : umax <= 2 ? 2 : 4;  // 2: K = 2560 (v7-2.9B) quantized rows
+    // emitting LayerNorm groups at U = 2 hold 16 weight units per wave (184 VGPRs: one workgroup
+    // per CU); with more row blocks than CUs, U = 1 (two round trips, 122 VGPRs, two per CU):
+    // v7-2.9B FFN key, 320 workgroups -- decode 469 -> 489 tok/s alone
+    static const int emit_u1 = [] {
+        const char * e = getenv("RWKV_MI355X_EMIT_U1");  // default on (0: off, A/B)
+        return e ? atoi(e) : 1;
+    }();
+    if (emit_u1 && emit && U == 2 && blocks > g_mv_cus) U = 1;
     bool ok = false;
     switch (wfix) {
         case W_F16: ok = launch_mv_shape<W_F16>(st, g, U, srck, form, emit, dim3(grid)); break;

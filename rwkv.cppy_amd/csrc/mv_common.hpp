@@ -712,9 +712,8 @@ bool launch_mv_shape(hipStream_t st, MVGroup & g, int U, int srck, int form, boo
         fprintf(stderr, "rwkv: LayerNorm matvec prologue needs K <= 4096 (K=%d)\n", K);
         return false;
     }
-#define MV_P(S, F, E)                                         \
+#define MV_PR(Rv, S, F, E)                                    \
     do {                                                      \
-        constexpr int Rv = (E) ? 8 : 2;                       \
         if (K <= 2048) {                                      \
             if (U == 1) MV_L(Rv, 1, S, F, E, 32);             \
             else if (U == 2) MV_L(Rv, 2, S, F, E, 32);        \
@@ -725,15 +724,22 @@ bool launch_mv_shape(hipStream_t st, MVGroup & g, int U, int srck, int form, boo
             else MV_L(Rv, 4, S, F, E, 64);                    \
         }                                                     \
     } while (0)
+    // not emitting: g.rows rows per wave (2, or 4 for large LayerNorm groups); emitting: 8
+#define MV_P(S, F, E)                                         \
+    do {                                                      \
+        if (g.rows == 4) MV_PR(4, S, F, false);               \
+        else MV_PR(2, S, F, false);                           \
+    } while (0)
     if (emit) {
-        if (form == 0) MV_P(MVK_LN, 0, true);
-        else MV_P(MVK_LN, 1, true);
+        if (form == 0) MV_PR(8, MVK_LN, 0, true);
+        else MV_PR(8, MVK_LN, 1, true);
     } else {
         if (form == 0) MV_P(MVK_LN, 0, false);
         else if (form == 1) MV_P(MVK_LN, 1, false);
         else MV_P(MVK_LN, 2, false);
     }
 #undef MV_P
+#undef MV_PR
 #undef MV_L
     return true;
 }

@@ -488,8 +488,15 @@ __global__ __launch_bounds__(1024) void k_ln_mix(LnMixArgs a) {
 }
 
 bool launch_ln_mix(hipStream_t st, const LnMixArgs & a) {
-    const dim3 grid((a.T + TOKS_PER_WG - 1) / TOKS_PER_WG, a.T <= 64 ? (a.C + 255) / 256 : 1),
-        block(256 * TOKS_PER_WG);
+    // long sequences: the channel blocks split over grid.y = ln_mix_y() (each workgroup computes
+    // its rows' LayerNorm statistics itself, so y > 1 repeats that work for a shorter store phase)
+    static const int ln_mix_y = [] {
+        const char * e = getenv("RWKV_MI355X_LNMIX_Y");
+        const int v = e ? atoi(e) : 1;
+        return v >= 1 && v <= 16 ? v : 1;
+    }();
+    const int gy = a.T <= 64 ? (a.C + 255) / 256 : std::min(ln_mix_y, (a.C + 255) / 256);
+    const dim3 grid((a.T + TOKS_PER_WG - 1) / TOKS_PER_WG, gy), block(256 * TOKS_PER_WG);
     const int tq = tile_q(a.out, a.n_out, a.C);
     if (tq == 1) hipLaunchKernelGGL(k_ln_mix<1>, grid, block, 0, st, a);
     else if (tq == 2) hipLaunchKernelGGL(k_ln_mix<2>, grid, block, 0, st, a);

@@ -541,8 +541,8 @@ struct Mix5Args {
 // each lane holds its channel's W2 column of that mix in registers (D floats, read once per token
 // tile); the tile's lora rows sit in LDS as [mix][i][token], so one 16-byte broadcast read gives
 // the i-th lora value of 4 tokens.  Per token the D-long fp32 fma chain runs in k_v6_mix5_dec's
-// order (sequential over i); 4 tokens' chains run side by side.  ~70 VGPRs: 6+ waves per SIMD.
-constexpr int MIX_TT = 32;
+// order (sequential over i); 4 tokens' chains run side by side (168 VGPRs: 3 waves per SIMD).
+constexpr int MIX_TT = 32;  // (64: 76.8 us)
 
 // TQ > 0: all five outputs are Q8 sequence-GEMM token tiles (TQ = 2: Q8_1); each lane's record
 // address is formed once (a workgroup's MIX_TT tokens lie in one QG_TOK-token tile) and the

@@ -1112,9 +1112,10 @@ __global__ __launch_bounds__(256) void k_v7_prep(int T, int H, int S, float * k,
                                                  const float * k_k, const float * k_a, const float * r_k, float * nb,
                                                  float * bb, float * bonus) {
     const int t = blockIdx.x, C = H * S;
-    for (int c0 = 0; c0 < C; c0 += blockDim.x) {
-        const int c = c0 + threadIdx.x;
-        if (c0 + (int)(threadIdx.x & ~63) >= C) continue;
+    // one 256-channel block (whole heads) per grid.y: no serial walk over the channel blocks
+    {
+        const int c0 = (int)blockIdx.y * blockDim.x, c = c0 + threadIdx.x;
+        if (c0 + (int)(threadIdx.x & ~63) >= C) return;  // whole wave out of range
         const size_t i = (size_t)t * C + c;
         const float kv = k[i];
         const float kkr = kv * k_k[c];
@@ -1138,7 +1139,8 @@ bool launch_v7_prep(hipStream_t st, int T, int H, int S, float * k, const float 
         fprintf(stderr, "rwkv: v7 head size %d unsupported\n", S);
         return false;
     }
-    hipLaunchKernelGGL(k_v7_prep, dim3(T), dim3(256), 0, st, T, H, S, k, a, r, k_k, k_a, r_k, nb, bb, bonus);
+    hipLaunchKernelGGL(k_v7_prep, dim3(T, (H * S + 255) / 256), dim3(256), 0, st, T, H, S, k, a, r, k_k, k_a, r_k, nb,
+                       bb, bonus);
     HIP_OK(hipGetLastError());
     return true;
 }

@@ -53,6 +53,9 @@ RWKV_API bool rwkv_mi355x_eval_layers(struct rwkv_context * ctx, const uint32_t 
 RWKV_API bool rwkv_mi355x_eval_layers_async(struct rwkv_context * ctx, const uint32_t * tokens, size_t T,
                                             uint32_t layer_begin, uint32_t layer_end, float * x_dev, float * vfirst_dev,
                                             bool compute_logits);
+/* The context's device logits buffer [n_vocab] (NULL for a NULL context).  It holds valid logits
+ * only after an evaluation that computed them: on the context holding the head (the last stage)
+ * with compute_logits / a logits request; otherwise its contents are stale. */
 RWKV_API float * rwkv_mi355x_logits_device(struct rwkv_context * ctx);
 
 /* A pipeline stage's context: only layers [layer_begin, layer_end) are uploaded (plus the

@@ -39,6 +39,9 @@
 #include <sys/stat.h>
 #ifdef _OPENMP
 #include <omp.h>
+#ifdef __AVX2__
+#include <immintrin.h>
+#endif
 #endif
 
 #define QK 32
@@ -577,6 +580,24 @@ static void ln_stats_gpu(const float * x, int64_t n, float eps, float * mean_out
     *scale_out = 1.0f / sqrtf(var + eps);
 }
 
+/* Exact integer dot of 32 int8 pairs (|w| <= 128, |x| <= 127: the Q8 activation quantizer's
+ * range), AVX2 form of ggml's x86 sign/maddubs trick; the plain loop elsewhere. */
+static inline int dot32_i8(const int8_t * w, const int8_t * x) {
+#ifdef __AVX2__
+    const __m256i vw = _mm256_loadu_si256((const __m256i *)w), vx = _mm256_loadu_si256((const __m256i *)x);
+    const __m256i p16 = _mm256_maddubs_epi16(_mm256_sign_epi8(vw, vw), _mm256_sign_epi8(vx, vw));
+    const __m256i p32 = _mm256_madd_epi16(p16, _mm256_set1_epi16(1));
+    __m128i s = _mm_add_epi32(_mm256_castsi256_si128(p32), _mm256_extracti128_si256(p32, 1));
+    s = _mm_add_epi32(s, _mm_shuffle_epi32(s, 0x4E));
+    s = _mm_add_epi32(s, _mm_shuffle_epi32(s, 0xB1));
+    return _mm_cvtsi128_si32(s);
+#else
+    int sumi = 0;
+    for (int j = 0; j < 32; j++) sumi += (int)w[j] * (int)x[j];
+    return sumi;
+#endif
+}
+
 /* quantized matmul in the kernels' association; weights unpacked once per row */
 static void matmul_gpu(int wtype, const uint8_t * W, int64_t K, int64_t M, const float * x, int64_t T, float * y) {
     const int nthr = oracle_get_threads();
@@ -628,37 +649,44 @@ static void matmul_gpu(int wtype, const uint8_t * W, int64_t K, int64_t M, const
             xd[t * nb + b] = h2f(xb);
             xs[t * nb + b] = one ? h2f(xb + 2) : 0.0f;
         }
-#pragma omp parallel num_threads(nthr)
-    {
-        int8_t * wi8 = (int8_t *)malloc((size_t)K);
-        float * dw = (float *)malloc((size_t)nb * sizeof(float));
-        float * mw = (float *)malloc((size_t)nb * sizeof(float));
+    /* weights unpacked once (int8 values, d, m per block), then (token tile x row tile) tasks so
+     * the activation tile stays in cache across the rows -- the same arithmetic per output */
+    int8_t * wi8 = (int8_t *)malloc((size_t)(M * K));
+    float * dw = (float *)malloc((size_t)(M * nb) * sizeof(float));
+    float * mw = (float *)malloc((size_t)(M * nb) * sizeof(float));
+#pragma omp parallel for schedule(static) num_threads(nthr)
+    for (int64_t m = 0; m < M; m++) {
         int wi[32];
-#pragma omp for schedule(static)
-        for (int64_t m = 0; m < M; m++) {
-            const uint8_t * wrow = W + (size_t)m * nb * wbb;
-            for (int64_t b = 0; b < nb; b++) {
-                block_ints(wtype, wrow + b * wbb, wi, &dw[b], &mw[b]);
-                for (int j = 0; j < 32; j++) wi8[b * 32 + j] = (int8_t)wi[j];
-            }
-            for (int64_t t = 0; t < T; t++) {
+        const uint8_t * wrow = W + (size_t)m * nb * wbb;
+        for (int64_t b = 0; b < nb; b++) {
+            block_ints(wtype, wrow + b * wbb, wi, &dw[m * nb + b], &mw[m * nb + b]);
+            for (int j = 0; j < 32; j++) wi8[m * K + b * 32 + j] = (int8_t)wi[j];
+        }
+    }
+    const int64_t TT = 32, MT = 32, ntt = (T + TT - 1) / TT, nmt = (M + MT - 1) / MT;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthr)
+    for (int64_t task = 0; task < ntt * nmt; task++) {
+        const int64_t t0 = (task / nmt) * TT, m0 = (task % nmt) * MT;
+        for (int64_t m = m0; m < m0 + MT && m < M; m++) {
+            const int8_t * wr = wi8 + m * K;
+            const float * dr = dw + m * nb, * mr = mw + m * nb;
+            for (int64_t t = t0; t < t0 + TT && t < T; t++) {
                 float acc[64], acc2[64];
                 for (int l = 0; l < 64; l++) acc[l] = acc2[l] = 0.0f;
                 const int8_t * xt = xi + t * K;
                 for (int64_t b = 0; b < nb; b++) {  /* block b -> lane b % 64, ascending */
-                    int sumi = 0;
-                    for (int j = 0; j < 32; j++) sumi += (int)wi8[b * 32 + j] * (int)xt[b * 32 + j];
-                    acc[b & 63] = fmaf(dw[b] * xd[t * nb + b], (float)sumi, acc[b & 63]);
-                    if (one) acc2[b & 63] += mw[b] * xs[t * nb + b];
+                    const int sumi = dot32_i8(wr + b * 32, xt + b * 32);
+                    acc[b & 63] = fmaf(dr[b] * xd[t * nb + b], (float)sumi, acc[b & 63]);
+                    if (one) acc2[b & 63] += mr[b] * xs[t * nb + b];
                 }
                 const float s = tree_f(acc, 64);
                 y[t * M + m] = one ? s + tree_f(acc2, 64) : s + 0.0f;
             }
         }
-        free(wi8);
-        free(dw);
-        free(mw);
     }
+    free(wi8);
+    free(dw);
+    free(mw);
     free(xq);
     free(xi);
     free(xd);

@@ -355,6 +355,7 @@ Engine::~Engine() {
     for (hipStream_t s : io_stream_)
         if (s) (void)hipStreamDestroy(s);
     for (hipEvent_t e : io_ev_) (void)hipEventDestroy(e);
+    if (io_entry_ev_) (void)hipEventDestroy(io_entry_ev_);
     drop_batch_graphs();
     for (float * p : bstate_)
         if (p) (void)hipFree(p);
@@ -1526,7 +1527,12 @@ bool Engine::eval_host_chunked(uint32_t token, const float * state_in, float * s
     if (!ensure_workspace(1)) return false;
     if (!io_stream_[0]) {
         for (auto & st : io_stream_) HIP_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        HIP_OK(hipEventCreateWithFlags(&io_entry_ev_, hipEventDisableTiming));
     }
+    // the copy streams start behind everything already queued on stream_ (an earlier
+    // rwkv_mi355x_eval_device(sync = false) may still be writing dstate_[cur_], the upload target)
+    HIP_OK(hipEventRecord(io_entry_ev_, stream_));
+    for (auto & st : io_stream_) HIP_OK(hipStreamWaitEvent(st, io_entry_ev_, 0));
     if (io_ev_.size() < 2 * (size_t)NC) {
         for (hipEvent_t e : io_ev_) (void)hipEventDestroy(e);
         io_ev_.assign(2 * NC, nullptr);
@@ -1660,25 +1666,37 @@ bool Engine::eval_layers(const uint32_t * tokens, size_t T, uint32_t l0, uint32_
 }
 
 // Names: x xa sx r k v g w y a nb bb vfirst fr lora bonus logits, slot<i>.<q|d|s|qsum|h|f>.
+// Returns -1 for an unknown name, a buffer that is not allocated, or more bytes than it holds.
 long long Engine::debug_copy(const char * name, void * out, size_t bytes) {
     if (!name || !out) return -1;
     const std::string n(name);
     const void * src = nullptr;
+    size_t cap_bytes = 0;
+    const size_t cap = (size_t)tcap_, C = m_->n_embed;
+    const size_t kmax = std::max<size_t>((size_t)m_->kmax, C);
     const std::pair<const char *, float *> fb[] = {{"x", x_}, {"xa", xa_}, {"sx", sx_}, {"r", r_}, {"k", k_},
         {"v", v_}, {"g", g_}, {"w", w_}, {"y", y_}, {"a", a_}, {"nb", nb_}, {"bb", bb_}, {"vfirst", vfirst_},
-        {"fr", fr_}, {"lora", lora_}, {"bonus", bonus_}, {"logits", logits_}};
+        {"fr", fr_}};
     for (const auto & p : fb)
-        if (n == p.first) src = p.second;
+        if (n == p.first) src = p.second, cap_bytes = cap * C * 4;
+    if (n == "lora") src = lora_, cap_bytes = cap * kmax * 4;
+    if (n == "bonus") src = bonus_, cap_bytes = cap * (size_t)std::max<int64_t>(1, m_->H) * 4;
+    if (n == "logits") src = logits_, cap_bytes = (size_t)m_->n_vocab * 4;
     if (!src && n.rfind("slot", 0) == 0) {
         const size_t dot = n.find('.');
         const int i = atoi(n.c_str() + 4);
         if (dot == std::string::npos || i < 0 || i >= kSlots) return -1;
         const std::string f = n.substr(dot + 1);
         const ActSlot & s = slots_[i];
-        src = f == "q" ? (const void *)s.q : f == "d" ? (const void *)s.d : f == "s" ? (const void *)s.s
-            : f == "qsum" ? (const void *)s.qsum : f == "h" ? (const void *)s.h : f == "f" ? (const void *)s.f : nullptr;
+        const size_t el = cap * kmax, nbk = el / 32 + 1;
+        if (f == "q") src = s.q, cap_bytes = el;
+        else if (f == "d") src = s.d, cap_bytes = nbk * 4;
+        else if (f == "s") src = s.s, cap_bytes = nbk * 4;
+        else if (f == "qsum") src = s.qsum, cap_bytes = nbk * 4;
+        else if (f == "h") src = s.h, cap_bytes = el * 2;
+        else if (f == "f") src = s.f, cap_bytes = el * 4;
     }
-    if (!src) return -1;
+    if (!src || bytes > cap_bytes) return -1;
     if (hipStreamSynchronize(stream_) != hipSuccess || hipMemcpy(out, src, bytes, hipMemcpyDeviceToHost) != hipSuccess)
         return -1;
     return (long long)bytes;

@@ -186,6 +186,7 @@ class Engine {
     int io_chunk_ = 4;
     hipStream_t io_stream_[2] = {nullptr, nullptr};
     std::vector<hipEvent_t> io_ev_;
+    hipEvent_t io_entry_ev_ = nullptr;  // work already queued on stream_ at entry (copy streams wait)
     std::vector<hipGraphExec_t> io_graphs_[2][2];  // [cur][logits] per chunk
     bool eval_host_chunked(uint32_t token, const float * state_in, float * state_out, float * logits_out);
     void drop_io_graphs();

@@ -210,6 +210,9 @@ static bool check_shapes(const ModelFile & mf) {
                "Model dimensions out of range");
     RWKV_CHECK(RWKV_ERROR_MODEL_PARAMS | RWKV_ERROR_DIMENSION, false, mf.arch_major < 5 || (H >= 1 && (uint64_t)H * S == C),
                "n_embed %u is not head_count %u x head_size %u", C, H, S);
+    // the v7 per-head prep kernels (k_v7_prep) cover channels in whole 64-lane waves
+    RWKV_CHECK(RWKV_ERROR_MODEL_PARAMS | RWKV_ERROR_UNSUPPORTED, false, mf.arch_major != 7 || C % 64 == 0,
+               "v7 models need n_embed %% 64 == 0 (n_embed %u)", C);
     const HostTensor * fk = mf.find("blocks.0.ffn.key.weight");
     const uint32_t F = fk->ne[1];
     bool ok = shape_is(mf, "blocks.0.ln0.weight", {C}, true) && shape_is(mf, "blocks.0.ln0.bias", {C}, true) &&

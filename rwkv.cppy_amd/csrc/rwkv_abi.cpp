@@ -288,7 +288,9 @@ RWKV_API bool rwkv_mi355x_eval_layers_async(struct rwkv_context * ctx, const uin
     return eval_layers(ctx, tokens, T, layer_begin, layer_end, x_dev, vfirst_dev, compute_logits, nullptr, false);
 }
 
-RWKV_API float * rwkv_mi355x_logits_device(struct rwkv_context * ctx) { return ctx->engine->device_logits(); }
+RWKV_API float * rwkv_mi355x_logits_device(struct rwkv_context * ctx) {
+    return ctx && ctx->engine ? ctx->engine->device_logits() : nullptr;
+}
 
 static bool eval_batch(struct rwkv_context * ctx, const uint32_t * tokens, size_t n, const float * state_in,
                        float * state_out, float * logits_out, bool dev) {

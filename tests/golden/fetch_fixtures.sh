@@ -16,3 +16,8 @@ done
 # RWKV v6: the FP32/FP16 tiny checkpoints are missing from the reference
 # (.MISSING_LARGE_BLOBS); only pre-quantized files exist.
 cp "$SRC/tiny-rwkv-6v0-3m-Q5_0.bin" "$SRC/tiny-rwkv-6v0-3m-Q5_1.bin" "$SRC/tiny-rwkv-6v0-3m-FP16-to-Q4_0.bin" "$DST/"
+# The other pre-quantized v6 files; FP32-to-Q5_0 / FP32-to-Q5_1 are byte-identical to -Q5_0 / -Q5_1
+# (same sha256) and are not copied (tests/test_gpu_parity.py DUP_V6 maps them).
+for q in FP16-to-Q4_1 FP16-to-Q5_0 FP16-to-Q5_1 FP32-to-Q4_0 FP32-to-Q4_1; do
+  cp "$SRC/tiny-rwkv-6v0-3m-$q.bin" "$DST/"
+done

@@ -89,3 +89,30 @@ def test_chunk_sizes(chunk):
     p = '/tmp/rwkv_pinned_v5.bin'
     assert lib.library.rwkv_mi355x_write_synthetic_model(p.encode(), 5, 1024, 512, 6, 0, b'Q5_1', 4)
     check(p, [9, 8, 7], False, chunk=chunk)
+
+
+def test_host_state_after_async_device_eval():
+    """rwkv_eval with a host state_in right after rwkv_mi355x_eval_device(sync = false): the chunked
+    upload must wait for the decode steps still queued on the context's stream (they write the
+    buffer the upload fills).  Equal to a fresh context given the same host state, bit for bit."""
+    lib = library()
+    L = lib.library
+    p = '/tmp/rwkv_async_v6.bin'
+    assert L.rwkv_mi355x_write_synthetic_model(p.encode(), 6, 4096, 2048, 4, 0, b'Q4_0', 6)
+    ctx = lib.rwkv_init_from_file(p, 1, 99)
+    ref = lib.rwkv_init_from_file(p, 1, 99)
+    n_state, n_vocab = L.rwkv_get_state_len(ctx.ptr), L.rwkv_get_n_vocab(ctx.ptr)
+    host = np.random.default_rng(5).standard_normal(n_state).astype(np.float32) * 0.1
+    out_a, out_r = np.zeros(n_state, np.float32), np.zeros(n_state, np.float32)
+    lg_a, lg_r = np.zeros(n_vocab, np.float32), np.zeros(n_vocab, np.float32)
+    assert L.rwkv_mi355x_state_upload(ctx.ptr, None)
+    for t in range(12):   # queued, not waited for
+        tok = np.array([t + 1], np.uint32)
+        assert L.rwkv_mi355x_eval_device(ctx.ptr, tok.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), 1, True,
+                                         None, False)
+    assert L.rwkv_eval(ctx.ptr, 77, host.ctypes.data_as(P_F), out_a.ctypes.data_as(P_F), lg_a.ctypes.data_as(P_F))
+    assert L.rwkv_eval(ref.ptr, 77, host.ctypes.data_as(P_F), out_r.ctypes.data_as(P_F), lg_r.ctypes.data_as(P_F))
+    assert_bits_equal(out_a, out_r, 'state after async device steps')
+    assert_bits_equal(lg_a, lg_r, 'logits after async device steps')
+    lib.rwkv_free(ctx)
+    lib.rwkv_free(ref)

@@ -83,6 +83,67 @@ def test_config_sequence_bit_exact(cfg_dir, name):
     m.free()
 
 
+def test_v5_7b_width_4096_tokens_in_chunks(cfg_dir):
+    """BASELINE config 5's workload: 4096 tokens through rwkv_eval_sequence_in_chunks with chunk 1024
+    (reference rwkv_eval.inc:158-221) at the v5-7B width (C 4096, FFN 14336, 64 heads), one layer so
+    the CPU oracle finishes in seconds.  Bit-exact against the oracle's GPU-association variant over
+    the whole sequence, and equal to one rwkv_eval_sequence call (which splits at 1024 itself)."""
+    path = cfg_model(cfg_dir, 'v5-7b-q4_1', layers=1)
+    toks = [int(t) for t in np.random.default_rng(10).integers(0, VOCAB, 4096)]
+    m = RWKVModel(library(), path)
+    lg, st = m.eval_sequence_in_chunks(toks, None, chunk_size=1024, use_numpy=True)
+    lg1, st1 = m.eval_sequence(toks, None, use_numpy=True)
+    m.free()
+    assert_bits_equal(lg1, lg, 'one call vs chunks of 1024: logits')
+    assert_bits_equal(st1, st, 'one call vs chunks of 1024: state')
+    glg, gst = gpu_variant(path, toks, sequence=True)
+    assert_bits_equal(lg, glg, 'T=4096 chunked logits')
+    assert_bits_equal(st, gst, 'T=4096 chunked state')
+
+
+def test_v7_2b9_width_four_stages(cfg_dir):
+    """BASELINE config 4's partition: four pipeline stages (one layer each) at the v7-2.9B width
+    (C 2560, H 40, Q5_1), composed over T-chunks through rwkv_mi355x_eval_layers on stage contexts
+    that hold only their own layers (rwkv_mi355x_init_from_file_layers), carrying x and v_first
+    between stages.  Equals one rwkv_eval_sequence of the whole model and the oracle, bit for bit."""
+    import ctypes
+    import torch
+    path = cfg_model(cfg_dir, 'v7-2b9-q5_1', layers=4)
+    toks = [int(t) for t in np.random.default_rng(11).integers(0, VOCAB, 70)]
+    L = library()
+    lib = L.library
+    m = RWKVModel(L, path)
+    ref_lg, ref_st = m.eval_sequence(toks, None, use_numpy=True)
+    m.free()
+    glg, gst = gpu_variant(path, toks, sequence=True)
+    assert_bits_equal(ref_lg, glg, 'whole-model logits vs oracle')
+    assert_bits_equal(ref_st, gst, 'whole-model state vs oracle')
+    fp = ctypes.POINTER(ctypes.c_float)
+    stages = []
+    for s in range(4):
+        ptr = lib.rwkv_mi355x_init_from_file_layers(path.encode(), 1, s, s + 1)
+        assert ptr, s
+        assert lib.rwkv_mi355x_state_upload(ptr, None)
+        stages.append(ptr)
+    C, n_vocab = lib.rwkv_get_n_embed(stages[0]), lib.rwkv_get_n_vocab(stages[0])
+    lg = np.zeros(n_vocab, np.float32)
+    for a in range(0, len(toks), 24):
+        ch = np.ascontiguousarray(np.asarray(toks[a:a + 24], np.uint32))
+        x = torch.zeros((2, len(ch), C), dtype=torch.float32, device='cuda')
+        for s, ptr in enumerate(stages):
+            last = s == 3
+            assert lib.rwkv_mi355x_eval_layers(ptr, ch.ctypes.data, len(ch), s, s + 1, x[0].data_ptr(),
+                                               x[1].data_ptr(), last, lg.ctypes.data_as(fp) if last else None)
+    n = lib.rwkv_get_state_buffer_element_count(stages[0])
+    per = n // 4
+    for s, ptr in enumerate(stages):
+        st = np.zeros(n, np.float32)
+        assert lib.rwkv_mi355x_state_download(ptr, st.ctypes.data_as(fp))
+        assert_bits_equal(st[s * per:(s + 1) * per], ref_st[s * per:(s + 1) * per], f'stage {s} state slice')
+        lib.rwkv_free(ptr)
+    assert_bits_equal(lg, ref_lg, 'four-stage logits')
+
+
 def test_v6_1b6_width_1024_tokens(cfg_dir):
     """The headline sequence length: 1024 tokens in one rwkv_eval_sequence at the v6-1B6 width."""
     path = cfg_model(cfg_dir, 'v6-1b6-q4_0')

@@ -28,10 +28,10 @@ def _ctx_eval_layers(L, ctx, toks, l0, l1, x, want_logits, n_vocab):
     return lg
 
 
-def _synthetic(tmp_path, arch, fmt, n_layer=5):
+def _synthetic(tmp_path, arch, fmt, n_layer=5, C=2048):
     L = library()
-    p = str(tmp_path / f'pipe{arch}{fmt}.bin')
-    assert L.library.rwkv_mi355x_write_synthetic_model(p.encode(), arch, 1024, 2048, n_layer, 0, fmt.encode(), 5)
+    p = str(tmp_path / f'pipe{arch}{fmt}C{C}L{n_layer}.bin')
+    assert L.library.rwkv_mi355x_write_synthetic_model(p.encode(), arch, 1024, C, n_layer, 0, fmt.encode(), 5)
     return p
 
 
@@ -101,15 +101,16 @@ def _rank_main(rank, world, port, path, toks, chunk, out_dir, async_):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('arch,fmt,chunk,world,async_', [(6, 'Q4_0', 16, 2, False), (7, 'Q5_1', 33, 2, True),
-                                                         (5, 'Q4_1', 20, 3, True)])
-def test_multi_process_pipeline_bit_exact(tmp_path, arch, fmt, chunk, world, async_):
+@pytest.mark.parametrize('arch,fmt,chunk,world,async_,C,n_layer', [
+    (6, 'Q4_0', 16, 2, False, 2048, 5), (7, 'Q5_1', 33, 2, True, 2048, 5), (5, 'Q4_1', 20, 3, True, 2048, 5),
+    (7, 'Q5_1', 24, 4, True, 2560, 4)])   # the last: BASELINE config 4's four stages at the v7-2.9B width
+def test_multi_process_pipeline_bit_exact(tmp_path, arch, fmt, chunk, world, async_, C, n_layer):
     """Stage contexts loaded with rwkv_mi355x_init_from_file_layers hold only their layers (HBM weight
     bytes ~1/world of the model's; the head only on the last stage) and the pipelined result equals
     one rwkv_eval_sequence bit for bit, synchronous and stream-ordered (async) stages alike."""
     import torch.multiprocessing as mp
     L = library()
-    p = _synthetic(tmp_path, arch, fmt)
+    p = _synthetic(tmp_path, arch, fmt, n_layer, C)
     toks = [int(t) for t in np.random.default_rng(4).integers(0, 1024, 70)]
     m = RWKVModel(L, p)
     ref_lg, ref_st = m.eval_sequence(toks, None, use_numpy=True)

@@ -21,6 +21,31 @@ RWKV_API bool rwkv_mi355x_state_upload(struct rwkv_context * ctx, const float * 
 /* Copies the device-resident state out to host memory. */
 RWKV_API bool rwkv_mi355x_state_download(struct rwkv_context * ctx, float * state);
 
+/* The state of layers [layer_begin, layer_end) only: `slice` holds those layers in the host layout
+ * (rwkv_mi355x_layer_state_len(ctx) floats per layer, layer_begin's first), so a pipeline stage or a
+ * caller that owns part of the layers moves just its part over PCIe.  Upload with slice == NULL
+ * resets those layers to the fresh state.  Layer ranges outside [0, n_layer) fail with
+ * RWKV_ERROR_ARGS. */
+RWKV_API size_t rwkv_mi355x_layer_state_len(const struct rwkv_context * ctx);
+RWKV_API bool rwkv_mi355x_state_upload_layers(struct rwkv_context * ctx, const float * slice, uint32_t layer_begin,
+                                              uint32_t layer_end);
+RWKV_API bool rwkv_mi355x_state_download_layers(struct rwkv_context * ctx, float * slice, uint32_t layer_begin,
+                                                uint32_t layer_end);
+/* State bytes this context has moved so far: out[0] host->device, out[1] device->host (the state
+ * entry points above and rwkv_eval's host state buffers). */
+RWKV_API void rwkv_mi355x_state_io_bytes(const struct rwkv_context * ctx, double out[2]);
+
+/* rwkv_clone_context onto GPU `device` (reference clone semantics, rwkv.h:93-99, rwkv.cpp:123-139:
+ * a new context with a fresh state sharing the parent's model).  The model is uploaded once per
+ * GPU -- the first clone on a GPU re-reads the parent's file (same layer range), later clones and
+ * their parent-device siblings share that copy -- so a server runs one replica per GPU of a node
+ * from one process.  device == the parent's GPU is rwkv_clone_context.  A device outside
+ * [0, device count) fails with RWKV_ERROR_ARGS (on the parent's error flags) and returns NULL. */
+RWKV_API struct rwkv_context * rwkv_mi355x_clone_context_on(struct rwkv_context * ctx, uint32_t n_threads,
+                                                            int device);
+/* The GPU a context evaluates on (-1 for NULL). */
+RWKV_API int rwkv_mi355x_context_device(const struct rwkv_context * ctx);
+
 /* rwkv_eval_sequence semantics on the device-resident state: tokens host array, T >= 1.
  * compute_logits: run the head on the last token (logits stay in HBM); logits_out (host, may be
  * NULL) additionally receives them.  No state crosses PCIe.  sync=false returns after

@@ -499,8 +499,8 @@ bool Engine::ensure_workspace(int T) {
     return true;
 }
 
-bool Engine::init_state(float * st) {
-    const size_t n = m_->state_len;
+bool Engine::init_state(float * st, size_t n) {
+    if (!n) n = m_->state_len;
     hipLaunchKernelGGL(k_init_state, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream_, st, n,
                        (int)m_->n_embed, m_->major == 4 ? 1 : 0);
     HIP_OK(hipGetLastError());
@@ -1496,6 +1496,7 @@ bool Engine::run_tokens_impl(const uint32_t * tokens, size_t T, bool want_logits
 bool Engine::state_upload(const float * state) {
     if (state) {
         HIP_OK(hipMemcpyAsync(dstate_[cur_], state, m_->state_len * 4, hipMemcpyHostToDevice, stream_));
+        io_h2d_ += m_->state_len * 4.0;
         return true;
     }
     return init_state(dstate_[cur_]);
@@ -1504,6 +1505,27 @@ bool Engine::state_upload(const float * state) {
 bool Engine::state_download(float * state) {
     HIP_OK(hipMemcpyAsync(state, dstate_[cur_], m_->state_len * 4, hipMemcpyDeviceToHost, stream_));
     HIP_OK(hipStreamSynchronize(stream_));
+    io_d2h_ += m_->state_len * 4.0;
+    return true;
+}
+
+// The host layout is per layer contiguous (rwkv_graph.inc:545-606), so layers [l0, l1) are one
+// range of the device-resident state: only that range crosses PCIe.
+bool Engine::state_upload_layers(const float * slice, uint32_t l0, uint32_t l1) {
+    const size_t per = layer_state_len(), off = (size_t)l0 * per, n = (size_t)(l1 - l0) * per;
+    if (slice) {
+        HIP_OK(hipMemcpyAsync(dstate_[cur_] + off, slice, n * 4, hipMemcpyHostToDevice, stream_));
+        io_h2d_ += n * 4.0;
+        return true;
+    }
+    return init_state(dstate_[cur_] + off, n);
+}
+
+bool Engine::state_download_layers(float * slice, uint32_t l0, uint32_t l1) {
+    const size_t per = layer_state_len(), off = (size_t)l0 * per, n = (size_t)(l1 - l0) * per;
+    HIP_OK(hipMemcpyAsync(slice, dstate_[cur_] + off, n * 4, hipMemcpyDeviceToHost, stream_));
+    HIP_OK(hipStreamSynchronize(stream_));
+    io_d2h_ += n * 4.0;
     return true;
 }
 
@@ -1571,6 +1593,7 @@ bool Engine::eval_host_chunked(uint32_t token, const float * state_in, float * s
         slice(0, off, bytes);
         HIP_OK(hipMemcpyAsync(din + off, state_in + off, bytes, hipMemcpyHostToDevice, io_stream_[0]));
         HIP_OK(hipEventRecord(in_ev[0], io_stream_[0]));
+        io_h2d_ += (double)bytes;
     } else if (!init_state(din)) {
         return false;
     }
@@ -1582,17 +1605,20 @@ bool Engine::eval_host_chunked(uint32_t token, const float * state_in, float * s
             slice(c + 1, off, bytes);
             HIP_OK(hipMemcpyAsync(din + off, state_in + off, bytes, hipMemcpyHostToDevice, io_stream_[0]));
             HIP_OK(hipEventRecord(in_ev[c + 1], io_stream_[0]));
+            io_h2d_ += (double)bytes;
         }
         if (state_out && c >= 1) {
             slice(c - 1, off, bytes);
             HIP_OK(hipStreamWaitEvent(io_stream_[1], done_ev[c - 1], 0));
             HIP_OK(hipMemcpyAsync(state_out + off, dout + off, bytes, hipMemcpyDeviceToHost, io_stream_[1]));
+            io_d2h_ += (double)bytes;
         }
     }
     if (state_out) {
         slice(NC - 1, off, bytes);
         HIP_OK(hipStreamWaitEvent(io_stream_[1], done_ev[NC - 1], 0));
         HIP_OK(hipMemcpyAsync(state_out + off, dout + off, bytes, hipMemcpyDeviceToHost, io_stream_[1]));
+        io_d2h_ += (double)bytes;
     }
     if (logits_out)
         HIP_OK(hipMemcpyAsync(logits_out, logits_, (size_t)m_->n_vocab * 4, hipMemcpyDeviceToHost, stream_));
@@ -1627,8 +1653,10 @@ bool Engine::eval(const uint32_t * tokens, size_t T, const float * state_in, flo
     if (!run_tokens(tokens, T, logits_out != nullptr)) return false;
     if (logits_out)
         HIP_OK(hipMemcpyAsync(logits_out, logits_, (size_t)m_->n_vocab * 4, hipMemcpyDeviceToHost, stream_));
-    if (state_out)
+    if (state_out) {
         HIP_OK(hipMemcpyAsync(state_out, dstate_[cur_], m_->state_len * 4, hipMemcpyDeviceToHost, stream_));
+        io_d2h_ += m_->state_len * 4.0;
+    }
     HIP_OK(hipStreamSynchronize(stream_));
     return true;
 }

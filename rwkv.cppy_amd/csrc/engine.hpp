@@ -95,6 +95,14 @@ class Engine {
     float * device_logits() const { return logits_; }
     bool state_upload(const float * state);
     bool state_download(float * state);
+    // the state of layers [l0, l1) only (a pipeline stage's or replica's slice); slice = those
+    // layers in the host layout, NULL on upload = fresh state for them
+    size_t layer_state_len() const { return m_->major >= 5 ? (size_t)m_->n_embed * (2 + (size_t)m_->S) : 5 * (size_t)m_->n_embed; }
+    bool state_upload_layers(const float * slice, uint32_t l0, uint32_t l1);
+    bool state_download_layers(float * slice, uint32_t l0, uint32_t l1);
+    // state bytes moved host->device / device->host by this context (state APIs and rwkv_eval)
+    double io_bytes_h2d() const { return io_h2d_; }
+    double io_bytes_d2h() const { return io_d2h_; }
     bool sync();
     hipStream_t stream() const { return stream_; }
     void set_timing(bool on);
@@ -106,7 +114,7 @@ class Engine {
 
   private:
     bool ensure_workspace(int T);
-    bool init_state(float * st);
+    bool init_state(float * st, size_t n = 0);
     bool forward(int T, const float * sin, float * sout, bool logits);
     bool forward_range(int T, const float * sin, float * sout, uint32_t l0, uint32_t l1, bool logits);
     bool forward_decode(const float * sin, float * sout, bool logits, uint32_t l0 = 0, uint32_t l1 = UINT32_MAX);
@@ -123,6 +131,7 @@ class Engine {
 
     DeviceModel * m_;
     hipStream_t stream_ = nullptr;
+    double io_h2d_ = 0, io_d2h_ = 0;
     int tcap_ = 0;
     std::vector<void *> ws_allocs_;
     float *x_ = nullptr, *xa_ = nullptr, *sx_ = nullptr, *r_ = nullptr, *k_ = nullptr, *v_ = nullptr, *g_ = nullptr;

@@ -184,6 +184,22 @@ __device__ __forceinline__ void qg_mfma(const QGOps<TI> & cur, v4i_t (&sv)[TI][2
 template <bool ONE, bool FIRST, int TI>
 __device__ __forceinline__ void qg_epi(const QGOps<TI> & cur, const v4i_t (&sv)[TI][2], float (&acc)[TI][2][4],
                                        float (&acc2)[TI][2][4]) {
+#ifdef QG_SCALAR
+    // scalar f32 operations (packed f32 beside MFMAs issues slower than two scalar ones)
+#pragma unroll
+    for (int i = 0; i < TI; i++) {
+        const float dw[4] = {cur.sd[i].x, cur.sd[i].y, cur.sd[i].z, cur.sd[i].w};
+        const float mw[4] = {cur.sm[i].x, cur.sm[i].y, cur.sm[i].z, cur.sm[i].w};
+#pragma unroll
+        for (int j = 0; j < 2; j++)
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const float si = __int_as_float(sv[i][j][q]) - QG_BIAS_F;
+                acc[i][j][q] = fmaf(dw[q] * cur.dx[j], si, FIRST ? 0.0f : acc[i][j][q]);
+                if constexpr (ONE) acc2[i][j][q] = (FIRST ? 0.0f : acc2[i][j][q]) + mw[q] * cur.sx[j];
+            }
+    }
+#else
     const qf2_t nbias = {-QG_BIAS_F, -QG_BIAS_F};
 #pragma unroll
     for (int i = 0; i < TI; i++)
@@ -208,6 +224,7 @@ __device__ __forceinline__ void qg_epi(const QGOps<TI> & cur, const v4i_t (&sv)[
                 }
             }
         }
+#endif
 }
 
 // y[t][m] = epi(total (+ total2)), as k_mm's red + red2.  A lane holds rows 4h..4h+3 of one

@@ -8,8 +8,10 @@
 #include <atomic>
 #include <inttypes.h>
 #include <exception>
+#include <map>
 #include <mutex>
 #include <string>
+#include <tuple>
 
 #include "../../include/rwkv.h"
 #include "../../include/rwkv_mi355x.h"
@@ -21,7 +23,19 @@ using namespace rwkvmi;
 struct SharedModel {
     DeviceModel dm;
     std::atomic<int> refcount{0};
+    // what was uploaded: a replica on another GPU (rwkv_mi355x_clone_context_on) re-reads it
+    std::string path;
+    uint32_t layer_begin = 0, layer_end = UINT32_MAX;
 };
+
+// One upload per (file, layer range, device): contexts cloned onto a GPU that already holds the
+// model share that copy (the reference's clones share one model, rwkv.cpp:123-139).  Guarded by
+// g_model_mutex.
+typedef std::tuple<std::string, uint32_t, uint32_t, int> ReplicaKey;
+static std::map<ReplicaKey, SharedModel *> g_replicas;
+static ReplicaKey replica_key(const SharedModel * sm, int device) {
+    return ReplicaKey(sm->path, sm->layer_begin, sm->layer_end, device);
+}
 
 struct rwkv_context {
     SharedModel * model = nullptr;
@@ -105,13 +119,23 @@ static struct rwkv_context * init_from_file(const char * path, const uint32_t n_
         RWKV_CHECK(RWKV_ERROR_MODEL | RWKV_ERROR_ALLOC, nullptr, false, "Failed to upload the model to the GPU");
     }
     mf.tensors.clear();
+    sm->path = path;
+    sm->layer_begin = layer_begin;
+    sm->layer_end = layer_end;
     rwkv_context * ctx = new_context(sm, n_threads);
     if (!ctx) {
         free_model(sm->dm);
         delete sm;
+        return nullptr;
     }
+    std::lock_guard<std::mutex> lk(g_model_mutex);
+    g_replicas.emplace(replica_key(sm, sm->dm.device), sm);  // first upload of this key wins
     return ctx;
 }
+
+// Every entry point that enqueues device work runs on the context's GPU (contexts of one process
+// may sit on different GPUs: rwkv_mi355x_clone_context_on).
+static void use_device(const rwkv_context * ctx) { (void)hipSetDevice(ctx->model->dm.device); }
 
 // No C++ exception crosses the C ABI: a failed host allocation (std::bad_alloc from a corrupt
 // file's sizes, say) becomes RWKV_ERROR_ALLOC and a NULL context.
@@ -137,10 +161,70 @@ RWKV_API struct rwkv_context * rwkv_mi355x_init_from_file_layers(const char * pa
 
 RWKV_API struct rwkv_context * rwkv_clone_context(struct rwkv_context * ctx, const uint32_t n_threads) {
     if (!ctx) return nullptr;
+    std::lock_guard<std::mutex> lk(g_model_mutex);
     rwkv_context * c = new_context(ctx->model, n_threads);
     if (c) c->print_errors = ctx->print_errors;
     return c;
 }
+
+RWKV_API struct rwkv_context * rwkv_mi355x_clone_context_on(struct rwkv_context * ctx, const uint32_t n_threads,
+                                                            const int device) {
+    if (!ctx) return nullptr;
+    ctx->last_error = RWKV_ERROR_NONE;
+    int ndev = 0;
+    (void)hipGetDeviceCount(&ndev);
+    CTX_CHECK(ctx, RWKV_ERROR_ARGS, nullptr, device >= 0 && device < ndev, "Device %d out of range (0 .. %d)", device,
+              ndev - 1);
+    SharedModel * src = ctx->model;
+    if (device == src->dm.device) return rwkv_clone_context(ctx, n_threads);
+    std::lock_guard<std::mutex> lk(g_model_mutex);
+    SharedModel * sm = nullptr;
+    auto it = g_replicas.find(replica_key(src, device));
+    if (it != g_replicas.end()) {
+        sm = it->second;
+    } else {
+        // first context on this GPU: upload the same file and layer range there
+        try {
+            ModelFile mf;
+            CTX_CHECK(ctx, RWKV_ERROR_MODEL | RWKV_ERROR_FILE, nullptr,
+                      load_model_file(src->path.c_str(), mf, src->layer_begin, src->layer_end),
+                      "Failed to re-read %s for device %d", src->path.c_str(), device);
+            sm = new (std::nothrow) SharedModel();
+            CTX_CHECK(ctx, RWKV_ERROR_CTX | RWKV_ERROR_ALLOC, nullptr, sm != nullptr, "Failed to allocate model");
+            sm->dm.device = device;
+            sm->path = src->path;
+            sm->layer_begin = src->layer_begin;
+            sm->layer_end = src->layer_end;
+            if (hipSetDevice(device) != hipSuccess || !upload_model(mf, sm->dm, src->layer_begin, src->layer_end)) {
+                free_model(sm->dm);
+                delete sm;
+                (void)hipSetDevice(src->dm.device);
+                CTX_CHECK(ctx, RWKV_ERROR_MODEL | RWKV_ERROR_ALLOC, nullptr, false, "Failed to upload the model to GPU %d",
+                          device);
+            }
+        } catch (const std::exception & e) {
+            if (sm) free_model(sm->dm);
+            delete sm;
+            CTX_CHECK(ctx, RWKV_ERROR_CTX | RWKV_ERROR_ALLOC, nullptr, false, "Failed to replicate %s: %s",
+                      src->path.c_str(), e.what());
+        }
+    }
+    rwkv_context * c = new_context(sm, n_threads);
+    (void)hipSetDevice(src->dm.device);
+    if (!c) {
+        if (it == g_replicas.end()) {
+            free_model(sm->dm);
+            delete sm;
+        }
+        ctx->last_error = ctx->last_error | RWKV_ERROR_CTX | RWKV_ERROR_ALLOC;
+        return nullptr;
+    }
+    c->print_errors = ctx->print_errors;
+    if (it == g_replicas.end()) g_replicas.emplace(replica_key(sm, device), sm);
+    return c;
+}
+
+RWKV_API int rwkv_mi355x_context_device(const struct rwkv_context * ctx) { return ctx ? ctx->model->dm.device : -1; }
 
 RWKV_API bool rwkv_eval(struct rwkv_context * ctx, const uint32_t token, const float * state_in, float * state_out,
                         float * logits_out) {
@@ -150,6 +234,7 @@ RWKV_API bool rwkv_eval(struct rwkv_context * ctx, const uint32_t token, const f
     CTX_CHECK(ctx, RWKV_ERROR_CTX | RWKV_ERROR_UNSUPPORTED, false, !ctx->model->dm.partial(),
               "This context holds layers [%u, %u) only (a pipeline stage): use rwkv_mi355x_eval_layers",
               ctx->model->dm.layer_lo, ctx->model->dm.layer_hi);
+    use_device(ctx);
     CTX_CHECK(ctx, RWKV_ERROR_CTX, false, ctx->engine->eval(&token, 1, state_in, state_out, logits_out), "GPU evaluation failed");
     return true;
 }
@@ -168,6 +253,7 @@ RWKV_API bool rwkv_eval_sequence(struct rwkv_context * ctx, const uint32_t * tok
         CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, tokens[i] < n_vocab, "Token at index %zu (%" PRIu32 ") is out of range (0 .. %zu)",
                   i, tokens[i], n_vocab - 1);
     }
+    use_device(ctx);
     CTX_CHECK(ctx, RWKV_ERROR_CTX, false, ctx->engine->eval(tokens, T, state_in, state_out, logits_out), "GPU evaluation failed");
     return true;
 }
@@ -208,6 +294,8 @@ RWKV_API void rwkv_free(struct rwkv_context * ctx) {
     delete ctx;
     std::lock_guard<std::mutex> lk(g_model_mutex);
     if (--sm->refcount == 0) {
+        auto it = g_replicas.find(replica_key(sm, sm->dm.device));
+        if (it != g_replicas.end() && it->second == sm) g_replicas.erase(it);
         (void)hipSetDevice(sm->dm.device);
         free_model(sm->dm);
         delete sm;
@@ -236,8 +324,48 @@ RWKV_API const char * rwkv_get_system_info_string(void) {
 
 // ------------------------------------------------------------------ additive extensions
 
-RWKV_API bool rwkv_mi355x_state_upload(struct rwkv_context * ctx, const float * state) { return ctx->engine->state_upload(state); }
-RWKV_API bool rwkv_mi355x_state_download(struct rwkv_context * ctx, float * state) { return ctx->engine->state_download(state); }
+RWKV_API bool rwkv_mi355x_state_upload(struct rwkv_context * ctx, const float * state) {
+    use_device(ctx);
+    return ctx->engine->state_upload(state);
+}
+RWKV_API bool rwkv_mi355x_state_download(struct rwkv_context * ctx, float * state) {
+    use_device(ctx);
+    return ctx->engine->state_download(state);
+}
+
+RWKV_API size_t rwkv_mi355x_layer_state_len(const struct rwkv_context * ctx) { return ctx->engine->layer_state_len(); }
+
+static bool layer_range_ok(rwkv_context * ctx, uint32_t l0, uint32_t l1) {
+    const uint32_t n = ctx->model->dm.n_layer;
+    CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, l0 < l1 && l1 <= n, "Bad layer range [%u, %u) for %u layers", l0, l1, n);
+    return true;
+}
+
+RWKV_API bool rwkv_mi355x_state_upload_layers(struct rwkv_context * ctx, const float * slice, uint32_t layer_begin,
+                                              uint32_t layer_end) {
+    ctx->last_error = RWKV_ERROR_NONE;
+    if (!layer_range_ok(ctx, layer_begin, layer_end)) return false;
+    use_device(ctx);
+    CTX_CHECK(ctx, RWKV_ERROR_CTX, false, ctx->engine->state_upload_layers(slice, layer_begin, layer_end),
+              "State upload failed");
+    return true;
+}
+
+RWKV_API bool rwkv_mi355x_state_download_layers(struct rwkv_context * ctx, float * slice, uint32_t layer_begin,
+                                                uint32_t layer_end) {
+    ctx->last_error = RWKV_ERROR_NONE;
+    if (!layer_range_ok(ctx, layer_begin, layer_end)) return false;
+    CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, slice != nullptr, "NULL state slice");
+    use_device(ctx);
+    CTX_CHECK(ctx, RWKV_ERROR_CTX, false, ctx->engine->state_download_layers(slice, layer_begin, layer_end),
+              "State download failed");
+    return true;
+}
+
+RWKV_API void rwkv_mi355x_state_io_bytes(const struct rwkv_context * ctx, double out[2]) {
+    out[0] = ctx->engine->io_bytes_h2d();
+    out[1] = ctx->engine->io_bytes_d2h();
+}
 
 RWKV_API bool rwkv_mi355x_eval_device(struct rwkv_context * ctx, const uint32_t * tokens, size_t T, bool compute_logits,
                                       float * logits_out, bool sync) {
@@ -247,6 +375,7 @@ RWKV_API bool rwkv_mi355x_eval_device(struct rwkv_context * ctx, const uint32_t 
               "This context holds layers [%u, %u) only (a pipeline stage)", ctx->model->dm.layer_lo, ctx->model->dm.layer_hi);
     for (size_t i = 0; i < T; i++)
         CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, tokens[i] < ctx->model->dm.n_vocab, "Token out of range");
+    use_device(ctx);
     CTX_CHECK(ctx, RWKV_ERROR_CTX, false, ctx->engine->eval_device(tokens, T, compute_logits || logits_out, logits_out, sync), "GPU evaluation failed");
     return true;
 }
@@ -269,6 +398,7 @@ static bool eval_layers(struct rwkv_context * ctx, const uint32_t * tokens, size
         CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, tokens != nullptr, "Tokens required at layer 0");
         for (size_t i = 0; i < T; i++) CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, tokens[i] < dm.n_vocab, "Token out of range");
     }
+    use_device(ctx);
     CTX_CHECK(ctx, RWKV_ERROR_CTX, false,
               ctx->engine->eval_layers(tokens, T, layer_begin, layer_end, x_dev, vfirst_dev, compute_logits, logits_out,
                                        sync),
@@ -306,6 +436,7 @@ static bool eval_batch(struct rwkv_context * ctx, const uint32_t * tokens, size_
     for (size_t i = 0; i < n; i++)
         CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, tokens[i] < dm.n_vocab, "Token at index %zu (%" PRIu32 ") is out of range",
                   i, tokens[i]);
+    use_device(ctx);
     CTX_CHECK(ctx, RWKV_ERROR_CTX, false, ctx->engine->eval_batch(tokens, n, state_in, state_out, logits_out, dev),
               "GPU evaluation failed");
     return true;
@@ -322,7 +453,10 @@ RWKV_API bool rwkv_mi355x_eval_batch_device(struct rwkv_context * ctx, const uin
 }
 
 
-RWKV_API bool rwkv_mi355x_sync(struct rwkv_context * ctx) { return ctx->engine->sync(); }
+RWKV_API bool rwkv_mi355x_sync(struct rwkv_context * ctx) {
+    use_device(ctx);
+    return ctx->engine->sync();
+}
 RWKV_API long long rwkv_mi355x_debug_buffer(struct rwkv_context * ctx, const char * name, void * out, size_t bytes) {
     return ctx && ctx->engine ? ctx->engine->debug_copy(name, out, bytes) : -1;
 }

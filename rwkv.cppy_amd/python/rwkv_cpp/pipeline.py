@@ -98,6 +98,60 @@ def pipeline_eval_sequence(stage_fn: StageFn, tokens: Sequence[int], chunk: int,
     return logits
 
 
+def layer_state_len(n_embed: int, arch_major: int, head_size: int = 64) -> int:
+    """Floats of one layer's state in the host layout (rwkv_graph.inc:545-606): v4 five [C] vectors,
+    v5+ token shifts [2][C] plus the heads' [H][S][S] wkv state."""
+    return 5 * n_embed if arch_major == 4 else n_embed * (2 + head_size)
+
+
+def scatter_state(full: Optional[np.ndarray], n_layer: int, layer_len: int, rank: int, world: int,
+                  group=None, wire_device: Optional[torch.device] = None) -> Optional[np.ndarray]:
+    """Rank 0 holds a whole host state (None: fresh states everywhere, nothing is sent); every rank
+    returns only its stage's slice, layers stage_layers(n_layer, world, rank) -- rank r receives
+    (l1 - l0) * layer_len floats and nothing else.  Returns None for a fresh state."""
+    wire = wire_device or torch.device('cpu')
+    fresh = torch.tensor([1 if full is None else 0], dtype=torch.int32, device=wire)
+    dist.broadcast(fresh, src=0, group=group)
+    if int(fresh.item()):
+        return None
+    l0, l1 = stage_layers(n_layer, world, rank)
+    if rank == 0:
+        if full.size != n_layer * layer_len:
+            raise ValueError(f'state has {full.size} floats, expected {n_layer * layer_len}')
+        sends = []
+        for r in range(1, world):
+            a, b = stage_layers(n_layer, world, r)
+            t = torch.from_numpy(np.ascontiguousarray(full[a * layer_len:b * layer_len])).to(wire)
+            sends.append((dist.isend(t, dst=r, group=group), t))
+        for w, _ in sends:
+            w.wait()
+        return np.ascontiguousarray(full[l0 * layer_len:l1 * layer_len])
+    buf = torch.empty((l1 - l0) * layer_len, dtype=torch.float32, device=wire)
+    dist.recv(buf, src=0, group=group)
+    return buf.cpu().numpy()
+
+
+def gather_state(part: np.ndarray, n_layer: int, layer_len: int, rank: int, world: int, group=None,
+                 wire_device: Optional[torch.device] = None) -> Optional[np.ndarray]:
+    """Inverse of scatter_state: every rank sends its stage's slice to rank 0, which returns the
+    whole state (None elsewhere)."""
+    wire = wire_device or torch.device('cpu')
+    l0, l1 = stage_layers(n_layer, world, rank)
+    if part.size != (l1 - l0) * layer_len:
+        raise ValueError(f'rank {rank}: slice has {part.size} floats, expected {(l1 - l0) * layer_len}')
+    if rank != 0:
+        dist.send(torch.from_numpy(np.ascontiguousarray(part, dtype=np.float32)).to(wire), dst=0, group=group)
+        return None
+    full = np.empty(n_layer * layer_len, np.float32)
+    full[l0 * layer_len:l1 * layer_len] = part
+    for r in range(1, world):
+        a, b = stage_layers(n_layer, world, r)
+        buf = torch.empty((b - a) * layer_len, dtype=torch.float32, device=wire)
+        dist.recv(buf, src=r, group=group)
+        full[a * layer_len:b * layer_len] = buf.cpu().numpy()
+    return full
+
+
 def model_n_layer(path: str) -> int:
     """n_layer from an rwkv.cpp file header (docs/FILE_FORMAT.md: magic, version, n_vocab, n_embed,
     n_layer, data_type as uint32)."""
@@ -147,6 +201,29 @@ class LibraryStage:
         ptr = None if state is None else state.ctypes.data
         if not self.lib.library.rwkv_mi355x_state_upload(self.ctx.ptr, ptr):
             raise ValueError('state upload failed')
+
+    def layer_range(self, world: int, rank: int) -> Tuple[int, int]:
+        return stage_layers(self.lib.library.rwkv_get_n_layer(self.ctx.ptr), world, rank)
+
+    def upload_state_slice(self, part: Optional[np.ndarray], l0: int, l1: int) -> None:
+        """Only layers [l0, l1) of the state cross PCIe (part = those layers, host layout; None =
+        fresh), rwkv_mi355x_state_upload_layers."""
+        if part is not None:
+            part = np.ascontiguousarray(part, dtype=np.float32)
+            n = (l1 - l0) * self.lib.library.rwkv_mi355x_layer_state_len(self.ctx.ptr)
+            if part.size != n:
+                raise ValueError(f'slice has {part.size} floats, expected {n}')
+        ok = self.lib.library.rwkv_mi355x_state_upload_layers(self.ctx.ptr, None if part is None else part.ctypes.data,
+                                                             l0, l1)
+        if not ok:
+            raise ValueError(f'state upload of layers [{l0}, {l1}) failed')
+
+    def download_state_slice(self, l0: int, l1: int) -> np.ndarray:
+        n = (l1 - l0) * self.lib.library.rwkv_mi355x_layer_state_len(self.ctx.ptr)
+        out = np.empty(n, np.float32)
+        if not self.lib.library.rwkv_mi355x_state_download_layers(self.ctx.ptr, out.ctypes.data, l0, l1):
+            raise ValueError(f'state download of layers [{l0}, {l1}) failed')
+        return out
 
     def __call__(self, tokens: np.ndarray, l0: int, l1: int, x: torch.Tensor, want_logits: bool):
         import ctypes

@@ -11,7 +11,7 @@ import ctypes
 import os
 import pathlib
 import sys
-from typing import List, Optional
+from typing import Tuple, List, Optional
 
 QUANTIZED_FORMAT_NAMES = ('Q4_0', 'Q4_1', 'Q5_0', 'Q5_1', 'Q8_0')
 
@@ -109,6 +109,18 @@ class RWKVSharedLibrary:
                                                ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                                ctypes.POINTER(ctypes.c_double)]
         L.rwkv_mi355x_kernel_stats.restype = ctypes.c_int
+        L.rwkv_mi355x_layer_state_len.argtypes = [vp]
+        L.rwkv_mi355x_layer_state_len.restype = sz
+        L.rwkv_mi355x_state_upload_layers.argtypes = [vp, vp, u32, u32]
+        L.rwkv_mi355x_state_upload_layers.restype = ctypes.c_bool
+        L.rwkv_mi355x_state_download_layers.argtypes = [vp, vp, u32, u32]
+        L.rwkv_mi355x_state_download_layers.restype = ctypes.c_bool
+        L.rwkv_mi355x_state_io_bytes.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]
+        L.rwkv_mi355x_state_io_bytes.restype = None
+        L.rwkv_mi355x_clone_context_on.argtypes = [vp, u32, ctypes.c_int]
+        L.rwkv_mi355x_clone_context_on.restype = vp
+        L.rwkv_mi355x_context_device.argtypes = [vp]
+        L.rwkv_mi355x_context_device.restype = ctypes.c_int
 
         self.nullptr = ctypes.cast(0, ctypes.c_void_p)
 
@@ -183,6 +195,20 @@ class RWKVSharedLibrary:
         if not self.library.rwkv_mi355x_eval_batch(ctx.ptr, ctypes.cast(arr, ctypes.c_void_p), len(tokens),
                                                    state_in_address, state_out_address, logits_out_address):
             raise ValueError('rwkv_mi355x_eval_batch failed, check stderr')
+
+    # ---- additive: replicas on other GPUs and per-layer state slices ------------------------
+    def rwkv_mi355x_clone_context_on(self, ctx: RWKVContext, thread_count: int, device: int) -> RWKVContext:
+        """rwkv_clone_context onto GPU `device` (the model is uploaded once per GPU)."""
+        ptr = self.library.rwkv_mi355x_clone_context_on(ctx.ptr, thread_count, device)
+        if ptr is None:
+            raise ValueError(f'rwkv_mi355x_clone_context_on(device={device}) failed, check stderr')
+        return RWKVContext(ptr)
+
+    def rwkv_mi355x_state_io_bytes(self, ctx: RWKVContext) -> Tuple[float, float]:
+        """State bytes this context moved so far: (host->device, device->host)."""
+        out = (ctypes.c_double * 2)()
+        self.library.rwkv_mi355x_state_io_bytes(ctx.ptr, out)
+        return out[0], out[1]
 
     def rwkv_get_system_info_string(self) -> str:
         return self.library.rwkv_get_system_info_string().decode('utf-8')

@@ -163,3 +163,66 @@ def test_stage_context_rejects_whole_model_calls(tmp_path):
     assert lib.rwkv_mi355x_eval_layers(ptr, t.ctypes.data, 3, 1, 3, x.data_ptr(), None, False, None)
     assert lib.rwkv_get_last_error(ptr) == 0
     lib.rwkv_free(ptr)
+
+
+def _slice_rank_main(rank, world, port, path, toks, chunk, out_dir, mid_path):
+    import sys
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.join(os.path.dirname(LIB_PATH), '..', 'python'))
+    from rwkv_cpp import RWKVSharedLibrary
+    from rwkv_cpp.pipeline import (LibraryStage, gather_state, model_n_layer, pipeline_eval_sequence, scatter_state,
+                                   stage_layers)
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        L = RWKVSharedLibrary(LIB_PATH)
+        stage = LibraryStage.from_file(L, path, rank, world, async_=True)
+        n_layer, C = model_n_layer(path), L.rwkv_get_n_embed(stage.ctx)
+        per = L.library.rwkv_mi355x_layer_state_len(stage.ctx.ptr)
+        l0, l1 = stage_layers(n_layer, world, rank)
+        mid = np.load(mid_path) if rank == 0 else None
+        part = scatter_state(mid, n_layer, per, rank, world)
+        stage.upload_state_slice(part, l0, l1)
+        lg = pipeline_eval_sequence(stage, toks, chunk, n_layer, C, stage.planes, rank, world,
+                                    torch.device('cuda', 0), wire_device=torch.device('cpu'))
+        whole = gather_state(stage.download_state_slice(l0, l1), n_layer, per, rank, world)
+        np.save(os.path.join(out_dir, f'io{rank}.npy'), np.array(L.rwkv_mi355x_state_io_bytes(stage.ctx)))
+        if whole is not None:
+            np.save(os.path.join(out_dir, 'state.npy'), whole)
+        if lg is not None:
+            np.save(os.path.join(out_dir, 'logits.npy'), lg)
+        L.rwkv_free(stage.ctx)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('arch,fmt,world', [(6, 'Q4_0', 2), (7, 'Q5_1', 3)])
+def test_pipeline_stages_move_only_their_state_slice(tmp_path, arch, fmt, world):
+    """starting from a mid-sequence host state held by rank 0, each stage receives,
+    uploads and downloads ONLY its layers' state slice (rwkv_mi355x_state_{upload,download}_layers;
+    the context's PCIe byte counters equal the slice size), and the gathered final state and the
+    logits equal one rwkv_eval_sequence from that state bit for bit."""
+    import torch.multiprocessing as mp
+    L = library()
+    p = _synthetic(tmp_path, arch, fmt, 5, 2048)
+    rng = np.random.default_rng(12)
+    pre = [int(t) for t in rng.integers(0, 1024, 9)]
+    toks = [int(t) for t in rng.integers(0, 1024, 40)]
+    m = RWKVModel(L, p)
+    _, mid = m.eval_sequence(pre, None, use_numpy=True)
+    ref_lg, ref_st = m.eval_sequence(toks, mid, use_numpy=True)
+    n_layer = L.rwkv_get_n_layer(m._ctx)
+    per = L.library.rwkv_mi355x_layer_state_len(m._ctx.ptr)
+    assert per * n_layer == len(mid)
+    m.free()
+    mid_path = str(tmp_path / 'mid.npy')
+    np.save(mid_path, mid)
+    mp.start_processes(_slice_rank_main, args=(world, _free_port(), p, toks, 16, str(tmp_path), mid_path),
+                       nprocs=world, start_method='spawn', join=True)
+    assert np.array_equal(np.load(tmp_path / 'logits.npy').view(np.uint32), ref_lg.view(np.uint32))
+    assert np.array_equal(np.load(tmp_path / 'state.npy').view(np.uint32), ref_st.view(np.uint32))
+    from rwkv_cpp.pipeline import stage_layers
+    for r in range(world):
+        l0, l1 = stage_layers(n_layer, world, r)
+        h2d, d2h = np.load(tmp_path / f'io{r}.npy')
+        assert h2d == d2h == (l1 - l0) * per * 4, (r, h2d, d2h)

@@ -16,7 +16,8 @@ from oracle_ctypes import OracleModel
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, 'rwkv.cppy_amd', 'python'))
-from rwkv_cpp.pipeline import pipeline_eval_sequence, stage_layers  # noqa: E402
+from rwkv_cpp.pipeline import (gather_state, layer_state_len, pipeline_eval_sequence, scatter_state,  # noqa: E402
+                               stage_layers)
 
 GOLD = os.path.join(REPO, 'tests', 'golden')
 MODELS = ['tiny-rwkv-4v0-660K-FP32.bin', 'tiny-rwkv-5v2-730K-FP32.bin', 'tiny-rwkv-6v0-3m-Q5_0.bin',
@@ -116,3 +117,51 @@ def test_pipeline_gloo_matches_whole_sequence(model, world, chunk, tmp_path):
         l0, l1 = stage_layers(m.n_layer, world, r)
         got = np.load(tmp_path / f'state{r}.npy')
         assert np.array_equal(got.view(np.uint32), ref_st[sl(l0, l1)].view(np.uint32)), f'rank {r} state slice'
+
+
+def _slice_rank_main(rank, world, port, path, chunk, out_dir):
+    """Rank 0 owns a whole (non-fresh) state; each stage receives only its slice, runs the pipeline
+    from it, and the final slices are gathered back on rank 0."""
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        stage = OracleStage(path)
+        m = stage.m
+        per = layer_state_len(m.n_embed, m.arch_major, m.head_size)
+        full = None
+        if rank == 0:
+            _, full = m.eval_sequence(TOKENS[:7])  # a real mid-sequence state
+        part = scatter_state(full, m.n_layer, per, rank, world)
+        l0, l1 = stage_layers(m.n_layer, world, rank)
+        np.save(os.path.join(out_dir, f'recv{rank}.npy'), part)
+        stage.state[l0 * per:l1 * per] = part  # only this stage's layers are ever read
+        planes = 2 if m.arch_major == 7 else 1
+        lg = pipeline_eval_sequence(stage, TOKENS[7:], chunk, m.n_layer, m.n_embed, planes, rank, world,
+                                    torch.device('cpu'))
+        whole = gather_state(stage.state[l0 * per:l1 * per], m.n_layer, per, rank, world)
+        if rank == 0:
+            np.save(os.path.join(out_dir, 'state.npy'), whole)
+        if lg is not None:
+            np.save(os.path.join(out_dir, 'logits.npy'), lg)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('model,world,chunk', [(MODELS[2], 2, 4), (MODELS[3], 3, 6), (MODELS[0], 2, 16)])
+def test_pipeline_state_slices_scatter_gather(model, world, chunk, tmp_path):
+    """Each stage moves exactly its own state slice (stage_layers), and a pipeline started from a
+    scattered mid-sequence state and gathered back equals one whole-sequence evaluation."""
+    path = os.path.join(GOLD, model)
+    mp.start_processes(_slice_rank_main, args=(world, _free_port(), path, chunk, str(tmp_path)), nprocs=world,
+                       start_method='spawn', join=True)
+    m = OracleModel(path)
+    _, mid = m.eval_sequence(TOKENS[:7])
+    ref_lg, ref_st = m.eval_sequence(TOKENS[7:], state_in=mid)
+    per = layer_state_len(m.n_embed, m.arch_major, m.head_size)
+    for r in range(world):
+        l0, l1 = stage_layers(m.n_layer, world, r)
+        got = np.load(tmp_path / f'recv{r}.npy')
+        assert got.size == (l1 - l0) * per, f'rank {r} received {got.size} floats'
+        assert np.array_equal(got.view(np.uint32), mid[l0 * per:l1 * per].view(np.uint32))
+    assert np.array_equal(np.load(tmp_path / 'state.npy').view(np.uint32), ref_st.view(np.uint32))
+    assert np.array_equal(np.load(tmp_path / 'logits.npy').view(np.uint32), ref_lg.view(np.uint32))

@@ -97,8 +97,10 @@ int main(int argc, char ** argv) {
             if (path == 0) ref = out;
             const bool same = !memcmp(ref.data(), out.data(), out.size() * 4);
             const double us = ms * 1e3 / reps, ops = 2.0 * s.M * s.K * T;
-            printf("%-26s %-14s %9.1f us  %7.1f TOPS  %s\n", s.name, path == 2 ? "k_mm" : path ? "qgemm-generic" : "qgemm",
-                   us, ops / us * 1e-6, path && path < 2 ? (same ? "bit-identical" : "DIFFERENT") : "");
+            unsigned long long h = 1469598103934665603ull;
+            for (float f : out) h = (h ^ __builtin_bit_cast(uint32_t, f)) * 1099511628211ull;
+            printf("%-26s %-14s %9.1f us  %7.1f TOPS  %s  hash %016llx\n", s.name, path == 2 ? "k_mm" : path ? "qgemm-generic" : "qgemm",
+                   us, ops / us * 1e-6, path && path < 2 ? (same ? "bit-identical" : "DIFFERENT") : "", h);
         }
     }
     return 0;

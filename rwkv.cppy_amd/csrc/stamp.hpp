@@ -4,7 +4,8 @@
 // expands every macro to nothing.  Each instrumented workgroup takes a slot in a per-CU ring
 // (one atomic on its CU's own counter at kernel start, so WGs never contend across CUs) and
 // thread 0 writes {start, mid, end, tag} with s_memrealtime (100 MHz, one clock for the whole
-// chip).  mid = the kernel's "inputs ready" point (after its first dependent wait).  The
+// chip) plus, in the tag word's top 20 bits, the shader-clock cycles (s_memtime) from start to
+// end, so tools/stamp_run.py reports the clock the chain runs at.  mid = the kernel's "inputs ready" point (after its first dependent wait).  The
 // engine dumps the rings to $RWKV_STAMP_OUT when the context is freed; tools/stamp_summary.py
 // splits them into launches by time order.
 #pragma once
@@ -40,6 +41,7 @@ __device__ __forceinline__ unsigned stamp_cu() {
     __shared__ unsigned long long stamp_x_[4];                                    \
     if (threadIdx.x < 4) stamp_x_[threadIdx.x] = 0;                               \
     unsigned long long stamp_t0_ = __builtin_amdgcn_s_memrealtime();              \
+    const unsigned long long stamp_c0_ = __builtin_amdgcn_s_memtime();            \
     unsigned long long stamp_t1_ = 0;                                             \
     unsigned stamp_slot_ = 0, stamp_cu_ = 0;                                      \
     if (threadIdx.x == 0 && g_stampctl.ctr) {                                     \
@@ -68,7 +70,8 @@ __device__ __forceinline__ unsigned stamp_cu() {
             r_[0] = stamp_t0_;                                                                           \
             r_[1] = stamp_t1_;                                                                           \
             r_[2] = __builtin_amdgcn_s_memrealtime();                                                    \
-            r_[3] = ((unsigned long long)(kid) << 32) | blockIdx.x;                                      \
+            const unsigned long long cyc_ = (__builtin_amdgcn_s_memtime() - stamp_c0_) & 0xFFFFFull;    \
+            r_[3] = (cyc_ << 44) | ((unsigned long long)(kid) << 32) | blockIdx.x;                      \
             for (int q_ = 0; q_ < 4; q_++) r_[4 + q_] = stamp_x_[q_];                                    \
         }                                                                                                \
     } while (0)

@@ -21,3 +21,6 @@ cp "$SRC/tiny-rwkv-6v0-3m-Q5_0.bin" "$SRC/tiny-rwkv-6v0-3m-Q5_1.bin" "$SRC/tiny-
 for q in FP16-to-Q4_1 FP16-to-Q5_0 FP16-to-Q5_1 FP32-to-Q4_0 FP32-to-Q4_1; do
   cp "$SRC/tiny-rwkv-6v0-3m-$q.bin" "$DST/"
 done
+# The World tokenizer's vocabulary (a data file the reference's tokenizer test reads,
+# python/rwkv_cpp/rwkv_world_tokenizer.test.py), so the harness tests run on the GPU box too.
+cp "$SRC/../python/rwkv_cpp/rwkv_vocab_v20230424.txt" "$DST/"

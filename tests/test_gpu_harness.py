@@ -50,3 +50,44 @@ def test_perplexity_and_greedy_generation_match_oracle(name):
     assert (loss, ppl, n) == (oloss, oppl, on)
     assert greedy(m) == gen_o
     m.free()
+
+
+def test_world_tokenizer_generation_on_gpu(tmp_path):
+    """The whole World-model harness on the GPU box: the reference's tokenizer vector text is
+    tokenized with the World vocabulary (the reference's data file, tests/golden), a synthetic
+    World-vocabulary v6 model (n_vocab 65536) evaluates the prompt and generates 12 tokens greedily
+    through the unchanged RWKVModel interface, and every logit and chosen token equals the
+    GPU-association oracle's; the generated ids decode back to text."""
+    from rwkv_cpp.world_tokenizer import WorldTokenizer
+    tok = WorldTokenizer(os.path.join(GOLD, 'rwkv_vocab_v20230424.txt'))
+    text = 'I\'ll \'d test блабла 以下は、]) -> <|endoftext|><|padding|> int'
+    ids = tok.encode(text)
+    assert ids[:4] == [74, 5229, 274, 101]
+    L = library()
+    p = str(tmp_path / 'world-v6.bin')
+    assert L.library.rwkv_mi355x_write_synthetic_model(p.encode(), 6, 65536, 256, 3, 0, b'Q5_1', 11)
+    m = RWKVModel(L, p)
+    set_variant(VARIANT_GPU)
+    try:
+        o = OracleAsModel(p)
+
+        def run(model):
+            logits, state = model.eval(ids[0], None, None, None, use_numpy=True)
+            for t in ids[1:]:
+                logits, state = model.eval(t, state, state, logits, use_numpy=True)
+            out, lgs = [], [logits.copy()]
+            for _ in range(12):
+                t = sampling.sample_logits(logits, temperature=0.0)
+                out.append(t)
+                logits, state = model.eval(t, state, state, logits, use_numpy=True)
+                lgs.append(logits.copy())
+            return out, np.stack(lgs)
+
+        gen_o, lg_o = run(o)
+    finally:
+        set_variant(0)
+    gen, lg = run(m)
+    m.free()
+    assert gen == gen_o
+    assert np.array_equal(lg.view(np.uint32), lg_o.view(np.uint32))
+    assert isinstance(tok.decode([t for t in gen if t in tok.index_to_token]), str)

@@ -2,8 +2,8 @@
 perplexity loop (rwkv.cppy_amd/python/rwkv_cpp/{world_tokenizer,sampling,perplexity}.py).
 
 Pins: the reference's tokenizer test vector (python/rwkv_cpp/rwkv_world_tokenizer.test.py:4-17,
-restated; the vocabulary is read from the reference checkout when it is present, and is not
-copied here); the perplexity loop over the CPU oracle, against a direct restatement of
+restated; the vocabulary is the reference's data file, copied to tests/golden by
+golden/fetch_fixtures.sh); the perplexity loop over the CPU oracle, against a direct restatement of
 measure_pexplexity.py:73-109's arithmetic.
 """
 import os
@@ -17,10 +17,9 @@ from rwkv_cpp import perplexity, sampling
 from rwkv_cpp.world_tokenizer import WorldTokenizer
 
 GOLD = os.path.join(os.path.dirname(__file__), 'golden')
-VOCAB = os.environ.get('RWKV_WORLD_VOCAB', '/root/reference/python/rwkv_cpp/rwkv_vocab_v20230424.txt')
+VOCAB = os.environ.get('RWKV_WORLD_VOCAB', os.path.join(GOLD, 'rwkv_vocab_v20230424.txt'))
 
 
-@pytest.mark.skipif(not os.path.isfile(VOCAB), reason='World vocabulary not available')
 def test_world_tokenizer_reference_vector():
     t = WorldTokenizer(VOCAB)
     text = 'I\'ll \'d test блабла 以下は、]) -> <|endoftext|><|padding|> int'

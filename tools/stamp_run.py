@@ -34,7 +34,7 @@ lib.rwkv_free(ctx)
 
 r = np.fromfile(out, dtype=np.uint64).reshape(-1, 8)
 r = r[np.argsort(r[:, 0], kind='stable')]
-kid = ((r[:, 3] >> 32) & 15).astype(np.int64)
+kid = ((r[:, 3] >> 32) & 15).astype(np.int64)  # kid bits 32..43, cycles 44..63
 names = {1: 'k_mva', 2: 'k_mv', 3: 'att6', 5: 'embed'}
 # launches: runs of equal kernel id in start order
 cuts = np.flatnonzero(np.diff(kid) != 0) + 1
@@ -63,6 +63,9 @@ for s in segs[a:b]:
         ok = xq > 0
         if ok.any():
             xs += f'  x{q} {np.percentile((xq[ok] - t0[ok]) / 100, 50):5.2f}'
+    cyc = (r[s, 3] >> 44).astype(np.float64)
+    ghz = np.percentile(cyc / np.maximum(dur * 1e3, 1e-9), 50)  # cycles per ns
     print(f'{nm:10s} {len(s):5d} {gap:6.2f} {(t0.max() - first) / 100:6.2f} {np.percentile(mid, 50):6.2f} '
-          f'{np.percentile(mid, 90):6.2f} {np.percentile(dur, 50):6.2f} {np.percentile(dur, 90):6.2f} {span:6.2f}{xs}')
+          f'{np.percentile(mid, 90):6.2f} {np.percentile(dur, 50):6.2f} {np.percentile(dur, 90):6.2f} {span:6.2f}'
+          f'  {ghz:4.2f}GHz{xs}')
     prev_end = last

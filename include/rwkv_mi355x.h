@@ -160,6 +160,10 @@ RWKV_API bool rwkv_mi355x_selftest_matmul(int wtype, const void * W, int K, int 
 // Self-test of the sequence GEMM: the same product as rwkv_mi355x_selftest_matmul computed by
 // the int8-MFMA kernel (quantized weight types only; T >= 2).
 RWKV_API bool rwkv_mi355x_selftest_gemm(int wtype, const void * W, int K, int M, const float * x, int T, float * y);
+/* The same with the GEMM's split-K form forced: split 1 = one workgroup per tile, 4 / 8 = the class
+ * tree in that many subtrees on as many workgroups plus the combine kernel (same bits). */
+RWKV_API bool rwkv_mi355x_selftest_gemm_split(int wtype, const void * W, int K, int M, const float * x, int T,
+                                              float * y, int split);
 
 #if defined(__cplusplus)
 }

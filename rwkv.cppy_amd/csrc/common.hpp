@@ -116,6 +116,8 @@ struct MMEntry {
     int epi;
     int block0;         // first workgroup of this entry
     int fuse_emit;      // qgemm: the epilogue emits `out` (Q8_0 tiles) itself; y is not written
+    size_t poff;        // qgemm split-K: this entry's partials at part + poff ([S][T][M], _1: twice)
+    int cblock0;        // qgemm split-K: first workgroup of this entry in the combine launch
 };
 
 constexpr int MM_MAX_ENTRIES = 8;
@@ -124,8 +126,9 @@ struct MMGroup {
     MMEntry e[MM_MAX_ENTRIES];
     int n;
     int T;
-    float * part;        // split-K partials (qgemm.hip, single small-M entries): QG_SPLIT x T x M floats
+    float * part;        // split-K partials (qgemm.hip): up to 8 x T x sum(M) floats (x2 for _1 formats)
     size_t part_floats;
+    int split;           // qgemm split-K: 0 = by tile count, 1 = never, 4 / 8 = forced
 };
 
 #define HIP_OK(x)                                                                             \

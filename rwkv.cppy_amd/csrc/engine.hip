@@ -591,6 +591,9 @@ bool Engine::mm_dispatch(MMGroup & g, int wtype) {
     // take the int8-MFMA sequence GEMM on token tiles instead (tile_acts_; also the same bits)
     if (bs_ && !(tile_acts_ && wtype_quantized(wtype))) {
         bool launched = false;
+        // float weights (the F16 head, LoRA) over 16+ contexts: the f32-MFMA form, same bits
+        if (!launch_fmm_group(stream_, g, wtype, &launched)) return false;
+        if (launched) return true;
         if (!launch_mvb_group(stream_, g, wtype, &launched)) return false;
         if (launched) return true;
         return launch_mm_group(stream_, g, wtype);
@@ -612,24 +615,32 @@ bool Engine::mm_dispatch(MMGroup & g, int wtype) {
         }
         gy_cap_ = need;
     }
-    // split-K partials for a single small-M entry (launch_qgemm decides)
-    if (g.n == 1 && g.e[0].W.M <= 256) {
-        const size_t pneed = (size_t)8 * g.T * g.e[0].W.M;
-        if (pneed > part_cap_) {
-            HIP_OK(hipStreamSynchronize(stream_));
-            drop_batch_graphs();
-            if (part_) (void)hipFree(part_);
-            part_ = nullptr;
-            part_cap_ = 0;
-            if (hipMalloc(&part_, pneed * 4 + 64) != hipSuccess) {
-                part_ = nullptr;
-                (void)hipGetLastError();
-                return false;
-            }
-            part_cap_ = pneed;
+    // split-K partials (launch_qgemm splits groups with few tiles: small T or small M)
+    {
+        const int rows = qg_rows(wtype), tilesT = (g.T + QG_TOK - 1) / QG_TOK;
+        size_t msum = 0, tiles = 0;
+        for (int i = 0; i < g.n; i++) {
+            msum += g.e[i].W.M;
+            tiles += (size_t)(g.e[i].W.M + rows - 1) / rows * tilesT;
         }
-        g.part = part_;
-        g.part_floats = part_cap_;
+        if (tiles < 1024) {
+            const size_t pneed = (size_t)8 * g.T * msum * (qg_one(wtype) ? 2 : 1);
+            if (pneed > part_cap_) {
+                HIP_OK(hipStreamSynchronize(stream_));
+                drop_batch_graphs();
+                if (part_) (void)hipFree(part_);
+                part_ = nullptr;
+                part_cap_ = 0;
+                if (hipMalloc(&part_, pneed * 4 + 64) != hipSuccess) {
+                    part_ = nullptr;
+                    (void)hipGetLastError();
+                    return false;
+                }
+                part_cap_ = pneed;
+            }
+            g.part = part_;
+            g.part_floats = part_cap_;
+        }
     }
     size_t off = 0;
     for (int i = 0; i < g.n; i++) {

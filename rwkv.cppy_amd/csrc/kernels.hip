@@ -334,6 +334,9 @@ bool launch_mm_group(hipStream_t st, MMGroup & g, int wtype) {
         const char * v = getenv("RWKV_MI355X_MM_SMALL");  // 0: small-K float matmuls on k_mm too
         return !(v && v[0] == '0');
     }();
+    bool fmm = false;
+    if (!launch_fmm_group(st, g, wtype, &fmm)) return false;
+    if (fmm) return true;
     if (small_on && launch_mm_small(st, g, wtype)) return true;
     switch (wtype) {
         case W_F32: return launch_mm_wf<W_F32>(st, g);

@@ -11,6 +11,8 @@ bool launch_mm_group(hipStream_t st, MMGroup & g, int wtype);
 // int8-MFMA sequence GEMM for quantized weights (qgemm.hip); same results as launch_mm_group.
 // Every entry needs y; emission is left to the caller (launch_act_from_f32).
 bool launch_qgemm(hipStream_t st, MMGroup & g, int wtype);
+// F16 / F32 weights over T >= 16 tokens on the f32 MFMA (mv_fmfma.hip); *launched = false: not covered
+bool launch_fmm_group(hipStream_t st, MMGroup & g, int wtype, bool * launched);
 // Batched decode matvec (mv_batch.hip): the T rows are T independent contexts; same results as
 // launch_mm_group.  *launched = false (and nothing enqueued) for shapes it does not cover.
 bool launch_mvb_group(hipStream_t st, MMGroup & g, int wtype, bool * launched);

@@ -34,7 +34,11 @@ int mva_rows() {
     }();
     return v;
 }
-void set_mv_device_cus(int n) { g_mv_cus = n > 0 ? n : 256; }
+extern int kQgCUs;
+void set_mv_device_cus(int n) {
+    g_mv_cus = n > 0 ? n : 256;
+    kQgCUs = g_mv_cus;
+}
 
 bool launch_mv_group(hipStream_t st, MVGroup & g) {
     bool emit = false;

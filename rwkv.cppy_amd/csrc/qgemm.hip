@@ -95,12 +95,12 @@ struct QGLayout {
 // rem = nb%64; step s of the walk is block l + 64 u.  Scalar state, advanced one step at a time.
 struct QGWalk {
     int q, rem, l, u, n;
-    __device__ __forceinline__ void init(int nb) {
+    __device__ __forceinline__ void init(int nb, int l0 = 0) {
         q = nb >> 6;
         rem = nb & 63;
-        l = 0;
+        l = l0;
         u = 0;
-        n = q + (rem > 0 ? 1 : 0);
+        n = q + (l0 < rem ? 1 : 0);
     }
     __device__ __forceinline__ int block() const { return l + 64 * u; }
     __device__ __forceinline__ void next() {
@@ -115,13 +115,13 @@ struct QGWalk {
 // This wave's share of chunk c: steps 8c + wave and 8c + wave + 4 (the walk is at the first of
 // them and is left at 8(c+1) + wave).
 template <int WF>
-__device__ __forceinline__ void qg_load_chunk(v4i_t rw, v4i_t ra, unsigned lds_buf, int c, QGWalk & wk, int nb,
+__device__ __forceinline__ void qg_load_chunk(v4i_t rw, v4i_t ra, unsigned lds_buf, int c, QGWalk & wk, int nsteps,
                                               int wave, int lane) {
     using Lt = QGLayout<WF>;
 #pragma unroll
     for (int h2 = 0; h2 < 2; h2++) {
         const int k = wave + 4 * h2;
-        if (c * QG_STEPS + k < nb) {
+        if (c * QG_STEPS + k < nsteps) {
             const int b = wk.block();
             const unsigned m = lds_buf + k * Lt::STEP;
             qg_record<Lt::WB>(rw, (unsigned)(b * Lt::WB), m, lane);
@@ -302,6 +302,28 @@ __device__ __forceinline__ void qg_store(const MMEntry & E, int T, int M, int to
         }
 }
 
+// Split-K: one split's subtree sums to its entry's partials [S][T][M] (_1 formats: the m*s
+// subtree sums follow as a second [S][T][M] array)
+template <bool ONE, int TI, int SPLIT>
+__device__ __forceinline__ void qg_store_part(float * part, int sidx, int T, int M, int tok0, int row0, int wt, int wr,
+                                              int r16, int h, const float (&sub)[TI][2][4], const float (&sub2)[TI][2][4]) {
+#pragma unroll
+    for (int i = 0; i < TI; i++)
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            const int t = tok0 + wt + 16 * j + r16;
+            const int m0 = row0 + wr + 16 * i + 4 * h;
+            if (t >= T) continue;
+            float * pp = part + ((size_t)sidx * T + t) * M + m0;
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                if (m0 + q < M) {
+                    pp[q] = sub[i][j][q];
+                    if constexpr (ONE) pp[(size_t)SPLIT * T * M + q] = sub2[i][j][q];
+                }
+        }
+}
+
 // Class-pair fold: the odd class (in c) closes N >= 1 levels of the binary counter: v = c, then
 // v = st[k] + v for k < N, into st[N] (N < 6) or the total (N = 6)
 template <bool ONE, int TI, int N>
@@ -332,17 +354,17 @@ __device__ __forceinline__ void qg_fold(float (&st)[6][TI][2][4], float (&st2)[6
 // as k_qgemm with the step bookkeeping resolved at compile time -- each 8-step chunk is
 // straight-line code (the class-pair folds after steps 1, 3, 5 close 1, 2, 1 levels; after step
 // 7, 3 + ctz(~chunk) levels), and the copy walk is blocks 8c + wave, 8c + wave + 4.
-// SPLIT > 1 (split-K for small M, _0 formats): workgroup s of a tile runs chunks
+// SPLIT > 1 (split-K when a group has few tiles): workgroup s of a tile runs chunks
 // [s * NCHL, (s + 1) * NCHL) -- a complete subtree of the perfect binary tree over the 64 classes --
-// and stores that subtree sum to g.part; k_qg_combine adds the SPLIT subtrees with the tree's top
-// levels and applies the epilogue, so results equal the unsplit kernel bit for bit.
+// and stores that subtree sum (and, _1 formats, the m*s subtree) to its entry's partials;
+// k_qg_combine adds the SPLIT subtrees with the tree's top levels and applies the epilogue (and
+// the emission), so results equal the unsplit kernel bit for bit.
 template <int WF, int SPLIT = 1>
 __global__ __launch_bounds__(256) void k_qgemm_k64(MMGroup g) {
     using Lt = QGLayout<WF>;
     constexpr bool ONE = Lt::ONE;
     constexpr int TI = Lt::TI;
     constexpr int NB = 64, NCH = NB / QG_STEPS, NCHL = NCH / SPLIT;
-    static_assert(SPLIT == 1 || !ONE, "split-K: _0 formats only");
     __shared__ __attribute__((aligned(16))) char smem[2][Lt::BUF];
     int e = 0;
 #pragma unroll 1
@@ -414,38 +436,50 @@ __global__ __launch_bounds__(256) void k_qgemm_k64(MMGroup g) {
     } else {
         // the subtree over this split's 8 * NCHL classes sits at level 3 + log2(NCHL)
         constexpr int LEV = NCHL == 1 ? 3 : NCHL == 2 ? 4 : 5;
-#pragma unroll
-        for (int i = 0; i < TI; i++)
-#pragma unroll
-            for (int j = 0; j < 2; j++) {
-                const int t = tok0 + wt + 16 * j + r16;
-                const int m0 = row0 + wr + 16 * i + 4 * h;
-                if (t >= T) continue;
-                float * pp = g.part + ((size_t)sidx * T + t) * M + m0;
-#pragma unroll
-                for (int q = 0; q < 4; q++)
-                    if (m0 + q < M) pp[q] = st[LEV][i][j][q];
-            }
+        qg_store_part<ONE, TI, SPLIT>(g.part + E.poff, sidx, T, M, tok0, row0, wt, wr, r16, h, st[LEV], st2[LEV]);
     }
 }
 
-// Top of the class tree over SPLIT = 8 subtrees, then qg_store's total (+ 0.0f) and epilogue
-__global__ __launch_bounds__(256) void k_qg_combine(MMEntry E, int T, int M, const float * part) {
-    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= (size_t)T * M) return;
+// Split-K combine for a whole group: the top of the class tree over the SPLIT subtrees (8: three
+// levels, 4: two), then qg_store's total (+ 0.0f, or + the m*s total for the _1 formats), the
+// entry's epilogue, y, and -- for emitting entries -- the next matmul's input (emit32: one
+// quantization block per 32 consecutive rows of a token, one half-wave).
+template <int SPLIT, bool ONE>
+__global__ __launch_bounds__(256) void k_qg_combine(MMGroup g) {
+    int e = 0;
+#pragma unroll 1
+    while (e + 1 < g.n && (int)blockIdx.x >= g.e[e + 1].cblock0) e++;
+    const MMEntry & E = g.e[e];
+    const int M = E.W.M, T = g.T;
+    const size_t i = (size_t)((int)blockIdx.x - E.cblock0) * 256 + threadIdx.x;
+    if (i >= (size_t)T * M) return;  // T * M % 32 == 0: half-waves stay whole
     const int t = (int)(i / M), m = (int)(i % M);
-    float p[8];
+    const float * pp = g.part + E.poff + (size_t)t * M + m;
+    const size_t ss = (size_t)T * M;
+    auto tree = [&](const float * p) {
+        float v[SPLIT];
 #pragma unroll
-    for (int s = 0; s < 8; s++) p[s] = part[((size_t)s * T + t) * M + m];
-    const float tot = ((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7]));
-    E.y[(size_t)t * E.ldy + m] = apply_epi(E, t, m, tot + 0.0f);
+        for (int s = 0; s < SPLIT; s++) v[s] = p[s * ss];
+        if constexpr (SPLIT == 8) return ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
+        else return (v[0] + v[1]) + (v[2] + v[3]);
+    };
+    const float tot = tree(pp);
+    float acc;
+    if constexpr (ONE) acc = tot + tree(pp + (size_t)SPLIT * ss);
+    else acc = tot + 0.0f;
+    const float v = apply_epi(E, t, m, acc);
+    E.y[(size_t)t * E.ldy + m] = v;
+    if (E.emit) emit32(E.out, t, m, v);
 }
 
-template <int WF>
+// SPLIT > 1: workgroup s of a tile walks classes [s * 64 / SPLIT, (s + 1) * 64 / SPLIT) only -- a
+// complete subtree of the class tree -- and stores the subtree sums (qg_store_part) for k_qg_combine.
+template <int WF, int SPLIT = 1>
 __global__ __launch_bounds__(256) void k_qgemm(MMGroup g) {
     using Lt = QGLayout<WF>;
     constexpr bool ONE = Lt::ONE;
     constexpr int TI = Lt::TI;
+    constexpr int CPS = 64 / SPLIT;  // classes per split
     __shared__ __attribute__((aligned(16))) char smem[2][Lt::BUF];
     int e = 0;
 #pragma unroll 1
@@ -453,7 +487,8 @@ __global__ __launch_bounds__(256) void k_qgemm(MMGroup g) {
     const MMEntry & E = g.e[e];
     const int M = E.W.M, K = E.W.K, T = g.T, nb = K >> 5;
     const int tilesT = (T + QG_TOK - 1) / QG_TOK;
-    const int local = (int)blockIdx.x - E.block0;
+    const int local0 = (int)blockIdx.x - E.block0;
+    const int sidx = local0 % SPLIT, local = local0 / SPLIT, l0 = sidx * CPS;
     const int mtile = local / tilesT, ttile = local % tilesT;
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int r16 = lane & 15, h = lane >> 4;
@@ -462,10 +497,12 @@ __global__ __launch_bounds__(256) void k_qgemm(MMGroup g) {
     const v4i_t rw = qg_rsrc(E.W.gt + (size_t)mtile * nb * Lt::WB);
     const v4i_t ra = qg_rsrc(E.in.tq + (size_t)ttile * nb * Lt::AB);
     const unsigned lds0 = __builtin_amdgcn_readfirstlane((unsigned)(unsigned long)(lds_void_t *)&smem[0][0]);
-    QGWalk ld;  // the loader's walk (this wave's steps)
-    ld.init(nb);
-    for (int i = 0; i < wave; i++) ld.next();
     const int cq = nb >> 6, crem = nb & 63;  // class sizes for the consumer
+    // this split's steps: the blocks of classes [l0, l0 + CPS)
+    const int nsteps = CPS * cq + min(max(crem - l0, 0), CPS);
+    QGWalk ld;  // the loader's walk (this wave's steps)
+    ld.init(nb, l0);
+    for (int i = 0; i < wave; i++) ld.next();
 
     // Per output: class sums in a binary counter (wave_sum63's tree).  Classes are walked in
     // pairs: the even class accumulates straight into level 0 (st[0]), the odd one into c, and
@@ -474,7 +511,7 @@ __global__ __launch_bounds__(256) void k_qgemm(MMGroup g) {
     float st[6][TI][2][4], st2[6][TI][2][4];
     float tot[TI][2][4], tot2[TI][2][4];
     float c[TI][2][4], c2[TI][2][4];
-    const int nchunks = (nb + QG_STEPS - 1) / QG_STEPS;
+    const int nchunks = (nsteps + QG_STEPS - 1) / QG_STEPS;
 
     int k = 0, cb = 0, cn = 1;  // step within the chunk, its buffer, next chunk to issue
     // one block: MFMAs from this step's LDS operands, then the fp32 block epilogue into acc
@@ -493,7 +530,7 @@ __global__ __launch_bounds__(256) void k_qgemm(MMGroup g) {
 #else
             if (cn < nchunks)
 #endif
-                qg_load_chunk<WF>(rw, ra, lds0 + cb * Lt::BUF, cn, ld, nb, wave, lane);
+                qg_load_chunk<WF>(rw, ra, lds0 + cb * Lt::BUF, cn, ld, nsteps, wave, lane);
             cn++;
             cb ^= 1;
             qg_read_ops<WF>(smem[cb], cur, wr, wt, r16, h);
@@ -550,14 +587,14 @@ __global__ __launch_bounds__(256) void k_qgemm(MMGroup g) {
         break;                                                                    \
     }
 
-    if (nchunks > 0) qg_load_chunk<WF>(rw, ra, lds0, 0, ld, nb, wave, lane);
+    if (nchunks > 0) qg_load_chunk<WF>(rw, ra, lds0, 0, ld, nsteps, wave, lane);
     qg_chunk_done();
-    if (nchunks > 1) qg_load_chunk<WF>(rw, ra, lds0 + Lt::BUF, 1, ld, nb, wave, lane);
+    if (nchunks > 1) qg_load_chunk<WF>(rw, ra, lds0 + Lt::BUF, 1, ld, nsteps, wave, lane);
     cn = 2;
     qg_read_ops<WF>(smem[0], cur, wr, wt, r16, h);
-    for (int pr = 0; pr < 32; pr++) {
-        run_class(2 * pr, st[0], st2[0]);
-        run_class(2 * pr + 1, c, c2);
+    for (int pr = 0; pr < CPS / 2; pr++) {  // pairs of this split's classes; folds by the relative index
+        run_class(l0 + 2 * pr, st[0], st2[0]);
+        run_class(l0 + 2 * pr + 1, c, c2);
         switch (__builtin_ctz(~(2 * pr + 1))) {
             QG_CASE(1, st[1], st2[1])
             QG_CASE(2, st[2], st2[2])
@@ -572,13 +609,19 @@ __global__ __launch_bounds__(256) void k_qgemm(MMGroup g) {
     // copies of a partial last chunk (or of none) were never waited for: drain before exit
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-    qg_store<ONE, TI>(E, T, M, tok0, row0, wt, wr, r16, h, tot, tot2);
+    if constexpr (SPLIT == 1) {
+        qg_store<ONE, TI>(E, T, M, tok0, row0, wt, wr, r16, h, tot, tot2);
+    } else {
+        constexpr int LEV = SPLIT == 8 ? 3 : 4;  // the subtree of CPS classes
+        qg_store_part<ONE, TI, SPLIT>(g.part + E.poff, sidx, T, M, tok0, row0, wt, wr, r16, h, st[LEV], st2[LEV]);
+    }
 }
 
 // Every entry must have y (the engine gives emitting entries a scratch y); emission into the
 // next matmul's activation format is a separate launch_act_from_f32 pass by the caller.  The
 // weights need their tile records (upload_mat) and the activations must be token tiles.
 int g_qgemm_generic = 0;  // 1: K = 2048 through the generic kernel too (tools, comparison)
+int kQgCUs = 256;          // compute units of the device (set_mv_device_cus): the split-K threshold
 
 bool launch_qgemm(hipStream_t st, MMGroup & g, int wtype) {
     const int rows = qg_rows(wtype);
@@ -605,20 +648,61 @@ bool launch_qgemm(hipStream_t st, MMGroup & g, int wtype) {
     const dim3 grid(blocks), block(256);
     bool k64 = true;
     for (int i = 0; i < g.n; i++) k64 = k64 && g.e[i].W.K == 2048;
-    // split-K: one small-M entry (e.g. the v6 maa LoRA W1, 160 rows: 48 tiles for 256 CUs)
-    const bool split = k64 && !g_qgemm_generic && g.n == 1 && !qg_one(wtype) && g.T >= 2 && !g.e[0].emit &&
-                       blocks < 256 && g.part && g.part_floats >= (size_t)8 * g.T * g.e[0].W.M;
-    if (split) {
-        const dim3 sgrid(blocks * 8);
-        switch (wtype) {
-            case W_Q4_0: hipLaunchKernelGGL((k_qgemm_k64<W_Q4_0, 8>), sgrid, block, 0, st, g); break;
-            case W_Q5_0: hipLaunchKernelGGL((k_qgemm_k64<W_Q5_0, 8>), sgrid, block, 0, st, g); break;
-            default: hipLaunchKernelGGL((k_qgemm_k64<W_Q8_0, 8>), sgrid, block, 0, st, g); break;
+    // split-K when the group has few tiles (batched decode's 64-context tiles, small-M entries such
+    // as the v6 maa LoRA W1): every tile's class tree in 4 or 8 subtrees on as many workgroups,
+    // combined (epilogue, emission) by k_qg_combine -- the same bits as the unsplit kernel
+    int split = g.split;
+    if (split == 0) split = blocks >= 2 * kQgCUs ? 1 : blocks * 4 >= 2 * kQgCUs ? 4 : 8;
+    if (split != 1 && split != 4 && split != 8) split = 1;
+    size_t pfl = 0;
+    if (split > 1) {
+        for (int i = 0; i < g.n; i++) {
+            g.e[i].poff = pfl;
+            pfl += (size_t)split * g.T * g.e[i].W.M * (qg_one(wtype) ? 2 : 1);
         }
+        if (!g.part || g.part_floats < pfl || g_qgemm_generic) split = 1;
+        for (int i = 0; i < g.n; i++)
+            if (g.e[i].W.M % 32) split = 1;  // combine: one emission block per half-wave
+    }
+    if (split > 1) {
+        // workgroup ranges of the entries in the split grid (SPLIT workgroups per tile)
+        for (int i = 0; i < g.n; i++) g.e[i].block0 *= split;
+        const dim3 sgrid(blocks * split);
+#define QG_SPLIT_L(WFv, SP)                                                                    \
+    do {                                                                                       \
+        if (k64) hipLaunchKernelGGL((k_qgemm_k64<WFv, SP>), sgrid, block, 0, st, g);           \
+        else hipLaunchKernelGGL((k_qgemm<WFv, SP>), sgrid, block, 0, st, g);                   \
+    } while (0)
+#define QG_SPLIT_T(SP)                                                                         \
+    do {                                                                                       \
+        switch (wtype) {                                                                       \
+            case W_Q4_0: QG_SPLIT_L(W_Q4_0, SP); break;                                        \
+            case W_Q4_1: QG_SPLIT_L(W_Q4_1, SP); break;                                        \
+            case W_Q5_0: QG_SPLIT_L(W_Q5_0, SP); break;                                        \
+            case W_Q5_1: QG_SPLIT_L(W_Q5_1, SP); break;                                        \
+            case W_Q8_0: QG_SPLIT_L(W_Q8_0, SP); break;                                        \
+            default: fprintf(stderr, "rwkv: qgemm type %d unsupported\n", wtype); return false; \
+        }                                                                                      \
+    } while (0)
+        if (split == 4) QG_SPLIT_T(4);
+        else QG_SPLIT_T(8);
+#undef QG_SPLIT_T
+#undef QG_SPLIT_L
         HIP_OK(hipGetLastError());
-        const size_t n = (size_t)g.T * g.e[0].W.M;
-        hipLaunchKernelGGL(k_qg_combine, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, g.e[0], g.T, g.e[0].W.M,
-                           g.part);
+        int cblocks = 0;
+        for (int i = 0; i < g.n; i++) {
+            g.e[i].cblock0 = cblocks;
+            g.e[i].fuse_emit = g.e[i].emit;  // the combine emits
+            cblocks += (int)(((size_t)g.T * g.e[i].W.M + 255) / 256);
+        }
+        const bool one = qg_one(wtype);
+        if (split == 4) {
+            if (one) hipLaunchKernelGGL((k_qg_combine<4, true>), dim3(cblocks), block, 0, st, g);
+            else hipLaunchKernelGGL((k_qg_combine<4, false>), dim3(cblocks), block, 0, st, g);
+        } else {
+            if (one) hipLaunchKernelGGL((k_qg_combine<8, true>), dim3(cblocks), block, 0, st, g);
+            else hipLaunchKernelGGL((k_qg_combine<8, false>), dim3(cblocks), block, 0, st, g);
+        }
         HIP_OK(hipGetLastError());
         return true;
     }

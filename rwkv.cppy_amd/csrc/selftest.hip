@@ -62,7 +62,8 @@ extern "C" RWKV_API bool rwkv_mi355x_selftest_quantize_act(int wtype, const floa
     return true;
 }
 
-static bool selftest_mm(int wtype, const void * W, int K, int M, const float * x, int T, float * y, bool mfma) {
+static bool selftest_mm(int wtype, const void * W, int K, int M, const float * x, int T, float * y, bool mfma,
+                        int split = 0) {
     if (K % 32 || T <= 0 || M <= 0) return false;
     HostTensor ht;
     ht.name = "selftest";
@@ -94,7 +95,13 @@ static bool selftest_mm(int wtype, const void * W, int K, int M, const float * x
         g.e[0].y = dy;
         g.e[0].ldy = M;
         g.e[0].epi = EPI_STORE;
-        ok = mfma ? launch_qgemm(nullptr, g, wtype) : launch_mm_group(nullptr, g, wtype);
+        g.split = split;
+        if (mfma) {
+            g.part_floats = (size_t)8 * T * M * 2;
+            g.part = (float *)b.alloc(g.part_floats * 4);
+            ok = g.part != nullptr;
+        }
+        ok = ok && (mfma ? launch_qgemm(nullptr, g, wtype) : launch_mm_group(nullptr, g, wtype));
     }
     ok = ok && hipDeviceSynchronize() == hipSuccess;
     ok = ok && hipMemcpy(y, dy, (size_t)T * M * 4, hipMemcpyDeviceToHost) == hipSuccess;
@@ -111,4 +118,11 @@ extern "C" RWKV_API bool rwkv_mi355x_selftest_gemm(int wtype, const void * W, in
                                                    float * y) {
     if (!wtype_quantized(wtype) || T < 2) return false;
     return selftest_mm(wtype, W, K, M, x, T, y, true);
+}
+
+// The same with the split-K form chosen: 1 = unsplit, 4 / 8 = that many class subtrees + combine.
+extern "C" RWKV_API bool rwkv_mi355x_selftest_gemm_split(int wtype, const void * W, int K, int M, const float * x,
+                                                         int T, float * y, int split) {
+    if (!wtype_quantized(wtype) || T < 2 || (split != 1 && split != 4 && split != 8)) return false;
+    return selftest_mm(wtype, W, K, M, x, T, y, true, split);
 }

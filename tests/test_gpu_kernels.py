@@ -34,6 +34,8 @@ def lib():
     L.rwkv_mi355x_selftest_matmul.restype = ctypes.c_bool
     L.rwkv_mi355x_selftest_gemm.argtypes = L.rwkv_mi355x_selftest_matmul.argtypes
     L.rwkv_mi355x_selftest_gemm.restype = ctypes.c_bool
+    L.rwkv_mi355x_selftest_gemm_split.argtypes = L.rwkv_mi355x_selftest_matmul.argtypes + [ctypes.c_int]
+    L.rwkv_mi355x_selftest_gemm_split.restype = ctypes.c_bool
     return L
 
 
@@ -79,8 +81,11 @@ def test_activation_quantizer_bit_exact(wfmt, afmt):
 
 
 @pytest.mark.parametrize('fmt', ['FP32', 'FP16', 'Q4_0', 'Q4_1', 'Q5_0', 'Q5_1', 'Q8_0'])
-@pytest.mark.parametrize('M,K,T', [(2048, 2048, 1), (100, 96, 1), (64, 7168, 1), (160, 2048, 5), (72, 320, 9)])
+@pytest.mark.parametrize('M,K,T', [(2048, 2048, 1), (100, 96, 1), (64, 7168, 1), (160, 2048, 5), (72, 320, 9),
+                                   (96, 2560, 16), (2560, 64, 40), (200, 2048, 64), (64, 160, 33)])
 def test_matmul_kernel(fmt, M, K, T):
+    """The sequence / batched matmul vs the GPU-association oracle, bit for bit; from T = 16 the FP16 and
+    FP32 weights run on the f32 MFMA (mv_fmfma.hip)."""
     rng = np.random.default_rng(M * 7 + K + T)
     w = (rng.standard_normal((M, K)) / np.sqrt(K)).astype(np.float32)
     x = rng.standard_normal((T, K)).astype(np.float32)
@@ -118,4 +123,24 @@ def test_mfma_gemm_matches_matmul_bit_exact(fmt, M, K, T):
     L = lib()
     assert L.rwkv_mi355x_selftest_matmul(TYPE_IDS[fmt], wb.ctypes.data, K, M, x.ctypes.data, T, y_mm.ctypes.data)
     assert L.rwkv_mi355x_selftest_gemm(TYPE_IDS[fmt], wb.ctypes.data, K, M, x.ctypes.data, T, y_g.ctypes.data)
+    assert np.array_equal(y_g.view(np.uint32), y_mm.view(np.uint32)), float(np.abs(y_g - y_mm).max())
+
+
+@pytest.mark.parametrize('fmt', ['Q4_0', 'Q4_1', 'Q5_0', 'Q5_1', 'Q8_0'])
+@pytest.mark.parametrize('M,K,T', [(2048, 2048, 64), (96, 7168, 40), (160, 2048, 128), (64, 768, 7), (2048, 64, 17)])
+@pytest.mark.parametrize('split', [1, 4, 8])
+def test_mfma_gemm_split_k_bit_exact(fmt, M, K, T, split):
+    """Split-K GEMM (the class tree in 4 or 8 subtrees on as many workgroups, k_qg_combine adding the
+    top levels) == the decode matvec association, bit for bit, for every format and K % 2048 != 0
+    (classes of unequal block counts, empty classes at K < 2048)."""
+    rng = np.random.default_rng(M * 7 + K * 3 + T + split)
+    w = (rng.standard_normal((M, K)) / np.sqrt(K)).astype(np.float32)
+    x = rng.standard_normal((T, K)).astype(np.float32)
+    wb = quantize_rows(fmt, w)
+    y_mm = np.zeros((T, M), np.float32)
+    y_g = np.zeros((T, M), np.float32)
+    L = lib()
+    assert L.rwkv_mi355x_selftest_matmul(TYPE_IDS[fmt], wb.ctypes.data, K, M, x.ctypes.data, T, y_mm.ctypes.data)
+    assert L.rwkv_mi355x_selftest_gemm_split(TYPE_IDS[fmt], wb.ctypes.data, K, M, x.ctypes.data, T, y_g.ctypes.data,
+                                             split)
     assert np.array_equal(y_g.view(np.uint32), y_mm.view(np.uint32)), float(np.abs(y_g - y_mm).max())

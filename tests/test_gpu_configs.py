@@ -16,6 +16,7 @@ import os
 
 import numpy as np
 import pytest
+import torch  # before librwkv initialises HIP (torch's own HIP runtime must come up first)
 
 from oracle_ctypes import assert_bits_equal, gpu_variant
 from rwkv_lib import RWKVModel, library

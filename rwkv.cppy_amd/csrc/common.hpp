@@ -129,6 +129,7 @@ struct MMGroup {
     float * part;        // split-K partials (qgemm.hip): up to 8 x T x sum(M) floats (x2 for _1 formats)
     size_t part_floats;
     int split;           // qgemm split-K: 0 = by tile count, 1 = never, 4 / 8 = forced
+    int fmm;             // float weights, T >= 16: 0 = f32-MFMA form when the grid fills the chip, 1 = always
 };
 
 #define HIP_OK(x)                                                                             \

@@ -396,7 +396,7 @@ bool Engine::init() {
     const char * io = getenv("RWKV_MI355X_STATE_PIPELINE");  // 0: host state copied whole (comparison)
     io_pipeline_ = !(io && io[0] == '0');
     const char * bg = getenv("RWKV_MI355X_BATCH_GEMM_MIN");  // contexts from which batches use the GEMM
-    batch_gemm_min_ = bg ? std::max(2, atoi(bg)) : 48;
+    batch_gemm_min_ = bg ? std::max(2, atoi(bg)) : 16;
     const char * ic = getenv("RWKV_MI355X_IO_CHUNK");  // layers per chunk graph (host-state decode)
     io_chunk_ = ic ? std::max(1, atoi(ic)) : 4;
     const char * sm = getenv("RWKV_MI355X_SPLIT_MAA");  // v6 decode: W1 and mix as two launches (comparison)

@@ -175,7 +175,7 @@ class Engine {
     // batched decode (eval_batch): state floats per context while a batched forward is built
     // (0 otherwise), the head's output rows, and the engine-owned staging buffers / graphs
     size_t bs_ = 0;
-    int batch_gemm_min_ = 48;
+    int batch_gemm_min_ = 16;
     float * head_out_ = nullptr;
     float * bstate_[2] = {nullptr, nullptr};
     float * blogits_ = nullptr;

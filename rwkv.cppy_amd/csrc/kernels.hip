@@ -628,6 +628,102 @@ __global__ __launch_bounds__(320) void k_v6_mix5(Mix5Args a) {
     }
 }
 
+// The same mixes on the f32 MFMA (round 3): m[t][c] = the fmaf chain over i of W2[c][i] * lora[t][i]
+// in order from 0 is exactly a chain of v_mfma_f32_16x16x4_f32 over i in quads (C first, k = 0..3
+// in order: tools/mfma_f32_probe.hip), so the mixes stay bit-identical to k_v6_mix5 and the decode's
+// k_v6_mix5_dec.  Workgroup = 5 waves, wave n = mix n over 32 channels x 64 tokens (2 x 4 tiles of
+// 16 x 16; operands straight from L2); the epilogue quantizes each token's 32 channels -- one Q8
+// block, held by lanes tok + 16 g of the D layout -- with xor-16/32 lane exchanges (order-free max
+// and integer sum, quant32's values) and stores them into the token-tile records (TQ = 1: Q8_0,
+// 2: Q8_1).
+typedef float mixf4 __attribute__((ext_vector_type(4)));
+template <int DM, int TQ>
+__global__ __launch_bounds__(320) void k_v6_mix5m(Mix5Args a) {
+    const int C = a.C, T = a.T;
+    const int lane = threadIdx.x & 63, n = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int ml = lane & 15, g = lane >> 4;
+    const float * maa_n = a.maa[0];
+    ActBuf out_n = a.out[0];
+#pragma unroll
+    for (int m = 1; m < 5; m++)
+        if (n == m) {
+            maa_n = a.maa[m];
+            out_n = a.out[m];
+        }
+    const int c0 = blockIdx.x * 32, t0 = blockIdx.y * 64;
+    // A operands: W2 (transposed [5][D][C]) of channels c0 + 16 ct + ml, i = 4 j + g
+    float wa[2][DM / 4];
+#pragma unroll
+    for (int ct = 0; ct < 2; ct++)
+#pragma unroll
+        for (int j = 0; j < DM / 4; j++) wa[ct][j] = a.w2[((size_t)n * DM + 4 * j + g) * C + c0 + 16 * ct + ml];
+    mixf4 acc[2][4];
+#pragma unroll
+    for (int nt = 0; nt < 4; nt++) {
+        // B operands: lora[t][n][i] of token t0 + 16 nt + ml, i = 4 j + g
+        const size_t tr = (size_t)min(t0 + 16 * nt + ml, T - 1) * 5 * DM + (size_t)n * DM + g;
+        float lb[DM / 4];
+#pragma unroll
+        for (int j = 0; j < DM / 4; j++) lb[j] = a.lora[tr + 4 * j];
+#pragma unroll
+        for (int ct = 0; ct < 2; ct++) {
+            mixf4 c = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int j = 0; j < DM / 4; j++) c = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[ct][j], lb[j], c, 0, 0, 0);
+            acc[ct][nt] = c;
+        }
+    }
+    // epilogue: lane holds channels c0 + 16 ct + 4 g + i of token t0 + 16 nt + ml
+    const int cb = c0 + 4 * g;
+    mixf4 mu[2];
+#pragma unroll
+    for (int ct = 0; ct < 2; ct++) mu[ct] = *(const mixf4 *)(maa_n + cb + 16 * ct);
+    uint8_t * rec = out_n.tq + ((size_t)(t0 / QG_TOK) * (C >> 5) + (c0 >> 5)) * qg_a_bytes(TQ == 2);
+#pragma unroll
+    for (int nt = 0; nt < 4; nt++) {
+        const int t = t0 + 16 * nt + ml;
+        const size_t ti = (size_t)min(t, T - 1) * C + cb;
+        float v[2][4];
+        float am = 0.0f;
+#pragma unroll
+        for (int ct = 0; ct < 2; ct++) {
+            const mixf4 xa = *(const mixf4 *)(a.xa + ti + 16 * ct), sx = *(const mixf4 *)(a.sx + ti + 16 * ct);
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                v[ct][i] = (acc[ct][nt][i] + mu[ct][i]) * sx[i] + xa[i];
+                am = fmaxf(am, fabsf(v[ct][i]));
+            }
+        }
+        am = fmaxf(am, __shfl_xor(am, 16));
+        am = fmaxf(am, __shfl_xor(am, 32));
+        const float id = (am != 0.0f) ? 127.f / am : 0.0f;
+        const float d = am / 127.f;
+        uint32_t packed[2];
+        int sum = 0;
+#pragma unroll
+        for (int ct = 0; ct < 2; ct++) {
+            packed[ct] = 0;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int q = (int)rintf(v[ct][i] * id);
+                sum += q;
+                packed[ct] |= ((uint32_t)q & 0xffu) << (8 * i);
+            }
+        }
+        sum += __shfl_xor(sum, 16);
+        sum += __shfl_xor(sum, 32);
+        if (t < T) {
+            const int tl = t % QG_TOK;
+#pragma unroll
+            for (int ct = 0; ct < 2; ct++) *(uint32_t *)(rec + ct * QG_TOK * 16 + tl * 16 + 4 * g) = packed[ct];
+            if (g == 0) {
+                ((float *)(rec + QG_A_D))[tl] = f16_round(d);
+                if constexpr (TQ == 2) ((float *)(rec + QG_A_S))[tl] = f16_round(d * (float)sum);
+            }
+        }
+    }
+}
+
 bool launch_v6_mix5(hipStream_t st, int T, int C, int D, const float * lora, const float * w2,
                     const float * const * maa, const float * xa, const float * sx, const ActBuf * outs) {
     Mix5Args a;
@@ -654,6 +750,23 @@ bool launch_v6_mix5(hipStream_t st, int T, int C, int D, const float * lora, con
             all = all && outs[n].tiled && outs[n].fmt == outs[0].fmt && outs[n].K == C &&
                   (outs[n].fmt == A_Q8_0 || outs[n].fmt == A_Q8_1);
         if (all) tq = outs[0].fmt == A_Q8_1 ? 2 : 1;
+    }
+    // the f32-MFMA form: tiled Q8 outputs, LoRA width 32 or 64, whole 32-channel blocks
+    static const bool mfma_on = [] {
+        const char * v = getenv("RWKV_MI355X_MIX5_MFMA");
+        return !(v && v[0] == '0');
+    }();
+    if (mfma_on && tq > 0 && (D == 32 || D == 64) && C % 32 == 0) {
+        const dim3 mgrid(C / 32, (T + 63) / 64);
+        if (D == 32) {
+            if (tq == 1) hipLaunchKernelGGL((k_v6_mix5m<32, 1>), mgrid, dim3(320), 0, st, a);
+            else hipLaunchKernelGGL((k_v6_mix5m<32, 2>), mgrid, dim3(320), 0, st, a);
+        } else {
+            if (tq == 1) hipLaunchKernelGGL((k_v6_mix5m<64, 1>), mgrid, dim3(320), 0, st, a);
+            else hipLaunchKernelGGL((k_v6_mix5m<64, 2>), mgrid, dim3(320), 0, st, a);
+        }
+        HIP_OK(hipGetLastError());
+        return true;
     }
 #define MIX5_L(DMv, TQv)                                                                  \
     do {                                                                                  \

@@ -13,9 +13,13 @@
 // exact in f32, so the MFMA runs the same IEEE operations as the matvec: results are bit-identical
 // to the single-token decode of every token / context.
 //
-// Workgroup: 4 waves x 16 rows (64 rows) x 16 * NT tokens; a wave's NT 16 x 16 tiles share its
-// weight loads.  Epilogue (apply_epi, y, emit32) in a workgroup pass over the tile from LDS, so an
-// emitting group's 32 consecutive rows of a token sit in one half-wave.
+// Workgroup: 4 waves over a 64-row x 64-token tile (a wave: 2 x 2 tiles of 16 x 16).  Operands are
+// staged through LDS one stage (16 steps = 16 units per row and per token) at a time: the workgroup
+// loads whole 16-byte units with coalesced global loads (the next stage's in flight while the current
+// one is multiplied) and writes them as [element pair kk][row][step] dword planes, so an MFMA
+// operand is one conflict-free ds_read_b32 per lane.  Epilogue (apply_epi, y, emit32) in a workgroup
+// pass over the tile from LDS, so an emitting group's 32 consecutive rows of a token sit in one
+// half-wave.
 #include "mv_common.hpp"
 
 #include <stdlib.h>
@@ -24,113 +28,190 @@ namespace rwkvmi {
 
 typedef float fmf4 __attribute__((ext_vector_type(4)));
 
+// Format constants: a unit is 16 bytes -- F16: 8 halves, two MFMAs (elements kk, kk + 4 of lane
+// (m, kk)); F32: 4 floats, one MFMA (element kk).  Lane l of the matvec holds units k = EL l + STR u.
 template <int WF>
 struct FUnit;
 template <>
-struct FUnit<W_F16> {  // 8 halves of a row: the A/B operands of two MFMAs
-    int4 v;
-    static constexpr int ELEMS = 8, STRIDE = 512;
-    __device__ __forceinline__ void load(const void * base, size_t row, int K, int k) {
-        v = *(const int4 *)((const __half *)base + row * K + k);
+struct FUnit<W_F16> {
+    static constexpr int EL = 8, STR = 512, MF = 2;
+    // dword kk of the LDS form: halves (kk, kk + 4) of the unit
+    __device__ __forceinline__ static uint32_t pack(const uint4 & v, int kk) {
+        const uint32_t lo = kk < 2 ? v.x : v.y, hi = kk < 2 ? v.z : v.w;
+        return (kk & 1) ? __builtin_amdgcn_perm(hi, lo, 0x07060302u) : __builtin_amdgcn_perm(hi, lo, 0x05040100u);
     }
-    // element kk (+4 for the second MFMA) of the unit, widened
-    __device__ __forceinline__ float get(int j) const {
-        const int w = j >> 1 == 0 ? v.x : j >> 1 == 1 ? v.y : j >> 1 == 2 ? v.z : v.w;
-        const half2_t h = __builtin_bit_cast(half2_t, w);
-        return (float)((j & 1) ? h.y : h.x);
+    __device__ __forceinline__ static float elem(uint32_t d, int h) {
+        return (float)__builtin_bit_cast(_Float16, (uint16_t)(h ? d >> 16 : d));
     }
 };
 template <>
-struct FUnit<W_F32> {  // the lane's element of a 4-float unit
-    float v;
-    static constexpr int ELEMS = 4, STRIDE = 256;
-    __device__ __forceinline__ void load(const void * base, size_t row, int K, int k) {
-        v = ((const float *)base)[row * K + k];
+struct FUnit<W_F32> {
+    static constexpr int EL = 4, STR = 256, MF = 1;
+    __device__ __forceinline__ static uint32_t pack(const uint4 & v, int kk) {
+        return kk == 0 ? v.x : kk == 1 ? v.y : kk == 2 ? v.z : v.w;
     }
+    __device__ __forceinline__ static float elem(uint32_t d, int) { return __uint_as_float(d); }
 };
 
-template <int WF, int NT>
-__global__ __launch_bounds__(256) void k_fmm(MMGroup g) {
-    extern __shared__ float red[];  // [16 * NT tokens][64 rows]
+constexpr int FM_SU = 16;                 // steps per stage
+constexpr int FM_RS = FM_SU + 1;          // dwords per (kk, row) line
+constexpr int FM_KS = 64 * FM_RS + 16;    // dwords per kk plane (= 16 mod 32: lanes kk, kk ^ 1 on disjoint banks)
+constexpr int FM_OP = 4 * FM_KS;          // one operand tile (64 rows or tokens)
+constexpr int FM_BUF = 2 * FM_OP;         // weights + activations
+
+template <int WF>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_fmm(MMGroup g) {
+    __shared__ uint32_t fsm[2 * FM_BUF];  // [2 buffers][W, X][kk][64][FM_RS]; after the loop: red[64 tok][64 rows]
+    using U = FUnit<WF>;
+    constexpr int EL = U::EL, STR = U::STR;
     int e = 0;
 #pragma unroll 1
     while (e + 1 < g.n && (int)blockIdx.x >= g.e[e + 1].block0) e++;
     const MMEntry & E = g.e[e];
     const int T = g.T, M = E.W.M, K = E.W.K;
-    const int tgroups = (T + 16 * NT - 1) / (16 * NT);
-    const int local = (int)blockIdx.x - E.block0;
+    const int tgroups = (T + 63) / 64;
+    int local = (int)blockIdx.x - E.block0;
+    {
+        // consecutive workgroups go round-robin to the 8 XCDs: give the token groups of one row tile
+        // consecutive indices on the same XCD, so its L2 serves their shared weight rows
+        const int nloc = (g.e[e + 1 < g.n ? e + 1 : e].block0 - E.block0);
+        const int ne = e + 1 < g.n ? nloc : (int)gridDim.x - E.block0;
+        if (tgroups > 1 && (E.block0 & 7) == 0 && (ne & 7) == 0) local = (local & 7) * (ne >> 3) + (local >> 3);
+    }
     const int rt = local / tgroups, tg = local % tgroups;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int ml = lane & 15, kk = lane >> 4;
-    const int row0 = rt * 64 + wave * 16, tok0 = tg * 16 * NT;
-    const size_t arow = (size_t)min(row0 + ml, M - 1);
-    size_t xrow[NT];
-#pragma unroll
-    for (int n = 0; n < NT; n++) xrow[n] = (size_t)min(tok0 + 16 * n + ml, T - 1);
-    const void * xin = WF == W_F16 ? (const void *)E.in.h : (const void *)E.in.f;
-    constexpr int EL = FUnit<WF>::ELEMS, STR = FUnit<WF>::STRIDE;
+    const int row0 = rt * 64, tok0 = tg * 64;
+    const int wr = (wave & 1) * 32, wt = (wave >> 1) * 32;
+    const char * wbase = (const char *)E.W.qs;
+    const char * xbase = WF == W_F16 ? (const char *)E.in.h : (const char *)E.in.f;
     const int units = (K + STR - 1) / STR;
+    // classes holding a unit (K < 64 units: the rest are zero leaves of the tree, folded below)
+    const int ncls = units > 1 ? 64 : min(64, (K + EL - 1) / EL);
+    const int nsteps = ncls * units;
+    const int nst = (nsteps + FM_SU - 1) / FM_SU;
+    const size_t rowb = (size_t)K * (WF == W_F16 ? 2 : 4);
 
-    fmf4 st[6][NT], c[NT], tot[NT];
-#pragma unroll 1
-    for (int l = 0; l < 64; l++) {
-        fmf4 acc[NT];
+    // loader: thread tid moves units q = tid + 256 p (p < 4) of each operand: line q >> 4, step q & 15
+    uint4 wv[4], xv[4];
+    auto gload = [&](int stg) {
 #pragma unroll
-        for (int n = 0; n < NT; n++) acc[n] = fmf4{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll 1
-        for (int u = 0; u < units; u++) {
-            const int k = EL * l + STR * u;
-            if (k >= K) break;  // uniform: the class has no more units (the matvec's unit_valid)
-            FUnit<WF> w;
-            w.load(E.W.qs, arow, K, WF == W_F16 ? k : k + kk);
-            FUnit<WF> x[NT];
+        for (int p = 0; p < 4; p++) {
+            const int q = tid + 256 * p, ln = q >> 4, j = q & 15;
+            const int s = min(stg * FM_SU + j, nsteps - 1);
+            const int l = s / units, u = s - l * units;
+            const int k = min(EL * l + STR * u, K - EL);  // a unit past K: clamped, never multiplied
+            const size_t kb = (size_t)k * (WF == W_F16 ? 2 : 4);
+            wv[p] = *(const uint4 *)(wbase + (size_t)min(row0 + ln, M - 1) * rowb + kb);
+            xv[p] = *(const uint4 *)(xbase + (size_t)min(tok0 + ln, T - 1) * rowb + kb);
+        }
+    };
+    auto lstore = [&](int buf) {
+        uint32_t * wb = fsm + buf * FM_BUF;
+        uint32_t * xb = wb + FM_OP;
 #pragma unroll
-            for (int n = 0; n < NT; n++) x[n].load(xin, xrow[n], K, WF == W_F16 ? k : k + kk);
-            if constexpr (WF == W_F16) {
-                const float a0 = w.get(kk), a1 = w.get(kk + 4);
+        for (int p = 0; p < 4; p++) {
+            const int q = tid + 256 * p, ln = q >> 4, j = q & 15;
 #pragma unroll
-                for (int n = 0; n < NT; n++) {
-                    acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, x[n].get(kk), acc[n], 0, 0, 0);
-                    acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, x[n].get(kk + 4), acc[n], 0, 0, 0);
-                }
-            } else {
-#pragma unroll
-                for (int n = 0; n < NT; n++) acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.v, x[n].v, acc[n], 0, 0, 0);
+            for (int c = 0; c < 4; c++) {
+                wb[c * FM_KS + ln * FM_RS + j] = U::pack(wv[p], c);
+                xb[c * FM_KS + ln * FM_RS + j] = U::pack(xv[p], c);
             }
         }
-        // binary counter over the classes (wave_sum63's tree): even classes open level 0, odd
-        // classes close ctz(~l) levels
-        if ((l & 1) == 0) {
+    };
+
+    fmf4 st[6][2][2], acc[2][2];
 #pragma unroll
-            for (int n = 0; n < NT; n++) st[0][n] = acc[n];
-        } else {
-            const int N = __builtin_ctz(~l);
+    for (int i = 0; i < 2; i++)
 #pragma unroll
-            for (int n = 0; n < NT; n++) c[n] = acc[n];
-#pragma unroll
-            for (int kx = 0; kx < 6; kx++)
-                if (kx < N)
-#pragma unroll
-                    for (int n = 0; n < NT; n++) c[n] = st[kx][n] + c[n];
-#pragma unroll
-            for (int kx = 1; kx < 6; kx++)
-                if (kx == N)
-#pragma unroll
-                    for (int n = 0; n < NT; n++) st[kx][n] = c[n];
-            if (N == 6)
-#pragma unroll
-                for (int n = 0; n < NT; n++) tot[n] = c[n];
-        }
+        for (int n = 0; n < 2; n++) acc[i][n] = fmf4{0.0f, 0.0f, 0.0f, 0.0f};
+    // binary counter over the classes (wave_sum63's tree): even classes open level 0, odd classes
+    // close ctz(~l) levels into level N (the total, N = 6: into level 0, free by then)
+#define FMM_CLOSE(NV)                                                                 \
+    case NV: {                                                                        \
+        _Pragma("unroll") for (int i = 0; i < 2; i++)                                 \
+        _Pragma("unroll") for (int n = 0; n < 2; n++) {                               \
+            fmf4 v_ = acc[i][n];                                                      \
+            _Pragma("unroll") for (int kx = 0; kx < NV; kx++) v_ = st[kx][i][n] + v_; \
+            st[NV < 6 ? NV : 0][i][n] = v_;  /* N = 6: the total, kept in level 0 */  \
+        }                                                                             \
+        break;                                                                        \
     }
-    // D layout: lane holds rows 4 * kk + i of the wave's 16, token ml of each 16-token tile
-#pragma unroll
-    for (int n = 0; n < NT; n++)
-#pragma unroll
-        for (int i = 0; i < 4; i++) red[(16 * n + ml) * 64 + wave * 16 + 4 * kk + i] = tot[n][i] + 0.0f;
+#define FMM_FOLD(L)                                                                   \
+    do {                                                                              \
+        if (((L) & 1) == 0) {                                                         \
+            _Pragma("unroll") for (int i = 0; i < 2; i++)                             \
+            _Pragma("unroll") for (int n = 0; n < 2; n++) st[0][i][n] = acc[i][n];    \
+        } else {                                                                      \
+            switch (__builtin_ctz(~(L))) {                                            \
+                FMM_CLOSE(1) FMM_CLOSE(2) FMM_CLOSE(3) FMM_CLOSE(4) FMM_CLOSE(5)      \
+                default: FMM_CLOSE(6)                                                 \
+            }                                                                         \
+        }                                                                             \
+        _Pragma("unroll") for (int i = 0; i < 2; i++)                                 \
+        _Pragma("unroll") for (int n = 0; n < 2; n++) acc[i][n] = fmf4{0.0f, 0.0f, 0.0f, 0.0f}; \
+    } while (0)
+
+    gload(0);
+    lstore(0);
     __syncthreads();
-    const int rw0 = rt * 64;
-    for (int i = threadIdx.x; i < 16 * NT * 64; i += 256) {
-        const int t = tok0 + i / 64, row = rw0 + i % 64;
+    int l = 0, u = 0;  // the step being multiplied
+#pragma unroll 1
+    for (int stg = 0; stg < nst; stg++) {
+        if (stg + 1 < nst) gload(stg + 1);  // in flight under this stage's MFMAs
+        const uint32_t * wb = fsm + (stg & 1) * FM_BUF + kk * FM_KS;
+        const uint32_t * xb = wb + FM_OP;
+        const int jn = min(FM_SU, nsteps - stg * FM_SU);
+        // step j's operands are in registers while step j + 1's are read
+        uint32_t a[2], b[2];
+        auto opread = [&](uint32_t (&a_)[2], uint32_t (&b_)[2], int j) {
+#pragma unroll
+            for (int i = 0; i < 2; i++) a_[i] = wb[(wr + 16 * i + ml) * FM_RS + j];
+#pragma unroll
+            for (int n = 0; n < 2; n++) b_[n] = xb[(wt + 16 * n + ml) * FM_RS + j];
+        };
+        opread(a, b, 0);
+#pragma unroll 1
+        for (int j = 0; j < jn; j++) {
+            uint32_t an[2], bn[2];
+            opread(an, bn, min(j + 1, jn - 1));
+            if (EL * l + STR * u < K) {  // uniform: the matvec's unit_valid
+#pragma unroll
+                for (int h = 0; h < U::MF; h++) {
+                    // the four tiles' chains interleaved: no MFMA waits on the one just issued
+#pragma unroll
+                    for (int i = 0; i < 2; i++)
+#pragma unroll
+                        for (int n = 0; n < 2; n++)
+                            acc[i][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(U::elem(a[i], h), U::elem(b[n], h), acc[i][n], 0, 0, 0);
+                }
+            }
+            if (++u == units) {
+                u = 0;
+                FMM_FOLD(l);
+                l++;
+            }
+#pragma unroll
+            for (int i = 0; i < 2; i++) a[i] = an[i], b[i] = bn[i];
+        }
+        if (stg + 1 < nst) lstore((stg + 1) & 1);
+        __syncthreads();
+    }
+#pragma unroll 1
+    for (; l < 64; l++) FMM_FOLD(l);  // classes without units: zero partials (the matvec adds them too)
+#undef FMM_FOLD
+#undef FMM_CLOSE
+    // D layout: lane holds rows 4 * kk + q of a 16-row tile, token ml of a 16-token tile
+    float * red = (float *)fsm;
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int n = 0; n < 2; n++)
+#pragma unroll
+            for (int q = 0; q < 4; q++) red[(wt + 16 * n + ml) * 64 + wr + 16 * i + 4 * kk + q] = st[0][i][n][q] + 0.0f;
+    __syncthreads();
+    for (int i = tid; i < 64 * 64; i += 256) {
+        const int t = tok0 + i / 64, row = row0 + i % 64;
         if (t >= T) break;  // i / 64 only grows: the rest of the pass is past T too (half-waves whole)
         float v = 0.0f;
         if (row < M) {
@@ -144,6 +225,8 @@ __global__ __launch_bounds__(256) void k_fmm(MMGroup g) {
 // MFMA float matmul for a group: F16 / F32 weights, T >= 16 tokens (or contexts), every entry's
 // input in the weight type's activation format, row-major (not tiled); emitting entries need M % 32
 // == 0.  Returns false with *launched = false when the group is outside that (caller keeps k_mm).
+int g_fmm_min_blocks = 512;
+
 bool launch_fmm_group(hipStream_t st, MMGroup & g, int wtype, bool * launched) {
     static const bool on = [] {
         const char * v = getenv("RWKV_MI355X_FMM");  // 0: float matmuls stay on k_mm / k_mvb
@@ -157,23 +240,20 @@ bool launch_fmm_group(hipStream_t st, MMGroup & g, int wtype, bool * launched) {
             return true;
         if (e.emit && e.W.M % 32) return true;
         if (wtype == W_F16 ? !e.in.h : !e.in.f) return true;
+        const uintptr_t xa = wtype == W_F16 ? (uintptr_t)e.in.h : (uintptr_t)e.in.f;
+        if (((uintptr_t)e.W.qs | xa) & 15) return true;  // 16-byte unit loads
     }
-    const int NT = g.T >= 32 ? 2 : 1;
-    const int tgroups = (g.T + 16 * NT - 1) / (16 * NT);
+    const int tgroups = (g.T + 63) / 64;
     int blocks = 0;
     for (int i = 0; i < g.n; i++) {
         g.e[i].block0 = blocks;
         blocks += (g.e[i].W.M + 63) / 64 * tgroups;
     }
-    if (!blocks) return true;
-    const size_t lds = (size_t)16 * NT * 64 * 4;
-    if (wtype == W_F16) {
-        if (NT == 2) hipLaunchKernelGGL((k_fmm<W_F16, 2>), dim3(blocks), dim3(256), lds, st, g);
-        else hipLaunchKernelGGL((k_fmm<W_F16, 1>), dim3(blocks), dim3(256), lds, st, g);
-    } else {
-        if (NT == 2) hipLaunchKernelGGL((k_fmm<W_F32, 2>), dim3(blocks), dim3(256), lds, st, g);
-        else hipLaunchKernelGGL((k_fmm<W_F32, 1>), dim3(blocks), dim3(256), lds, st, g);
-    }
+    // a grid far below the chip's size (the v7 LoRA first stages: 64-160 rows) keeps k_mm_small,
+    // which spreads such shapes over more workgroups
+    if (blocks < g_fmm_min_blocks && !g.fmm) return true;
+    if (wtype == W_F16) hipLaunchKernelGGL(k_fmm<W_F16>, dim3(blocks), dim3(256), 0, st, g);
+    else hipLaunchKernelGGL(k_fmm<W_F32>, dim3(blocks), dim3(256), 0, st, g);
     HIP_OK(hipGetLastError());
     *launched = true;
     return true;

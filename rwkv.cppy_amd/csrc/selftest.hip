@@ -96,6 +96,7 @@ static bool selftest_mm(int wtype, const void * W, int K, int M, const float * x
         g.e[0].ldy = M;
         g.e[0].epi = EPI_STORE;
         g.split = split;
+        g.fmm = 1;  // the f32-MFMA form for float weights whenever it applies (T >= 16)
         if (mfma) {
             g.part_floats = (size_t)8 * T * M * 2;
             g.part = (float *)b.alloc(g.part_floats * 4);

@@ -82,7 +82,8 @@ def test_activation_quantizer_bit_exact(wfmt, afmt):
 
 @pytest.mark.parametrize('fmt', ['FP32', 'FP16', 'Q4_0', 'Q4_1', 'Q5_0', 'Q5_1', 'Q8_0'])
 @pytest.mark.parametrize('M,K,T', [(2048, 2048, 1), (100, 96, 1), (64, 7168, 1), (160, 2048, 5), (72, 320, 9),
-                                   (96, 2560, 16), (2560, 64, 40), (200, 2048, 64), (64, 160, 33)])
+                                   (96, 2560, 16), (2560, 64, 40), (200, 2048, 64), (64, 160, 33),
+                                   (4096, 2048, 128), (512, 7168, 80)])
 def test_matmul_kernel(fmt, M, K, T):
     """The sequence / batched matmul vs the GPU-association oracle, bit for bit; from T = 16 the FP16 and
     FP32 weights run on the f32 MFMA (mv_fmfma.hip)."""

@@ -61,8 +61,9 @@ struct ActBuf {
 // Records the int8-MFMA GEMM (qgemm.hip) copies global->LDS as whole, contiguous pieces:
 //   weights     per (row tile of qg_rows rows, block b), ordered [row tile][b]:
 //                 [rows x 32 int8 (the block's integer weights, offset applied: q-8 / q-16 for
-//                  _0, q for _1, 5th bit merged)][rows x f32 d][_1: rows x f32 m] (the fp16
-//                  scales widened exactly, so the GEMM epilogue needs no conversion)
+//                  _0, q for _1, 5th bit merged)][rows x f32 d] (the fp16 scales widened exactly,
+//                  so the GEMM epilogue needs no conversion); the _1 formats' mins m go to DMat::mt
+//                  ([block][row] f32), read by the m*s chain kernel (qgemm.hip k_qg_msum)
 //   activations per (QG_TOK-token tile, block b), ordered [token tile][b]:
 //                 [2 halves x QG_TOK tokens x 16 B int8][QG_TOK x f32 d][Q8_1: QG_TOK x f32 s]
 constexpr int QG_TOK = 64;
@@ -72,10 +73,11 @@ constexpr int QG_TOK = 64;
 // r + 8 sharing banks (2-way conflicts on every read, 49% of LDS cycles in the PMC profile).
 __host__ __device__ constexpr int qg_w_off(int r, int byte) { return r * 32 + (byte ^ (((r >> 3) & 1) << 4)); }
 __host__ __device__ constexpr bool qg_one(int wt) { return wt == W_Q4_1 || wt == W_Q5_1; }
-__host__ __device__ constexpr int qg_rows(int wt) { return qg_one(wt) ? 32 : 64; }
+__host__ __device__ constexpr int qg_rows(int) { return 64; }
 __host__ __device__ constexpr int qg_w_d(int wt) { return qg_rows(wt) * 32; }
-__host__ __device__ constexpr int qg_w_m(int wt) { return qg_w_d(wt) + qg_rows(wt) * 4; }
-__host__ __device__ constexpr int qg_w_bytes(int wt) { return qg_w_m(wt) + (qg_one(wt) ? qg_rows(wt) * 4 : 0); }
+__host__ __device__ constexpr int qg_w_bytes(int wt) { return qg_w_d(wt) + qg_rows(wt) * 4; }
+// DMat::mt row stride (rows padded with zeros to a multiple of 16, k_qg_msum's row tiles)
+__host__ __device__ constexpr int qm_stride(int M) { return (M + 15) / 16 * 16; }
 constexpr int QG_A_D = 2 * QG_TOK * 16;
 constexpr int QG_A_S = QG_A_D + QG_TOK * 4;
 __host__ __device__ constexpr int qg_a_bytes(bool one) { return QG_A_S + (one ? QG_TOK * 4 : 0); }
@@ -88,6 +90,7 @@ struct DMat {
     const uint32_t * qh;    // Q5 high bits
     const void * sc;        // u16 d  or u32 (d | m<<16)
     const uint8_t * gt;     // the same blocks as sequence-GEMM tile records (qg_w_*), quantized types
+    const float * mt;       // _1 formats with tile records: the mins m as f32, [K / 32][qm_stride(M)]
 };
 
 enum Epi : int {
@@ -116,8 +119,9 @@ struct MMEntry {
     int epi;
     int block0;         // first workgroup of this entry
     int fuse_emit;      // qgemm: the epilogue emits `out` (Q8_0 tiles) itself; y is not written
-    size_t poff;        // qgemm split-K: this entry's partials at part + poff ([S][T][M], _1: twice)
+    size_t poff;        // qgemm split-K: this entry's partials at part + poff ([S][T][M])
     int cblock0;        // qgemm split-K: first workgroup of this entry in the combine launch
+    size_t moff;        // qgemm _1 formats: this entry's m*s totals at m2 + moff ([M][T])
 };
 
 constexpr int MM_MAX_ENTRIES = 8;
@@ -126,10 +130,12 @@ struct MMGroup {
     MMEntry e[MM_MAX_ENTRIES];
     int n;
     int T;
-    float * part;        // split-K partials (qgemm.hip): up to 8 x T x sum(M) floats (x2 for _1 formats)
+    float * part;        // split-K partials (qgemm.hip): up to 8 x T x sum(M) floats
     size_t part_floats;
+    float * m2;          // qgemm _1 formats: the m*s chain totals, [M][T] per entry (k_qg_msum)
+    size_t m2_floats;
     int split;           // qgemm split-K: 0 = by tile count, 1 = never, 4 / 8 = forced
-    int fmm;             // float weights, T >= 16: 0 = f32-MFMA form when the grid fills the chip, 1 = always
+    int fmm;             // float weights: 0 = f32-MFMA form from T = 32, 1 = from T = 16
 };
 
 #define HIP_OK(x)                                                                             \

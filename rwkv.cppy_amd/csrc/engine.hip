@@ -106,6 +106,7 @@ bool upload_mat(DeviceModel & dm, const HostTensor * t, DMat & out, bool count_b
     }
     out.type = (int)t->type;
     out.gt = nullptr;
+    out.mt = nullptr;
     out.K = (int)t->ne[0];
     out.M = (int)t->ne[1];
     const size_t M = out.M, K = out.K;
@@ -187,15 +188,20 @@ bool upload_mat(DeviceModel & dm, const HostTensor * t, DMat & out, bool count_b
                         }
                         const float d = f16_to_f32(one ? (uint16_t)(sc32[i] & 0xFFFFu) : sc16[i]);
                         memcpy(rec + qg_w_d(wt) + r * 4, &d, 4);
-                        if (one) {
-                            const float m = f16_to_f32((uint16_t)(sc32[i] >> 16));
-                            memcpy(rec + qg_w_m(wt) + r * 4, &m, 4);
-                        }
                     }
                 }
             uint8_t * dg = dalloc<uint8_t>(dm, gt.size());
             if (!dg || hipMemcpy(dg, gt.data(), gt.size(), hipMemcpyHostToDevice) != hipSuccess) return false;
             out.gt = dg;
+            if (one) {  // the mins, block-major, for the m*s chain kernel
+                const size_t MS = qm_stride((int)M);  // rows padded to k_qg_msum's 8-row loads
+                std::vector<float> mt(nb * MS, 0.0f);
+                for (size_t r = 0; r < M; r++)
+                    for (size_t b = 0; b < nb; b++) mt[b * MS + r] = f16_to_f32((uint16_t)(sc32[r * nb + b] >> 16));
+                float * dmt = dalloc<float>(dm, mt.size());
+                if (!dmt || hipMemcpy(dmt, mt.data(), mt.size() * 4, hipMemcpyHostToDevice) != hipSuccess) return false;
+                out.mt = dmt;
+            }
         }
     }
     if (count_bytes) {
@@ -362,6 +368,7 @@ Engine::~Engine() {
     if (blogits_) (void)hipFree(blogits_);
     if (gy_) (void)hipFree(gy_);
     if (part_) (void)hipFree(part_);
+    if (m2_) (void)hipFree(m2_);
     for (void * p : ws_allocs_) (void)hipFree(p);
     if (htokens_) (void)hipHostFree(htokens_);
     collect_timing();
@@ -583,12 +590,37 @@ void Engine::set_timing(bool on) {
     if (on) stats_.clear();
 }
 
+// Split-K partial scratch of at least n floats (grows; captured batched graphs point at the old one)
+bool Engine::ensure_part(size_t n) {
+    if (n <= part_cap_) return true;
+    HIP_OK(hipStreamSynchronize(stream_));
+    drop_batch_graphs();
+    if (part_) (void)hipFree(part_);
+    part_ = nullptr;
+    part_cap_ = 0;
+    if (hipMalloc(&part_, n * 4 + 64) != hipSuccess) {
+        part_ = nullptr;
+        (void)hipGetLastError();
+        return false;
+    }
+    part_cap_ = n;
+    return true;
+}
+
 // Sequence matmuls on quantized weights go to the int8-MFMA GEMM; entries that only emit get
 // a scratch y, and emission is a separate quantization pass (same bits as k_mm's epilogue).
 bool Engine::mm_dispatch(MMGroup & g, int wtype) {
     // batched decode (bs_ > 0): the decode matvec over the contexts (k_mvb; k_mm for shapes it
     // does not cover -- the same bits); from batch_gemm_min_ contexts on, the quantized matmuls
     // take the int8-MFMA sequence GEMM on token tiles instead (tile_acts_; also the same bits)
+    if (!wtype_quantized(wtype) && g.T >= 32) {
+        // k_fmm may split the class tree of a small grid (the v7 LoRA first stage): partials
+        size_t msum = 0;
+        for (int i = 0; i < g.n; i++) msum += g.e[i].W.M;
+        if (!ensure_part((size_t)8 * g.T * msum)) return false;
+        g.part = part_;
+        g.part_floats = part_cap_;
+    }
     if (bs_ && !(tile_acts_ && wtype_quantized(wtype))) {
         bool launched = false;
         // float weights (the F16 head, LoRA) over 16+ contexts: the f32-MFMA form, same bits
@@ -624,22 +656,27 @@ bool Engine::mm_dispatch(MMGroup & g, int wtype) {
             tiles += (size_t)(g.e[i].W.M + rows - 1) / rows * tilesT;
         }
         if (tiles < 1024) {
-            const size_t pneed = (size_t)8 * g.T * msum * (qg_one(wtype) ? 2 : 1);
-            if (pneed > part_cap_) {
+            if (!ensure_part((size_t)8 * g.T * msum)) return false;
+            g.part = part_;
+            g.part_floats = part_cap_;
+        }
+        if (qg_one(wtype)) {
+            const size_t mneed = (size_t)g.T * msum;
+            if (mneed > m2_cap_) {
                 HIP_OK(hipStreamSynchronize(stream_));
                 drop_batch_graphs();
-                if (part_) (void)hipFree(part_);
-                part_ = nullptr;
-                part_cap_ = 0;
-                if (hipMalloc(&part_, pneed * 4 + 64) != hipSuccess) {
-                    part_ = nullptr;
+                if (m2_) (void)hipFree(m2_);
+                m2_ = nullptr;
+                m2_cap_ = 0;
+                if (hipMalloc(&m2_, mneed * 4 + 64) != hipSuccess) {
+                    m2_ = nullptr;
                     (void)hipGetLastError();
                     return false;
                 }
-                part_cap_ = pneed;
+                m2_cap_ = mneed;
             }
-            g.part = part_;
-            g.part_floats = part_cap_;
+            g.m2 = m2_;
+            g.m2_floats = m2_cap_;
         }
     }
     size_t off = 0;
@@ -908,9 +945,11 @@ bool Engine::layer_v6(int l, int T, const float * si, float * so) {
     if (!b.run(*this, T)) return false;
     // order w, k, v, r, g (rwkv_graph.inc:336-346)
     ActBuf outs[5] = {A(1, L.decay_w1), A(2, L.att_k), A(3, L.att_v), A(4, L.att_r), A(5, L.att_g)};
-    // batched decode: the decode kernel's per-(mix, channel) arithmetic over the contexts
-    if (bs_ ? !launch_v6_mix5_dec(stream_, C, D, xa_, nullptr, lora_, L.maa_w2t, L.maa, outs, T, sx_)
-            : !launch_v6_mix5(stream_, T, C, D, lora_, L.maa_w2t, L.maa, xa_, sx_, outs))
+    // batched decode: the decode kernel's per-(mix, channel) arithmetic over the contexts; from
+    // batch_gemm_min_ contexts on (token-tile outputs) the sequence kernel's f32-MFMA form over the
+    // contexts as tokens -- W2 read once per 64 contexts instead of once per context, same bits
+    if ((bs_ && !tile_acts_) ? !launch_v6_mix5_dec(stream_, C, D, xa_, nullptr, lora_, L.maa_w2t, L.maa, outs, T, sx_)
+                             : !launch_v6_mix5(stream_, T, C, D, lora_, L.maa_w2t, L.maa, xa_, sx_, outs))
         return false;
     ActBuf dl = A(6, L.decay_w2);
     // decay tail by threads (k_att6_dec's rows) when Wd2 is quantized; dl fp32 then reuses lora_

@@ -166,10 +166,13 @@ class Engine {
     static constexpr size_t kMvScratch = 4u << 20;
     bool replay_mv_timing();
     bool mm_dispatch(MMGroup & g, int wtype);
+    bool ensure_part(size_t n);
     float * gy_ = nullptr;     // scratch y of emit-only GEMM entries
     size_t gy_cap_ = 0;
-    float * part_ = nullptr;   // split-K partials (launch_qgemm)
+    float * part_ = nullptr;   // split-K partials (launch_qgemm, k_fmm)
     size_t part_cap_ = 0;
+    float * m2_ = nullptr;     // _1 formats: m*s chain totals (launch_qgemm, k_qg_msum)
+    size_t m2_cap_ = 0;
     bool use_mm_ = false;
     bool tile_acts_ = false;  // Aview: Q8 activations in sequence-GEMM tiles (forward, T >= 2)
     // batched decode (eval_batch): state floats per context while a batched forward is built

@@ -498,7 +498,10 @@ bool launch_ln_mix(hipStream_t st, const LnMixArgs & a) {
         const int v = e ? atoi(e) : 1;
         return v >= 1 && v <= 16 ? v : 1;
     }();
-    const int gy = a.T <= 64 ? (a.C + 255) / 256 : std::min(ln_mix_y, (a.C + 255) / 256);
+    // fewer token groups than ~2 per CU (short sequences, batched decode): the channel blocks over
+    // grid.y until the grid holds about 512 workgroups
+    const int tgs = (a.T + TOKS_PER_WG - 1) / TOKS_PER_WG, cbs = (a.C + 255) / 256;
+    const int gy = a.T <= 64 ? cbs : tgs < 256 ? std::min(cbs, (512 + tgs - 1) / tgs) : std::min(ln_mix_y, cbs);
     const dim3 grid((a.T + TOKS_PER_WG - 1) / TOKS_PER_WG, gy), block(256 * TOKS_PER_WG);
     const int tq = tile_q(a.out, a.n_out, a.C);
     if (tq == 1) hipLaunchKernelGGL(k_ln_mix<1>, grid, block, 0, st, a);

@@ -13,6 +13,8 @@ bool launch_mm_group(hipStream_t st, MMGroup & g, int wtype);
 bool launch_qgemm(hipStream_t st, MMGroup & g, int wtype);
 // F16 / F32 weights over T >= 16 tokens on the f32 MFMA (mv_fmfma.hip); *launched = false: not covered
 bool launch_fmm_group(hipStream_t st, MMGroup & g, int wtype, bool * launched);
+bool launch_qg_combine(hipStream_t st, MMGroup & g, int split);
+extern int kQgCUs;
 // Batched decode matvec (mv_batch.hip): the T rows are T independent contexts; same results as
 // launch_mm_group.  *launched = false (and nothing enqueued) for shapes it does not cover.
 bool launch_mvb_group(hipStream_t st, MMGroup & g, int wtype, bool * launched);

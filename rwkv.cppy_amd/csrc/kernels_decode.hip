@@ -35,11 +35,9 @@ int mva_rows() {
     return v;
 }
 extern int kQgCUs;
-extern int g_fmm_min_blocks;
 void set_mv_device_cus(int n) {
     g_mv_cus = n > 0 ? n : 256;
     kQgCUs = g_mv_cus;
-    g_fmm_min_blocks = 2 * g_mv_cus;
 }
 
 bool launch_mv_group(hipStream_t st, MVGroup & g) {

@@ -59,7 +59,11 @@ constexpr int FM_KS = 64 * FM_RS + 16;    // dwords per kk plane (= 16 mod 32: l
 constexpr int FM_OP = 4 * FM_KS;          // one operand tile (64 rows or tokens)
 constexpr int FM_BUF = 2 * FM_OP;         // weights + activations
 
-template <int WF>
+// SPLIT > 1 (grids of few tiles, e.g. the v7 LoRA first stage): workgroup s of a tile walks classes
+// [s 64 / SPLIT, (s + 1) 64 / SPLIT) only -- a complete subtree of the class tree -- and stores the
+// subtree sums to the entry's partials; k_qg_combine adds the tree's top levels, applies the epilogue
+// and emits: the same bits as the unsplit kernel.
+template <int WF, int SPLIT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_fmm(MMGroup g) {
     __shared__ uint32_t fsm[2 * FM_BUF];  // [2 buffers][W, X][kk][64][FM_RS]; after the loop: red[64 tok][64 rows]
     using U = FUnit<WF>;
@@ -78,6 +82,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         const int ne = e + 1 < g.n ? nloc : (int)gridDim.x - E.block0;
         if (tgroups > 1 && (E.block0 & 7) == 0 && (ne & 7) == 0) local = (local & 7) * (ne >> 3) + (local >> 3);
     }
+    const int sidx = local % SPLIT;
+    local /= SPLIT;
     const int rt = local / tgroups, tg = local % tgroups;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int ml = lane & 15, kk = lane >> 4;
@@ -88,7 +94,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const int units = (K + STR - 1) / STR;
     // classes holding a unit (K < 64 units: the rest are zero leaves of the tree, folded below)
     const int ncls = units > 1 ? 64 : min(64, (K + EL - 1) / EL);
-    const int nsteps = ncls * units;
+    // this workgroup's classes [l0, l0 + ncls_w) (SPLIT > 1: ncls = 64, K >= 512)
+    const int l0 = sidx * (64 / SPLIT), ncls_w = SPLIT > 1 ? 64 / SPLIT : ncls;
+    const int sbase = l0 * units, nsteps = ncls_w * units;
     const int nst = (nsteps + FM_SU - 1) / FM_SU;
     const size_t rowb = (size_t)K * (WF == W_F16 ? 2 : 4);
 
@@ -98,7 +106,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
         for (int p = 0; p < 4; p++) {
             const int q = tid + 256 * p, ln = q >> 4, j = q & 15;
-            const int s = min(stg * FM_SU + j, nsteps - 1);
+            const int s = sbase + min(stg * FM_SU + j, nsteps - 1);
             const int l = s / units, u = s - l * units;
             const int k = min(EL * l + STR * u, K - EL);  // a unit past K: clamped, never multiplied
             const size_t kb = (size_t)k * (WF == W_F16 ? 2 : 4);
@@ -155,7 +163,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     gload(0);
     lstore(0);
     __syncthreads();
-    int l = 0, u = 0;  // the step being multiplied
+    int l = l0, u = 0;  // the step being multiplied
 #pragma unroll 1
     for (int stg = 0; stg < nst; stg++) {
         if (stg + 1 < nst) gload(stg + 1);  // in flight under this stage's MFMAs
@@ -188,7 +196,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             }
             if (++u == units) {
                 u = 0;
-                FMM_FOLD(l);
+                FMM_FOLD(l - l0);  // the subtree's own counter (l0 = 0 unsplit)
                 l++;
             }
 #pragma unroll
@@ -197,10 +205,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         if (stg + 1 < nst) lstore((stg + 1) & 1);
         __syncthreads();
     }
+    if constexpr (SPLIT == 1) {
 #pragma unroll 1
-    for (; l < 64; l++) FMM_FOLD(l);  // classes without units: zero partials (the matvec adds them too)
+        for (; l < 64; l++) FMM_FOLD(l);  // classes without units: zero partials (the matvec adds them too)
+    }
 #undef FMM_FOLD
 #undef FMM_CLOSE
+    if constexpr (SPLIT > 1) {
+        // the subtree of 64 / SPLIT classes closed at level log2(64 / SPLIT)
+        constexpr int LEV = SPLIT == 4 ? 4 : 3;
+        float * part = g.part + E.poff + (size_t)sidx * T * M;
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+#pragma unroll
+            for (int n = 0; n < 2; n++) {
+                const int t = tok0 + wt + 16 * n + ml;
+                if (t >= T) continue;
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int row = row0 + wr + 16 * i + 4 * kk + q;
+                    if (row < M) part[(size_t)t * M + row] = st[LEV][i][n][q];
+                }
+            }
+        return;
+    }
     // D layout: lane holds rows 4 * kk + q of a 16-row tile, token ml of a 16-token tile
     float * red = (float *)fsm;
 #pragma unroll
@@ -225,15 +253,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 // MFMA float matmul for a group: F16 / F32 weights, T >= 16 tokens (or contexts), every entry's
 // input in the weight type's activation format, row-major (not tiled); emitting entries need M % 32
 // == 0.  Returns false with *launched = false when the group is outside that (caller keeps k_mm).
-int g_fmm_min_blocks = 512;
-
 bool launch_fmm_group(hipStream_t st, MMGroup & g, int wtype, bool * launched) {
     static const bool on = [] {
         const char * v = getenv("RWKV_MI355X_FMM");  // 0: float matmuls stay on k_mm / k_mvb
         return !(v && v[0] == '0');
     }();
     *launched = false;
-    if (!on || (wtype != W_F16 && wtype != W_F32) || g.T < 16) return true;
+    // below 32 tokens (contexts) the 64-token tile is mostly padding: k_mvb / k_mm_small stay
+    if (!on || (wtype != W_F16 && wtype != W_F32) || g.T < 16 || (g.T < 32 && !g.fmm)) return true;
+    // short rows over few tokens (the v7 LoRA second stages, K <= 320, in a batched decode step: a
+    // few steps against the stage and epilogue overhead) stay on k_mvb (22 us vs 51 us at B = 32);
+    // over a sequence k_fmm wins (135 us vs k_mm_small's 177 us at T = 1024)
+    for (int i = 0; i < g.n && !g.fmm && g.T < 256; i++)
+        if (g.e[i].W.K < 512) return true;
     for (int i = 0; i < g.n; i++) {
         const MMEntry & e = g.e[i];
         if (e.W.type != wtype || e.W.K % 32 || e.in.tiled || e.in.fmt != act_fmt_for(wtype) || e.in.K != e.W.K)
@@ -249,12 +281,35 @@ bool launch_fmm_group(hipStream_t st, MMGroup & g, int wtype, bool * launched) {
         g.e[i].block0 = blocks;
         blocks += (g.e[i].W.M + 63) / 64 * tgroups;
     }
-    // a grid far below the chip's size (the v7 LoRA first stages: 64-160 rows) keeps k_mm_small,
-    // which spreads such shapes over more workgroups
-    if (blocks < g_fmm_min_blocks && !g.fmm) return true;
-    if (wtype == W_F16) hipLaunchKernelGGL(k_fmm<W_F16>, dim3(blocks), dim3(256), 0, st, g);
-    else hipLaunchKernelGGL(k_fmm<W_F32>, dim3(blocks), dim3(256), 0, st, g);
+    // a grid of a few workgroups (the v7 LoRA first stage over 32 contexts: 10) is slower than the
+    // matvec forms, which spread such shapes over more workgroups
+    if (blocks < 128 && !g.fmm) return true;
+    // below 2 workgroups per CU: split the class tree (4 or 8 subtrees) when the partials fit
+    int split = g.split == 4 || g.split == 8 ? g.split : blocks >= 2 * kQgCUs ? 1 : blocks * 4 >= 2 * kQgCUs ? 4 : 8;
+    if (g.split == 1) split = 1;
+    if (split > 1) {
+        size_t pfl = 0;
+        bool ok = g.part != nullptr;
+        for (int i = 0; i < g.n; i++) {
+            g.e[i].poff = pfl;
+            pfl += (size_t)split * g.T * g.e[i].W.M;
+            ok = ok && g.e[i].W.K >= 512 && g.e[i].W.M % 32 == 0;
+        }
+        if (!ok || g.part_floats < pfl) split = 1;
+    }
+#define FMM_L(WFv)                                                                                               \
+    do {                                                                                                         \
+        if (split == 4) hipLaunchKernelGGL((k_fmm<WFv, 4>), dim3(blocks * 4), dim3(256), 0, st, g);             \
+        else if (split == 8) hipLaunchKernelGGL((k_fmm<WFv, 8>), dim3(blocks * 8), dim3(256), 0, st, g);        \
+        else hipLaunchKernelGGL((k_fmm<WFv, 1>), dim3(blocks), dim3(256), 0, st, g);                             \
+    } while (0)
+    if (split > 1)
+        for (int i = 0; i < g.n; i++) g.e[i].block0 *= split;
+    if (wtype == W_F16) FMM_L(W_F16);
+    else FMM_L(W_F32);
+#undef FMM_L
     HIP_OK(hipGetLastError());
+    if (split > 1 && !launch_qg_combine(st, g, split)) return false;
     *launched = true;
     return true;
 }

@@ -79,16 +79,18 @@ constexpr int QG_STEPS = 8;  // blocks per chunk
 template <int WF>
 struct QGLayout {
     static constexpr bool ONE = qg_one(WF);
-    static constexpr int TI = ONE ? 1 : 2;
+    static constexpr int TI = 2;
     static constexpr int ROWS = qg_rows(WF);        // = 32 * TI
     static constexpr int WB = qg_w_bytes(WF);       // weight record
-    static constexpr int AB = qg_a_bytes(ONE);      // activation record
-    static constexpr int STEP = WB + AB;            // LDS bytes per step: [weight rec][act rec]
+    static constexpr int AB = qg_a_bytes(ONE);      // activation record (stride)
+    static constexpr int AC = QG_A_S;               // of which copied: the int8 values and d (Q8_1's s
+                                                    // feeds k_qg_msum, not this kernel)
+    static constexpr int STEP = WB + AC;            // LDS bytes per step: [weight rec][act rec]
     static constexpr int BUF = STEP * QG_STEPS;
     static constexpr int WP = (WB + 1023) / 1024;   // copy instructions per record
-    static constexpr int AP = (AB + 1023) / 1024;
+    static constexpr int AP = (AC + 1023) / 1024;
     static constexpr int JOBS = WP + AP;
-    static_assert(ROWS == 32 * TI && WB % 16 == 0 && AB % 16 == 0, "qgemm layout");
+    static_assert(ROWS == 32 * TI && WB % 16 == 0 && AB % 16 == 0 && AC % 16 == 0, "qgemm layout");
 };
 
 // Class-major walk over the blocks: class l (= b mod 64) has n = q + (l < rem) blocks, q = nb/64,
@@ -125,7 +127,7 @@ __device__ __forceinline__ void qg_load_chunk(v4i_t rw, v4i_t ra, unsigned lds_b
             const int b = wk.block();
             const unsigned m = lds_buf + k * Lt::STEP;
             qg_record<Lt::WB>(rw, (unsigned)(b * Lt::WB), m, lane);
-            qg_record<Lt::AB>(ra, (unsigned)(b * Lt::AB), m + Lt::WB, lane);
+            qg_record<Lt::AC>(ra, (unsigned)(b * Lt::AB), m + Lt::WB, lane);
         }
 #pragma unroll
         for (int i = 0; i < 4; i++) wk.next();
@@ -136,8 +138,8 @@ __device__ __forceinline__ void qg_load_chunk(v4i_t rw, v4i_t ra, unsigned lds_b
 template <int TI>
 struct QGOps {
     long af[TI], xf[2];
-    float4 sd[TI], sm[TI];  // d (m) of the 4 D-layout rows 4h..4h+3 of each 16-row tile
-    float dx[2], sx[2];
+    float4 sd[TI];  // d of the 4 D-layout rows 4h..4h+3 of each 16-row tile
+    float dx[2];
 };
 
 template <int WF>
@@ -149,7 +151,6 @@ __device__ __forceinline__ void qg_read_ops(const char * sp, QGOps<QGLayout<WF>:
         o.af[i] = *(const long *)(sp + qg_w_off(wr + 16 * i + r16, h * 8));  // int8 row, k = 8h..8h+7
         const int ro = wr + 16 * i + 4 * h;
         o.sd[i] = *(const float4 *)(sp + qg_w_d(WF) + ro * 4);
-        if constexpr (Lt::ONE) o.sm[i] = *(const float4 *)(sp + qg_w_m(WF) + ro * 4);
     }
     const char * ap = sp + Lt::WB;
 #pragma unroll
@@ -157,7 +158,6 @@ __device__ __forceinline__ void qg_read_ops(const char * sp, QGOps<QGLayout<WF>:
         const int tl = wt + 16 * j + r16;
         o.xf[j] = *(const long *)(ap + (h >> 1) * QG_TOK * 16 + tl * 16 + (h & 1) * 8);
         o.dx[j] = *(const float *)(ap + QG_A_D + tl * 4);
-        if constexpr (Lt::ONE) o.sx[j] = *(const float *)(ap + QG_A_S + tl * 4);
     }
 }
 
@@ -179,34 +179,16 @@ __device__ __forceinline__ void qg_mfma(const QGOps<TI> & cur, v4i_t (&sv)[TI][2
         for (int j = 0; j < 2; j++) sv[i][j] = __builtin_amdgcn_mfma_i32_16x16x32_i8(cur.af[i], cur.xf[j], bias, 0, 0, 0);
 }
 
-// The fp32 block epilogue: acc = fma(d_w * d_x, sumi, acc) (+ acc2 += m_w * s_x), rows in pairs;
-// FIRST: the class's first block (its chain starts from 0)
-template <bool ONE, bool FIRST, int TI>
-__device__ __forceinline__ void qg_epi(const QGOps<TI> & cur, const v4i_t (&sv)[TI][2], float (&acc)[TI][2][4],
-                                       float (&acc2)[TI][2][4]) {
-#ifdef QG_SCALAR
-    // scalar f32 operations (packed f32 beside MFMAs issues slower than two scalar ones)
-#pragma unroll
-    for (int i = 0; i < TI; i++) {
-        const float dw[4] = {cur.sd[i].x, cur.sd[i].y, cur.sd[i].z, cur.sd[i].w};
-        const float mw[4] = {cur.sm[i].x, cur.sm[i].y, cur.sm[i].z, cur.sm[i].w};
-#pragma unroll
-        for (int j = 0; j < 2; j++)
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const float si = __int_as_float(sv[i][j][q]) - QG_BIAS_F;
-                acc[i][j][q] = fmaf(dw[q] * cur.dx[j], si, FIRST ? 0.0f : acc[i][j][q]);
-                if constexpr (ONE) acc2[i][j][q] = (FIRST ? 0.0f : acc2[i][j][q]) + mw[q] * cur.sx[j];
-            }
-    }
-#else
+// The fp32 block epilogue: acc = fma(d_w * d_x, sumi, acc), rows in pairs (packed f32: bitwise the
+// scalar operations, tools/pk_probe.hip); FIRST: the class's first block (its chain starts from 0)
+template <bool FIRST, int TI>
+__device__ __forceinline__ void qg_epi(const QGOps<TI> & cur, const v4i_t (&sv)[TI][2], float (&acc)[TI][2][4]) {
     const qf2_t nbias = {-QG_BIAS_F, -QG_BIAS_F};
 #pragma unroll
     for (int i = 0; i < TI; i++)
 #pragma unroll
         for (int qp = 0; qp < 2; qp++) {
             const qf2_t dw = qp ? qf2_t{cur.sd[i].z, cur.sd[i].w} : qf2_t{cur.sd[i].x, cur.sd[i].y};
-            const qf2_t mw = qp ? qf2_t{cur.sm[i].z, cur.sm[i].w} : qf2_t{cur.sm[i].x, cur.sm[i].y};
 #pragma unroll
             for (int j = 0; j < 2; j++) {
                 const qf2_t dx = {cur.dx[j], cur.dx[j]};
@@ -215,24 +197,17 @@ __device__ __forceinline__ void qg_epi(const QGOps<TI> & cur, const v4i_t (&sv)[
                 const qf2_t a = __builtin_elementwise_fma(dw * dx, si, a0);
                 acc[i][j][2 * qp] = a.x;
                 acc[i][j][2 * qp + 1] = a.y;
-                if constexpr (ONE) {
-                    const qf2_t sx = {cur.sx[j], cur.sx[j]};
-                    const qf2_t b0 = FIRST ? qf2_t{0.0f, 0.0f} : qf2_t{acc2[i][j][2 * qp], acc2[i][j][2 * qp + 1]};
-                    const qf2_t b = b0 + mw * sx;
-                    acc2[i][j][2 * qp] = b.x;
-                    acc2[i][j][2 * qp + 1] = b.y;
-                }
             }
         }
-#endif
 }
 
-// y[t][m] = epi(total (+ total2)), as k_mm's red + red2.  A lane holds rows 4h..4h+3 of one
-// token: one 16-byte access per (token, 4 rows) when aligned.
-template <bool ONE, int TI>
-__device__ __forceinline__ void qg_store(const MMEntry & E, int T, int M, int tok0, int row0, int wt, int wr, int r16,
-                                         int h, const float (&tot)[TI][2][4], const float (&tot2)[TI][2][4]) {
-    if constexpr (TI == 2 && !ONE) {
+// y[t][m] = epi(total + t2), t2 = the m*s total (m2, _1 formats; k_qg_msum) or +0.0f, as k_mm's
+// red + red2.  A lane holds rows 4h..4h+3 of one token: one 16-byte access per (token, 4 rows)
+// when aligned.
+template <int TI>
+__device__ __forceinline__ void qg_store(const MMEntry & E, const float * m2, int T, int M, int tok0, int row0, int wt,
+                                         int wr, int r16, int h, const float (&tot)[TI][2][4]) {
+    if constexpr (TI == 2) {
         if (E.fuse_emit) {
             // The wave's 32 rows (wr % 32 == 0) of a token are one quantization block of the next
             // matmul's input: lanes r16 + 16 h hold rows 16 i + 4 h + q.  quant32 / store32's values:
@@ -240,16 +215,22 @@ __device__ __forceinline__ void qg_store(const MMEntry & E, int T, int M, int to
 #pragma unroll
             for (int j = 0; j < 2; j++) {
                 const int t = tok0 + wt + 16 * j + r16;
+                const int tc = min(t, T - 1);
                 float v[2][4];
                 float am = 0.0f;
 #pragma unroll
-                for (int i = 0; i < 2; i++)
+                for (int i = 0; i < 2; i++) {
+                    const int mb = row0 + wr + 16 * i + 4 * h;
+                    float t2q[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+                    if (m2)
+#pragma unroll
+                        for (int q = 0; q < 4; q++) t2q[q] = m2[(size_t)(mb + q) * T + tc];
 #pragma unroll
                     for (int q = 0; q < 4; q++) {
-                        const int m = row0 + wr + 16 * i + 4 * h + q;
-                        v[i][q] = apply_epi_v(E, m, tot[i][j][q] + 0.0f, 0.0f, 0.0f);
+                        v[i][q] = apply_epi_v(E, mb + q, tot[i][j][q] + t2q[q], 0.0f, 0.0f);
                         am = fmaxf(am, fabsf(v[i][q]));
                     }
+                }
                 am = fmaxf(am, __shfl_xor(am, 16));
                 am = fmaxf(am, __shfl_xor(am, 32));
                 const float d = am / 127.f;
@@ -282,7 +263,7 @@ __device__ __forceinline__ void qg_store(const MMEntry & E, int T, int M, int to
             if (t >= T || m0 >= M) continue;
             float acc[4];
 #pragma unroll
-            for (int q = 0; q < 4; q++) acc[q] = ONE ? tot[i][j][q] + tot2[i][j][q] : tot[i][j][q] + 0.0f;
+            for (int q = 0; q < 4; q++) acc[q] = tot[i][j][q] + (m2 && m0 + q < M ? m2[(size_t)(m0 + q) * T + t] : 0.0f);
             float * yp = E.y + (size_t)t * E.ldy + m0;
             if (vec) {
                 float4 yv = make_float4(0.f, 0.f, 0.f, 0.f), av = yv;
@@ -302,11 +283,10 @@ __device__ __forceinline__ void qg_store(const MMEntry & E, int T, int M, int to
         }
 }
 
-// Split-K: one split's subtree sums to its entry's partials [S][T][M] (_1 formats: the m*s
-// subtree sums follow as a second [S][T][M] array)
-template <bool ONE, int TI, int SPLIT>
+// Split-K: one split's subtree sums to its entry's partials [S][T][M]
+template <int TI>
 __device__ __forceinline__ void qg_store_part(float * part, int sidx, int T, int M, int tok0, int row0, int wt, int wr,
-                                              int r16, int h, const float (&sub)[TI][2][4], const float (&sub2)[TI][2][4]) {
+                                              int r16, int h, const float (&sub)[TI][2][4]) {
 #pragma unroll
     for (int i = 0; i < TI; i++)
 #pragma unroll
@@ -317,18 +297,14 @@ __device__ __forceinline__ void qg_store_part(float * part, int sidx, int T, int
             float * pp = part + ((size_t)sidx * T + t) * M + m0;
 #pragma unroll
             for (int q = 0; q < 4; q++)
-                if (m0 + q < M) {
-                    pp[q] = sub[i][j][q];
-                    if constexpr (ONE) pp[(size_t)SPLIT * T * M + q] = sub2[i][j][q];
-                }
+                if (m0 + q < M) pp[q] = sub[i][j][q];
         }
 }
 
 // Class-pair fold: the odd class (in c) closes N >= 1 levels of the binary counter: v = c, then
 // v = st[k] + v for k < N, into st[N] (N < 6) or the total (N = 6)
-template <bool ONE, int TI, int N>
-__device__ __forceinline__ void qg_fold(float (&st)[6][TI][2][4], float (&st2)[6][TI][2][4], const float (&c)[TI][2][4],
-                                        const float (&c2)[TI][2][4], float (&tot)[TI][2][4], float (&tot2)[TI][2][4]) {
+template <int TI, int N>
+__device__ __forceinline__ void qg_fold(float (&st)[6][TI][2][4], const float (&c)[TI][2][4], float (&tot)[TI][2][4]) {
 #pragma unroll
     for (int i = 0; i < TI; i++)
 #pragma unroll
@@ -340,13 +316,6 @@ __device__ __forceinline__ void qg_fold(float (&st)[6][TI][2][4], float (&st2)[6
                 for (int kk = 0; kk < N; kk++) v = st[kk][i][j][q] + v;
                 if constexpr (N < 6) st[N][i][j][q] = v;
                 else tot[i][j][q] = v;
-                if constexpr (ONE) {
-                    float v2 = c2[i][j][q];
-#pragma unroll
-                    for (int kk = 0; kk < N; kk++) v2 = st2[kk][i][j][q] + v2;
-                    if constexpr (N < 6) st2[N][i][j][q] = v2;
-                    else tot2[i][j][q] = v2;
-                }
             }
 }
 
@@ -388,12 +357,13 @@ __global__ __launch_bounds__(256) void k_qgemm_k64(MMGroup g) {
             const int k = wave + 4 * h2, b = c * QG_STEPS + k;
             const unsigned m = buf + k * Lt::STEP;
             qg_record<Lt::WB>(rw, (unsigned)(b * Lt::WB), m, lane);
-            qg_record<Lt::AB>(ra, (unsigned)(b * Lt::AB), m + Lt::WB, lane);
+            qg_record<Lt::AC>(ra, (unsigned)(b * Lt::AB), m + Lt::WB, lane);
         }
     };
-    float st[6][TI][2][4], st2[6][TI][2][4];
-    float tot[TI][2][4], tot2[TI][2][4];
-    float c[TI][2][4], c2[TI][2][4];
+    const float * m2 = ONE ? g.m2 + E.moff : nullptr;
+    float st[6][TI][2][4];
+    float tot[TI][2][4];
+    float c[TI][2][4];
     load(ch0, lds0);
     qg_chunk_done();
     if (NCHL > 1) load(ch0 + 1, lds0 + Lt::BUF);
@@ -409,19 +379,19 @@ __global__ __launch_bounds__(256) void k_qgemm_k64(MMGroup g) {
             QGOps<TI> nxt = cur;
             if (k + 1 < QG_STEPS) qg_read_ops<WF>(buf + (k + 1) * Lt::STEP, nxt, wr, wt, r16, h);
             if (k & 1) {
-                qg_epi<ONE, true, TI>(cur, sv, c, c2);
-                if (k == 1 || k == 5) qg_fold<ONE, TI, 1>(st, st2, c, c2, tot, tot2);
-                else if (k == 3) qg_fold<ONE, TI, 2>(st, st2, c, c2, tot, tot2);
+                qg_epi<true, TI>(cur, sv, c);
+                if (k == 1 || k == 5) qg_fold<TI, 1>(st, c, tot);
+                else if (k == 3) qg_fold<TI, 2>(st, c, tot);
                 else {
                     switch (__builtin_ctz(~ch)) {
-                        case 0: qg_fold<ONE, TI, 3>(st, st2, c, c2, tot, tot2); break;
-                        case 1: qg_fold<ONE, TI, 4>(st, st2, c, c2, tot, tot2); break;
-                        case 2: qg_fold<ONE, TI, 5>(st, st2, c, c2, tot, tot2); break;
-                        default: qg_fold<ONE, TI, 6>(st, st2, c, c2, tot, tot2); break;
+                        case 0: qg_fold<TI, 3>(st, c, tot); break;
+                        case 1: qg_fold<TI, 4>(st, c, tot); break;
+                        case 2: qg_fold<TI, 5>(st, c, tot); break;
+                        default: qg_fold<TI, 6>(st, c, tot); break;
                     }
                 }
             } else {
-                qg_epi<ONE, true, TI>(cur, sv, st[0], st2[0]);
+                qg_epi<true, TI>(cur, sv, st[0]);
             }
             cur = nxt;
         }
@@ -432,11 +402,12 @@ __global__ __launch_bounds__(256) void k_qgemm_k64(MMGroup g) {
         }
     }
     if constexpr (SPLIT == 1) {
-        qg_store<ONE, TI>(E, T, M, tok0, row0, wt, wr, r16, h, tot, tot2);
+        qg_store<TI>(E, m2, T, M, tok0, row0, wt, wr, r16, h, tot);
     } else {
         // the subtree over this split's 8 * NCHL classes sits at level 3 + log2(NCHL)
         constexpr int LEV = NCHL == 1 ? 3 : NCHL == 2 ? 4 : 5;
-        qg_store_part<ONE, TI, SPLIT>(g.part + E.poff, sidx, T, M, tok0, row0, wt, wr, r16, h, st[LEV], st2[LEV]);
+        (void)m2;
+        qg_store_part<TI>(g.part + E.poff, sidx, T, M, tok0, row0, wt, wr, r16, h, st[LEV]);
     }
 }
 
@@ -465,10 +436,10 @@ __global__ __launch_bounds__(256) void k_qg_combine(MMGroup g) {
     };
     const float tot = tree(pp);
     float acc;
-    if constexpr (ONE) acc = tot + tree(pp + (size_t)SPLIT * ss);
+    if constexpr (ONE) acc = tot + g.m2[E.moff + (size_t)m * T + t];
     else acc = tot + 0.0f;
     const float v = apply_epi(E, t, m, acc);
-    E.y[(size_t)t * E.ldy + m] = v;
+    if (E.y) E.y[(size_t)t * E.ldy + m] = v;  // (k_fmm's emit-only entries have none)
     if (E.emit) emit32(E.out, t, m, v);
 }
 
@@ -508,9 +479,9 @@ __global__ __launch_bounds__(256) void k_qgemm(MMGroup g) {
     // pairs: the even class accumulates straight into level 0 (st[0]), the odd one into c, and
     // the pair then folds upward -- no copies or resets of accumulators between classes (each
     // class's first block starts its chain from 0 in a peeled step).
-    float st[6][TI][2][4], st2[6][TI][2][4];
-    float tot[TI][2][4], tot2[TI][2][4];
-    float c[TI][2][4], c2[TI][2][4];
+    float st[6][TI][2][4];
+    float tot[TI][2][4];
+    float c[TI][2][4];
     const int nchunks = (nsteps + QG_STEPS - 1) / QG_STEPS;
 
     int k = 0, cb = 0, cn = 1;  // step within the chunk, its buffer, next chunk to issue
@@ -518,7 +489,7 @@ __global__ __launch_bounds__(256) void k_qgemm(MMGroup g) {
     // LDS operands of the current step live in registers (cur); the next step's are read while
     // this step's epilogue runs, except across a chunk boundary (its buffer is not ready yet).
     QGOps<TI> cur;
-    auto step = [&](auto first, float (&acc)[TI][2][4], float (&acc2)[TI][2][4]) {
+    auto step = [&](auto first, float (&acc)[TI][2][4]) {
         constexpr bool FIRST = decltype(first)::value;
         // Chunk consumed: switch buffers (wave-uniform).  Done before this step's MFMAs, not
         // after them, so no branch separates an MFMA from the reads of its result.
@@ -543,34 +514,34 @@ __global__ __launch_bounds__(256) void k_qgemm(MMGroup g) {
             qg_mfma<TI>(cur, sv);
             QGOps<TI> nxt = cur;
             if (k + 1 < QG_STEPS) qg_read_ops<WF>(smem[cb] + (k + 1) * Lt::STEP, nxt, wr, wt, r16, h);
-            qg_epi<ONE, FIRST, TI>(cur, sv, acc, acc2);
+            qg_epi<FIRST, TI>(cur, sv, acc);
             cur = nxt;
         }
         k++;
     };
     using T1 = std::integral_constant<bool, true>;
     using T0 = std::integral_constant<bool, false>;
-    auto zero_acc = [&](float (&acc)[TI][2][4], float (&acc2)[TI][2][4]) {
+    auto zero_acc = [&](float (&acc)[TI][2][4]) {
 #pragma unroll
         for (int i = 0; i < TI; i++)
 #pragma unroll
             for (int j = 0; j < 2; j++)
 #pragma unroll
-                for (int q = 0; q < 4; q++) acc[i][j][q] = acc2[i][j][q] = 0.0f;
+                for (int q = 0; q < 4; q++) acc[i][j][q] = 0.0f;
     };
     // all blocks of class l into acc (a class without blocks, nb < 64, is a zero leaf)
-    auto run_class = [&](int l, float (&acc)[TI][2][4], float (&acc2)[TI][2][4]) {
+    auto run_class = [&](int l, float (&acc)[TI][2][4]) {
         const int n = cq + (l < crem ? 1 : 0);
         if (n == 0) {
-            zero_acc(acc, acc2);
+            zero_acc(acc);
             return;
         }
-        step(T1{}, acc, acc2);
-        for (int u = 1; u < n; u++) step(T0{}, acc, acc2);
+        step(T1{}, acc);
+        for (int u = 1; u < n; u++) step(T0{}, acc);
     };
 
     // odd class l (in c) closes ctz(~l) >= 1 levels: v = c, then v = st[k] + v for k < N
-#define QG_CASE(N, DST, DST2)                                                     \
+#define QG_CASE(N, DST)                                                           \
     case N: {                                                                     \
         _Pragma("unroll") for (int i = 0; i < TI; i++)                            \
         _Pragma("unroll") for (int j = 0; j < 2; j++)                             \
@@ -578,11 +549,6 @@ __global__ __launch_bounds__(256) void k_qgemm(MMGroup g) {
             float v = c[i][j][q];                                                 \
             for (int kk = 0; kk < N; kk++) v = st[kk][i][j][q] + v;               \
             DST[i][j][q] = v;                                                     \
-            if constexpr (ONE) {                                                  \
-                float v2 = c2[i][j][q];                                           \
-                for (int kk = 0; kk < N; kk++) v2 = st2[kk][i][j][q] + v2;        \
-                DST2[i][j][q] = v2;                                               \
-            }                                                                     \
         }                                                                         \
         break;                                                                    \
     }
@@ -593,16 +559,16 @@ __global__ __launch_bounds__(256) void k_qgemm(MMGroup g) {
     cn = 2;
     qg_read_ops<WF>(smem[0], cur, wr, wt, r16, h);
     for (int pr = 0; pr < CPS / 2; pr++) {  // pairs of this split's classes; folds by the relative index
-        run_class(l0 + 2 * pr, st[0], st2[0]);
-        run_class(l0 + 2 * pr + 1, c, c2);
+        run_class(l0 + 2 * pr, st[0]);
+        run_class(l0 + 2 * pr + 1, c);
         switch (__builtin_ctz(~(2 * pr + 1))) {
-            QG_CASE(1, st[1], st2[1])
-            QG_CASE(2, st[2], st2[2])
-            QG_CASE(3, st[3], st2[3])
-            QG_CASE(4, st[4], st2[4])
-            QG_CASE(5, st[5], st2[5])
+            QG_CASE(1, st[1])
+            QG_CASE(2, st[2])
+            QG_CASE(3, st[3])
+            QG_CASE(4, st[4])
+            QG_CASE(5, st[5])
             default:
-            QG_CASE(6, tot, tot2)
+            QG_CASE(6, tot)
         }
     }
 #undef QG_CASE
@@ -610,11 +576,169 @@ __global__ __launch_bounds__(256) void k_qgemm(MMGroup g) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
     if constexpr (SPLIT == 1) {
-        qg_store<ONE, TI>(E, T, M, tok0, row0, wt, wr, r16, h, tot, tot2);
+        qg_store<TI>(E, ONE ? g.m2 + E.moff : nullptr, T, M, tok0, row0, wt, wr, r16, h, tot);
     } else {
         constexpr int LEV = SPLIT == 8 ? 3 : 4;  // the subtree of CPS classes
-        qg_store_part<ONE, TI, SPLIT>(g.part + E.poff, sidx, T, M, tok0, row0, wt, wr, r16, h, st[LEV], st2[LEV]);
+        qg_store_part<TI>(g.part + E.poff, sidx, T, M, tok0, row0, wt, wr, r16, h, st[LEV]);
     }
+}
+
+// The _1 formats' m*s chains, in the matvec's association: for class l (= b mod 64) the chain
+// acc = acc + m_w[b] * s_x[b] over b = l + 64 u ascending, from 0; the 64 class sums folded by
+// wave_sum63's tree (the binary counter of the GEMM).  Independent of the int8 dot, so it runs as
+// its own VALU pass ahead of the GEMM -- whose tiles then carry one chain, 64 rows, like _0 -- and
+// the GEMM epilogue (or k_qg_combine) adds these totals: the same y bits.
+// Workgroup = 64 rows (lane = row) x 32 tokens (wave w: tokens 8w..8w+7).  Stages of 8 classes: all
+// their blocks' m_w (64 rows) and s_x (32 tokens) are copied to LDS with coalesced loads -- the next
+// stage's in flight while this one is accumulated -- so a block costs a lane one b32 read (its m_w)
+// and two broadcast b128 reads (the wave's 8 s_x) for 8 multiply-adds.
+// Output m2[row][token] (row-major over rows).
+constexpr int QM_CLS = 8;  // classes per stage
+// NMAX = blocks per class rounded up to 1 / 2 / 4 / 8 (K <= 16384); slot (u, lc) at u * 8 + lc holds
+// m_w of the workgroup's 64 rows and s_x of its 32 tokens for block lc + 8 sg + 64 u
+template <int NMAX>
+__global__ __launch_bounds__(256) void k_qg_msum(MMGroup g) {
+    constexpr int NSLOT = QM_CLS * NMAX;
+    __shared__ __attribute__((aligned(16))) float qw[2][NSLOT][64];
+    __shared__ __attribute__((aligned(16))) float qx[2][NSLOT][32];
+    const int T = g.T, tgs = (T + 31) / 32;
+    int e = 0, base = 0;
+#pragma unroll 1
+    for (; e + 1 < g.n; e++) {
+        const int n_e = (g.e[e].W.M + 63) / 64 * tgs;
+        if ((int)blockIdx.x < base + n_e) break;
+        base += n_e;
+    }
+    const MMEntry & E = g.e[e];
+    const int M = E.W.M, nb = E.W.K >> 5, MS = qm_stride(M);
+    const int local = (int)blockIdx.x - base;
+    const int rt = local / tgs, tg = local % tgs;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r0 = rt * 64, tok0 = tg * 32;
+    const int cq = nb >> 6, crem = nb & 63;
+    const size_t AB = qg_a_bytes(true);
+    // loaders: m_w row lane of slots wave + 4 k; s_x token tid & 31 of slots (tid >> 5) + 8 k.  A block
+    // past its class's count is clamped (loaded, never read).
+    const float * wrow = E.W.mt + min(r0 + lane, MS - 1);
+    const int tx = min(tok0 + (tid & 31), T - 1);
+    const float * xrow = (const float *)(E.in.tq + (size_t)(tx / QG_TOK) * nb * AB + QG_A_S) + tx % QG_TOK;
+    constexpr int LW = NSLOT / 4, LX = NSLOT / 8;
+    float lw[LW], lx[LX];
+    auto blk = [&](int sg, int sl) {
+        const int lc = sl & 7, u = sl >> 3, l = sg * QM_CLS + lc;
+        return u < cq + (l < crem ? 1 : 0) ? l + 64 * u : l;  // (l < nb whenever the class has a block)
+    };
+    auto gload = [&](int sg) {
+#pragma unroll
+        for (int k = 0; k < LW; k++) lw[k] = wrow[(size_t)min(blk(sg, wave + 4 * k), nb - 1) * MS];
+#pragma unroll
+        for (int k = 0; k < LX; k++) lx[k] = xrow[(size_t)min(blk(sg, (tid >> 5) + 8 * k), nb - 1) * (AB / 4)];
+    };
+    auto lstore = [&](int buf) {
+#pragma unroll
+        for (int k = 0; k < LW; k++) qw[buf][wave + 4 * k][lane] = lw[k];
+#pragma unroll
+        for (int k = 0; k < LX; k++) qx[buf][(tid >> 5) + 8 * k][tid & 31] = lx[k];
+    };
+    float st[6][8], acc[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) acc[k] = 0.0f;
+#define QM_CLOSE(N)                                                   \
+    case N: {                                                         \
+        _Pragma("unroll") for (int k = 0; k < 8; k++) {               \
+            float v = acc[k];                                         \
+            for (int kk = 0; kk < N; kk++) v = st[kk][k] + v;         \
+            st[N < 6 ? N : 0][k] = v;  /* N = 6: the total */         \
+        }                                                             \
+        break;                                                        \
+    }
+    gload(0);
+    lstore(0);
+    __syncthreads();
+#pragma unroll 1
+    for (int sg = 0; sg < 64 / QM_CLS; sg++) {
+        if (sg + 1 < 64 / QM_CLS) gload(sg + 1);  // in flight under this stage
+        const int buf = sg & 1;
+        // a class's operands (all NMAX slots; slots past its block count hold stale values, never
+        // used) are read before the previous class's arithmetic (NMAX <= 2: double-buffered registers)
+        struct Ops {
+            float w[NMAX];
+            float4 s0[NMAX], s1[NMAX];
+        };
+        auto rd = [&](Ops & o, int lc) {
+#pragma unroll
+            for (int u = 0; u < NMAX; u++) {
+                o.w[u] = qw[buf][u * 8 + lc][lane];
+                o.s0[u] = *(const float4 *)&qx[buf][u * 8 + lc][8 * wave];
+                o.s1[u] = *(const float4 *)&qx[buf][u * 8 + lc][8 * wave + 4];
+            }
+        };
+        auto mac = [&](const Ops & o, int n) {
+#pragma unroll
+            for (int u = 0; u < NMAX; u++) {
+                if (u >= n) break;  // uniform
+                const float sx[8] = {o.s0[u].x, o.s0[u].y, o.s0[u].z, o.s0[u].w, o.s1[u].x, o.s1[u].y, o.s1[u].z, o.s1[u].w};
+#pragma unroll
+                for (int k = 0; k < 8; k++) acc[k] = acc[k] + o.w[u] * sx[k];
+            }
+        };
+        auto fold = [&](int l) {
+            if ((l & 1) == 0) {
+#pragma unroll
+                for (int k = 0; k < 8; k++) st[0][k] = acc[k];
+            } else {
+                switch (__builtin_ctz(~l)) { QM_CLOSE(1) QM_CLOSE(2) QM_CLOSE(3) QM_CLOSE(4) QM_CLOSE(5) default: QM_CLOSE(6) }
+            }
+#pragma unroll
+            for (int k = 0; k < 8; k++) acc[k] = 0.0f;
+        };
+        if constexpr (NMAX <= 2) {
+            Ops o0, o1;
+            rd(o0, 0);
+#pragma unroll
+            for (int lc = 0; lc < QM_CLS; lc += 2) {
+                const int l = sg * QM_CLS + lc;
+                rd(o1, lc + 1);
+                mac(o0, cq + (l < crem ? 1 : 0));
+                fold(l);
+                if (lc + 2 < QM_CLS) rd(o0, lc + 2);
+                mac(o1, cq + (l + 1 < crem ? 1 : 0));
+                fold(l + 1);
+            }
+        } else {
+#pragma unroll 1
+            for (int lc = 0; lc < QM_CLS; lc++) {
+                const int l = sg * QM_CLS + lc;
+                Ops o;
+                rd(o, lc);
+                mac(o, cq + (l < crem ? 1 : 0));
+                fold(l);
+            }
+        }
+        if (sg + 1 < 64 / QM_CLS) lstore((sg + 1) & 1);
+        __syncthreads();
+    }
+#undef QM_CLOSE
+    const int r = r0 + lane;
+    if (r >= M) return;
+    float * out = g.m2 + E.moff + (size_t)r * T + tok0 + 8 * wave;
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+        if (tok0 + 8 * wave + k < T) out[k] = st[0][k];
+}
+
+// The combine of a split group whose entries' partials sit at g.part + poff (k_fmm's split form)
+bool launch_qg_combine(hipStream_t st, MMGroup & g, int split) {
+    int cblocks = 0;
+    for (int i = 0; i < g.n; i++) {
+        g.e[i].cblock0 = cblocks;
+        cblocks += (int)(((size_t)g.T * g.e[i].W.M + 255) / 256);
+    }
+    if (split == 4) hipLaunchKernelGGL((k_qg_combine<4, false>), dim3(cblocks), dim3(256), 0, st, g);
+    else if (split == 8) hipLaunchKernelGGL((k_qg_combine<8, false>), dim3(cblocks), dim3(256), 0, st, g);
+    else return false;
+    HIP_OK(hipGetLastError());
+    return true;
 }
 
 // Every entry must have y (the engine gives emitting entries a scratch y); emission into the
@@ -638,10 +762,40 @@ bool launch_qgemm(hipStream_t st, MMGroup & g, int wtype) {
         blocks += (e.W.M + rows - 1) / rows * tilesT;
     }
     if (!blocks) return true;
+    if (qg_one(wtype)) {
+        // the m*s chain totals first (k_qg_msum), read by the GEMM epilogue / the combine
+        size_t mfl = 0;
+        int mblocks = 0, nmax = 0;
+        const int tgs = (g.T + 31) / 32;
+        for (int i = 0; i < g.n; i++) {
+            if (!g.e[i].W.mt) {
+                fprintf(stderr, "rwkv: qgemm _1 entry %d without mins\n", i);
+                return false;
+            }
+            g.e[i].moff = mfl;
+            mfl += (size_t)g.T * g.e[i].W.M;
+            mblocks += (g.e[i].W.M + 63) / 64 * tgs;
+            const int nbi = g.e[i].W.K / 32, nmi = nbi / 64 + (nbi % 64 ? 1 : 0);
+            nmax = std::max(nmax, nmi);
+        }
+        if (!g.m2 || g.m2_floats < mfl) {
+            fprintf(stderr, "rwkv: qgemm _1 group needs %zu m*s floats, has %zu\n", mfl, g.m2 ? g.m2_floats : (size_t)0);
+            return false;
+        }
+        if (nmax <= 1) hipLaunchKernelGGL(k_qg_msum<1>, dim3(mblocks), dim3(256), 0, st, g);
+        else if (nmax <= 2) hipLaunchKernelGGL(k_qg_msum<2>, dim3(mblocks), dim3(256), 0, st, g);
+        else if (nmax <= 4) hipLaunchKernelGGL(k_qg_msum<4>, dim3(mblocks), dim3(256), 0, st, g);
+        else if (nmax <= 8) hipLaunchKernelGGL(k_qg_msum<8>, dim3(mblocks), dim3(256), 0, st, g);
+        else {
+            fprintf(stderr, "rwkv: qgemm _1 group: K above the m*s pass's 16384\n");
+            return false;
+        }
+        HIP_OK(hipGetLastError());
+    }
     // Q8_0 emission fused into the epilogue (the Q4_0 / Q5_0 / Q8_0 GEMMs: a wave holds 32 rows)
     for (int i = 0; i < g.n; i++) {
         MMEntry & e = g.e[i];
-        e.fuse_emit = !qg_one(wtype) && e.emit && e.out.tiled && e.out.fmt == A_Q8_0 && e.out.tq && e.out.K == e.W.M &&
+        e.fuse_emit = e.emit && e.out.tiled && e.out.fmt == A_Q8_0 && e.out.tq && e.out.K == e.W.M &&
                       e.W.M % 64 == 0 && e.ldy == e.W.M && e.epi != EPI_ADD && e.epi != EPI_SIGMUL_ADD &&
                       e.epi != EPI_VMIX7 && e.epi != EPI_DECAY6 && e.epi != EPI_DECAY7 && e.epi != EPI_SIGMOID_BIAS;
     }
@@ -658,7 +812,7 @@ bool launch_qgemm(hipStream_t st, MMGroup & g, int wtype) {
     if (split > 1) {
         for (int i = 0; i < g.n; i++) {
             g.e[i].poff = pfl;
-            pfl += (size_t)split * g.T * g.e[i].W.M * (qg_one(wtype) ? 2 : 1);
+            pfl += (size_t)split * g.T * g.e[i].W.M;
         }
         if (!g.part || g.part_floats < pfl || g_qgemm_generic) split = 1;
         for (int i = 0; i < g.n; i++)

@@ -97,10 +97,13 @@ static bool selftest_mm(int wtype, const void * W, int K, int M, const float * x
         g.e[0].epi = EPI_STORE;
         g.split = split;
         g.fmm = 1;  // the f32-MFMA form for float weights whenever it applies (T >= 16)
+        g.part_floats = (size_t)8 * T * M;
+        g.part = (float *)b.alloc(g.part_floats * 4);
+        ok = g.part != nullptr;
         if (mfma) {
-            g.part_floats = (size_t)8 * T * M * 2;
-            g.part = (float *)b.alloc(g.part_floats * 4);
-            ok = g.part != nullptr;
+            g.m2_floats = (size_t)T * M;
+            g.m2 = (float *)b.alloc(g.m2_floats * 4);
+            ok = ok && g.m2 != nullptr;
         }
         ok = ok && (mfma ? launch_qgemm(nullptr, g, wtype) : launch_mm_group(nullptr, g, wtype));
     }
@@ -112,7 +115,7 @@ static bool selftest_mm(int wtype, const void * W, int K, int M, const float * x
 
 extern "C" RWKV_API bool rwkv_mi355x_selftest_matmul(int wtype, const void * W, int K, int M, const float * x, int T,
                                                      float * y) {
-    return selftest_mm(wtype, W, K, M, x, T, y, false);
+    return selftest_mm(wtype, W, K, M, x, T, y, false, 1);  // unsplit (the float matmuls' reference form)
 }
 
 extern "C" RWKV_API bool rwkv_mi355x_selftest_gemm(int wtype, const void * W, int K, int M, const float * x, int T,
@@ -121,9 +124,11 @@ extern "C" RWKV_API bool rwkv_mi355x_selftest_gemm(int wtype, const void * W, in
     return selftest_mm(wtype, W, K, M, x, T, y, true);
 }
 
-// The same with the split-K form chosen: 1 = unsplit, 4 / 8 = that many class subtrees + combine.
+// The same with the split-K form chosen: 1 = unsplit, 4 / 8 = that many class subtrees + combine
+// (quantized: the int8-MFMA GEMM; F16 / F32 over 16+ tokens, K >= 512: k_fmm).
 extern "C" RWKV_API bool rwkv_mi355x_selftest_gemm_split(int wtype, const void * W, int K, int M, const float * x,
                                                          int T, float * y, int split) {
-    if (!wtype_quantized(wtype) || T < 2 || (split != 1 && split != 4 && split != 8)) return false;
-    return selftest_mm(wtype, W, K, M, x, T, y, true, split);
+    if (split != 1 && split != 4 && split != 8) return false;
+    if (wtype_quantized(wtype)) return T >= 2 && selftest_mm(wtype, W, K, M, x, T, y, true, split);
+    return (wtype == W_F16 || wtype == W_F32) && T >= 16 && K >= 512 && selftest_mm(wtype, W, K, M, x, T, y, false, split);
 }

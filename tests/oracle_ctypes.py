@@ -122,8 +122,13 @@ TYPE_IDS = {'FP32': 0, 'FP16': 1, 'Q4_0': 2, 'Q4_1': 3, 'Q5_0': 7, 'Q5_1': 8, 'Q
 
 
 def quantize_rows(fmt, x):
-    """File quantizer on a [M, K] float32 matrix -> raw block bytes."""
+    """File quantizer on a [M, K] float32 matrix -> raw block bytes (FP32 / FP16: the raw rows, as the
+    converter writes them)."""
     x = np.ascontiguousarray(x, dtype=np.float32)
+    if fmt == 'FP32':
+        return x.reshape(-1).view(np.uint8).copy()
+    if fmt == 'FP16':
+        return x.astype(np.float16).reshape(-1).view(np.uint8).copy()
     t = TYPE_IDS[fmt]
     M, K = x.shape
     bb = lib().oracle_block_bytes(t)

@@ -127,6 +127,25 @@ def test_mfma_gemm_matches_matmul_bit_exact(fmt, M, K, T):
     assert np.array_equal(y_g.view(np.uint32), y_mm.view(np.uint32)), float(np.abs(y_g - y_mm).max())
 
 
+@pytest.mark.parametrize('fmt', ['FP32', 'FP16'])
+@pytest.mark.parametrize('M,K,T', [(576, 2560, 64), (128, 2048, 100), (96, 4096, 33), (64, 512, 16)])
+@pytest.mark.parametrize('split', [4, 8])
+def test_fmm_split_k_bit_exact(fmt, M, K, T, split):
+    """Float matmuls on the f32 MFMA with the class tree split into 4 or 8 subtrees (k_fmm<WF, SPLIT> +
+    k_qg_combine) == the unsplit k_fmm (itself == the oracle, test_matmul_kernel), bit for bit."""
+    rng = np.random.default_rng(M * 5 + K + T * 3 + split)
+    w = (rng.standard_normal((M, K)) / np.sqrt(K)).astype(np.float32)
+    x = rng.standard_normal((T, K)).astype(np.float32)
+    wb = quantize_rows(fmt, w)
+    y_mm = np.zeros((T, M), np.float32)
+    y_s = np.zeros((T, M), np.float32)
+    L = lib()
+    assert L.rwkv_mi355x_selftest_matmul(TYPE_IDS[fmt], wb.ctypes.data, K, M, x.ctypes.data, T, y_mm.ctypes.data)
+    assert L.rwkv_mi355x_selftest_gemm_split(TYPE_IDS[fmt], wb.ctypes.data, K, M, x.ctypes.data, T, y_s.ctypes.data,
+                                             split)
+    assert np.array_equal(y_s.view(np.uint32), y_mm.view(np.uint32)), float(np.abs(y_s - y_mm).max())
+
+
 @pytest.mark.parametrize('fmt', ['Q4_0', 'Q4_1', 'Q5_0', 'Q5_1', 'Q8_0'])
 @pytest.mark.parametrize('M,K,T', [(2048, 2048, 64), (96, 7168, 40), (160, 2048, 128), (64, 768, 7), (2048, 64, 17)])
 @pytest.mark.parametrize('split', [1, 4, 8])

@@ -1,0 +1,13 @@
+#!/bin/bash
+# msum v4 (paired single-block classes, ring 8) + fmm gate (K>=512, >=128 WGs).
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
+timeout -k 10 400 python3 -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_batch.py -x -q --timeout 200 --timeout-method thread > gpurun_out/p20_k.log 2>&1 || { tail -30 gpurun_out/p20_k.log; exit 1; }
+tail -1 gpurun_out/p20_k.log
+timeout -k 10 400 python3 bench.py --config v7-2b9-q5_1 --steps 8 --warmup 2 --batch "32,128" --seq-reps 2 --abi-steps 0 --skip-cpu --timing-steps 1 > gpurun_out/p20_v7.log 2>&1 || { tail -5 gpurun_out/p20_v7.log; exit 1; }
+grep -E "seq-eval|decode" gpurun_out/p20_v7.log | cut -c1-200
+timeout -k 10 400 python3 bench.py --config v5-7b-q4_1 --steps 8 --warmup 2 --batch "32" --seq-reps 2 --abi-steps 0 --skip-cpu --timing-steps 1 > gpurun_out/p20_v5.log 2>&1 || { tail -5 gpurun_out/p20_v5.log; exit 1; }
+grep -E "seq-eval|decode" gpurun_out/p20_v5.log | cut -c1-200
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof_v7seq6 -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --config v7-2b9-q5_1 --steps 2 --warmup 1 --batch "32" --batch-steps 4 --seq-reps 2 --abi-steps 0 --skip-cpu --timing-steps 1 > $GRAFT_REPO_ROOT/gpurun_out/prof_v7seq6.log 2>&1 || exit 1
+python3 $GRAFT_REPO_ROOT/tools/top_kernels.py $GRAFT_REPO_ROOT/gpurun_out/prof_v7seq6/run_kernel_stats.csv 14
+echo done

@@ -1376,32 +1376,56 @@ __global__ __launch_bounds__(256) void k_wkv7_s64(int T, int H, const float * r,
         const int n = min(WKV7_TC, T - t0);
         const bool nx = t0 + WKV7_TC < T;
         if (nx) load(t0 + WKV7_TC);  // in flight during this chunk
-#pragma unroll 4
-        for (int tt = 0; tt < n; tt++) {
-            const float4 av = *(const float4 *)&sa_[buf][tt][4 * g];
-            const float4 kq = *(const float4 *)&sk[buf][tt][4 * g];
-            const float4 wq = *(const float4 *)&sw[buf][tt][4 * g];
-            const float4 bq = *(const float4 *)&sb[buf][tt][4 * g];
-            const float4 rq = *(const float4 *)&sr[buf][tt][4 * g];
-            const float vi = sv[buf][tt][il];
+        // token tt's operands are in registers while token tt + 1's are read (the LDS latency stays
+        // off the recurrence's critical path); whole chunks fully unrolled
+        struct Op {
+            float4 a, k, w, b, r;
+            float v;
+        };
+        auto rd = [&](Op & o, int tt) __attribute__((always_inline)) {
+            o.a = *(const float4 *)&sa_[buf][tt][4 * g];
+            o.k = *(const float4 *)&sk[buf][tt][4 * g];
+            o.w = *(const float4 *)&sw[buf][tt][4 * g];
+            o.b = *(const float4 *)&sb[buf][tt][4 * g];
+            o.r = *(const float4 *)&sr[buf][tt][4 * g];
+            o.v = sv[buf][tt][il];
+        };
+        auto tok = [&](const Op & o, int tt) __attribute__((always_inline)) {
             float sa = 0.0f;
-            sa += av.x * st[0];
-            sa += av.y * st[1];
-            sa += av.z * st[2];
-            sa += av.w * st[3];
+            sa += o.a.x * st[0];
+            sa += o.a.y * st[1];
+            sa += o.a.z * st[2];
+            sa += o.a.w * st[3];
             sa = row_bfly16(sa);
-            const float kk[4] = {kq.x, kq.y, kq.z, kq.w}, ww[4] = {wq.x, wq.y, wq.z, wq.w};
-            const float bb[4] = {bq.x, bq.y, bq.z, bq.w}, rr[4] = {rq.x, rq.y, rq.z, rq.w};
+            const float kk[4] = {o.k.x, o.k.y, o.k.z, o.k.w}, ww[4] = {o.w.x, o.w.y, o.w.z, o.w.w};
+            const float bb[4] = {o.b.x, o.b.y, o.b.z, o.b.w}, rr[4] = {o.r.x, o.r.y, o.r.z, o.r.w};
             float acc = 0.0f;
 #pragma unroll
             for (int e = 0; e < 4; e++) {
-                const float kv = vi * kk[e];
+                const float kv = o.v * kk[e];
                 const float ns = st[e] * ww[e] + kv + sa * bb[e];
                 st[e] = ns;
                 acc += ns * rr[e];
             }
             acc = row_bfly16(acc);
             if (g == 0) sy[buf][tt][il] = acc;
+        };
+        Op cur, nxt;
+        rd(cur, 0);
+        if (n == WKV7_TC) {
+#pragma unroll
+            for (int tt = 0; tt < WKV7_TC; tt++) {
+                if (tt + 1 < WKV7_TC) rd(nxt, tt + 1);
+                tok(cur, tt);
+                cur = nxt;
+            }
+        } else {
+#pragma unroll 1
+            for (int tt = 0; tt < n; tt++) {
+                rd(nxt, min(tt + 1, n - 1));
+                tok(cur, tt);
+                cur = nxt;
+            }
         }
         if (nx) store(buf ^ 1);
         __syncthreads();

@@ -21,6 +21,7 @@
 #include "kernels.hpp"
 
 #include <stdio.h>
+#include <stdlib.h>
 #include <type_traits>
 
 // m0 in the copy asm's clobber list is a reserved register: the compiler re-sets m0 before each of
@@ -432,6 +433,7 @@ __global__ __launch_bounds__(256) void k_qg_combine(MMGroup g) {
 #pragma unroll
         for (int s = 0; s < SPLIT; s++) v[s] = p[s * ss];
         if constexpr (SPLIT == 8) return ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
+        else if constexpr (SPLIT == 2) return v[0] + v[1];
         else return (v[0] + v[1]) + (v[2] + v[3]);
     };
     const float tot = tree(pp);
@@ -578,7 +580,7 @@ __global__ __launch_bounds__(256) void k_qgemm(MMGroup g) {
     if constexpr (SPLIT == 1) {
         qg_store<TI>(E, ONE ? g.m2 + E.moff : nullptr, T, M, tok0, row0, wt, wr, r16, h, tot);
     } else {
-        constexpr int LEV = SPLIT == 8 ? 3 : 4;  // the subtree of CPS classes
+        constexpr int LEV = SPLIT == 8 ? 3 : SPLIT == 4 ? 4 : 5;  // the subtree of CPS classes
         qg_store_part<TI>(g.part + E.poff, sidx, T, M, tok0, row0, wt, wr, r16, h, st[LEV]);
     }
 }
@@ -588,16 +590,185 @@ __global__ __launch_bounds__(256) void k_qgemm(MMGroup g) {
 // wave_sum63's tree (the binary counter of the GEMM).  Independent of the int8 dot, so it runs as
 // its own VALU pass ahead of the GEMM -- whose tiles then carry one chain, 64 rows, like _0 -- and
 // the GEMM epilogue (or k_qg_combine) adds these totals: the same y bits.
-// Workgroup = 64 rows (lane = row) x 32 tokens (wave w: tokens 8w..8w+7).  Stages of 8 classes: all
+// Workgroup = 64 rows x 64 tokens (lane: 4 rows x 4 tokens; wave w: tokens 16w..16w+15).  Stages of 8 classes: all
 // their blocks' m_w (64 rows) and s_x (32 tokens) are copied to LDS with coalesced loads -- the next
-// stage's in flight while this one is accumulated -- so a block costs a lane one b32 read (its m_w)
-// and two broadcast b128 reads (the wave's 8 s_x) for 8 multiply-adds.
+// stage's in flight while this one is accumulated -- so a block costs a lane two b128 reads (4 rows'
+// m_w, 4 tokens' s_x) for 16 multiply-adds.
 // Output m2[row][token] (row-major over rows).
 constexpr int QM_CLS = 8;  // classes per stage
 // NMAX = blocks per class rounded up to 1 / 2 / 4 / 8 (K <= 16384); slot (u, lc) at u * 8 + lc holds
 // m_w of the workgroup's 64 rows and s_x of its 32 tokens for block lc + 8 sg + 64 u
 template <int NMAX>
 __global__ __launch_bounds__(256) void k_qg_msum(MMGroup g) {
+    constexpr int NSLOT = QM_CLS * NMAX;
+    __shared__ __attribute__((aligned(16))) float qw[2][NSLOT][64];
+    __shared__ __attribute__((aligned(16))) float qx[2][NSLOT][64];
+    const int T = g.T, tgs = (T + 63) / 64;
+    int e = 0, base = 0;
+#pragma unroll 1
+    for (; e + 1 < g.n; e++) {
+        const int n_e = (g.e[e].W.M + 63) / 64 * tgs;
+        if ((int)blockIdx.x < base + n_e) break;
+        base += n_e;
+    }
+    const MMEntry & E = g.e[e];
+    const int M = E.W.M, nb = E.W.K >> 5, MS = qm_stride(M);
+    const int local = (int)blockIdx.x - base;
+    const int rt = local / tgs, tg = local % tgs;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int rq = lane & 15, tq = lane >> 4;  // this lane: rows 4 rq + r, tokens 16 wave + 4 tq + c
+    const int r0 = rt * 64, tok0 = tg * 64;
+    const int cq = nb >> 6, crem = nb & 63;
+    const size_t AB = qg_a_bytes(true);
+    // loaders: slot wave + 4 k -- m_w of row lane, s_x of token lane.  A block past its class's count
+    // is clamped (loaded, never read).
+    const float * wrow = E.W.mt + min(r0 + lane, MS - 1);
+    const int tx = min(tok0 + lane, T - 1);
+    const float * xrow = (const float *)(E.in.tq + (size_t)(tx / QG_TOK) * nb * AB + QG_A_S) + tx % QG_TOK;
+    constexpr int LS = NSLOT / 4;
+    float lw[LS], lx[LS];
+    auto blk = [&](int sg, int sl) {
+        const int lc = sl & 7, u = sl >> 3, l = sg * QM_CLS + lc;
+        return min(u < cq + (l < crem ? 1 : 0) ? l + 64 * u : l, nb - 1);
+    };
+    auto gload = [&](int sg) {
+#pragma unroll
+        for (int k = 0; k < LS; k++) {
+            const int b = blk(sg, wave + 4 * k);
+            lw[k] = wrow[(size_t)b * MS];
+            lx[k] = xrow[(size_t)b * (AB / 4)];
+        }
+    };
+    auto lstore = [&](int buf) {
+#pragma unroll
+        for (int k = 0; k < LS; k++) {
+            qw[buf][wave + 4 * k][lane] = lw[k];
+            qx[buf][wave + 4 * k][lane] = lx[k];
+        }
+    };
+    float st[6][16], acc[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) acc[k] = 0.0f;
+#define QM_CLOSE(N)                                                   \
+    case N: {                                                         \
+        _Pragma("unroll") for (int k = 0; k < 16; k++) {              \
+            float v = acc[k];                                         \
+            for (int kk = 0; kk < N; kk++) v = st[kk][k] + v;         \
+            st[N < 6 ? N : 0][k] = v;  /* N = 6: the total */         \
+        }                                                             \
+        break;                                                        \
+    }
+    gload(0);
+    lstore(0);
+    __syncthreads();
+#pragma unroll 1
+    for (int sg = 0; sg < 64 / QM_CLS; sg++) {
+        if (sg + 1 < 64 / QM_CLS) gload(sg + 1);  // in flight under this stage
+        const int buf = sg & 1;
+        // a class's operands (all NMAX slots; slots past its block count hold stale values, never
+        // used) are read before the previous class's arithmetic (NMAX <= 2: double-buffered registers)
+        struct Ops {
+            float4 w[NMAX], x[NMAX];
+        };
+        auto rd = [&](Ops & o, int lc) {
+#pragma unroll
+            for (int u = 0; u < NMAX; u++) {
+                o.w[u] = *(const float4 *)&qw[buf][u * 8 + lc][4 * rq];
+                o.x[u] = *(const float4 *)&qx[buf][u * 8 + lc][16 * wave + 4 * tq];
+            }
+        };
+        auto mac = [&](const Ops & o, int n) {
+#pragma unroll
+            for (int u = 0; u < NMAX; u++) {
+                if (u >= n) break;  // uniform
+                const float wv[4] = {o.w[u].x, o.w[u].y, o.w[u].z, o.w[u].w};
+                const float xv[4] = {o.x[u].x, o.x[u].y, o.x[u].z, o.x[u].w};
+#pragma unroll
+                for (int r = 0; r < 4; r++)
+#pragma unroll
+                    for (int c = 0; c < 4; c++) acc[4 * r + c] = acc[4 * r + c] + wv[r] * xv[c];
+            }
+        };
+        auto fold = [&](int l) {
+            if ((l & 1) == 0) {
+#pragma unroll
+                for (int k = 0; k < 16; k++) st[0][k] = acc[k];
+            } else {
+                switch (__builtin_ctz(~l)) { QM_CLOSE(1) QM_CLOSE(2) QM_CLOSE(3) QM_CLOSE(4) QM_CLOSE(5) default: QM_CLOSE(6) }
+            }
+#pragma unroll
+            for (int k = 0; k < 16; k++) acc[k] = 0.0f;
+        };
+        if constexpr (NMAX <= 2) {
+            Ops o0, o1;
+            rd(o0, 0);
+#pragma unroll
+            for (int lc = 0; lc < QM_CLS; lc += 2) {
+                const int l = sg * QM_CLS + lc;
+                rd(o1, lc + 1);
+                mac(o0, cq + (l < crem ? 1 : 0));
+                fold(l);
+                if (lc + 2 < QM_CLS) rd(o0, lc + 2);
+                mac(o1, cq + (l + 1 < crem ? 1 : 0));
+                fold(l + 1);
+            }
+        } else {
+            // 4 blocks of a class at a time (their reads issued together)
+#pragma unroll 1
+            for (int lc = 0; lc < QM_CLS; lc++) {
+                const int l = sg * QM_CLS + lc, n = cq + (l < crem ? 1 : 0);
+                float4 w4[1][4], x4[1][4];
+                auto rd4 = [&](int h, int u0) {
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        const int u = min(u0 + q, NMAX - 1);
+                        w4[h][q] = *(const float4 *)&qw[buf][u * 8 + lc][4 * rq];
+                        x4[h][q] = *(const float4 *)&qx[buf][u * 8 + lc][16 * wave + 4 * tq];
+                    }
+                };
+                auto mac4 = [&](int h, int u0) {
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        if (u0 + q >= n) break;  // uniform
+                        const float wv[4] = {w4[h][q].x, w4[h][q].y, w4[h][q].z, w4[h][q].w};
+                        const float xv[4] = {x4[h][q].x, x4[h][q].y, x4[h][q].z, x4[h][q].w};
+#pragma unroll
+                        for (int r = 0; r < 4; r++)
+#pragma unroll
+                            for (int c = 0; c < 4; c++) acc[4 * r + c] = acc[4 * r + c] + wv[r] * xv[c];
+                    }
+                };
+                rd4(0, 0);
+                mac4(0, 0);
+                if (NMAX > 4 && n > 4) {
+                    rd4(0, 4);
+                    mac4(0, 4);
+                }
+                fold(l);
+            }
+        }
+        if (sg + 1 < 64 / QM_CLS) lstore((sg + 1) & 1);
+        __syncthreads();
+    }
+#undef QM_CLOSE
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int row = r0 + 4 * rq + r;
+        if (row >= M) continue;
+        float * out = g.m2 + E.moff + (size_t)row * T;
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const int t = tok0 + 16 * wave + 4 * tq + c;
+            if (t < T) out[t] = st[0][4 * r + c];
+        }
+    }
+}
+
+// The long-class form (5-8 blocks per class: K > 8192): lane = row, wave = 8 tokens, workgroup = 64
+// rows x 32 tokens; a lane's m_w is one b32 read and the wave's 8 s_x two broadcast b128 reads per
+// block (the 4 x 4 register tiles of k_qg_msum need 260 VGPRs at this depth: one wave per SIMD).
+template <int NMAX>
+__global__ __launch_bounds__(256) void k_qg_msum_rows(MMGroup g) {
     constexpr int NSLOT = QM_CLS * NMAX;
     __shared__ __attribute__((aligned(16))) float qw[2][NSLOT][64];
     __shared__ __attribute__((aligned(16))) float qx[2][NSLOT][32];
@@ -765,8 +936,8 @@ bool launch_qgemm(hipStream_t st, MMGroup & g, int wtype) {
     if (qg_one(wtype)) {
         // the m*s chain totals first (k_qg_msum), read by the GEMM epilogue / the combine
         size_t mfl = 0;
-        int mblocks = 0, nmax = 0;
-        const int tgs = (g.T + 31) / 32;
+        int mblocks = 0, mblocks8 = 0, nmax = 0;
+        const int tgs = (g.T + 63) / 64;
         for (int i = 0; i < g.n; i++) {
             if (!g.e[i].W.mt) {
                 fprintf(stderr, "rwkv: qgemm _1 entry %d without mins\n", i);
@@ -775,6 +946,7 @@ bool launch_qgemm(hipStream_t st, MMGroup & g, int wtype) {
             g.e[i].moff = mfl;
             mfl += (size_t)g.T * g.e[i].W.M;
             mblocks += (g.e[i].W.M + 63) / 64 * tgs;
+            mblocks8 += (g.e[i].W.M + 63) / 64 * ((g.T + 31) / 32);
             const int nbi = g.e[i].W.K / 32, nmi = nbi / 64 + (nbi % 64 ? 1 : 0);
             nmax = std::max(nmax, nmi);
         }
@@ -782,10 +954,16 @@ bool launch_qgemm(hipStream_t st, MMGroup & g, int wtype) {
             fprintf(stderr, "rwkv: qgemm _1 group needs %zu m*s floats, has %zu\n", mfl, g.m2 ? g.m2_floats : (size_t)0);
             return false;
         }
-        if (nmax <= 1) hipLaunchKernelGGL(k_qg_msum<1>, dim3(mblocks), dim3(256), 0, st, g);
+        // the 4 x 4 register-tile form over 64-token tiles; the row form (32-token tiles) for 32 or
+        // fewer tokens (contexts) and for classes of 5-8 blocks
+        const bool rows = g.T <= 32 || nmax > 4;
+        if (rows && nmax <= 1) hipLaunchKernelGGL(k_qg_msum_rows<1>, dim3(mblocks8), dim3(256), 0, st, g);
+        else if (rows && nmax <= 2) hipLaunchKernelGGL(k_qg_msum_rows<2>, dim3(mblocks8), dim3(256), 0, st, g);
+        else if (rows && nmax <= 4) hipLaunchKernelGGL(k_qg_msum_rows<4>, dim3(mblocks8), dim3(256), 0, st, g);
+        else if (rows && nmax <= 8) hipLaunchKernelGGL(k_qg_msum_rows<8>, dim3(mblocks8), dim3(256), 0, st, g);
+        else if (nmax <= 1) hipLaunchKernelGGL(k_qg_msum<1>, dim3(mblocks), dim3(256), 0, st, g);
         else if (nmax <= 2) hipLaunchKernelGGL(k_qg_msum<2>, dim3(mblocks), dim3(256), 0, st, g);
         else if (nmax <= 4) hipLaunchKernelGGL(k_qg_msum<4>, dim3(mblocks), dim3(256), 0, st, g);
-        else if (nmax <= 8) hipLaunchKernelGGL(k_qg_msum<8>, dim3(mblocks), dim3(256), 0, st, g);
         else {
             fprintf(stderr, "rwkv: qgemm _1 group: K above the m*s pass's 16384\n");
             return false;
@@ -806,8 +984,14 @@ bool launch_qgemm(hipStream_t st, MMGroup & g, int wtype) {
     // as the v6 maa LoRA W1): every tile's class tree in 4 or 8 subtrees on as many workgroups,
     // combined (epilogue, emission) by k_qg_combine -- the same bits as the unsplit kernel
     int split = g.split;
-    if (split == 0) split = blocks >= 2 * kQgCUs ? 1 : blocks * 4 >= 2 * kQgCUs ? 4 : 8;
-    if (split != 1 && split != 4 && split != 8) split = 1;
+    // (RWKV_MI355X_QG_SPLIT2=1: two subtrees for groups of 1-2 tiles per CU -- A/B)
+    static const bool split2 = [] {
+        const char * v = getenv("RWKV_MI355X_QG_SPLIT2");
+        return v && v[0] == '1';
+    }();
+    if (split == 0)
+        split = blocks >= 2 * kQgCUs ? 1 : (split2 && blocks >= kQgCUs) ? 2 : blocks * 4 >= 2 * kQgCUs ? 4 : 8;
+    if (split != 1 && split != 2 && split != 4 && split != 8) split = 1;
     size_t pfl = 0;
     if (split > 1) {
         for (int i = 0; i < g.n; i++) {
@@ -838,7 +1022,8 @@ bool launch_qgemm(hipStream_t st, MMGroup & g, int wtype) {
             default: fprintf(stderr, "rwkv: qgemm type %d unsupported\n", wtype); return false; \
         }                                                                                      \
     } while (0)
-        if (split == 4) QG_SPLIT_T(4);
+        if (split == 2) QG_SPLIT_T(2);
+        else if (split == 4) QG_SPLIT_T(4);
         else QG_SPLIT_T(8);
 #undef QG_SPLIT_T
 #undef QG_SPLIT_L
@@ -850,7 +1035,10 @@ bool launch_qgemm(hipStream_t st, MMGroup & g, int wtype) {
             cblocks += (int)(((size_t)g.T * g.e[i].W.M + 255) / 256);
         }
         const bool one = qg_one(wtype);
-        if (split == 4) {
+        if (split == 2) {
+            if (one) hipLaunchKernelGGL((k_qg_combine<2, true>), dim3(cblocks), block, 0, st, g);
+            else hipLaunchKernelGGL((k_qg_combine<2, false>), dim3(cblocks), block, 0, st, g);
+        } else if (split == 4) {
             if (one) hipLaunchKernelGGL((k_qg_combine<4, true>), dim3(cblocks), block, 0, st, g);
             else hipLaunchKernelGGL((k_qg_combine<4, false>), dim3(cblocks), block, 0, st, g);
         } else {

@@ -128,7 +128,7 @@ extern "C" RWKV_API bool rwkv_mi355x_selftest_gemm(int wtype, const void * W, in
 // (quantized: the int8-MFMA GEMM; F16 / F32 over 16+ tokens, K >= 512: k_fmm).
 extern "C" RWKV_API bool rwkv_mi355x_selftest_gemm_split(int wtype, const void * W, int K, int M, const float * x,
                                                          int T, float * y, int split) {
-    if (split != 1 && split != 4 && split != 8) return false;
+    if (split != 1 && split != 2 && split != 4 && split != 8) return false;
     if (wtype_quantized(wtype)) return T >= 2 && selftest_mm(wtype, W, K, M, x, T, y, true, split);
     return (wtype == W_F16 || wtype == W_F32) && T >= 16 && K >= 512 && selftest_mm(wtype, W, K, M, x, T, y, false, split);
 }

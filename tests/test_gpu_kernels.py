@@ -148,7 +148,7 @@ def test_fmm_split_k_bit_exact(fmt, M, K, T, split):
 
 @pytest.mark.parametrize('fmt', ['Q4_0', 'Q4_1', 'Q5_0', 'Q5_1', 'Q8_0'])
 @pytest.mark.parametrize('M,K,T', [(2048, 2048, 64), (96, 7168, 40), (160, 2048, 128), (64, 768, 7), (2048, 64, 17)])
-@pytest.mark.parametrize('split', [1, 4, 8])
+@pytest.mark.parametrize('split', [1, 2, 4, 8])
 def test_mfma_gemm_split_k_bit_exact(fmt, M, K, T, split):
     """Split-K GEMM (the class tree in 4 or 8 subtrees on as many workgroups, k_qg_combine adding the
     top levels) == the decode matvec association, bit for bit, for every format and K % 2048 != 0

@@ -2,6 +2,7 @@
 // the shapes it serves -- the batched F16 head, the v7 LoRA stages, an FP16 model's layer matmul --
 // with random F16 weights and activations, and prints an output hash (for A/B of variants).
 #include "mv_fmfma.hip"
+#include "qgemm.hip"
 
 #include <string.h>
 #include <vector>
@@ -29,7 +30,10 @@ int main() {
     struct Shape { const char * name; int M, K, T; };
     Shape shapes[] = {{"head B=128 (65536x2048)", 65536, 2048, 128}, {"head B=64", 65536, 2048, 64},
                       {"v7 LoRA-1 (576x2560) T=1024", 576, 2560, 1024}, {"v7 LoRA-2 (2560x96) T=1024", 2560, 96, 1024},
-                      {"v7 g LoRA-2 (2560x320) T=1024", 2560, 320, 1024}, {"FP16 layer (2048x2048) T=1024", 2048, 2048, 1024}};
+                      {"v7 g LoRA-2 (2560x320) T=1024", 2560, 320, 1024}, {"FP16 layer (2048x2048) T=1024", 2048, 2048, 1024},
+                      {"K sweep 2560x32", 2560, 32, 1024}, {"K sweep 2560x128", 2560, 128, 1024},
+                      {"K sweep 2560x512", 2560, 512, 1024}, {"K sweep 2560x1024", 2560, 1024, 1024},
+                      {"T sweep 2560x96 T=256", 2560, 96, 256}, {"M sweep 640x96 T=1024", 640, 96, 1024}};
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));

@@ -206,8 +206,43 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         __syncthreads();
     }
     if constexpr (SPLIT == 1) {
+        // classes without units (K < 64 units): zero leaves, which the matvec adds too.  An aligned run
+        // of 2^j of them is a +0 node of level j (0 + 0 = +0 all the way up), merged into the counter
+        // like any node -- v = st[k] + v while bit k of its position is set -- so the tail costs at most
+        // six merges instead of one fold per class.
 #pragma unroll 1
-        for (; l < 64; l++) FMM_FOLD(l);  // classes without units: zero partials (the matvec adds them too)
+        while (l < 64) {
+            const int j = __builtin_ctz(l);  // l + 2^j <= 64: l is a multiple of 2^j
+            fmf4 v[2][2];
+#pragma unroll
+            for (int i = 0; i < 2; i++)
+#pragma unroll
+                for (int n = 0; n < 2; n++) v[i][n] = fmf4{0.0f, 0.0f, 0.0f, 0.0f};
+            bool placed = false;
+#pragma unroll
+            for (int k = 0; k < 6; k++) {
+                if (k < j || placed) continue;  // uniform
+                if ((l >> k) & 1) {
+#pragma unroll
+                    for (int i = 0; i < 2; i++)
+#pragma unroll
+                        for (int n = 0; n < 2; n++) v[i][n] = st[k][i][n] + v[i][n];
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 2; i++)
+#pragma unroll
+                        for (int n = 0; n < 2; n++) st[k][i][n] = v[i][n];
+                    placed = true;
+                }
+            }
+            if (!placed) {  // the root: the total, kept in level 0
+#pragma unroll
+                for (int i = 0; i < 2; i++)
+#pragma unroll
+                    for (int n = 0; n < 2; n++) st[0][i][n] = v[i][n];
+            }
+            l += 1 << j;
+        }
     }
 #undef FMM_FOLD
 #undef FMM_CLOSE

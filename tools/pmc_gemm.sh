@@ -10,6 +10,6 @@ for ctr in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_AC
            "TCC_HIT_sum TCC_MISS_sum" "FETCH_SIZE"; do
   n=$((n+1))
   timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-trace -d $ROOT/gpurun_out/pmcg_${TAG}_$n -o run --output-format csv -- \
-      python3 $ROOT/bench.py --steps 2 --warmup 1 --skip-cpu --seq-reps 1 --abi-steps 0 --timing-steps 1 \
+      python3 $ROOT/bench.py --steps 2 --warmup 1 --skip-cpu --seq-reps 1 --abi-steps 0 --timing-steps 1 --batch "" \
       > $ROOT/gpurun_out/pmcg_${TAG}_$n.log 2>&1 || exit $?
 done

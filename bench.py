@@ -33,6 +33,8 @@ sys.path.insert(0, os.path.join(REPO, 'tests'))
 METRIC = 'tokens/sec RWKV-v6-World-1B6 Q4_0 decode + seq-eval @1/2/4/8 GPU; HBM GB/s vs peak'
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 INT8_MFMA_PEAK_TOPS = 5000.0  # dense int8 MFMA: 2x the ~2.5 PF dense bf16 rate (MI355X_MICROARCH.md, Matrix cores)
+# decode kernels that stream layer / head weights (the roofline's pooled kernel class)
+STREAM_KERNELS = ('k_mv', 'k_mva', 'k_v6_maa_dec', 'k_v6_att_fused', 'k_mvsig')
 
 CONFIGS = {
     # name: arch, n_vocab, n_embed, n_layer, ffn (0 = arch default), format, label
@@ -79,8 +81,17 @@ def decode_parity(L, ctx, om, tokens, olg0, ost0, n_vocab, state_len, tok_arr, P
     blg, bst = oracle_run(VARIANT_GPU)
     lg_ne = int(np.count_nonzero(glg.view(np.uint32) != blg.view(np.uint32)))
     st_ne = int(np.count_nonzero(gst.view(np.uint32) != bst.view(np.uint32)))
-    nlg1, nst1 = oracle_run(1)
-    log(f'parity oracle runs (GPU association + variant 1, {ntok} tokens each): {time.time() - t:.1f}s')
+    # the noise band: the largest distance any re-associated oracle variant (1..7: reversed
+    # accumulation order, scalar ggml dot, fp32 accumulators -- tests/oracle_ctypes.py noise_band)
+    # keeps from variant 0 on the same tokens
+    band_lg, band_st, worst = 0.0, 0.0, 0
+    for v in range(1, 8):
+        nlg, nst = oracle_run(v)
+        dl = float(np.abs(nlg - olg0).max())
+        if dl > band_lg:
+            band_lg, worst = dl, v
+        band_st = max(band_st, float(np.abs(nst - ost0).max()))
+    log(f'parity oracle runs (GPU association + variants 1..7, {ntok} tokens each): {time.time() - t:.1f}s')
     parity = {
         'bit_exact_vs_gpu_association_oracle': lg_ne == 0 and st_ne == 0, 'bit_exact_tokens': ntok,
         'logits_differing': lg_ne, 'state_values_differing': st_ne, 'tokens': ntok,
@@ -88,9 +99,10 @@ def decode_parity(L, ctx, om, tokens, olg0, ost0, n_vocab, state_len, tok_arr, P
         'max_abs_dlogit': float(np.abs(glg - olg0).max()),
         'max_abs_dstate': float(np.abs(gst - ost0).max()),
         'max_abs_logit': float(np.abs(olg0).max()),
-        'noise_band': {'what': 'oracle variant 1 (reversed accumulation order) vs variant 0, same tokens',
-                       'max_abs_dlogit': float(np.abs(nlg1 - olg0).max()),
-                       'max_abs_dstate': float(np.abs(nst1 - ost0).max())},
+        'noise_band': {'what': 'largest distance of oracle variants 1..7 (re-associated restatements: reversed '
+                               'order, scalar ggml dot, fp32 accumulators) from variant 0, same tokens',
+                       'max_abs_dlogit': band_lg, 'max_abs_dstate': band_st, 'widest_variant': worst},
+        'within_1p5x_band': float(np.abs(glg - olg0).max()) <= 1.5 * max(band_lg, 1e-3),
         'tolerance_note': 'north-star 1e-3 logit bound applies to the FP32 fixtures (tests/test_gpu_parity.py); '
                           'on quantized weights two valid restatements differ by the noise band',
     }
@@ -116,6 +128,9 @@ def main():
     ap.add_argument('--batch', default='8,32,64,128', help='batched decode sizes (contexts per step; "" = none)')
     ap.add_argument('--batch-steps', type=int, default=32)
     ap.add_argument('--model-dir', default=os.environ.get('RWKV_BENCH_DIR', '/tmp/rwkv_bench'))
+    ap.add_argument('--decode-only', action='store_true',
+                    help='only the timed device-resident decode (warmup + steps, graph replays): the run a '
+                         'rocprofv3 kernel trace of the decode chain is taken from (profiles/)')
     args = ap.parse_args()
     errors = []  # any entry makes the run exit non-zero after the JSON line
 
@@ -201,6 +216,8 @@ def main():
     ms_per_step = elapsed * 1e3 / args.steps
     value = world * args.steps / elapsed
     log(f'decode: {ms_per_step * 1e3:.1f} us/token, {value:.1f} tok/s aggregate over {world} GPU(s)')
+    if args.decode_only:
+        args.batch, args.seq_reps, args.abi_steps, args.skip_cpu = '', 0, 0, True
 
     # ---------------- batched multi-context decode ----------------
     # B independent contexts advance one token each per step (rwkv_mi355x_eval_batch_device: states
@@ -348,6 +365,8 @@ def main():
     roofline = None
     timing_steps = max(1, args.timing_steps)
     try:
+        if args.decode_only:
+            raise StopIteration
         assert L.rwkv_mi355x_state_upload(ctx.ptr, None)
         L.rwkv_mi355x_set_kernel_timing(ctx.ptr, True)
         for i in range(timing_steps):
@@ -358,29 +377,48 @@ def main():
         for k in kstats:
             log(f"  {k['name']:<18} launches {k['launches']:5d} avg {k['ms'] / k['launches'] * 1e3:8.2f} us "
                 f"{k['bytes'] / k['launches'] / 1e6:8.3f} MB/launch -> {k['bytes'] / k['ms'] / 1e6:8.1f} GB/s")
-        # the decode matvec (all k_mv / k_mva launches, head included) is the dominant kernel class
-        dom = next((k for k in kstats if k['name'] == 'k_mv'), kstats[0] if kstats else None)
-        if dom is None:
+        # the dominant kernel class: the decode kernels that stream the weights -- every k_mv
+        # (LayerNorm-prologue groups, head) / k_mva (activation-input groups) launch, the fused v6
+        # maa launch and the fused v6 r,k,v,g + attention launch -- pooled; each launch timed by an
+        # event pair bound to its own dispatch (hipExtLaunchKernelGGL: the begin / end timestamps a
+        # rocprofv3 kernel trace reports), on the engine's stream, over timing_steps eager decode steps
+        pool = [k for k in kstats if k['name'] in STREAM_KERNELS and k['bytes'] > 0]
+        if not pool:
             raise RuntimeError('no decode kernel timings recorded')
-        avg_us = dom['ms'] / dom['launches'] * 1e3
-        bytes_per_launch = dom['bytes'] / dom['launches']
+        p_ms = sum(k['ms'] for k in pool)
+        p_launches = sum(k['launches'] for k in pool)
+        p_bytes = sum(k['bytes'] for k in pool)
+        avg_us = p_ms / p_launches * 1e3
+        bytes_per_launch = p_bytes / p_launches
         achieved = bytes_per_launch / (avg_us * 1e-6) / 1e9
         traffic = None
         pmc = os.path.join(REPO, 'profiles', 'pmc_traffic.json')
         if os.path.isfile(pmc):
-            t = json.load(open(pmc)).get(args.config, {}).get(dom['name'])
+            t = json.load(open(pmc)).get(args.config, {}).get('decode_stream')
             if t:
                 traffic = t['traffic_bytes_per_launch']
         dbytes = L.rwkv_mi355x_decode_bytes(ctx.ptr, True)
+        all_ms = sum(k['ms'] for k in kstats)
         roofline = {
-            'kernel': dom['name'], 'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+            'kernel': 'decode weight-streaming kernels (' + ', '.join(sorted(k['name'] for k in pool)) + '), pooled',
+            'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
             'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic,
             'avg_launch_us': round(avg_us, 3), 'algorithmic_bytes_per_launch': round(bytes_per_launch),
-            'launches_per_token': round(dom['launches'] / timing_steps, 1),
+            'launches_per_token': round(p_launches / timing_steps, 1),
+            'method': 'per-dispatch HIP events (hipExtLaunchKernelGGL start/stop) on the engine stream, '
+                      f'{timing_steps} eager decode steps; profiles/*decode_only* holds the rocprofv3 trace '
+                      'of the graph-replayed decode for the same kernels',
+            'per_kernel': {k['name']: {'launches_per_token': round(k['launches'] / timing_steps, 1),
+                                       'avg_us': round(k['ms'] / k['launches'] * 1e3, 3),
+                                       'GBps': round(k['bytes'] / (k['ms'] * 1e-3) / 1e9, 1) if k['bytes'] else None}
+                           for k in kstats},
+            'kernel_time_us_per_token': round(all_ms / timing_steps * 1e3, 1),
             'decode_bytes_per_token': round(dbytes),
             'decode_GBps_end_to_end': round(dbytes / (ms_per_step * 1e-3) / 1e9, 1),
             'decode_frac_end_to_end': round(dbytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
         }
+    except StopIteration:
+        pass
     except Exception as e:
         errors.append(f'roofline: {e!r}')
         log(f'roofline failed: {e!r}')
@@ -440,10 +478,12 @@ def main():
                     break
             cpu_s = time.perf_counter() - t4
             cpu = {'value': round(ntok / cpu_s, 3), 'unit': 'tokens/s', 'cores': olib().oracle_get_threads(),
+                   'threads': olib().oracle_get_threads(), 'host_cpus': os.cpu_count(),
                    'kind': 'port',
                    'sample': f'{label} single-token decode (logits on), {ntok} tokens from a fresh state, '
                              f'{cpu_s:.1f}s; oracle/ C restatement of the reference CPU arithmetic '
-                             f'(ggml Q8 activation quantization + int8 block dots), OpenMP over rows'}
+                             f'(ggml Q8 activation quantization + int8 block dots), OpenMP over rows; cores = OpenMP '
+                             f'threads used (OMP_NUM_THREADS, else min(16, host CPUs)), host_cpus = os.cpu_count()'}
             log(f'cpu baseline: {cpu["value"]} tok/s on {cpu["cores"]} threads (load {load_s:.1f}s)')
         except Exception as e:
             errors.append(f'cpu_baseline: {e!r}')
@@ -486,7 +526,7 @@ def main():
                 errors.append('parity missing')
             elif not parity['bit_exact_vs_gpu_association_oracle']:
                 errors.append('parity: GPU decode not bit-exact to the GPU-association oracle')
-        if roofline is None:
+        if roofline is None and not args.decode_only:
             errors.append('roofline missing')
         if args.seq_reps > 0 and seq_roofline is None:
             errors.append('seq_roofline missing')

@@ -39,13 +39,21 @@
 #include <sys/stat.h>
 #ifdef _OPENMP
 #include <omp.h>
+#endif
 #ifdef __AVX2__
 #include <immintrin.h>
-#endif
 #endif
 
 #define QK 32
 #define ORACLE_MAX_TENSORS 16384
+
+/* test infrastructure: an allocation failure aborts loudly instead of returning a half-computed result */
+static void oracle_need(int ok, const char * what) {
+    if (!ok) {
+        fprintf(stderr, "oracle: out of memory (%s)\n", what);
+        abort();
+    }
+}
 
 /* ------------------------------------------------------------------ fp16 */
 
@@ -637,11 +645,12 @@ static void matmul_gpu(int wtype, const uint8_t * W, int64_t K, int64_t M, const
     const int64_t nb = K / QK;
     const size_t wbb = oracle_block_bytes(wtype);
     uint8_t * xq = (uint8_t *)malloc((size_t)(T * nb * abb));
-    for (int64_t t = 0; t < T; t++) oracle_quantize_act(atype, x + t * K, xq + t * nb * abb, K);
     /* activations unpacked: int8 values, d, s per block */
     int8_t * xi = (int8_t *)malloc((size_t)(T * K));
     float * xd = (float *)malloc((size_t)(T * nb) * sizeof(float));
     float * xs = (float *)malloc((size_t)(T * nb) * sizeof(float));
+    oracle_need(xq && xi && xd && xs, "matmul_gpu activations");
+    for (int64_t t = 0; t < T; t++) oracle_quantize_act(atype, x + t * K, xq + t * nb * abb, K);
     for (int64_t t = 0; t < T; t++)
         for (int64_t b = 0; b < nb; b++) {
             const uint8_t * xb = xq + (t * nb + b) * abb;
@@ -654,6 +663,7 @@ static void matmul_gpu(int wtype, const uint8_t * W, int64_t K, int64_t M, const
     int8_t * wi8 = (int8_t *)malloc((size_t)(M * K));
     float * dw = (float *)malloc((size_t)(M * nb) * sizeof(float));
     float * mw = (float *)malloc((size_t)(M * nb) * sizeof(float));
+    oracle_need(wi8 && dw && mw, "matmul_gpu weights");
 #pragma omp parallel for schedule(static) num_threads(nthr)
     for (int64_t m = 0; m < M; m++) {
         int wi[32];

@@ -17,6 +17,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <hip/hip_fp16.h>
 #include <stdint.h>
 #include <stddef.h>
@@ -137,6 +138,29 @@ struct MMGroup {
     int split;           // qgemm split-K: 0 = by tile count, 1 = never, 4 / 8 = forced
     int fmm;             // float weights: 0 = f32-MFMA form from T = 32, 1 = from T = 16
 };
+
+// Per-launch kernel timing (bench roofline).  While a context times its kernels (Engine::set_timing),
+// g_klt points at its timer and RK_LAUNCH launches through hipExtLaunchKernelGGL with a start /
+// stop event pair: the runtime binds both to the dispatch itself, so their elapsed time is the
+// kernel's own execution span -- the begin/end timestamps rocprofv3's kernel trace reports --
+// not the gaps between launches.  Otherwise RK_LAUNCH is hipLaunchKernelGGL.
+struct KLaunchTimer {
+    virtual ~KLaunchTimer() {}
+    virtual bool begin(hipEvent_t * a, hipEvent_t * b) = 0;
+    virtual void end(const char * kernel) = 0;
+};
+extern thread_local KLaunchTimer * g_klt;
+
+#define RK_LAUNCH(kern, grid, block, lds, st, ...)                                                  \
+    do {                                                                                            \
+        hipEvent_t rk_a_ = nullptr, rk_b_ = nullptr;                                                \
+        if (::rwkvmi::g_klt && ::rwkvmi::g_klt->begin(&rk_a_, &rk_b_)) {                            \
+            hipExtLaunchKernelGGL(kern, grid, block, lds, st, rk_a_, rk_b_, 0u, __VA_ARGS__);       \
+            ::rwkvmi::g_klt->end(#kern);                                                            \
+        } else {                                                                                    \
+            hipLaunchKernelGGL(kern, grid, block, lds, st, __VA_ARGS__);                            \
+        }                                                                                           \
+    } while (0)
 
 #define HIP_OK(x)                                                                             \
     do {                                                                                      \

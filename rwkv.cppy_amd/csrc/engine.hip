@@ -18,6 +18,8 @@
 
 namespace rwkvmi {
 
+thread_local KLaunchTimer * g_klt = nullptr;
+
 #ifdef RWKV_STAMP
 // Diagnostic builds (stamp.hpp): every kernel translation unit registers a setter for its copy
 // of the device-side control block; the rings are dumped to $RWKV_STAMP_OUT when an engine dies.
@@ -394,6 +396,16 @@ bool Engine::init() {
     }
     HIP_OK(hipMalloc(&logits_, (size_t)m_->n_vocab * sizeof(float) + 16));
     ws_allocs_.push_back(logits_);
+    // in-launch hand-off counters (k_v6_att_fused): zero once here, re-armed by the kernels
+    HIP_OK(hipMalloc(&hcnt_, kHandoffWords * 4));
+    ws_allocs_.push_back(hcnt_);
+    HIP_OK(hipMemset(hcnt_, 0, kHandoffWords * 4));
+    {
+        const size_t ng = 4 * (size_t)m_->n_embed + 128;  // k_v6_att_fused granules (4 C + D)
+        HIP_OK(hipMalloc(&hgran_, ng * 8));
+        ws_allocs_.push_back(hgran_);
+        HIP_OK(hipMemset(hgran_, 0, ng * 8));
+    }
     const char * g = getenv("RWKV_MI355X_NO_GRAPH");
     use_graphs_ = !(g && g[0] == '1');
     const char * gd = getenv("RWKV_MI355X_GENERIC_DECODE");
@@ -430,8 +442,7 @@ bool Engine::ensure_workspace(int T) {
     // keep state and logits, drop the rest; until every allocation below has succeeded the
     // workspace counts as absent (tcap_ = 0, pointers null), so a failed grow can never leave a
     // capacity that points at freed or missing buffers
-    std::vector<void *> keep = {dstate_[0], dstate_[1], logits_};
-    if (mv_scratch_) keep.push_back(mv_scratch_);
+    std::vector<void *> keep = {dstate_[0], dstate_[1], logits_, hcnt_, hgran_};
     for (void * p : ws_allocs_) {
         bool k = false;
         for (void * q : keep) k |= (p == q);
@@ -508,7 +519,7 @@ bool Engine::ensure_workspace(int T) {
 
 bool Engine::init_state(float * st, size_t n) {
     if (!n) n = m_->state_len;
-    hipLaunchKernelGGL(k_init_state, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream_, st, n,
+    RK_LAUNCH(k_init_state, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream_, st, n,
                        (int)m_->n_embed, m_->major == 4 ? 1 : 0);
     HIP_OK(hipGetLastError());
     return true;
@@ -583,6 +594,8 @@ static double act_bytes(const ActBuf & a, double T) {
     }
 }
 
+static double wbytes(const DMat & W) { return (double)type_nbytes((uint32_t)W.type, (uint64_t)W.M * W.K); }
+
 void Engine::set_timing(bool on) {
     (void)hipStreamSynchronize(stream_);
     collect_timing();
@@ -614,12 +627,22 @@ bool Engine::mm_dispatch(MMGroup & g, int wtype) {
     // does not cover -- the same bits); from batch_gemm_min_ contexts on, the quantized matmuls
     // take the int8-MFMA sequence GEMM on token tiles instead (tile_acts_; also the same bits)
     if (!wtype_quantized(wtype) && g.T >= 32) {
-        // k_fmm may split the class tree of a small grid (the v7 LoRA first stage): partials
+        // k_fmm may split the class tree of a small grid (the v7 LoRA first stage): partials, only
+        // when launch_fmm_group's rule can split this group (below 2 workgroups per CU)
         size_t msum = 0;
-        for (int i = 0; i < g.n; i++) msum += g.e[i].W.M;
-        if (!ensure_part((size_t)8 * g.T * msum)) return false;
-        g.part = part_;
-        g.part_floats = part_cap_;
+        int blocks = 0;
+        bool splittable = true;
+        for (int i = 0; i < g.n; i++) {
+            msum += g.e[i].W.M;
+            blocks += (g.e[i].W.M + 63) / 64 * ((g.T + 63) / 64);
+            splittable = splittable && g.e[i].W.K >= 512 && g.e[i].W.M % 32 == 0;
+        }
+        if (splittable && blocks < 2 * kQgCUs) {
+            const size_t split = (size_t)blocks * 4 >= (size_t)2 * kQgCUs ? 4 : 8;
+            if (!ensure_part(split * g.T * msum)) return false;
+            g.part = part_;
+            g.part_floats = part_cap_;
+        }
     }
     if (bs_ && !(tile_acts_ && wtype_quantized(wtype))) {
         bool launched = false;
@@ -1152,94 +1175,53 @@ bool Engine::forward_range(int T, const float * sin, float * sout, uint32_t l0, 
 }
 
 bool Engine::mv(MVGroup & g) {
-    if (!timing_) return launch_mv_group(stream_, g);
-    // timing: account the group like mm_launch does, under the kernel name "k_mv<2>"
-    double bytes = 0, flops = 0;
-    for (int i = 0; i < g.n; i++) {
-        const MVEntry & e = g.e[i];
-        bytes += (double)type_nbytes((uint32_t)e.W.type, (uint64_t)e.W.M * e.W.K);
-        bytes += e.src == SRC_ACT ? act_bytes(e.act, 1) : (double)e.W.K * 4 * (e.src == SRC_LNMIX ? 5 : 1);
-        bytes += (double)e.W.M * 4 * ((e.epi == EPI_ADD || e.epi == EPI_SIGMUL_ADD || e.epi == EPI_VMIX7) ? 2 : 1);
-        flops += 2.0 * e.W.M * e.W.K;
+    if (timing_) {
+        // the group's single launch is timed by its own dispatch events (RK_LAUNCH, g_klt)
+        double bytes = 0, flops = 0;
+        for (int i = 0; i < g.n; i++) {
+            const MVEntry & e = g.e[i];
+            bytes += (double)type_nbytes((uint32_t)e.W.type, (uint64_t)e.W.M * e.W.K);
+            bytes += e.src == SRC_ACT ? act_bytes(e.act, 1) : (double)e.W.K * 4 * (e.src == SRC_LNMIX ? 5 : 1);
+            bytes += (double)e.W.M * 4 * ((e.epi == EPI_ADD || e.epi == EPI_SIGMUL_ADD || e.epi == EPI_VMIX7) ? 2 : 1);
+            flops += 2.0 * e.W.M * e.W.K;
+        }
+        kt_bytes_ = bytes;
+        kt_flops_ = flops;
     }
-    // decode matvecs are timed by replay (replay_mv_timing); the group is logged, and launched
-    // here untimed so the step's results are exactly the untimed path's
-    mv_log_.push_back(MVLog{g, bytes, flops});
     return launch_mv_group(stream_, g);
 }
 
-// Timing of the decode matvecs: the step's k_mv groups are replayed back to back in one graph,
-// bracketed by a single HIP event pair on the engine stream, with every output pointer
-// redirected to scratch (the replay reads the step's real inputs and weights, and leaves state
-// and activations untouched).  Per-launch time = elapsed / launches: the kernels run as in the
-// decode graph (one inter-kernel gap each), without per-kernel event markers.
-bool Engine::replay_mv_timing() {
-    if (mv_log_.empty()) return true;
-    if (!mv_scratch_) {
-        HIP_OK(hipMalloc(&mv_scratch_, kMvScratch));
-        ws_allocs_.push_back(mv_scratch_);
-        HIP_OK(hipMemset(mv_scratch_, 0, kMvScratch));
-    }
-    float * sf = (float *)mv_scratch_;
-    char * sa = (char *)mv_scratch_ + kMvScratch / 2;
-    std::vector<MVGroup> groups;
-    double bytes = 0, flops = 0;
-    for (const MVLog & l : mv_log_) {
-        MVGroup g = l.g;
-        for (int i = 0; i < g.n; i++) {
-            MVEntry & e = g.e[i];
-            if ((size_t)e.W.M * 4 > kMvScratch / 4 || (size_t)e.W.K * 4 > kMvScratch / 4) return false;
-            e.y = sf;
-            if (e.carry_out) e.carry_out = sf + kMvScratch / 16;
-            if (e.emit) {
-                ActBuf & o = e.act_out;
-                o.f = (float *)sa;
-                o.h = (__half *)sa;
-                o.q = (int8_t *)sa;
-                o.d = (float *)(sa + kMvScratch / 8);
-                o.s = o.d + kMvScratch / 64;
-                o.qsum = (int *)(o.s + kMvScratch / 64);
-            }
-        }
-        groups.push_back(g);
-        bytes += l.bytes;
-        flops += l.flops;
-    }
-    hipGraph_t gr = nullptr;
-    hipGraphExec_t ge = nullptr;
-    HIP_OK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
-    bool ok = true;
-    for (MVGroup & g : groups) ok = ok && launch_mv_group(stream_, g);
-    HIP_OK(hipStreamEndCapture(stream_, &gr));
-    if (!ok) {
-        (void)hipGraphDestroy(gr);
-        return false;
-    }
-    HIP_OK(hipGraphInstantiate(&ge, gr, nullptr, nullptr, 0));
-    (void)hipGraphDestroy(gr);
+// KLaunchTimer (common.hpp): while a decode step is timed, every RK_LAUNCH takes an event pair
+// bound to its dispatch; the algorithmic bytes / flops set by the caller just before (kt_bytes_)
+// go to the first launch after them.
+bool Engine::begin(hipEvent_t * a, hipEvent_t * b) {
     if (event_pool_.size() < 2) {
         hipEvent_t x, y;
-        HIP_OK(hipEventCreate(&x));
-        HIP_OK(hipEventCreate(&y));
+        if (hipEventCreate(&x) != hipSuccess) return false;
+        if (hipEventCreate(&y) != hipSuccess) {
+            (void)hipEventDestroy(x);
+            return false;
+        }
         event_pool_.push_back(x);
         event_pool_.push_back(y);
     }
-    hipEvent_t a = event_pool_[0], b = event_pool_[1];
-    HIP_OK(hipGraphLaunch(ge, stream_));  // warm (instruction caches, code objects)
-    HIP_OK(hipEventRecord(a, stream_));
-    HIP_OK(hipGraphLaunch(ge, stream_));
-    HIP_OK(hipEventRecord(b, stream_));
-    HIP_OK(hipEventSynchronize(b));
-    float ms = 0;
-    HIP_OK(hipEventElapsedTime(&ms, a, b));
-    (void)hipGraphExecDestroy(ge);
-    KernelStat & s = stats_[add_stat("k_mv")];
-    s.total_ms += ms;
-    s.total_bytes += bytes;
-    s.total_flops += flops;
-    s.launches += (long long)groups.size();
-    mv_log_.clear();
+    *a = event_pool_.back();
+    event_pool_.pop_back();
+    *b = event_pool_.back();
+    event_pool_.pop_back();
+    kt_a_ = *a;
+    kt_b_ = *b;
     return true;
+}
+
+void Engine::end(const char * kernel) {
+    // "(k_mva<WFIX, Rv, Uv>)" -> "k_mva"
+    std::string n(kernel);
+    while (!n.empty() && (n[0] == '(' || n[0] == ' ')) n.erase(0, 1);
+    const size_t cut = n.find_first_of("<) ");
+    if (cut != std::string::npos) n.resize(cut);
+    pending_.push_back(Pending{add_stat(n), kt_a_, kt_b_, kt_bytes_, kt_flops_});
+    kt_bytes_ = kt_flops_ = 0;
 }
 
 // Builder for decode matvec groups.
@@ -1349,6 +1331,11 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits, uint32
             ActBuf outs[5] = {A(1, L.decay_w1), A(2, L.att_k), A(3, L.att_v), A(4, L.att_r), A(5, L.att_g)};
             if (v6_maa_dec_supported(C, D, L.maa_w1.type) && !split_maa_) {
                 // W1 rows + mix in one launch (mv_maa.hip)
+                if (timing_) {
+                    // W1, W2 (fp32), x / carry / LN / maa vectors in, carry and 5 Q8 mixes out
+                    kt_bytes_ = wbytes(L.maa_w1) + 5.0 * D * C * 4 + 11.0 * C * 4 + C * 4.0 + 5 * act_bytes(outs[0], 1);
+                    kt_flops_ = 2.0 * L.maa_w1.M * L.maa_w1.K + 2.0 * 5 * D * C;
+                }
                 if (!launch_v6_maa_dec(stream_, C, D, L.maa_w1, x_, si + C, so + C, L.ln1_w, L.ln1_b, L.maa_x,
                                        L.maa_w2t, L.maa, outs))
                     return false;
@@ -1359,17 +1346,10 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits, uint32
                 if (!launch_v6_mix5_dec(stream_, C, D, so + C, si + C, lora_, L.maa_w2t, L.maa, outs))
                     return false;
             }
-            MV c;
             const int mats[5] = {3, 1, 2, 4, 0};  // r, k, v, g, w
             float * ys[5] = {r_, k_, v_, g_, dsmall_[0]};
             const DMat * Ws[5] = {&L.att_r, &L.att_k, &L.att_v, &L.att_g, &L.decay_w1};
             const int epis[5] = {EPI_STORE, EPI_STORE, EPI_STORE, EPI_SILU, EPI_TANH};
-            for (int i = 0; i < 5; i++) {
-                MVEntry & e = c.add(*Ws[i], ys[i], epis[i]);
-                e.src = SRC_ACT;
-                e.act = outs[mats[i]];
-            }
-            if (!mv(c.g)) return false;
             Att6Dec a;
             memset(&a, 0, sizeof(a));
             a.H = H;
@@ -1389,7 +1369,42 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits, uint32
             a.lnx_b = L.att_lnx_b;
             a.eps = 64e-5f;
             if (!att_out(a, c_wo, L.att_o)) return false;
-            if (!launch_att6_dec(stream_, a)) return false;
+            // r, k, v, g, Wd1 rows and the per-head attention in one launch (mv_att6f.hip), else
+            // the k_mva group + k_att6_dec pair (the same bits)
+            Att6Fused f;
+            memset(&f, 0, sizeof(f));
+            f.H = H;
+            f.C = C;
+            f.D = L.decay_w1.M;
+            for (int i = 0; i < 4; i++) {
+                f.W[i] = *Ws[i];
+                f.x[i] = outs[mats[i]];
+            }
+            f.wd1 = L.decay_w1;
+            f.xw = outs[mats[4]];
+            f.att = a;
+            f.gran = hgran_;
+            f.cnt = hcnt_;
+            f.err = hcnt_ + kHandoffWords - 1;
+            if (v6_att_fused_supported(f)) {
+                if (timing_) {
+                    // r, k, v, g, Wd1, Wd2 weights, their 5 Q8 inputs, the head state in and out,
+                    // u / decay / ln_x vectors, r / k / v / g / dl written (sc1) and read back, Wo's input out
+                    kt_bytes_ = 4 * wbytes(L.att_r) + wbytes(L.decay_w1) + wbytes(L.decay_w2) + 5 * act_bytes(outs[0], 1) +
+                                2.0 * H * S * S * 4 + 4.0 * C * 4 + 2.0 * (4.0 * C + f.D) * 4 + act_bytes(a.yq, 1);
+                    kt_flops_ = 2.0 * (4.0 * C + f.D) * C + 2.0 * C * f.D;
+                }
+                if (!launch_v6_att_fused(stream_, f)) return false;
+            } else {
+                MV c;
+                for (int i = 0; i < 5; i++) {
+                    MVEntry & e = c.add(*Ws[i], ys[i], epis[i]);
+                    e.src = SRC_ACT;
+                    e.act = outs[mats[i]];
+                }
+                if (!mv(c.g)) return false;
+                if (!launch_att6_dec(stream_, a)) return false;
+            }
             if (!mv(c_wo.g)) return false;
         } else {
             // v7, order r, w, k, v, a, g of x_rwkvag (rwkv_graph.inc:404-413)
@@ -1461,13 +1476,42 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits, uint32
             src_lnmix(ek, x_, si, L.ln2_w, L.ln2_b, muk, form, so);
             ek.emit = 1;
             ek.act_out = kin;
-            src_lnmix(b.add(L.ffn_r, fr_, EPI_STORE), x_, si, L.ln2_w, L.ln2_b, mur, form);
+            // the receptance rows go with the value rows (k_mvsig) when the key launch can emit
+            // their input: one launch of 224 workgroups for the key instead of 288 for key +
+            // receptance (more workgroups than CUs), and fr_ never leaves the wave
+            MVEntry sv, sr;
+            memset(&sv, 0, sizeof(sv));
+            memset(&sr, 0, sizeof(sr));
+            sv.W = L.ffn_v;
+            sv.src = SRC_ACT;
+            sv.act = kin;
+            sv.y = x_;
+            sv.epi = EPI_SIGMUL_ADD;
+            sr.W = L.ffn_r;
+            sr.src = SRC_ACT;
+            sr.act = A(7, L.ffn_r);
+            sr.epi = EPI_STORE;
+            const bool sig = L.ffn_r.type == L.ffn_k.type && mv_sigmul_supported(sv, sr);
+            if (sig) {
+                ek.mu2 = mur;
+                ek.act2_out = sr.act;
+            } else {
+                src_lnmix(b.add(L.ffn_r, fr_, EPI_STORE), x_, si, L.ln2_w, L.ln2_b, mur, form);
+            }
             if (!mv(b.g)) return false;
-            MV c;
-            MVEntry & ev = c.add(L.ffn_v, x_, EPI_SIGMUL_ADD, fr_);
-            ev.src = SRC_ACT;
-            ev.act = kin;
-            if (!mv(c.g)) return false;
+            if (sig) {
+                if (timing_) {
+                    kt_bytes_ = wbytes(L.ffn_v) + wbytes(L.ffn_r) + act_bytes(kin, 1) + act_bytes(sr.act, 1) + 2.0 * C * 4;
+                    kt_flops_ = 2.0 * ((double)L.ffn_v.M * L.ffn_v.K + (double)L.ffn_r.M * L.ffn_r.K);
+                }
+                if (!launch_mv_sigmul(stream_, sv, sr)) return false;
+            } else {
+                MV c;
+                MVEntry & ev = c.add(L.ffn_v, x_, EPI_SIGMUL_ADD, fr_);
+                ev.src = SRC_ACT;
+                ev.act = kin;
+                if (!mv(c.g)) return false;
+            }
         }
     }
     if (logits && l1 == m_->n_layer) {
@@ -1511,12 +1555,13 @@ bool Engine::run_tokens_impl(const uint32_t * tokens, size_t T, bool want_logits
         }
         const bool lg = last && want_logits;
         if (timing_) {
-            // eager launches bracketed by events; the delay kernel holds the GPU while the host
-            // queues the whole step, so the event pairs time kernels rather than submission gaps
-            mv_log_.clear();
-            if (!forward((int)n, dstate_[cur_], dstate_[cur_ ^ 1], lg)) return false;
-            if (n == 1 && !replay_mv_timing()) return false;
-            mv_log_.clear();
+            // eager launches; a decode step's kernels each carry a dispatch-bound event pair
+            // (RK_LAUNCH through g_klt), the sequence path's matmul groups an event pair around
+            // the group (mm_launch)
+            if (n == 1) g_klt = this;
+            const bool ok = forward((int)n, dstate_[cur_], dstate_[cur_ ^ 1], lg);
+            g_klt = nullptr;
+            if (!ok) return false;
         } else if (n == 1 && use_graphs_) {
             hipGraphExec_t & ge = graphs_[cur_][lg ? 1 : 0];
             if (!ge) {
@@ -1760,6 +1805,8 @@ long long Engine::debug_copy(const char * name, void * out, size_t bytes) {
     if (n == "lora") src = lora_, cap_bytes = cap * kmax * 4;
     if (n == "bonus") src = bonus_, cap_bytes = cap * (size_t)std::max<int64_t>(1, m_->H) * 4;
     if (n == "logits") src = logits_, cap_bytes = (size_t)m_->n_vocab * 4;
+    if (n == "handoff") src = hcnt_, cap_bytes = kHandoffWords * 4;  // in-launch counters, [last] = timeout flag
+    if (n == "granules") src = hgran_, cap_bytes = (4 * C + 128) * 8;  // k_v6_att_fused hand-off granules
     if (!src && n.rfind("slot", 0) == 0) {
         const size_t dot = n.find('.');
         const int i = atoi(n.c_str() + 4);
@@ -1833,7 +1880,7 @@ bool Engine::eval_batch(const uint32_t * tokens, size_t B, const float * state_i
     // input states: device pointer as given, else staged into bstate_[0] (NULL = fresh states)
     const float * sin = state_in;
     if (!state_in) {
-        hipLaunchKernelGGL(k_init_state, dim3((unsigned)((B * n + 255) / 256)), dim3(256), 0, stream_, bstate_[0],
+        RK_LAUNCH(k_init_state, dim3((unsigned)((B * n + 255) / 256)), dim3(256), 0, stream_, bstate_[0],
                            B * n, (int)m_->n_embed, m_->major == 4 ? 1 : 0);
         HIP_OK(hipGetLastError());
         sin = bstate_[0];

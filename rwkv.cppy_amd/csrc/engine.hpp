@@ -76,10 +76,12 @@ struct KernelStat {
     double total_flops = 0;
 };
 
-class Engine {
+class Engine : public KLaunchTimer {
   public:
     explicit Engine(DeviceModel * m) : m_(m) {}
     ~Engine();
+    bool begin(hipEvent_t * a, hipEvent_t * b) override;
+    void end(const char * kernel) override;
 
     bool init();
     // ABI-level evaluation (host buffers).  tokens host, T >= 1.
@@ -144,6 +146,9 @@ class Engine {
     ActSlot slots_[kSlots];
     float * dstate_[2] = {nullptr, nullptr};
     int cur_ = 0;
+    static constexpr int kHandoffWords = 256;  // in-launch hand-off counters; the last word = timeout flag
+    unsigned * hcnt_ = nullptr;
+    unsigned long long * hgran_ = nullptr;  // in-launch hand-off granules (k_v6_att_fused)
     hipGraphExec_t graphs_[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // [cur][logits]
     bool use_graphs_ = true;
     bool split_maa_ = false;       // RWKV_MI355X_SPLIT_MAA=1: v6 decode W1 + mix as two launches
@@ -157,14 +162,8 @@ class Engine {
     };
 
     int add_stat(const std::string & name);
-    struct MVLog {
-        MVGroup g;
-        double bytes, flops;
-    };
-    std::vector<MVLog> mv_log_;
-    void * mv_scratch_ = nullptr;
-    static constexpr size_t kMvScratch = 4u << 20;
-    bool replay_mv_timing();
+    double kt_bytes_ = 0, kt_flops_ = 0;  // algorithmic work of the next timed launch
+    hipEvent_t kt_a_ = nullptr, kt_b_ = nullptr;
     bool mm_dispatch(MMGroup & g, int wtype);
     bool ensure_part(size_t n);
     float * gy_ = nullptr;     // scratch y of emit-only GEMM entries

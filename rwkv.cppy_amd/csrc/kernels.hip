@@ -184,15 +184,15 @@ static bool launch_mm_wf(hipStream_t st, MMGroup & g) {
     if (blocks == 0) return true;
     dim3 grid(blocks), block(256);
     if (T == 1) {
-        if (emit) hipLaunchKernelGGL((k_mm<WF, 8, 1>), grid, block, 0, st, g);
-        else hipLaunchKernelGGL((k_mm<WF, 2, 1>), grid, block, 0, st, g);
+        if (emit) RK_LAUNCH((k_mm<WF, 8, 1>), grid, block, 0, st, g);
+        else RK_LAUNCH((k_mm<WF, 2, 1>), grid, block, 0, st, g);
     } else {
         // token spans so that the grid has ~4096 workgroups (at most one span per 4 tokens)
         // (batched decode, T <= 16 over >= 256 row blocks: one span, every weight read once)
         const int gy = (T <= 16 && blocks >= 256) ? 1 : std::max(1, std::min((T + 3) / 4, 4096 / blocks));
         const dim3 grid2(blocks, gy);
-        if (emit) hipLaunchKernelGGL((k_mm<WF, 8, 4>), grid2, block, 0, st, g);
-        else hipLaunchKernelGGL((k_mm<WF, 2, 4>), grid2, block, 0, st, g);
+        if (emit) RK_LAUNCH((k_mm<WF, 8, 4>), grid2, block, 0, st, g);
+        else RK_LAUNCH((k_mm<WF, 2, 4>), grid2, block, 0, st, g);
     }
     HIP_OK(hipGetLastError());
     return true;
@@ -324,8 +324,8 @@ static bool launch_mm_small(hipStream_t st, MMGroup & g, int wtype) {
     const int wstride = kmax * ES + 16;  // padded row: 16-byte reads of 16 lanes spread over banks
     const size_t lds = (size_t)64 * wstride + (size_t)MMS_TB * kmax * ES;
     const dim3 grid(blocks, (g.T + MMS_TB - 1) / MMS_TB);
-    if (wtype == W_F16) hipLaunchKernelGGL(k_mm_small<W_F16>, grid, dim3(256), lds, st, g, wstride);
-    else hipLaunchKernelGGL(k_mm_small<W_F32>, grid, dim3(256), lds, st, g, wstride);
+    if (wtype == W_F16) RK_LAUNCH(k_mm_small<W_F16>, grid, dim3(256), lds, st, g, wstride);
+    else RK_LAUNCH(k_mm_small<W_F32>, grid, dim3(256), lds, st, g, wstride);
     return hipGetLastError() == hipSuccess;
 }
 
@@ -359,7 +359,7 @@ __global__ void k_delay(unsigned long long ticks) {
 }
 
 bool launch_delay(hipStream_t st, int us) {
-    hipLaunchKernelGGL(k_delay, dim3(1), dim3(64), 0, st, (unsigned long long)us * 100ull);  // 100 MHz clock
+    RK_LAUNCH(k_delay, dim3(1), dim3(64), 0, st, (unsigned long long)us * 100ull);  // 100 MHz clock
     HIP_OK(hipGetLastError());
     return true;
 }
@@ -386,7 +386,7 @@ __global__ __launch_bounds__(256) void k_embed_ln(const uint32_t * tokens, DMat 
 
 bool launch_embed_ln(hipStream_t st, const uint32_t * tokens, int T, const DMat & emb, const float * w,
                      const float * b, float * x) {
-    hipLaunchKernelGGL(k_embed_ln, dim3(T), dim3(256), 0, st, tokens, emb, w, b, x);
+    RK_LAUNCH(k_embed_ln, dim3(T), dim3(256), 0, st, tokens, emb, w, b, x);
     HIP_OK(hipGetLastError());
     return true;
 }
@@ -504,9 +504,9 @@ bool launch_ln_mix(hipStream_t st, const LnMixArgs & a) {
     const int gy = a.T <= 64 ? cbs : tgs < 256 ? std::min(cbs, (512 + tgs - 1) / tgs) : std::min(ln_mix_y, cbs);
     const dim3 grid((a.T + TOKS_PER_WG - 1) / TOKS_PER_WG, gy), block(256 * TOKS_PER_WG);
     const int tq = tile_q(a.out, a.n_out, a.C);
-    if (tq == 1) hipLaunchKernelGGL(k_ln_mix<1>, grid, block, 0, st, a);
-    else if (tq == 2) hipLaunchKernelGGL(k_ln_mix<2>, grid, block, 0, st, a);
-    else hipLaunchKernelGGL(k_ln_mix<0>, grid, block, 0, st, a);
+    if (tq == 1) RK_LAUNCH(k_ln_mix<1>, grid, block, 0, st, a);
+    else if (tq == 2) RK_LAUNCH(k_ln_mix<2>, grid, block, 0, st, a);
+    else RK_LAUNCH(k_ln_mix<0>, grid, block, 0, st, a);
     HIP_OK(hipGetLastError());
     return true;
 }
@@ -526,7 +526,7 @@ __global__ __launch_bounds__(256) void k_ln_emit(int C, const float * x, const f
 
 bool launch_ln_emit(hipStream_t st, int C, const float * x, const float * w, const float * b, const ActBuf & out,
                     int rows) {
-    hipLaunchKernelGGL(k_ln_emit, dim3(rows), dim3(256), 0, st, C, x, w, b, out);
+    RK_LAUNCH(k_ln_emit, dim3(rows), dim3(256), 0, st, C, x, w, b, out);
     HIP_OK(hipGetLastError());
     return true;
 }
@@ -762,19 +762,19 @@ bool launch_v6_mix5(hipStream_t st, int T, int C, int D, const float * lora, con
     if (mfma_on && tq > 0 && (D == 32 || D == 64) && C % 32 == 0) {
         const dim3 mgrid(C / 32, (T + 63) / 64);
         if (D == 32) {
-            if (tq == 1) hipLaunchKernelGGL((k_v6_mix5m<32, 1>), mgrid, dim3(320), 0, st, a);
-            else hipLaunchKernelGGL((k_v6_mix5m<32, 2>), mgrid, dim3(320), 0, st, a);
+            if (tq == 1) RK_LAUNCH((k_v6_mix5m<32, 1>), mgrid, dim3(320), 0, st, a);
+            else RK_LAUNCH((k_v6_mix5m<32, 2>), mgrid, dim3(320), 0, st, a);
         } else {
-            if (tq == 1) hipLaunchKernelGGL((k_v6_mix5m<64, 1>), mgrid, dim3(320), 0, st, a);
-            else hipLaunchKernelGGL((k_v6_mix5m<64, 2>), mgrid, dim3(320), 0, st, a);
+            if (tq == 1) RK_LAUNCH((k_v6_mix5m<64, 1>), mgrid, dim3(320), 0, st, a);
+            else RK_LAUNCH((k_v6_mix5m<64, 2>), mgrid, dim3(320), 0, st, a);
         }
         HIP_OK(hipGetLastError());
         return true;
     }
 #define MIX5_L(DMv, TQv)                                                                  \
     do {                                                                                  \
-        if (D == DMv) hipLaunchKernelGGL((k_v6_mix5<DMv, TQv, true>), grid, dim3(320), 0, st, a); \
-        else hipLaunchKernelGGL((k_v6_mix5<DMv, TQv, false>), grid, dim3(320), 0, st, a);         \
+        if (D == DMv) RK_LAUNCH((k_v6_mix5<DMv, TQv, true>), grid, dim3(320), 0, st, a); \
+        else RK_LAUNCH((k_v6_mix5<DMv, TQv, false>), grid, dim3(320), 0, st, a);         \
     } while (0)
     if (D <= 32) {
         if (tq == 1) MIX5_L(32, 1);
@@ -889,12 +889,12 @@ bool launch_wkv4(hipStream_t st, int T, int C, const float * r, const float * k,
                  const float * first, const float * decay, const float * state_in, float * state_out,
                  const ActBuf & out, int bs) {
     if (T > 1 && !bs && C % 64 == 0) {  // whole waves of channels
-        hipLaunchKernelGGL(k_wkv4_seq, dim3((C + 63) / 64), dim3(64), 0, st, T, C, r, k, v, first, decay, state_in,
+        RK_LAUNCH(k_wkv4_seq, dim3((C + 63) / 64), dim3(64), 0, st, T, C, r, k, v, first, decay, state_in,
                            state_out, out);
         HIP_OK(hipGetLastError());
         return true;
     }
-    hipLaunchKernelGGL(k_wkv4, dim3((C + 255) / 256, bs ? T : 1), dim3(256), 0, st, T, C, r, k, v, first, decay,
+    RK_LAUNCH(k_wkv4, dim3((C + 255) / 256, bs ? T : 1), dim3(256), 0, st, T, C, r, k, v, first, decay,
                        state_in, state_out, out, bs);
     HIP_OK(hipGetLastError());
     return true;
@@ -1195,7 +1195,7 @@ bool launch_wkv6(hipStream_t st, int T, int H, int S, const float * k, const flo
                  float * y, int bs) {
     const int nz = bs ? T : 1;
     if (S == 64) {
-#define WKV6_L(P, N) hipLaunchKernelGGL((k_wkv6_s64<P, N>), dim3(H, 16 / (N), nz), dim3(64 * (N)), 0, st, T, H, k, v, r, u, w, state_in, state_out, y, bs)
+#define WKV6_L(P, N) RK_LAUNCH((k_wkv6_s64<P, N>), dim3(H, 16 / (N), nz), dim3(64 * (N)), 0, st, T, H, k, v, r, u, w, state_in, state_out, y, bs)
         const int nwv = g_wkv6_nwv;
         if (w_per_token) {
             if (nwv == 1) WKV6_L(true, 1);
@@ -1213,12 +1213,12 @@ bool launch_wkv6(hipStream_t st, int T, int H, int S, const float * k, const flo
     const int G = pick_groups(S), IPG = S / G;
     dim3 grid(H, 1, nz), block(S * G);
     switch (IPG) {
-        case 1: hipLaunchKernelGGL(k_wkv6<1>, grid, block, 0, st, T, H, S, G, k, v, r, u, w, w_per_token, state_in, state_out, y, bs); break;
-        case 2: hipLaunchKernelGGL(k_wkv6<2>, grid, block, 0, st, T, H, S, G, k, v, r, u, w, w_per_token, state_in, state_out, y, bs); break;
-        case 4: hipLaunchKernelGGL(k_wkv6<4>, grid, block, 0, st, T, H, S, G, k, v, r, u, w, w_per_token, state_in, state_out, y, bs); break;
-        case 8: hipLaunchKernelGGL(k_wkv6<8>, grid, block, 0, st, T, H, S, G, k, v, r, u, w, w_per_token, state_in, state_out, y, bs); break;
-        case 16: hipLaunchKernelGGL(k_wkv6<16>, grid, block, 0, st, T, H, S, G, k, v, r, u, w, w_per_token, state_in, state_out, y, bs); break;
-        case 32: hipLaunchKernelGGL(k_wkv6<32>, grid, block, 0, st, T, H, S, G, k, v, r, u, w, w_per_token, state_in, state_out, y, bs); break;
+        case 1: RK_LAUNCH(k_wkv6<1>, grid, block, 0, st, T, H, S, G, k, v, r, u, w, w_per_token, state_in, state_out, y, bs); break;
+        case 2: RK_LAUNCH(k_wkv6<2>, grid, block, 0, st, T, H, S, G, k, v, r, u, w, w_per_token, state_in, state_out, y, bs); break;
+        case 4: RK_LAUNCH(k_wkv6<4>, grid, block, 0, st, T, H, S, G, k, v, r, u, w, w_per_token, state_in, state_out, y, bs); break;
+        case 8: RK_LAUNCH(k_wkv6<8>, grid, block, 0, st, T, H, S, G, k, v, r, u, w, w_per_token, state_in, state_out, y, bs); break;
+        case 16: RK_LAUNCH(k_wkv6<16>, grid, block, 0, st, T, H, S, G, k, v, r, u, w, w_per_token, state_in, state_out, y, bs); break;
+        case 32: RK_LAUNCH(k_wkv6<32>, grid, block, 0, st, T, H, S, G, k, v, r, u, w, w_per_token, state_in, state_out, y, bs); break;
         default: fprintf(stderr, "rwkv: unsupported head size %d\n", S); return false;
     }
     HIP_OK(hipGetLastError());
@@ -1258,7 +1258,7 @@ bool launch_v7_prep(hipStream_t st, int T, int H, int S, float * k, const float 
         fprintf(stderr, "rwkv: v7 head size %d unsupported\n", S);
         return false;
     }
-    hipLaunchKernelGGL(k_v7_prep, dim3(T, (H * S + 255) / 256), dim3(256), 0, st, T, H, S, k, a, r, k_k, k_a, r_k, nb,
+    RK_LAUNCH(k_v7_prep, dim3(T, (H * S + 255) / 256), dim3(256), 0, st, T, H, S, k, a, r, k_k, k_a, r_k, nb,
                        bb, bonus);
     HIP_OK(hipGetLastError());
     return true;
@@ -1444,7 +1444,7 @@ bool launch_wkv7(hipStream_t st, int T, int H, int S, const float * r, const flo
                  float * y, int bs) {
     const int nz = bs ? T : 1;
     if (S == 64) {
-        hipLaunchKernelGGL(k_wkv7_s64, dim3(H, 4, nz), dim3(256), 0, st, T, H, r, w, k, v, a, b, state_in, state_out, y,
+        RK_LAUNCH(k_wkv7_s64, dim3(H, 4, nz), dim3(256), 0, st, T, H, r, w, k, v, a, b, state_in, state_out, y,
                            bs);
         HIP_OK(hipGetLastError());
         return true;
@@ -1452,12 +1452,12 @@ bool launch_wkv7(hipStream_t st, int T, int H, int S, const float * r, const flo
     const int G = pick_groups(S), JPG = S / G;
     dim3 grid(H, 1, nz), block(S * G);
     switch (JPG) {
-        case 1: hipLaunchKernelGGL(k_wkv7<1>, grid, block, 0, st, T, H, S, G, r, w, k, v, a, b, state_in, state_out, y, bs); break;
-        case 2: hipLaunchKernelGGL(k_wkv7<2>, grid, block, 0, st, T, H, S, G, r, w, k, v, a, b, state_in, state_out, y, bs); break;
-        case 4: hipLaunchKernelGGL(k_wkv7<4>, grid, block, 0, st, T, H, S, G, r, w, k, v, a, b, state_in, state_out, y, bs); break;
-        case 8: hipLaunchKernelGGL(k_wkv7<8>, grid, block, 0, st, T, H, S, G, r, w, k, v, a, b, state_in, state_out, y, bs); break;
-        case 16: hipLaunchKernelGGL(k_wkv7<16>, grid, block, 0, st, T, H, S, G, r, w, k, v, a, b, state_in, state_out, y, bs); break;
-        case 32: hipLaunchKernelGGL(k_wkv7<32>, grid, block, 0, st, T, H, S, G, r, w, k, v, a, b, state_in, state_out, y, bs); break;
+        case 1: RK_LAUNCH(k_wkv7<1>, grid, block, 0, st, T, H, S, G, r, w, k, v, a, b, state_in, state_out, y, bs); break;
+        case 2: RK_LAUNCH(k_wkv7<2>, grid, block, 0, st, T, H, S, G, r, w, k, v, a, b, state_in, state_out, y, bs); break;
+        case 4: RK_LAUNCH(k_wkv7<4>, grid, block, 0, st, T, H, S, G, r, w, k, v, a, b, state_in, state_out, y, bs); break;
+        case 8: RK_LAUNCH(k_wkv7<8>, grid, block, 0, st, T, H, S, G, r, w, k, v, a, b, state_in, state_out, y, bs); break;
+        case 16: RK_LAUNCH(k_wkv7<16>, grid, block, 0, st, T, H, S, G, r, w, k, v, a, b, state_in, state_out, y, bs); break;
+        case 32: RK_LAUNCH(k_wkv7<32>, grid, block, 0, st, T, H, S, G, r, w, k, v, a, b, state_in, state_out, y, bs); break;
         default: fprintf(stderr, "rwkv: unsupported head size %d\n", S); return false;
     }
     HIP_OK(hipGetLastError());
@@ -1502,9 +1502,9 @@ bool launch_groupnorm(hipStream_t st, int T, int H, int S, float eps, const floa
     }
     const dim3 grid((T + TOKS_PER_WG - 1) / TOKS_PER_WG, (H * S + 255) / 256), block(256 * TOKS_PER_WG);
     const int tq = tile_q(&out, 1, H * S);
-    if (tq == 1) hipLaunchKernelGGL(k_groupnorm<1>, grid, block, 0, st, T, H, S, eps, y, w, b, mode, g, v, bonus, out);
-    else if (tq == 2) hipLaunchKernelGGL(k_groupnorm<2>, grid, block, 0, st, T, H, S, eps, y, w, b, mode, g, v, bonus, out);
-    else hipLaunchKernelGGL(k_groupnorm<0>, grid, block, 0, st, T, H, S, eps, y, w, b, mode, g, v, bonus, out);
+    if (tq == 1) RK_LAUNCH(k_groupnorm<1>, grid, block, 0, st, T, H, S, eps, y, w, b, mode, g, v, bonus, out);
+    else if (tq == 2) RK_LAUNCH(k_groupnorm<2>, grid, block, 0, st, T, H, S, eps, y, w, b, mode, g, v, bonus, out);
+    else RK_LAUNCH(k_groupnorm<0>, grid, block, 0, st, T, H, S, eps, y, w, b, mode, g, v, bonus, out);
     HIP_OK(hipGetLastError());
     return true;
 }
@@ -1516,7 +1516,7 @@ __global__ void k_fill(float * p, size_t n, float value) {
 
 bool launch_fill(hipStream_t st, float * p, size_t n, float value) {
     if (!n) return true;
-    hipLaunchKernelGGL(k_fill, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, p, n, value);
+    RK_LAUNCH(k_fill, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, p, n, value);
     HIP_OK(hipGetLastError());
     return true;
 }
@@ -1541,9 +1541,9 @@ bool launch_act_from_f32(hipStream_t st, const float * x, int T, int K, const Ac
     if (K % 32) return false;
     const dim3 grid((T + TOKS_PER_WG - 1) / TOKS_PER_WG, std::min((K + 255) / 256, 8)), block(256 * TOKS_PER_WG);
     const int tq = tile_q(&out, 1, K);
-    if (tq == 1) hipLaunchKernelGGL(k_act_from_f32<1>, grid, block, 0, st, x, T, K, out);
-    else if (tq == 2) hipLaunchKernelGGL(k_act_from_f32<2>, grid, block, 0, st, x, T, K, out);
-    else hipLaunchKernelGGL(k_act_from_f32<0>, grid, block, 0, st, x, T, K, out);
+    if (tq == 1) RK_LAUNCH(k_act_from_f32<1>, grid, block, 0, st, x, T, K, out);
+    else if (tq == 2) RK_LAUNCH(k_act_from_f32<2>, grid, block, 0, st, x, T, K, out);
+    else RK_LAUNCH(k_act_from_f32<0>, grid, block, 0, st, x, T, K, out);
     HIP_OK(hipGetLastError());
     return true;
 }

@@ -107,6 +107,8 @@ struct MVEntry {
     const float * lnw, * lnb, * mu;
     int form;                // 0: xa*mu + (xp - xp*mu)   1: (xp - xa)*mu + xa   2: xa (plain LN)
     float * carry_out;       // entry's first workgroup writes xa here (new *_xx state)
+    const float * mu2;       // SRC_LNMIX: the entry's first workgroup also emits the mix with mu2
+    ActBuf act2_out;         // (same LayerNorm and token shift) into act2_out (row 0, global)
     float * y;               // fp32 [M] (may be null when emitting)
     const float * aux;
     const float * bias;
@@ -153,6 +155,12 @@ void set_mv_device_cus(int n);
 bool launch_mv_group(hipStream_t st, MVGroup & g);
 int mva_rows();
 
+// Decode channel mix (v4/v5/v6): y[row] += sigmoid(Wr[row] . xr) * (Wv[row] . k) in one launch
+// (mv_sig.hip, k_mvsig): ev = the value matvec (SRC_ACT, y = the residual stream), er = the
+// receptance matvec (SRC_ACT, same rows).  Same bits as the receptance matvec + EPI_SIGMUL_ADD.
+bool mv_sigmul_supported(const MVEntry & ev, const MVEntry & er);
+bool launch_mv_sigmul(hipStream_t st, const MVEntry & ev, const MVEntry & er);
+
 // v6 token-shift mixes with the maa LoRA (rwkv_graph.inc:308-346); xa = LN(x) is the new
 // att_xx carry already written by the W1 matvec prologue; w2t is time_maa_w2 transposed to
 // [5][D][C]; emits the five mixed vectors w,k,v,r,g.
@@ -190,6 +198,22 @@ struct Att6Dec {
     size_t bs;
 };
 bool launch_att6_dec(hipStream_t st, const Att6Dec & a);
+
+// v6 decode: the r, k, v, g and decay-LoRA first-stage matvecs plus the per-head attention core
+// in one launch (mv_att6f.hip); bit-identical to the k_mva group + launch_att6_dec pair.
+struct Att6Fused {
+    int H, C, D;
+    DMat W[4];       // att_r, att_k, att_v, att_g (M = K = C)
+    ActBuf x[4];     // their inputs (the maa mixes xr, xk, xv, xg)
+    DMat wd1;        // time_decay_w1 (M = D, K = C)
+    ActBuf xw;       // its input
+    Att6Dec att;     // wd2, decay, u, sin, sout, lnx_w, lnx_b, eps, yq
+    unsigned long long * gran;  // 4 C + D zeroed 8-byte granules: r, k, v, silu(g), tanh(Wd1 . xw)
+    unsigned * cnt;  // one zeroed word: heads that have read the decay granules
+    unsigned * err;  // set on a hand-off timeout
+};
+bool v6_att_fused_supported(const Att6Fused & a);
+bool launch_v6_att_fused(hipStream_t st, const Att6Fused & a);
 
 // Sequence v6 decay LoRA tail (T >= 2): w[t][c] = exp(-exp(Wd2[c] . Q8(dl[t]) + decay[c])) with
 // k_att6_dec's per-row arithmetic; dl fp32 [T][D].  Quantized Wd2 with D <= 512 only.

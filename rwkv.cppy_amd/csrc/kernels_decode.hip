@@ -215,46 +215,12 @@ bool launch_v6_mix5_dec(hipStream_t st, int C, int D, const float * xa, const fl
         return false;
     }
     dim3 grid((C + 255) / 256, 5, nb > 1 ? nb : 1);
-    hipLaunchKernelGGL(k_v6_mix5_dec, grid, dim3(256), 0, st, a);
+    RK_LAUNCH(k_v6_mix5_dec, grid, dim3(256), 0, st, a);
     HIP_OK(hipGetLastError());
     return true;
 }
 
 // --------------------------------------------------------------------------- v5/v6 attention (decode)
-// wave_sum63's fixed tree applied to partials held by one thread: p[l] is what lane l of the
-// batched kernel (k_mm) accumulates for a row whose units fit in lanes 0..31 (one unit each).
-__device__ __forceinline__ float tree16(const float * p) {
-    const float q0 = (p[0] + p[1]) + (p[2] + p[3]);
-    const float q1 = (p[4] + p[5]) + (p[6] + p[7]);
-    const float q2 = (p[8] + p[9]) + (p[10] + p[11]);
-    const float q3 = (p[12] + p[13]) + (p[14] + p[15]);
-    return (q0 + q1) + (q2 + q3);
-}
-__device__ __forceinline__ float tree_wave32(const float (&p)[32]) {
-    const float r0 = tree16(p), r1 = tree16(p + 16);
-    return (0.0f + 0.0f) + (r1 + r0);
-}
-
-// One row of the v6 decay LoRA tail by one thread: lanes 0..nl-1 of k_mm's row (nl <= NL <= 32,
-// one unit each); the first PF units were prefetched into wp[].  Partials of lanes >= NL are
-// compile-time zeros, so the tree folds to the nonzero part.
-template <int WF, int PF, int NL, bool NT = true>
-__device__ __forceinline__ float decay_row_thread(const DMat & W, int row, const ActBuf & act, int nl,
-                                                  const WBlk (&wp)[PF > 0 ? PF : 1]) {
-    float p[32], p2[32];
-#pragma unroll
-    for (int l = 0; l < 32; l++) {
-        p[l] = p2[l] = 0.0f;
-        if (l < NL && l < nl) {
-            const WBlk w = (l < PF) ? wp[l < PF ? l : 0] : load_unit<WF, NT>(W, row, 0, l);
-            const AUnit x = load_act_unit<WF, true>(act, 0, l);
-            dot_unit<WF>(w, x, p[l], p2[l]);
-        }
-    }
-    constexpr bool one = WF == W_Q4_1 || WF == W_Q5_1;
-    return one ? tree_wave32(p) + tree_wave32(p2) : tree_wave32(p) + 0.0f;
-}
-
 // One row by one wave, exactly k_mm's loop (any K).
 template <int WF>
 __device__ __forceinline__ float decay_row_wave(const DMat & W, int row, const ActBuf & act, int lane) {
@@ -485,8 +451,8 @@ bool launch_att6_dec(hipStream_t st, const Att6Dec & a) {
     const bool s64 = a.S == 64;
 #define ATT6(WFv, PFv)                                                                         \
     do {                                                                                       \
-        if (s64) hipLaunchKernelGGL((k_att6_dec<WFv, PFv, 64>), grid, block, lds, st, a);      \
-        else hipLaunchKernelGGL((k_att6_dec<WFv, PFv, 0>), grid, block, lds, st, a);           \
+        if (s64) RK_LAUNCH((k_att6_dec<WFv, PFv, 64>), grid, block, lds, st, a);      \
+        else RK_LAUNCH((k_att6_dec<WFv, PFv, 0>), grid, block, lds, st, a);           \
     } while (0)
     if (a.w) {
         ATT6(-2, 0);  // v5: no decay LoRA
@@ -554,11 +520,11 @@ bool launch_v6_decay_seq(hipStream_t st, int T, int C, const DMat & wd2, const f
     const dim3 grid((T + DECAY_TT - 1) / DECAY_TT, (C + 255) / 256);
     const int lds = DECAY_TT * ((lds_bytes_for(act_fmt_for(wd2.type), wd2.K) + 15) & ~15);
     switch (wd2.type) {
-        case W_Q4_0: hipLaunchKernelGGL(k_v6_decay_seq<W_Q4_0>, grid, dim3(256), lds, st, T, C, wd2, dl, decay, w); break;
-        case W_Q4_1: hipLaunchKernelGGL(k_v6_decay_seq<W_Q4_1>, grid, dim3(256), lds, st, T, C, wd2, dl, decay, w); break;
-        case W_Q5_0: hipLaunchKernelGGL(k_v6_decay_seq<W_Q5_0>, grid, dim3(256), lds, st, T, C, wd2, dl, decay, w); break;
-        case W_Q5_1: hipLaunchKernelGGL(k_v6_decay_seq<W_Q5_1>, grid, dim3(256), lds, st, T, C, wd2, dl, decay, w); break;
-        default: hipLaunchKernelGGL(k_v6_decay_seq<W_Q8_0>, grid, dim3(256), lds, st, T, C, wd2, dl, decay, w); break;
+        case W_Q4_0: RK_LAUNCH(k_v6_decay_seq<W_Q4_0>, grid, dim3(256), lds, st, T, C, wd2, dl, decay, w); break;
+        case W_Q4_1: RK_LAUNCH(k_v6_decay_seq<W_Q4_1>, grid, dim3(256), lds, st, T, C, wd2, dl, decay, w); break;
+        case W_Q5_0: RK_LAUNCH(k_v6_decay_seq<W_Q5_0>, grid, dim3(256), lds, st, T, C, wd2, dl, decay, w); break;
+        case W_Q5_1: RK_LAUNCH(k_v6_decay_seq<W_Q5_1>, grid, dim3(256), lds, st, T, C, wd2, dl, decay, w); break;
+        default: RK_LAUNCH(k_v6_decay_seq<W_Q8_0>, grid, dim3(256), lds, st, T, C, wd2, dl, decay, w); break;
     }
     HIP_OK(hipGetLastError());
     return true;
@@ -668,11 +634,11 @@ bool launch_att7_dec(hipStream_t st, const Att7Dec & a) {
     }
     dim3 grid(a.H, a.nb > 1 ? a.nb : 1), block(threads);
     switch (JPG) {
-        case 1: hipLaunchKernelGGL(k_att7_dec<1>, grid, block, 0, st, a); break;
-        case 2: hipLaunchKernelGGL(k_att7_dec<2>, grid, block, 0, st, a); break;
-        case 4: hipLaunchKernelGGL(k_att7_dec<4>, grid, block, 0, st, a); break;
-        case 8: hipLaunchKernelGGL(k_att7_dec<8>, grid, block, 0, st, a); break;
-        case 16: hipLaunchKernelGGL(k_att7_dec<16>, grid, block, 0, st, a); break;
+        case 1: RK_LAUNCH(k_att7_dec<1>, grid, block, 0, st, a); break;
+        case 2: RK_LAUNCH(k_att7_dec<2>, grid, block, 0, st, a); break;
+        case 4: RK_LAUNCH(k_att7_dec<4>, grid, block, 0, st, a); break;
+        case 8: RK_LAUNCH(k_att7_dec<8>, grid, block, 0, st, a); break;
+        case 16: RK_LAUNCH(k_att7_dec<16>, grid, block, 0, st, a); break;
         default: return false;
     }
     HIP_OK(hipGetLastError());

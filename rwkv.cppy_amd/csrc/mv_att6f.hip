@@ -1,0 +1,331 @@
+// mv_att6f.hip -- v6 decode: the r, k, v, g and decay-LoRA-first-stage matvecs and the per-head
+// attention core (rwkv_graph.inc:349-384) in ONE launch.
+//
+// Before: k_mva over the 4*C + D rows (one launch), then k_att6_dec (one workgroup per head, a
+// second launch that waits at the kernel boundary for every row although head h reads only its
+// own 64 channels of r, k, v, g -- plus the D decay-LoRA values every head shares).  Here the
+// grid is 8 workgroups per head: workgroup (h, s) computes 32 of head h's 256 r/k/v/g rows (4
+// waves x 8 rows, exactly k_mva's lane/unit order, wave_sum63 tree and epilogues, so the values
+// are bit-identical) and, on a fifth wave, the decay-LoRA rows of its slot (non-reducers first).  The rows are
+// published write-through (sc1 stores, every storing wave drained, then one agent-scope counter
+// add per workgroup: MI355X_MICROARCH.md "Valid forms", row 1), and workgroup (h, 0) -- which
+// loaded the head's state, decay-tail weights and per-channel operands while its own rows
+// streamed -- waits for its head's 8 arrivals and the D decay rows, reads them with sc1 loads and
+// runs k_att6_dec's arithmetic (decay tail, wkv6, GroupNorm, gate, Q8 emission of Wo's input).
+// The waiting workgroups are producers first, so the wait can never hold a slot a producer
+// needs; every spin is bounded (a timeout sets *err and the results are garbage, never a hang).
+// Counters are re-armed inside the launch by their last readers, so a replayed graph needs no
+// memset node.
+//
+// The state update uses 16-byte accesses: wave g owns keys 16g..16g+15, lane (kk, jq) keys
+// 16g + 4kk + q (q < 4) of value columns 4jq..4jq+3.  Each output column's sum keeps
+// k_att6_dec's association: ((t0 + t1) + t2) + t3 per 4-key run (from +0), (p0 + p1) + (p2 + p3)
+// per 16-key group, (s0 + s2) + (s1 + s3) over the groups.
+#include "mv_common.hpp"
+
+#include <stdlib.h>
+
+namespace rwkvmi {
+
+typedef __attribute__((address_space(1))) float gfloat_t;
+typedef __attribute__((address_space(1))) unsigned gunsigned_t;
+
+__device__ __forceinline__ void st_sc1(float * p, float v) {
+    __hip_atomic_store((gfloat_t *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const float * p) {
+    return __hip_atomic_load((gfloat_t *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned ldu_sc1(unsigned * p) {
+    return __hip_atomic_load((gunsigned_t *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void stu_sc1(unsigned * p, unsigned v) {
+    __hip_atomic_store((gunsigned_t *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned addu(unsigned * p, unsigned v) {
+    return __hip_atomic_fetch_add((gunsigned_t *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+constexpr int AF_P = 8;   // workgroups per head
+constexpr int AF_R = 8;   // rows per wave (4 waves x 8 rows x 8 workgroups = 4 x 64 rows)
+__device__ __forceinline__ int af_slot(int sidx, int h, int H) { return sidx > 0 ? (sidx - 1) * H + h : (AF_P - 1) * H + h; }
+
+// R rows of one matrix by one wave: k_mva's loads, dots, tree and epilogue (lane r: row r)
+template <int WF, int R, int U>
+__device__ __forceinline__ float af_rows(const DMat & W, const ActBuf & x, int row0, int epi, int lane) {
+    const int M = W.M, K = W.K;
+    int rows[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) rows[r] = min(row0 + r, M - 1);
+    WBlk w[R][U];
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+        for (int r = 0; r < R; r++) w[r][u] = load_unit<WF>(W, rows[r], u, lane);
+    AUnit xu[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) xu[u] = load_act_unit<WF, false>(x, u, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    float acc[R], acc2[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) acc[r] = acc2[r] = 0.0f;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const bool valid = unit_valid<WF>(K, u, lane);
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            float t = acc[r], t2 = acc2[r];
+            dot_unit<WF>(w[r][u], xu[u], t, t2);
+            acc[r] = valid ? t : acc[r];
+            acc2[r] = valid ? t2 : acc2[r];
+        }
+    }
+    constexpr bool one = WF == W_Q4_1 || WF == W_Q5_1;
+    float sr[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) sr[r] = one ? wave_sum63(acc[r]) + wave_sum63(acc2[r]) : wave_sum63(acc[r]) + 0.0f;
+    const float s = lane_row_sum<R>(sr, lane);
+    return epi == EPI_SILU ? siluf_(s) : epi == EPI_TANH ? rk_tanhf(s) : s;
+}
+
+typedef __attribute__((address_space(1))) unsigned long long gu64_t;
+
+// One granule = {tag 1 (high word), value bits (low word)}, ONE aligned 8-byte sc1 store: the data is
+// its own flag (MI355X_MICROARCH.md hand-off R2, guide Guideline 16).  A consumer sweeps its
+// granules until every tag reads 1 and then clears them to 0 (sc1), so the next launch can never
+// see a stale value: a granule is only ever 0 (empty) or this launch's value.
+__device__ __forceinline__ void gran_put(unsigned long long * g, float v) {
+    __hip_atomic_store((gu64_t *)g, (1ull << 32) | (unsigned long long)__float_as_uint(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long gran_get(const unsigned long long * g) {
+    return __hip_atomic_load((gu64_t *)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void gran_clear(unsigned long long * g) {
+    __hip_atomic_store((gu64_t *)g, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One wave sweeps N granules per lane (stride S) until every tag is set; bounded (timeout: *err).
+template <int N>
+__device__ __forceinline__ void gran_sweep(const unsigned long long * g, int stride, bool (&live)[N], float (&v)[N],
+                                           unsigned * err) {
+    for (unsigned it = 0;; it++) {
+        bool ok = true;
+        unsigned long long x[N];
+#pragma unroll
+        for (int k = 0; k < N; k++) x[k] = live[k] ? gran_get(g + k * stride) : (1ull << 32);
+#pragma unroll
+        for (int k = 0; k < N; k++) {
+            v[k] = __uint_as_float((unsigned)x[k]);
+            ok = ok && (x[k] >> 32) == 1ull;
+        }
+        if (__all(ok)) return;
+        if (it >= (1u << 20)) {
+            stu_sc1(err, 1u);
+            return;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+template <int WF, int U, int WD>
+__global__ __launch_bounds__(320) void k_v6_att_fused(Att6Fused a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];  // Q8 image of dl (decay tail input)
+    __shared__ __attribute__((aligned(16))) float sr[64], sk[64], sv[64], sg[64], sw[64], su[64];
+    __shared__ __attribute__((aligned(16))) float part[16][64];
+    constexpr int S = 64;
+    const int wg = (int)blockIdx.x, h = wg / AF_P, sidx = wg % AF_P, H = a.H, C = a.C, D = a.D;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const bool red = sidx == 0;
+    const int c0 = h * S;
+    const Att6Dec & at = a.att;
+    const size_t hb = (size_t)h * S * S;
+    const int jq = lane & 15, kk = lane >> 4;
+    unsigned long long * const gdl = a.gran + 4 * (size_t)C;
+    STAMP_BEGIN();
+    // ---- the reducer's head operands first (state rows, per-channel vectors, decay-tail weights):
+    // they stream in with this workgroup's own weight rows
+    float4 st[4];
+    WBlk wp[4];
+    float lnw_c = 0.0f, lnb_c = 0.0f, dec_c = 0.0f, u_c = 0.0f;
+    if (red) {
+        if (wave < 4) {
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                st[q] = *(const float4 *)(at.sin + hb + (size_t)(16 * wave + 4 * kk + q) * S + 4 * jq);
+        }
+        if (wave == 0) {
+            lnw_c = at.lnx_w[c0 + lane];
+            lnb_c = at.lnx_b[c0 + lane];
+            u_c = at.u[c0 + lane];
+        }
+        if (wave == 4) {
+            dec_c = at.decay[c0 + lane];
+            const int nb = at.wd2.K >> 5;
+#pragma unroll
+            for (int l = 0; l < 4; l++) wp[l] = load_wblk<WD>(at.wd2, (size_t)(c0 + lane) * nb + min(l, nb - 1));
+        }
+    }
+    // ---- this workgroup's rows, each published as a granule: wave w -> matrix (4 s + w) / 8
+    // (r, k, v, g), rows of head h; wave 4 -> decay LoRA rows (EPI_TANH) of its slot, the
+    // non-reducer workgroups' slots first (slot = (s - 1) H + h for s > 0, 7H + h for the reducers)
+    if (wave < 4) {
+        const int wh = sidx * 4 + wave, m = wh >> 3, row0 = c0 + (wh & 7) * AF_R;
+        const DMat W = m == 0 ? a.W[0] : m == 1 ? a.W[1] : m == 2 ? a.W[2] : a.W[3];
+        const ActBuf x = m == 0 ? a.x[0] : m == 1 ? a.x[1] : m == 2 ? a.x[2] : a.x[3];
+        const float v = af_rows<WF, AF_R, U>(W, x, row0, m == 3 ? EPI_SILU : EPI_STORE, lane);
+        if (lane < AF_R) gran_put(a.gran + (size_t)m * C + row0 + lane, v);
+    } else {
+        for (int d = af_slot(sidx, h, H); d < D; d += AF_P * H) {
+            const float v = af_rows<WF, 1, U>(a.wd1, a.xw, d, EPI_TANH, lane);
+            if (lane == 0) gran_put(gdl + d, v);
+        }
+    }
+    if (!red) {
+        STAMP_END_NS(6);
+        return;
+    }
+    // ---- reducer.  Waves 0..3 sweep r, k, v, g of the head's channels (lane = channel); wave 4
+    // sweeps the decay LoRA values and runs the decay tail (k_att6_dec's arithmetic) meanwhile.
+    if (wave < 4) {
+        unsigned long long * g = a.gran + (size_t)wave * C + c0 + lane;
+        bool live[1] = {true};
+        float v[1];
+        gran_sweep<1>(g, 0, live, v, a.err);
+        float * dst = wave == 0 ? sr : wave == 1 ? sk : wave == 2 ? sv : sg;
+        dst[lane] = v[0];
+        gran_clear(g);
+        if (wave == 0) {
+            su[lane] = u_c;
+            STAMP_MID();
+        }
+    } else {
+        bool live[2] = {lane < D, lane + 64 < D};
+        float v[2];
+        gran_sweep<2>(gdl + lane, 64, live, v, a.err);
+        // every head reads the decay values: the last reader clears them
+        unsigned n = 0;
+        if (lane == 0) n = addu(a.cnt, 1u);
+        n = (unsigned)__shfl((int)n, 0);
+        if (n == (unsigned)H - 1) {
+            if (lane < D) gran_clear(gdl + lane);
+            if (lane + 64 < D) gran_clear(gdl + lane + 64);
+            if (lane == 0) stu_sc1(a.cnt, 0u);
+        }
+        const ActBuf act = lds_act(smem, act_fmt_for(WD), D);
+        if (lane < D) emit32(act, 0, lane, v[0]);  // lanes 0..31 / 32..63: whole quantization blocks
+        if (lane + 64 < D) emit32(act, 0, lane + 64, v[1]);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        // decay tail of channel c0 + lane: w = exp(-exp(Wd2 . dl + decay)), rwkv_graph.inc:357-367
+        const float s = decay_row_thread<WD, 4, 4>(at.wd2, c0 + lane, act, at.wd2.K >> 5, wp);
+        sw[lane] = rk_expf(-rk_expf(s + dec_c));
+    }
+    __syncthreads();
+    STAMP_X(0);
+    // wkv6 (ggml_rwkv_wkv6): keys 16 wave + 4 kk + q, value columns 4 jq + c
+    if (wave < 4) {
+        const int i0 = 16 * wave + 4 * kk;
+        const float4 k4 = *(const float4 *)(sk + i0), u4 = *(const float4 *)(su + i0);
+        const float4 r4 = *(const float4 *)(sr + i0), w4 = *(const float4 *)(sw + i0);
+        const float4 v4 = *(const float4 *)(sv + 4 * jq);
+        const float kq[4] = {k4.x, k4.y, k4.z, k4.w}, uq[4] = {u4.x, u4.y, u4.z, u4.w};
+        const float rq[4] = {r4.x, r4.y, r4.z, r4.w}, wq[4] = {w4.x, w4.y, w4.z, w4.w};
+        const float vj[4] = {v4.x, v4.y, v4.z, v4.w};
+        float p[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const float prev[4] = {st[q].x, st[q].y, st[q].z, st[q].w};
+            float nw[4];
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const float kv = vj[c] * kq[q];
+                const float temp = kv * uq[q] + prev[c];
+                const float t = temp * rq[q];
+                p[c] += t;
+                nw[c] = prev[c] * wq[q] + kv;
+            }
+            *(float4 *)(at.sout + hb + (size_t)(i0 + q) * S + 4 * jq) = make_float4(nw[0], nw[1], nw[2], nw[3]);
+        }
+        *(float4 *)&part[4 * wave + kk][4 * jq] = make_float4(p[0], p[1], p[2], p[3]);
+    }
+    __syncthreads();
+    STAMP_X(1);
+    // GroupNorm over the head (ggml_norm, fp64 sums) * ln_x + b, * g; emitted as Wo's input
+    if (wave == 0) {
+        float sgp[4];
+#pragma unroll
+        for (int gg = 0; gg < 4; gg++)
+            sgp[gg] = (part[4 * gg][lane] + part[4 * gg + 1][lane]) + (part[4 * gg + 2][lane] + part[4 * gg + 3][lane]);
+        const float x = (sgp[0] + sgp[2]) + (sgp[1] + sgp[3]);
+        const double s = group_tree_sum_d((double)x, S);
+        const float mean = (float)div_count(s, S);
+        const float d = x - mean;
+        const double s2 = group_tree_sum_d((double)(d * d), S);
+        const float var = (float)div_count(s2, S);
+        const float scale = 1.0f / sqrtf(var + at.eps);
+        float o = d * scale;
+        o = o * lnw_c;
+        o = o + lnb_c;
+        o = o * sg[lane];
+        emit32(at.yq, 0, c0 + lane, o);
+    }
+    STAMP_END(6);
+}
+
+bool v6_att_fused_supported(const Att6Fused & a) {
+    static const bool on = [] {
+        const char * v = getenv("RWKV_MI355X_ATT_FUSED");  // 0: the two-launch form (A/B)
+        return !(v && v[0] == '0');
+    }();
+    if (!on || a.att.S != 64 || a.C != a.H * 64 || a.att.w || a.att.yq.fmt < 0 || a.att.yq.tiled) return false;
+    if (!a.gran) return false;
+    const int t = a.W[0].type;
+    if (!wtype_quantized(t) || a.wd1.type != t || mv_units(t, a.C) > 2) return false;
+    for (int m = 0; m < 4; m++)
+        if (a.W[m].type != t || a.W[m].M != a.C || a.W[m].K != a.C || a.x[m].fmt != act_fmt_for(t) || a.x[m].K != a.C)
+            return false;
+    if (a.wd1.M != a.D || a.wd1.K != a.C || a.xw.fmt != act_fmt_for(t) || a.xw.K != a.C) return false;
+    if (!wtype_quantized(a.att.wd2.type) || a.att.wd2.M != a.C || a.att.wd2.K != a.D) return false;
+    // the decay tail's PF = 4 units per row and one emission half-wave per 32 decay rows
+    if (a.D % 32 || a.D > 128) return false;  // two granules per lane of the sweeping wave
+    return a.cnt && a.err;
+}
+
+template <int WF, int U>
+static void launch_af_wd(hipStream_t st, const Att6Fused & a, int lds) {
+    const dim3 grid(AF_P * a.H), block(320);
+    switch (a.att.wd2.type) {
+        case W_Q4_0: RK_LAUNCH((k_v6_att_fused<WF, U, W_Q4_0>), grid, block, lds, st, a); break;
+        case W_Q4_1: RK_LAUNCH((k_v6_att_fused<WF, U, W_Q4_1>), grid, block, lds, st, a); break;
+        case W_Q5_0: RK_LAUNCH((k_v6_att_fused<WF, U, W_Q5_0>), grid, block, lds, st, a); break;
+        case W_Q5_1: RK_LAUNCH((k_v6_att_fused<WF, U, W_Q5_1>), grid, block, lds, st, a); break;
+        default: RK_LAUNCH((k_v6_att_fused<WF, U, W_Q8_0>), grid, block, lds, st, a); break;
+    }
+}
+
+bool launch_v6_att_fused(hipStream_t st, const Att6Fused & a) {
+    if (!v6_att_fused_supported(a)) {
+        fprintf(stderr, "rwkv: fused v6 attention decode: unsupported shape\n");
+        return false;
+    }
+    const int lds = lds_bytes_for(act_fmt_for(a.att.wd2.type), a.D);
+    const bool u1 = mv_units(a.W[0].type, a.C) <= 1;
+#define AF_T(WFv)                                                  \
+    do {                                                           \
+        if (u1) launch_af_wd<WFv, 1>(st, a, lds);                  \
+        else launch_af_wd<WFv, 2>(st, a, lds);                     \
+    } while (0)
+    switch (a.W[0].type) {
+        case W_Q4_0: AF_T(W_Q4_0); break;
+        case W_Q4_1: AF_T(W_Q4_1); break;
+        case W_Q5_0: AF_T(W_Q5_0); break;
+        case W_Q5_1: AF_T(W_Q5_1); break;
+        default: AF_T(W_Q8_0); break;
+    }
+#undef AF_T
+    HIP_OK(hipGetLastError());
+    return true;
+}
+
+}  // namespace rwkvmi

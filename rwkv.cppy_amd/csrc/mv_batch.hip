@@ -125,7 +125,7 @@ static bool launch_mvb_wf(hipStream_t st, MMGroup & g, bool emit, int U) {
     if (!blocks) return true;
     const dim3 grid(blocks), block(256);
     const size_t lds = (size_t)g.T * RW * 4;
-#define MVB(Rv, Uv, Ev) hipLaunchKernelGGL((k_mvb<WF, Rv, Uv, Ev>), grid, block, lds, st, g)
+#define MVB(Rv, Uv, Ev) RK_LAUNCH((k_mvb<WF, Rv, Uv, Ev>), grid, block, lds, st, g)
     if (emit) {
         if (U == 1) MVB(8, 1, true);
         else MVB(8, 2, true);

@@ -325,6 +325,40 @@ __device__ __forceinline__ float epi_apply(int epi, float acc, const EpiIn & p) 
     }
 }
 
+// wave_sum63's fixed tree applied to partials held by one thread: p[l] is what lane l of the
+// batched kernel (k_mm) accumulates for a row whose units fit in lanes 0..31 (one unit each).
+__device__ __forceinline__ float tree16(const float * p) {
+    const float q0 = (p[0] + p[1]) + (p[2] + p[3]);
+    const float q1 = (p[4] + p[5]) + (p[6] + p[7]);
+    const float q2 = (p[8] + p[9]) + (p[10] + p[11]);
+    const float q3 = (p[12] + p[13]) + (p[14] + p[15]);
+    return (q0 + q1) + (q2 + q3);
+}
+__device__ __forceinline__ float tree_wave32(const float (&p)[32]) {
+    const float r0 = tree16(p), r1 = tree16(p + 16);
+    return (0.0f + 0.0f) + (r1 + r0);
+}
+
+// One row of the v6 decay LoRA tail by one thread: lanes 0..nl-1 of k_mm's row (nl <= NL <= 32,
+// one unit each); the first PF units were prefetched into wp[].  Partials of lanes >= NL are
+// compile-time zeros, so the tree folds to the nonzero part.
+template <int WF, int PF, int NL, bool NT = true>
+__device__ __forceinline__ float decay_row_thread(const DMat & W, int row, const ActBuf & act, int nl,
+                                                  const WBlk (&wp)[PF > 0 ? PF : 1]) {
+    float p[32], p2[32];
+#pragma unroll
+    for (int l = 0; l < 32; l++) {
+        p[l] = p2[l] = 0.0f;
+        if (l < NL && l < nl) {
+            const WBlk w = (l < PF) ? wp[l < PF ? l : 0] : load_unit<WF, NT>(W, row, 0, l);
+            const AUnit x = load_act_unit<WF, true>(act, 0, l);
+            dot_unit<WF>(w, x, p[l], p2[l]);
+        }
+    }
+    constexpr bool one = WF == W_Q4_1 || WF == W_Q5_1;
+    return one ? tree_wave32(p) + tree_wave32(p2) : tree_wave32(p) + 0.0f;
+}
+
 // One workgroup = NW waves x R rows (RW = NW*R rows per row block).  E == 0: the input is an
 // activation buffer in global memory (SRC_ACT, NW = 4); E > 0: the prologue builds it in LDS
 // (SRC_F32 / SRC_LNMIX, K <= 64*NW*E; NW = 16 so the per-wave prologue work is short).
@@ -420,6 +454,22 @@ __device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, int b0, in
             }
 #endif
             __syncthreads();
+            if constexpr (SRCK == MVK_LN && FORM != 2) {
+                // the entry's first workgroup: the same LayerNorm output mixed with mu2 into a
+                // global activation row (the channel-mix receptance input of k_mvsig), while the
+                // dot waves stream the weights
+                if (Ent.mu2 && wgi == (int)blockIdx.x - b0) {
+                    MVEntry E2 = Ent;
+                    E2.mu = Ent.mu2;
+#pragma unroll
+                    for (int q = 0; q < LCW; q++)
+                        if (pw + q * NW < nch) {
+                            ld8(ci[q].m, Ent.mu2 + min(kc[q], K - 8));
+                            chunk_store<WF, SRCK, FORM>(E2, Ent.act2_out, ci[q], mean, scale, false, kc[q], kc[q] < K,
+                                                        lane);
+                        }
+                }
+            }
             // take part in the dot waves' barriers, then leave (to the kernel's common end)
             for (;;) {
                 if constexpr (EMIT) __syncthreads();
@@ -662,6 +712,92 @@ __global__ __launch_bounds__(256) void k_mva(int b1, int b2, int b3, int b4, int
     STAMP_END(1);
 }
 
+// Channel mix value + receptance in one launch (decode v4/v5/v6, rwkv_graph.inc:484-531):
+// y[row] += sigmoid(Wr[row] . xr) * (Wv[row] . k).  Wave w of the workgroup owns rows row0..row0+R-1 of
+// BOTH matrices (Wv units U over the FFN width, Wr units U2 over n_embed), so the receptance of
+// a row never leaves the wave; each product is k_mva's arithmetic (lane/unit order, wave_sum63
+// tree), and the epilogue is EPI_SIGMUL_ADD with aux = the receptance row (EPI_STORE) -- the same
+// bits as the Wr matvec + k_mva pair it replaces.  hv: Wv / k / y, hr: Wr / xr.
+template <int WF, int R, int U, int U2>
+__global__ __launch_bounds__(256) void k_mvsig(MVHot hv, MVHot hr) {
+    DMat W, W2;
+    W.type = W2.type = WF;
+    W.M = W2.M = hv.M;
+    W.K = hv.K;
+    W2.K = hr.K;
+    W.qs = hv.qs, W.qh = hv.qh, W.sc = hv.sc;
+    W2.qs = hr.qs, W2.qh = hr.qh, W2.sc = hr.sc;
+    ActBuf a, a2;
+    a.K = hv.K, a.q = (int8_t *)hv.aq, a.d = (float *)hv.ad, a.s = (float *)hv.as, a.qsum = (int *)hv.aqsum;
+    a2.K = hr.K, a2.q = (int8_t *)hr.aq, a2.d = (float *)hr.ad, a2.s = (float *)hr.as, a2.qsum = (int *)hr.aqsum;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int M = hv.M;
+    STAMP_BEGIN();
+    const int row0 = (int)blockIdx.x * (4 * R) + wave * R;
+    int rows[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) rows[r] = min(row0 + r, M - 1);
+    WBlk w[R][U], w2[R][U2];
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+        for (int r = 0; r < R; r++) w[r][u] = load_unit<WF>(W, rows[r], u, lane);
+#pragma unroll
+    for (int u = 0; u < U2; u++)
+#pragma unroll
+        for (int r = 0; r < R; r++) w2[r][u] = load_unit<WF>(W2, rows[r], u, lane);
+    AUnit x[U], x2[U2];
+#pragma unroll
+    for (int u = 0; u < U; u++) x[u] = load_act_unit<WF, false>(a, u, lane);
+#pragma unroll
+    for (int u = 0; u < U2; u++) x2[u] = load_act_unit<WF, false>(a2, u, lane);
+    const float yv = hv.y[min(row0 + min(lane, R - 1), M - 1)];
+    __builtin_amdgcn_sched_barrier(0);
+    STAMP_MID();
+    constexpr bool one = WF == W_Q4_1 || WF == W_Q5_1;
+    float sv[R], sr[R];
+    {
+        float acc[R], acc2[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) acc[r] = acc2[r] = 0.0f;
+#pragma unroll
+        for (int u = 0; u < U2; u++) {
+            const bool valid = unit_valid<WF>(W2.K, u, lane);
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                float t = acc[r], t2 = acc2[r];
+                dot_unit<WF>(w2[r][u], x2[u], t, t2);
+                acc[r] = valid ? t : acc[r];
+                acc2[r] = valid ? t2 : acc2[r];
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < R; r++) sr[r] = one ? wave_sum63(acc[r]) + wave_sum63(acc2[r]) : wave_sum63(acc[r]) + 0.0f;
+    }
+    {
+        float acc[R], acc2[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) acc[r] = acc2[r] = 0.0f;
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const bool valid = unit_valid<WF>(W.K, u, lane);
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                float t = acc[r], t2 = acc2[r];
+                dot_unit<WF>(w[r][u], x[u], t, t2);
+                acc[r] = valid ? t : acc[r];
+                acc2[r] = valid ? t2 : acc2[r];
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < R; r++) sv[r] = one ? wave_sum63(acc[r]) + wave_sum63(acc2[r]) : wave_sum63(acc[r]) + 0.0f;
+    }
+    const float rr = lane_row_sum<R>(sr, lane), vv = lane_row_sum<R>(sv, lane);
+    const float v = yv + sigmoidf_(rr) * vv;  // EPI_SIGMUL_ADD, aux = the receptance row
+    if (lane < R && row0 + lane < M) hv.y[row0 + lane] = v;
+    STAMP_END(7);
+}
+
 // One weight-type translation unit (mv_*.hip) instantiates every launch shape for WFIX.
 // LayerNorm prologues hold the normalized vector in registers: LNP = 32 (K <= 2048) or 64
 // (K <= 4096) elements per lane.
@@ -671,13 +807,13 @@ bool launch_mv_shape(hipStream_t st, MVGroup & g, int U, int srck, int form, boo
     int b[MM_MAX_ENTRIES];
     for (int i = 1; i < MM_MAX_ENTRIES; i++) b[i] = i < g.n ? g.e[i].block0 : INT_MAX;
 #define MV_L(Rv, Uv, S, F, E, P)                                                                              \
-    hipLaunchKernelGGL((k_mv<Rv, Uv, S, F, E, WFIX, P>), grid, dim3((S) == MVK_ACT ? 256 : 512), g.lds_bytes, st, \
+    RK_LAUNCH((k_mv<Rv, Uv, S, F, E, WFIX, P>), grid, dim3((S) == MVK_ACT ? 256 : 512), g.lds_bytes, st, \
                        b[1], b[2], b[3], b[4], b[5], b[6], b[7], g)
     const int K = g.e[0].W.K;
     if constexpr (WFIX >= 0) {
         if (srck == MVK_ACT && !emit && g.units_max <= U) {
 #define MVA_R(Rv, Uv) \
-    hipLaunchKernelGGL((k_mva<WFIX, Rv, Uv>), grid, dim3(256), 0, st, b[1], b[2], b[3], b[4], b[5], b[6], b[7], g)
+    RK_LAUNCH((k_mva<WFIX, Rv, Uv>), grid, dim3(256), 0, st, b[1], b[2], b[3], b[4], b[5], b[6], b[7], g)
 #define MVA_L(Uv)                          \
     do {                                   \
         if (g.rows == 2) MVA_R(2, Uv);     \

@@ -334,9 +334,9 @@ bool launch_fmm_group(hipStream_t st, MMGroup & g, int wtype, bool * launched) {
     }
 #define FMM_L(WFv)                                                                                               \
     do {                                                                                                         \
-        if (split == 4) hipLaunchKernelGGL((k_fmm<WFv, 4>), dim3(blocks * 4), dim3(256), 0, st, g);             \
-        else if (split == 8) hipLaunchKernelGGL((k_fmm<WFv, 8>), dim3(blocks * 8), dim3(256), 0, st, g);        \
-        else hipLaunchKernelGGL((k_fmm<WFv, 1>), dim3(blocks), dim3(256), 0, st, g);                             \
+        if (split == 4) RK_LAUNCH((k_fmm<WFv, 4>), dim3(blocks * 4), dim3(256), 0, st, g);             \
+        else if (split == 8) RK_LAUNCH((k_fmm<WFv, 8>), dim3(blocks * 8), dim3(256), 0, st, g);        \
+        else RK_LAUNCH((k_fmm<WFv, 1>), dim3(blocks), dim3(256), 0, st, g);                             \
     } while (0)
     if (split > 1)
         for (int i = 0; i < g.n; i++) g.e[i].block0 *= split;

@@ -194,9 +194,9 @@ static bool launch_maa_t(hipStream_t st, const MaaDec & a, int lds, int units) {
     const dim3 grid((a.C + cpw - 1) / cpw, 5);
 #define MAA_L(Rv, Uv, P)                                                                                           \
     do {                                                                                                           \
-        if (cpw == 64) hipLaunchKernelGGL((k_v6_maa_dec<WF, Rv, Uv, P, (Rv) * 4, 64>), grid, dim3(512), lds, st, a); \
-        else if (cpw == 128) hipLaunchKernelGGL((k_v6_maa_dec<WF, Rv, Uv, P, (Rv) * 4, 128>), grid, dim3(512), lds, st, a); \
-        else hipLaunchKernelGGL((k_v6_maa_dec<WF, Rv, Uv, P, (Rv) * 4, 256>), grid, dim3(512), lds, st, a);      \
+        if (cpw == 64) RK_LAUNCH((k_v6_maa_dec<WF, Rv, Uv, P, (Rv) * 4, 64>), grid, dim3(512), lds, st, a); \
+        else if (cpw == 128) RK_LAUNCH((k_v6_maa_dec<WF, Rv, Uv, P, (Rv) * 4, 128>), grid, dim3(512), lds, st, a); \
+        else RK_LAUNCH((k_v6_maa_dec<WF, Rv, Uv, P, (Rv) * 4, 256>), grid, dim3(512), lds, st, a);      \
     } while (0)
 #define MAA_P(Rv, Uv) \
     do { if (a.C <= 2048) MAA_L(Rv, Uv, 32); else MAA_L(Rv, Uv, 64); } while (0)

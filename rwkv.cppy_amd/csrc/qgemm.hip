@@ -877,12 +877,30 @@ __global__ __launch_bounds__(256) void k_qg_msum_rows(MMGroup g) {
                 fold(l + 1);
             }
         } else {
+            // 4 blocks of a class at a time (their reads issued together), in ascending order: the
+            // registers stay bounded for any NMAX (16: K <= 32768, e.g. a 20480-wide FFN value)
 #pragma unroll 1
             for (int lc = 0; lc < QM_CLS; lc++) {
-                const int l = sg * QM_CLS + lc;
-                Ops o;
-                rd(o, lc);
-                mac(o, cq + (l < crem ? 1 : 0));
+                const int l = sg * QM_CLS + lc, n = cq + (l < crem ? 1 : 0);
+#pragma unroll 1
+                for (int u0 = 0; u0 < n; u0 += 4) {
+                    float w4[4];
+                    float4 a4[4], b4[4];
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        const int u = min(u0 + q, NMAX - 1);
+                        w4[q] = qw[buf][u * 8 + lc][lane];
+                        a4[q] = *(const float4 *)&qx[buf][u * 8 + lc][8 * wave];
+                        b4[q] = *(const float4 *)&qx[buf][u * 8 + lc][8 * wave + 4];
+                    }
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        if (u0 + q >= n) break;  // uniform
+                        const float sx[8] = {a4[q].x, a4[q].y, a4[q].z, a4[q].w, b4[q].x, b4[q].y, b4[q].z, b4[q].w};
+#pragma unroll
+                        for (int k = 0; k < 8; k++) acc[k] = acc[k] + w4[q] * sx[k];
+                    }
+                }
                 fold(l);
             }
         }
@@ -905,8 +923,8 @@ bool launch_qg_combine(hipStream_t st, MMGroup & g, int split) {
         g.e[i].cblock0 = cblocks;
         cblocks += (int)(((size_t)g.T * g.e[i].W.M + 255) / 256);
     }
-    if (split == 4) hipLaunchKernelGGL((k_qg_combine<4, false>), dim3(cblocks), dim3(256), 0, st, g);
-    else if (split == 8) hipLaunchKernelGGL((k_qg_combine<8, false>), dim3(cblocks), dim3(256), 0, st, g);
+    if (split == 4) RK_LAUNCH((k_qg_combine<4, false>), dim3(cblocks), dim3(256), 0, st, g);
+    else if (split == 8) RK_LAUNCH((k_qg_combine<8, false>), dim3(cblocks), dim3(256), 0, st, g);
     else return false;
     HIP_OK(hipGetLastError());
     return true;
@@ -957,15 +975,16 @@ bool launch_qgemm(hipStream_t st, MMGroup & g, int wtype) {
         // the 4 x 4 register-tile form over 64-token tiles; the row form (32-token tiles) for 32 or
         // fewer tokens (contexts) and for classes of 5-8 blocks
         const bool rows = g.T <= 32 || nmax > 4;
-        if (rows && nmax <= 1) hipLaunchKernelGGL(k_qg_msum_rows<1>, dim3(mblocks8), dim3(256), 0, st, g);
-        else if (rows && nmax <= 2) hipLaunchKernelGGL(k_qg_msum_rows<2>, dim3(mblocks8), dim3(256), 0, st, g);
-        else if (rows && nmax <= 4) hipLaunchKernelGGL(k_qg_msum_rows<4>, dim3(mblocks8), dim3(256), 0, st, g);
-        else if (rows && nmax <= 8) hipLaunchKernelGGL(k_qg_msum_rows<8>, dim3(mblocks8), dim3(256), 0, st, g);
-        else if (nmax <= 1) hipLaunchKernelGGL(k_qg_msum<1>, dim3(mblocks), dim3(256), 0, st, g);
-        else if (nmax <= 2) hipLaunchKernelGGL(k_qg_msum<2>, dim3(mblocks), dim3(256), 0, st, g);
-        else if (nmax <= 4) hipLaunchKernelGGL(k_qg_msum<4>, dim3(mblocks), dim3(256), 0, st, g);
+        if (rows && nmax <= 1) RK_LAUNCH(k_qg_msum_rows<1>, dim3(mblocks8), dim3(256), 0, st, g);
+        else if (rows && nmax <= 2) RK_LAUNCH(k_qg_msum_rows<2>, dim3(mblocks8), dim3(256), 0, st, g);
+        else if (rows && nmax <= 4) RK_LAUNCH(k_qg_msum_rows<4>, dim3(mblocks8), dim3(256), 0, st, g);
+        else if (rows && nmax <= 8) RK_LAUNCH(k_qg_msum_rows<8>, dim3(mblocks8), dim3(256), 0, st, g);
+        else if (rows && nmax <= 16) RK_LAUNCH(k_qg_msum_rows<16>, dim3(mblocks8), dim3(256), 0, st, g);
+        else if (nmax <= 1) RK_LAUNCH(k_qg_msum<1>, dim3(mblocks), dim3(256), 0, st, g);
+        else if (nmax <= 2) RK_LAUNCH(k_qg_msum<2>, dim3(mblocks), dim3(256), 0, st, g);
+        else if (nmax <= 4) RK_LAUNCH(k_qg_msum<4>, dim3(mblocks), dim3(256), 0, st, g);
         else {
-            fprintf(stderr, "rwkv: qgemm _1 group: K above the m*s pass's 16384\n");
+            fprintf(stderr, "rwkv: qgemm _1 group: K above the m*s pass's 32768\n");
             return false;
         }
         HIP_OK(hipGetLastError());
@@ -1008,8 +1027,8 @@ bool launch_qgemm(hipStream_t st, MMGroup & g, int wtype) {
         const dim3 sgrid(blocks * split);
 #define QG_SPLIT_L(WFv, SP)                                                                    \
     do {                                                                                       \
-        if (k64) hipLaunchKernelGGL((k_qgemm_k64<WFv, SP>), sgrid, block, 0, st, g);           \
-        else hipLaunchKernelGGL((k_qgemm<WFv, SP>), sgrid, block, 0, st, g);                   \
+        if (k64) RK_LAUNCH((k_qgemm_k64<WFv, SP>), sgrid, block, 0, st, g);           \
+        else RK_LAUNCH((k_qgemm<WFv, SP>), sgrid, block, 0, st, g);                   \
     } while (0)
 #define QG_SPLIT_T(SP)                                                                         \
     do {                                                                                       \
@@ -1036,36 +1055,36 @@ bool launch_qgemm(hipStream_t st, MMGroup & g, int wtype) {
         }
         const bool one = qg_one(wtype);
         if (split == 2) {
-            if (one) hipLaunchKernelGGL((k_qg_combine<2, true>), dim3(cblocks), block, 0, st, g);
-            else hipLaunchKernelGGL((k_qg_combine<2, false>), dim3(cblocks), block, 0, st, g);
+            if (one) RK_LAUNCH((k_qg_combine<2, true>), dim3(cblocks), block, 0, st, g);
+            else RK_LAUNCH((k_qg_combine<2, false>), dim3(cblocks), block, 0, st, g);
         } else if (split == 4) {
-            if (one) hipLaunchKernelGGL((k_qg_combine<4, true>), dim3(cblocks), block, 0, st, g);
-            else hipLaunchKernelGGL((k_qg_combine<4, false>), dim3(cblocks), block, 0, st, g);
+            if (one) RK_LAUNCH((k_qg_combine<4, true>), dim3(cblocks), block, 0, st, g);
+            else RK_LAUNCH((k_qg_combine<4, false>), dim3(cblocks), block, 0, st, g);
         } else {
-            if (one) hipLaunchKernelGGL((k_qg_combine<8, true>), dim3(cblocks), block, 0, st, g);
-            else hipLaunchKernelGGL((k_qg_combine<8, false>), dim3(cblocks), block, 0, st, g);
+            if (one) RK_LAUNCH((k_qg_combine<8, true>), dim3(cblocks), block, 0, st, g);
+            else RK_LAUNCH((k_qg_combine<8, false>), dim3(cblocks), block, 0, st, g);
         }
         HIP_OK(hipGetLastError());
         return true;
     }
     if (k64 && !g_qgemm_generic) {
         switch (wtype) {
-            case W_Q4_0: hipLaunchKernelGGL(k_qgemm_k64<W_Q4_0>, grid, block, 0, st, g); break;
-            case W_Q4_1: hipLaunchKernelGGL(k_qgemm_k64<W_Q4_1>, grid, block, 0, st, g); break;
-            case W_Q5_0: hipLaunchKernelGGL(k_qgemm_k64<W_Q5_0>, grid, block, 0, st, g); break;
-            case W_Q5_1: hipLaunchKernelGGL(k_qgemm_k64<W_Q5_1>, grid, block, 0, st, g); break;
-            case W_Q8_0: hipLaunchKernelGGL(k_qgemm_k64<W_Q8_0>, grid, block, 0, st, g); break;
+            case W_Q4_0: RK_LAUNCH(k_qgemm_k64<W_Q4_0>, grid, block, 0, st, g); break;
+            case W_Q4_1: RK_LAUNCH(k_qgemm_k64<W_Q4_1>, grid, block, 0, st, g); break;
+            case W_Q5_0: RK_LAUNCH(k_qgemm_k64<W_Q5_0>, grid, block, 0, st, g); break;
+            case W_Q5_1: RK_LAUNCH(k_qgemm_k64<W_Q5_1>, grid, block, 0, st, g); break;
+            case W_Q8_0: RK_LAUNCH(k_qgemm_k64<W_Q8_0>, grid, block, 0, st, g); break;
             default: fprintf(stderr, "rwkv: qgemm type %d unsupported\n", wtype); return false;
         }
         HIP_OK(hipGetLastError());
         return true;
     }
     switch (wtype) {
-        case W_Q4_0: hipLaunchKernelGGL(k_qgemm<W_Q4_0>, grid, block, 0, st, g); break;
-        case W_Q4_1: hipLaunchKernelGGL(k_qgemm<W_Q4_1>, grid, block, 0, st, g); break;
-        case W_Q5_0: hipLaunchKernelGGL(k_qgemm<W_Q5_0>, grid, block, 0, st, g); break;
-        case W_Q5_1: hipLaunchKernelGGL(k_qgemm<W_Q5_1>, grid, block, 0, st, g); break;
-        case W_Q8_0: hipLaunchKernelGGL(k_qgemm<W_Q8_0>, grid, block, 0, st, g); break;
+        case W_Q4_0: RK_LAUNCH(k_qgemm<W_Q4_0>, grid, block, 0, st, g); break;
+        case W_Q4_1: RK_LAUNCH(k_qgemm<W_Q4_1>, grid, block, 0, st, g); break;
+        case W_Q5_0: RK_LAUNCH(k_qgemm<W_Q5_0>, grid, block, 0, st, g); break;
+        case W_Q5_1: RK_LAUNCH(k_qgemm<W_Q5_1>, grid, block, 0, st, g); break;
+        case W_Q8_0: RK_LAUNCH(k_qgemm<W_Q8_0>, grid, block, 0, st, g); break;
         default: fprintf(stderr, "rwkv: qgemm type %d unsupported\n", wtype); return false;
     }
     HIP_OK(hipGetLastError());

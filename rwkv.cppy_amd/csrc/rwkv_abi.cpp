@@ -325,17 +325,22 @@ RWKV_API const char * rwkv_get_system_info_string(void) {
 // ------------------------------------------------------------------ additive extensions
 
 RWKV_API bool rwkv_mi355x_state_upload(struct rwkv_context * ctx, const float * state) {
+    if (!ctx || !ctx->engine) return false;
     use_device(ctx);
     return ctx->engine->state_upload(state);
 }
 RWKV_API bool rwkv_mi355x_state_download(struct rwkv_context * ctx, float * state) {
+    if (!ctx || !ctx->engine || !state) return false;
     use_device(ctx);
     return ctx->engine->state_download(state);
 }
 
-RWKV_API size_t rwkv_mi355x_layer_state_len(const struct rwkv_context * ctx) { return ctx->engine->layer_state_len(); }
+RWKV_API size_t rwkv_mi355x_layer_state_len(const struct rwkv_context * ctx) {
+    return ctx && ctx->engine ? ctx->engine->layer_state_len() : 0;
+}
 
 static bool layer_range_ok(rwkv_context * ctx, uint32_t l0, uint32_t l1) {
+    if (!ctx || !ctx->engine) return false;
     const uint32_t n = ctx->model->dm.n_layer;
     CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, l0 < l1 && l1 <= n, "Bad layer range [%u, %u) for %u layers", l0, l1, n);
     return true;
@@ -363,12 +368,14 @@ RWKV_API bool rwkv_mi355x_state_download_layers(struct rwkv_context * ctx, float
 }
 
 RWKV_API void rwkv_mi355x_state_io_bytes(const struct rwkv_context * ctx, double out[2]) {
-    out[0] = ctx->engine->io_bytes_h2d();
-    out[1] = ctx->engine->io_bytes_d2h();
+    if (!out) return;
+    out[0] = ctx && ctx->engine ? ctx->engine->io_bytes_h2d() : 0.0;
+    out[1] = ctx && ctx->engine ? ctx->engine->io_bytes_d2h() : 0.0;
 }
 
 RWKV_API bool rwkv_mi355x_eval_device(struct rwkv_context * ctx, const uint32_t * tokens, size_t T, bool compute_logits,
                                       float * logits_out, bool sync) {
+    if (!ctx || !ctx->engine) return false;
     ctx->last_error = RWKV_ERROR_NONE;
     CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, T > 0 && tokens != nullptr, "Sequence length is 0");
     CTX_CHECK(ctx, RWKV_ERROR_CTX | RWKV_ERROR_UNSUPPORTED, false, !ctx->model->dm.partial(),
@@ -383,6 +390,7 @@ RWKV_API bool rwkv_mi355x_eval_device(struct rwkv_context * ctx, const uint32_t 
 static bool eval_layers(struct rwkv_context * ctx, const uint32_t * tokens, size_t T, uint32_t layer_begin,
                         uint32_t layer_end, float * x_dev, float * vfirst_dev, bool compute_logits, float * logits_out,
                         bool sync) {
+    if (!ctx || !ctx->engine) return false;
     ctx->last_error = RWKV_ERROR_NONE;
     CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, sync || logits_out == nullptr, "Asynchronous stage: logits stay on the device");
     const DeviceModel & dm = ctx->model->dm;
@@ -424,6 +432,7 @@ RWKV_API float * rwkv_mi355x_logits_device(struct rwkv_context * ctx) {
 
 static bool eval_batch(struct rwkv_context * ctx, const uint32_t * tokens, size_t n, const float * state_in,
                        float * state_out, float * logits_out, bool dev) {
+    if (!ctx || !ctx->engine) return false;
     ctx->last_error = RWKV_ERROR_NONE;
     const DeviceModel & dm = ctx->model->dm;
     CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, n > 0 && tokens != nullptr, "Batch is empty");
@@ -454,21 +463,28 @@ RWKV_API bool rwkv_mi355x_eval_batch_device(struct rwkv_context * ctx, const uin
 
 
 RWKV_API bool rwkv_mi355x_sync(struct rwkv_context * ctx) {
+    if (!ctx || !ctx->engine) return false;
     use_device(ctx);
     return ctx->engine->sync();
 }
 RWKV_API long long rwkv_mi355x_debug_buffer(struct rwkv_context * ctx, const char * name, void * out, size_t bytes) {
     return ctx && ctx->engine ? ctx->engine->debug_copy(name, out, bytes) : -1;
 }
-RWKV_API void * rwkv_mi355x_stream(struct rwkv_context * ctx) { return (void *)ctx->engine->stream(); }
-RWKV_API float * rwkv_mi355x_device_state(struct rwkv_context * ctx) { return ctx->engine->device_state(); }
+RWKV_API void * rwkv_mi355x_stream(struct rwkv_context * ctx) {
+    return ctx && ctx->engine ? (void *)ctx->engine->stream() : nullptr;
+}
+RWKV_API float * rwkv_mi355x_device_state(struct rwkv_context * ctx) {
+    return ctx && ctx->engine ? ctx->engine->device_state() : nullptr;
+}
 
 RWKV_API double rwkv_mi355x_weight_bytes(const struct rwkv_context * ctx, bool with_head) {
+    if (!ctx) return 0.0;
     const DeviceModel & dm = ctx->model->dm;
     return dm.layer_weight_bytes + (with_head ? dm.head_weight_bytes : 0.0);
 }
 
 RWKV_API double rwkv_mi355x_decode_bytes(const struct rwkv_context * ctx, bool with_logits) {
+    if (!ctx) return 0.0;
     const DeviceModel & dm = ctx->model->dm;
     // weights + per-token small parameters + state read and written + embedding row
     double b = dm.layer_weight_bytes + dm.small_param_bytes + 2.0 * (double)dm.state_len * 4.0;
@@ -478,11 +494,17 @@ RWKV_API double rwkv_mi355x_decode_bytes(const struct rwkv_context * ctx, bool w
 }
 
 RWKV_API double rwkv_mi355x_matmul_flops_per_token(const struct rwkv_context * ctx, bool with_head) {
+    if (!ctx) return 0.0;
     const DeviceModel & dm = ctx->model->dm;
     return dm.layer_flops + (with_head ? dm.head_flops : 0.0);
 }
 
 RWKV_API void rwkv_mi355x_arch(const struct rwkv_context * ctx, int64_t out[4]) {
+    if (!out) return;
+    if (!ctx) {
+        out[0] = out[1] = out[2] = out[3] = 0;
+        return;
+    }
     const DeviceModel & dm = ctx->model->dm;
     out[0] = dm.major;
     out[1] = dm.minor;
@@ -490,11 +512,14 @@ RWKV_API void rwkv_mi355x_arch(const struct rwkv_context * ctx, int64_t out[4]) 
     out[3] = dm.S;
 }
 
-RWKV_API void rwkv_mi355x_set_kernel_timing(struct rwkv_context * ctx, bool on) { ctx->engine->set_timing(on); }
+RWKV_API void rwkv_mi355x_set_kernel_timing(struct rwkv_context * ctx, bool on) {
+    if (ctx && ctx->engine) ctx->engine->set_timing(on);
+}
 
 RWKV_API int rwkv_mi355x_kernel_stats(struct rwkv_context * ctx, int index, char * name, size_t name_len,
                                       long long * launches, double * total_ms, double * total_bytes,
                                       double * total_flops) {
+    if (!ctx || !ctx->engine) return 0;
     const auto & st = ctx->engine->stats();
     if (index < 0 || index >= (int)st.size()) return (int)st.size();
     const KernelStat & k = st[index];

@@ -98,9 +98,10 @@ def pipeline_eval_sequence(stage_fn: StageFn, tokens: Sequence[int], chunk: int,
     return logits
 
 
-def layer_state_len(n_embed: int, arch_major: int, head_size: int = 64) -> int:
+def layer_state_len(n_embed: int, arch_major: int, head_size: int) -> int:
     """Floats of one layer's state in the host layout (rwkv_graph.inc:545-606): v4 five [C] vectors,
-    v5+ token shifts [2][C] plus the heads' [H][S][S] wkv state."""
+    v5+ token shifts [2][C] plus the heads' [H][S][S] wkv state.  For a library context use
+    LibraryStage.layer_len (rwkv_mi355x_layer_state_len), the layout the library actually uses."""
     return 5 * n_embed if arch_major == 4 else n_embed * (2 + head_size)
 
 
@@ -197,6 +198,11 @@ class LibraryStage:
         library.library.rwkv_mi355x_arch(ctx.ptr, arch)
         return cls(library, ctx, library.library.rwkv_get_n_vocab(ctx.ptr), int(arch[0]), async_=async_)
 
+    @property
+    def layer_len(self) -> int:
+        """Floats of one layer's state slice, from the library (Engine::layer_state_len)."""
+        return int(self.lib.library.rwkv_mi355x_layer_state_len(self.ctx.ptr))
+
     def reset_state(self, state: Optional[np.ndarray] = None) -> None:
         ptr = None if state is None else state.ctypes.data
         if not self.lib.library.rwkv_mi355x_state_upload(self.ctx.ptr, ptr):
@@ -210,7 +216,7 @@ class LibraryStage:
         fresh), rwkv_mi355x_state_upload_layers."""
         if part is not None:
             part = np.ascontiguousarray(part, dtype=np.float32)
-            n = (l1 - l0) * self.lib.library.rwkv_mi355x_layer_state_len(self.ctx.ptr)
+            n = (l1 - l0) * self.layer_len
             if part.size != n:
                 raise ValueError(f'slice has {part.size} floats, expected {n}')
         ok = self.lib.library.rwkv_mi355x_state_upload_layers(self.ctx.ptr, None if part is None else part.ctypes.data,
@@ -219,7 +225,7 @@ class LibraryStage:
             raise ValueError(f'state upload of layers [{l0}, {l1}) failed')
 
     def download_state_slice(self, l0: int, l1: int) -> np.ndarray:
-        n = (l1 - l0) * self.lib.library.rwkv_mi355x_layer_state_len(self.ctx.ptr)
+        n = (l1 - l0) * self.layer_len
         out = np.empty(n, np.float32)
         if not self.lib.library.rwkv_mi355x_state_download_layers(self.ctx.ptr, out.ctypes.data, l0, l1):
             raise ValueError(f'state download of layers [{l0}, {l1}) failed')

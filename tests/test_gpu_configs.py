@@ -155,3 +155,30 @@ def test_v6_1b6_width_1024_tokens(cfg_dir):
     assert_bits_equal(lg, glg, 'T=1024 logits')
     assert_bits_equal(st, gst, 'T=1024 state')
     m.free()
+
+
+def test_v6_decode_handoff_many_tokens(cfg_dir):
+    """The fused v6 decode launch (mv_att6f.hip: r, k, v, g and decay-LoRA rows + per-head attention,
+    an in-launch granule hand-off per head) at the v6-1B6 width over many tokens: serial decode equals
+    one sequence evaluation bit for bit (the sequence path has no hand-off), and afterwards every
+    granule is cleared, the reader counter re-armed and the timeout flag clear."""
+    import ctypes
+    path = cfg_model(cfg_dir, 'v6-1b6-q4_0')
+    toks = [int(t) for t in np.random.default_rng(12).integers(0, VOCAB, 48)]
+    m = RWKVModel(library(), path)
+    lg, st = gpu_serial(m, toks)
+    slg, sst = m.eval_sequence(toks, None, use_numpy=True)
+    assert_bits_equal(lg, slg, 'decode vs sequence logits')
+    assert_bits_equal(st, sst, 'decode vs sequence state')
+    words = np.ones(256, np.uint32)
+    n = library().library.rwkv_mi355x_debug_buffer(m._ctx.ptr, b'handoff', words.ctypes.data_as(ctypes.c_void_p),
+                                                   words.nbytes)
+    assert n == words.nbytes
+    assert not words.any(), f'hand-off words not re-armed / timeout: {np.nonzero(words)[0][:8]}'
+    C = 2048
+    gran = np.ones(4 * C + 128, np.uint64)
+    n = library().library.rwkv_mi355x_debug_buffer(m._ctx.ptr, b'granules', gran.ctypes.data_as(ctypes.c_void_p),
+                                                   gran.nbytes)
+    assert n == gran.nbytes
+    assert not gran.any(), f'hand-off granules not cleared: {np.nonzero(gran)[0][:8]}'
+    m.free()

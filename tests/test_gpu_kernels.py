@@ -113,8 +113,9 @@ def test_matmul_kernel(fmt, M, K, T):
 
 @pytest.mark.parametrize('fmt', ['Q4_0', 'Q4_1', 'Q5_0', 'Q5_1', 'Q8_0'])
 @pytest.mark.parametrize('M,K,T', [(2048, 2048, 70), (100, 96, 3), (64, 7168, 33), (160, 2048, 64), (72, 320, 9),
-                                   (2048, 64, 17), (40, 4096, 2)])
+                                   (2048, 64, 17), (40, 4096, 2), (64, 20480, 40), (96, 14336, 70)])
 def test_mfma_gemm_matches_matmul_bit_exact(fmt, M, K, T):
+    """K up to 20480 (a 14B-class FFN value width): the _1 formats' m*s pass at 9-16 blocks per class."""
     rng = np.random.default_rng(M * 3 + K * 5 + T)
     w = (rng.standard_normal((M, K)) / np.sqrt(K)).astype(np.float32)
     x = rng.standard_normal((T, K)).astype(np.float32)
@@ -147,7 +148,8 @@ def test_fmm_split_k_bit_exact(fmt, M, K, T, split):
 
 
 @pytest.mark.parametrize('fmt', ['Q4_0', 'Q4_1', 'Q5_0', 'Q5_1', 'Q8_0'])
-@pytest.mark.parametrize('M,K,T', [(2048, 2048, 64), (96, 7168, 40), (160, 2048, 128), (64, 768, 7), (2048, 64, 17)])
+@pytest.mark.parametrize('M,K,T', [(2048, 2048, 64), (96, 7168, 40), (160, 2048, 128), (64, 768, 7), (2048, 64, 17),
+                                   (64, 20480, 16)])
 @pytest.mark.parametrize('split', [1, 2, 4, 8])
 def test_mfma_gemm_split_k_bit_exact(fmt, M, K, T, split):
     """Split-K GEMM (the class tree in 4 or 8 subtrees on as many workgroups, k_qg_combine adding the

@@ -128,6 +128,9 @@ def main():
     ap.add_argument('--batch', default='8,32,64,128', help='batched decode sizes (contexts per step; "" = none)')
     ap.add_argument('--batch-steps', type=int, default=32)
     ap.add_argument('--model-dir', default=os.environ.get('RWKV_BENCH_DIR', '/tmp/rwkv_bench'))
+    ap.add_argument('--roofline-only', action='store_true',
+                    help='only the roofline timing pass (eager decode steps, per-dispatch events): the run whose '
+                         'rocprofv3 trace must reproduce the line\'s roofline (profiles/)')
     ap.add_argument('--decode-only', action='store_true',
                     help='only the timed device-resident decode (warmup + steps, graph replays): the run a '
                          'rocprofv3 kernel trace of the decode chain is taken from (profiles/)')
@@ -205,7 +208,7 @@ def main():
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.warmup, args.warmup + args.steps):
+    for i in range(args.warmup, args.warmup + (0 if args.roofline_only else args.steps)):
         step(i)
     L.rwkv_mi355x_sync(ctx.ptr)
     torch.cuda.synchronize()
@@ -216,7 +219,7 @@ def main():
     ms_per_step = elapsed * 1e3 / args.steps
     value = world * args.steps / elapsed
     log(f'decode: {ms_per_step * 1e3:.1f} us/token, {value:.1f} tok/s aggregate over {world} GPU(s)')
-    if args.decode_only:
+    if args.decode_only or args.roofline_only:
         args.batch, args.seq_reps, args.abi_steps, args.skip_cpu = '', 0, 0, True
 
     # ---------------- batched multi-context decode ----------------
@@ -405,9 +408,11 @@ def main():
             'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic,
             'avg_launch_us': round(avg_us, 3), 'algorithmic_bytes_per_launch': round(bytes_per_launch),
             'launches_per_token': round(p_launches / timing_steps, 1),
-            'method': 'per-dispatch HIP events (hipExtLaunchKernelGGL start/stop) on the engine stream, '
-                      f'{timing_steps} eager decode steps; profiles/*decode_only* holds the rocprofv3 trace '
-                      'of the graph-replayed decode for the same kernels',
+            'method': 'per-dispatch HIP events (hipExtLaunchKernelGGL start/stop: the dispatch timestamps '
+                      'rocprofv3 reports) on the engine stream over '
+                      f'{timing_steps} eager decode steps; profiles/ holds the rocprofv3 kernel trace of this pass '
+                      '(bench.py --roofline-only, reproduces these averages) and of the graph-replayed decode '
+                      '(bench.py --decode-only, which the profiler itself slows down)',
             'per_kernel': {k['name']: {'launches_per_token': round(k['launches'] / timing_steps, 1),
                                        'avg_us': round(k['ms'] / k['launches'] * 1e3, 3),
                                        'GBps': round(k['bytes'] / (k['ms'] * 1e-3) / 1e9, 1) if k['bytes'] else None}

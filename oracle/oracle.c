@@ -554,10 +554,22 @@ static double ln_tree8(const float * v) {
     const double b = ((double)v[4] + (double)v[5]) + ((double)v[6] + (double)v[7]);
     return a + b;
 }
+/* The device's one-pass LayerNorm statistics (device_common.hpp ln_chunk_sums / ln_finish): per
+ * 512-element chunk, lane l's 8 elements and their exact fp64 squares summed as pairwise trees,
+ * the 64 lanes folded by wave_sum63's tree, chunks added in order; mean = S1/n,
+ * var = max(S2/n - mean^2, 0) in fp64, each rounded to f32 once.  ggml_norm's second pass sums
+ * fp32-rounded (x - mean)^2 instead: the same quantity up to those roundings (variant 0). */
+static double ln_tree8_sq(const float v[8]) {
+    double q[8];
+    for (int j = 0; j < 8; j++) q[j] = (double)v[j] * (double)v[j];
+    const double a = (q[0] + q[1]) + (q[2] + q[3]);
+    const double b = (q[4] + q[5]) + (q[6] + q[7]);
+    return a + b;
+}
 static void ln_stats_gpu(const float * x, int64_t n, float eps, float * mean_out, float * scale_out) {
-    double lanes[64];
+    double lanes[64], lanes2[64];
     const int64_t nc = (n + 511) / 512;
-    double s = 0.0;
+    double s = 0.0, q = 0.0;
     for (int64_t c = 0; c < nc; c++) {
         for (int l = 0; l < 64; l++) {
             float v[8];
@@ -566,26 +578,16 @@ static void ln_stats_gpu(const float * x, int64_t n, float eps, float * mean_out
                 v[j] = k < n ? x[k] : 0.0f;
             }
             lanes[l] = ln_tree8(v);
+            lanes2[l] = ln_tree8_sq(v);
         }
         s += tree_d(lanes, 64);
+        q += tree_d(lanes2, 64);
     }
-    const float mean = (float)(s / (double)n);
-    double q = 0.0;
-    for (int64_t c = 0; c < nc; c++) {
-        for (int l = 0; l < 64; l++) {
-            float v[8];
-            for (int j = 0; j < 8; j++) {
-                const int64_t k = c * 512 + 8 * l + j;
-                const float d = (k < n ? x[k] : 0.0f) - mean;
-                v[j] = k < n ? d * d : 0.0f;
-            }
-            lanes[l] = ln_tree8(v);
-        }
-        q += tree_d(lanes, 64);
-    }
-    const float var = (float)(q / (double)n);
-    *mean_out = mean;
-    *scale_out = 1.0f / sqrtf(var + eps);
+    const double md = s / (double)n;
+    double vd = q / (double)n - md * md;
+    vd = vd > 0.0 ? vd : 0.0;
+    *mean_out = (float)md;
+    *scale_out = 1.0f / sqrtf((float)vd + eps);
 }
 
 /* Exact integer dot of 32 int8 pairs (|w| <= 128, |x| <= 127: the Q8 activation quantizer's

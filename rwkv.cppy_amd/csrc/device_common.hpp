@@ -412,13 +412,17 @@ __device__ __forceinline__ double group_tree_sum_d(double v, int width) {
     return v;
 }
 
-// LayerNorm statistics (ggml_norm semantics: fp64 sums, two passes, population variance) in
-// the CHUNK association that every LayerNorm on the device and the oracle's GPU variant share:
+// LayerNorm statistics (ggml_norm: fp64 accumulation, population variance) in ONE pass, in the
+// CHUNK association that every LayerNorm on the device and the oracle's GPU variant share:
 // x is cut into 512-element chunks; lane l of a chunk owns its 8 consecutive elements 8l..8l+7
-// (two 16-byte loads), summed as an fp64 pairwise tree; the chunk's 64 lane sums fold by
-// wave_sum63's tree; chunk sums are added in ascending chunk order.  Elements past K count as
-// zeros (K % 8 == 0).  The decode prologues spread the chunks over several waves and exchange
-// the chunk sums through LDS; the sequence kernels walk the chunks in one wave -- same bits.
+// (two 16-byte loads), whose values and exact squares ((double)x * (double)x: 48 significant
+// bits) are summed as fp64 pairwise trees; a chunk's 64 lane sums fold by wave_sum63's tree;
+// chunk sums are added in ascending chunk order.  Elements past K count as zeros (K % 8 == 0).
+// mean = S1 / K, var = max(S2 / K - mean_d^2, 0) in fp64, rounded to f32 once (ln_finish).
+// ggml's second pass sums fp32-rounded (x - mean_f32)^2; this one-pass form is the same
+// quantity without those roundings (every statistic needs one exchange instead of two).  The
+// decode prologues spread the chunks over several waves and exchange the chunk sums through
+// LDS; the sequence kernels walk the chunks in one wave -- same bits.
 constexpr int LN_CHUNK = 512;
 
 __device__ __forceinline__ double ln_tree8(const float (&v)[8]) {
@@ -426,27 +430,31 @@ __device__ __forceinline__ double ln_tree8(const float (&v)[8]) {
     const double b = ((double)v[4] + (double)v[5]) + ((double)v[6] + (double)v[7]);
     return a + b;
 }
-// sum of one chunk's elements (every lane gets it); x = this lane's 8 elements
-__device__ __forceinline__ double ln_chunk_sum(const float (&x)[8], bool valid) {
+__device__ __forceinline__ double ln_tree8_sq(const float (&v)[8]) {
+    double q[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) q[j] = (double)v[j] * (double)v[j];
+    const double a = (q[0] + q[1]) + (q[2] + q[3]);
+    const double b = (q[4] + q[5]) + (q[6] + q[7]);
+    return a + b;
+}
+// sums of one chunk's elements and squares (every lane gets them); x = this lane's 8 elements
+__device__ __forceinline__ void ln_chunk_sums(const float (&x)[8], bool valid, double & s1, double & s2) {
     float v[8];
 #pragma unroll
     for (int j = 0; j < 8; j++) v[j] = valid ? x[j] : 0.0f;
-    return wave_allsum_d(ln_tree8(v));
+    const double a = ln_tree8(v), b = ln_tree8_sq(v);  // two independent DPP chains
+    s1 = wave_allsum_d(a);
+    s2 = wave_allsum_d(b);
 }
-// sum of one chunk's (x - mean)^2
-__device__ __forceinline__ double ln_chunk_sq(const float (&x)[8], bool valid, float mean) {
-    float v[8];
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-        const float d = x[j] - mean;
-        v[j] = valid ? d * d : 0.0f;
-    }
-    return wave_allsum_d(ln_tree8(v));
+__device__ __forceinline__ void ln_finish(double s1, double s2, int K, float eps, float & mean, float & scale) {
+    const double md = div_count(s1, K);
+    double vd = div_count(s2, K) - md * md;
+    vd = vd > 0.0 ? vd : 0.0;
+    mean = (float)md;
+    scale = 1.0f / sqrtf((float)vd + eps);
 }
-__device__ __forceinline__ float ln_scale(double sq, int K, float eps) {
-    const float var = (float)div_count(sq, K);
-    return 1.0f / sqrtf(var + eps);
-}
+
 
 __device__ __forceinline__ void ln_load8(float (&v)[8], const float * x, int k, int K) {
     const float * p = x + min(k, K - 8);
@@ -460,50 +468,38 @@ template <int NC>
 __device__ __forceinline__ void ln_stats_regs(const float (&x)[NC][8], int nc, int K, float eps, float & mean,
                                               float & scale) {
     const int lane = threadIdx.x & 63;
-    double cs[NC];
+    double c1[NC], c2[NC];
 #pragma unroll
-    for (int c = 0; c < NC; c++) cs[c] = c < nc ? ln_chunk_sum(x[c], c * LN_CHUNK + lane * 8 < K) : 0.0;
-    double s = 0.0;
-#pragma unroll
-    for (int c = 0; c < NC; c++)
-        if (c < nc) s += cs[c];
-    mean = (float)div_count(s, K);
-#pragma unroll
-    for (int c = 0; c < NC; c++) cs[c] = c < nc ? ln_chunk_sq(x[c], c * LN_CHUNK + lane * 8 < K, mean) : 0.0;
-    double q = 0.0;
+    for (int c = 0; c < NC; c++) {
+        c1[c] = c2[c] = 0.0;
+        if (c < nc) ln_chunk_sums(x[c], c * LN_CHUNK + lane * 8 < K, c1[c], c2[c]);
+    }
+    double s1 = 0.0, s2 = 0.0;
 #pragma unroll
     for (int c = 0; c < NC; c++)
-        if (c < nc) q += cs[c];
-    scale = ln_scale(q, K, eps);
+        if (c < nc) s1 += c1[c], s2 += c2[c];
+    ln_finish(s1, s2, K, eps, mean, scale);
 }
 
-// One wave, any K (x 16-byte aligned): the chunks in order, kept in registers for the second
-// pass up to 4 chunks (K <= 2048), reloaded beyond.
+// One wave, any K (x 16-byte aligned): the chunks in ascending order, 4 in flight at a time.
 __device__ inline void ln_stats_wave(const float * x, int K, float eps, float & mean, float & scale) {
     const int lane = threadIdx.x & 63, nc = (K + LN_CHUNK - 1) / LN_CHUNK;
-    float v[4][8];
+    double s1 = 0.0, s2 = 0.0;
+    for (int c0 = 0; c0 < nc; c0 += 4) {
+        float v[4][8];
 #pragma unroll
-    for (int c = 0; c < 4; c++) ln_load8(v[c], x, min(c, nc - 1) * LN_CHUNK + lane * 8, K);
-    double s = 0.0;
+        for (int c = 0; c < 4; c++) ln_load8(v[c], x, min(c0 + c, nc - 1) * LN_CHUNK + lane * 8, K);
+        double c1[4], c2[4];
 #pragma unroll
-    for (int c = 0; c < 4; c++)
-        if (c < nc) s += ln_chunk_sum(v[c], c * LN_CHUNK + lane * 8 < K);
-    for (int c = 4; c < nc; c++) {
-        float t[8];
-        ln_load8(t, x, c * LN_CHUNK + lane * 8, K);
-        s += ln_chunk_sum(t, c * LN_CHUNK + lane * 8 < K);
+        for (int c = 0; c < 4; c++) {
+            c1[c] = c2[c] = 0.0;
+            if (c0 + c < nc) ln_chunk_sums(v[c], (c0 + c) * LN_CHUNK + lane * 8 < K, c1[c], c2[c]);
+        }
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+            if (c0 + c < nc) s1 += c1[c], s2 += c2[c];
     }
-    mean = (float)div_count(s, K);
-    double q = 0.0;
-#pragma unroll
-    for (int c = 0; c < 4; c++)
-        if (c < nc) q += ln_chunk_sq(v[c], c * LN_CHUNK + lane * 8 < K, mean);
-    for (int c = 4; c < nc; c++) {
-        float t[8];
-        ln_load8(t, x, c * LN_CHUNK + lane * 8, K);
-        q += ln_chunk_sq(t, c * LN_CHUNK + lane * 8 < K, mean);
-    }
-    scale = ln_scale(q, K, eps);
+    ln_finish(s1, s2, K, eps, mean, scale);
 }
 
 __device__ __forceinline__ void ln_stats_any(const float * x, int K, float eps, float & mean, float & scale) {

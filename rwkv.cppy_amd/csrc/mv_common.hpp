@@ -409,29 +409,24 @@ __device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, int b0, in
 #endif
             float mean = 0.0f, scale = 0.0f;
             if constexpr (SRCK == MVK_LN) {
-                // LayerNorm statistics in the chunk association (device_common.hpp): each wave
-                // sums its chunks, the chunk sums meet in LDS (two barriers the dot waves join)
+                // LayerNorm statistics in the chunk association (device_common.hpp, one pass):
+                // each wave sums its chunks and their squares, the chunk sums meet in LDS (one
+                // barrier the dot waves join)
                 __shared__ double ln_part[2][8];
 #pragma unroll
                 for (int q = 0; q < LCW; q++)
                     if (pw + q * NW < nch) {
-                        const double cs = ln_chunk_sum(ci[q].x, kc[q] < K);
-                        if (lane == 0) ln_part[0][pw + q * NW] = cs;
+                        double c1, c2;
+                        ln_chunk_sums(ci[q].x, kc[q] < K, c1, c2);
+                        if (lane == 0) {
+                            ln_part[0][pw + q * NW] = c1;
+                            ln_part[1][pw + q * NW] = c2;
+                        }
                     }
                 asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-                double sm = 0.0;
-                for (int c = 0; c < nch; c++) sm += ln_part[0][c];
-                mean = (float)div_count(sm, K);
-#pragma unroll
-                for (int q = 0; q < LCW; q++)
-                    if (pw + q * NW < nch) {
-                        const double cs = ln_chunk_sq(ci[q].x, kc[q] < K, mean);
-                        if (lane == 0) ln_part[1][pw + q * NW] = cs;
-                    }
-                asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-                double sq = 0.0;
-                for (int c = 0; c < nch; c++) sq += ln_part[1][c];
-                scale = ln_scale(sq, K, 1e-5f);
+                double s1 = 0.0, s2 = 0.0;
+                for (int c = 0; c < nch; c++) s1 += ln_part[0][c], s2 += ln_part[1][c];
+                ln_finish(s1, s2, K, 1e-5f, mean, scale);
             }
 #ifdef RWKV_STAMP
             if (pw == 0 && stamp_x && lane == 0) stamp_x[1] = __builtin_amdgcn_s_memrealtime() + (scale == 1.2345f);
@@ -497,9 +492,8 @@ __device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, int b0, in
 #pragma unroll
         for (int r = 0; r < R; r++) w[r][u] = load_unit<WF>(W, rows[r], u, lane);
     if constexpr (SRCK == MVK_LN) {
-        // the prologue's two statistics barriers, right after the weight issue (no wait on
-        // this wave's loads; the epilogue operands are fetched after them)
-        asm volatile("s_barrier" ::: "memory");
+        // the prologue's statistics barrier, right after the weight issue (no wait on this
+        // wave's loads; the epilogue operands are fetched after it)
         asm volatile("s_barrier" ::: "memory");
     }
     // epilogue operands: !EMIT lane r < R runs row row0 + r's epilogue; EMIT thread tid < RW row tid
@@ -558,6 +552,9 @@ __device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, int b0, in
 #pragma unroll
             for (int r = 0; r < R; r++)
                 if (lane == 63) red[wave * R + r] = s[r];
+#ifdef RWKV_STAMP
+            if (wave == 0 && stamp_x && lane == 0) stamp_x[3] = __builtin_amdgcn_s_memrealtime() + (s[0] == 1.2345f);
+#endif
             __syncthreads();
             PROBE(2);
             if (tid < RW) {

@@ -56,8 +56,7 @@ __global__ __launch_bounds__(512) void k_v6_maa_dec(MaaDec a) {
         for (int u = 0; u < U; u++)
 #pragma unroll
             for (int r = 0; r < R; r++) w[r][u] = load_unit<WF, false>(W, rows[r], u, lane);
-        // the prologue's two LayerNorm statistics barriers, right after the weight issue
-        asm volatile("s_barrier" ::: "memory");
+        // the prologue's LayerNorm statistics barrier, right after the weight issue
         asm volatile("s_barrier" ::: "memory");
         // this thread's mix channel: W2 column, carry, maa
         const int c = blockIdx.x * CPW + tid;
@@ -135,29 +134,24 @@ __global__ __launch_bounds__(512) void k_v6_maa_dec(MaaDec a) {
     }
     asm volatile("s_barrier" ::: "memory");  // input loads issued ahead of the weight stream
     if (pw == 0) STAMP_X(0);
-    // LayerNorm statistics, chunk association (device_common.hpp); the dot waves join the two
-    // exchange barriers
+    // LayerNorm statistics, chunk association, one pass (device_common.hpp); the dot waves join
+    // the exchange barrier
     __shared__ double ln_part[2][8];
 #pragma unroll
     for (int q = 0; q < LCW; q++)
         if (pw + 4 * q < nch) {
-            const double cs = ln_chunk_sum(ci[q].x, kc[q] < K);
-            if (lane == 0) ln_part[0][pw + 4 * q] = cs;
+            double c1, c2;
+            ln_chunk_sums(ci[q].x, kc[q] < K, c1, c2);
+            if (lane == 0) {
+                ln_part[0][pw + 4 * q] = c1;
+                ln_part[1][pw + 4 * q] = c2;
+            }
         }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    double sm = 0.0;
-    for (int c = 0; c < nch; c++) sm += ln_part[0][c];
-    const float mean = (float)div_count(sm, K);
-#pragma unroll
-    for (int q = 0; q < LCW; q++)
-        if (pw + 4 * q < nch) {
-            const double cs = ln_chunk_sq(ci[q].x, kc[q] < K, mean);
-            if (lane == 0) ln_part[1][pw + 4 * q] = cs;
-        }
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    double sq = 0.0;
-    for (int c = 0; c < nch; c++) sq += ln_part[1][c];
-    const float scale = ln_scale(sq, K, 1e-5f);
+    double s1 = 0.0, s2 = 0.0;
+    for (int c = 0; c < nch; c++) s1 += ln_part[0][c], s2 += ln_part[1][c];
+    float mean, scale;
+    ln_finish(s1, s2, K, 1e-5f, mean, scale);
 #ifdef RWKV_STAMP
     if (pw == 0 && lane == 0) stamp_x_[1] = __builtin_amdgcn_s_memrealtime() + (scale == 1.2345f);
 #endif

@@ -165,7 +165,9 @@ def main():
         return float(t.item())
 
     import rwkv_cpp
-    lib = rwkv_cpp.RWKVSharedLibrary(os.path.join(REPO, 'rwkv.cppy_amd', 'build', 'librwkv.so'))
+    # RWKV_MI355X_BENCH_LIB: an alternative build of the same library for A/B runs (tools/r4_quick.sh)
+    lib = rwkv_cpp.RWKVSharedLibrary(os.environ.get('RWKV_MI355X_BENCH_LIB')
+                                     or os.path.join(REPO, 'rwkv.cppy_amd', 'build', 'librwkv.so'))
     L = lib.library
     arch, V, C, NL, F, fmt, label = CONFIGS[args.config]
     os.makedirs(args.model_dir, exist_ok=True)

@@ -92,6 +92,21 @@ RWKV_API float * rwkv_mi355x_logits_device(struct rwkv_context * ctx);
 RWKV_API struct rwkv_context * rwkv_mi355x_init_from_file_layers(const char * path, uint32_t n_threads,
                                                                  uint32_t layer_begin, uint32_t layer_end);
 
+/* The layer pipeline behind the reference entry points: n_stages stage contexts in
+ * this process, stage i on GPU devices[i] (NULL: i modulo the device count) holding the contiguous
+ * layers [i*L/P .. (i+1)*L/P) (earlier stages take the extra layers; the embedding on stage 0, the
+ * head on the last).  rwkv_eval / rwkv_eval_sequence[_in_chunks] on the returned context (stage 0)
+ * run every stage: the sequence is cut into chunks of >= 256 tokens, chunk c's residual stream
+ * (and v7's v_first) crosses from stage s to s+1 by a peer copy over xGMI while stage s starts
+ * chunk c+1; results are bit-identical to a single-GPU context.  rwkv_clone_context clones the
+ * pipeline (same stages and GPUs, weights shared).  The same context is what rwkv_init_from_file
+ * returns when RWKV_MI355X_PIPELINE=P (P >= 2) is set (devices: RWKV_MI355X_PIPELINE_DEVICES, a
+ * comma list).  The device-resident entry points refuse a pipeline context (it is partial). */
+RWKV_API struct rwkv_context * rwkv_mi355x_init_pipeline(const char * path, uint32_t n_threads, int n_stages,
+                                                         const int * devices);
+/* Stages of a context: P for a pipeline context, 1 otherwise (0 for NULL). */
+RWKV_API int rwkv_mi355x_pipeline_stages(const struct rwkv_context * ctx);
+
 /* Batched decode (multi-context serving): n_contexts independent sequences of this
  * model advance ONE token each in one pass -- the rwkv_eval of each context, with every weight byte
  * read once per step for all of them (the reference runs clones side by side instead:

@@ -191,6 +191,15 @@ __device__ __forceinline__ void store32(const ActBuf & a, int t, int k, const Q3
     }
 }
 
+// An activation record's fields forced into registers at this point (the kernarg loads issued and
+// waited here, at the kernel's start, instead of on the critical path where they are first used).
+__device__ __forceinline__ void pin_act(const ActBuf & a) {
+    asm volatile("" ::"s"(a.q), "s"(a.d));
+    asm volatile("" ::"s"(a.s), "s"(a.qsum));
+    asm volatile("" ::"s"(a.h), "s"(a.f));
+    asm volatile("" ::"s"(a.tq), "s"(a.fmt), "s"(a.K), "s"(a.tiled));
+}
+
 // Emit one element per lane into an activation buffer.  The 32 lanes of each half-wave must
 // hold the 32 consecutive elements of one block (k & 31 == lane & 31) of the same row t, and
 // all 32 must call (block-uniform control flow).

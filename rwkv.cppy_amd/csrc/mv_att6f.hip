@@ -143,6 +143,15 @@ __global__ __launch_bounds__(320) void k_v6_att_fused(Att6Fused a) {
     const int jq = lane & 15, kk = lane >> 4;
     unsigned long long * const gdl = a.gran + 4 * (size_t)C;
     STAMP_BEGIN();
+    // the reducer's late scalars (Wo input record, hand-off words, eps) in SGPRs now
+    const ActBuf yq = at.yq;
+    unsigned * const cnt = a.cnt;
+    unsigned * const err = a.err;
+    const float eps = at.eps;
+    if (red) {
+        pin_act(yq);
+        asm volatile("" ::"s"(cnt), "s"(err), "s"(eps));
+    }
     // ---- the reducer's head operands first (state rows, per-channel vectors, decay-tail weights):
     // they stream in with this workgroup's own weight rows
     float4 st[4];
@@ -191,7 +200,7 @@ __global__ __launch_bounds__(320) void k_v6_att_fused(Att6Fused a) {
         unsigned long long * g = a.gran + (size_t)wave * C + c0 + lane;
         bool live[1] = {true};
         float v[1];
-        gran_sweep<1>(g, 0, live, v, a.err);
+        gran_sweep<1>(g, 0, live, v, err);
         float * dst = wave == 0 ? sr : wave == 1 ? sk : wave == 2 ? sv : sg;
         dst[lane] = v[0];
         gran_clear(g);
@@ -202,15 +211,15 @@ __global__ __launch_bounds__(320) void k_v6_att_fused(Att6Fused a) {
     } else {
         bool live[2] = {lane < D, lane + 64 < D};
         float v[2];
-        gran_sweep<2>(gdl + lane, 64, live, v, a.err);
+        gran_sweep<2>(gdl + lane, 64, live, v, err);
         // every head reads the decay values: the last reader clears them
         unsigned n = 0;
-        if (lane == 0) n = addu(a.cnt, 1u);
+        if (lane == 0) n = addu(cnt, 1u);
         n = (unsigned)__shfl((int)n, 0);
         if (n == (unsigned)H - 1) {
             if (lane < D) gran_clear(gdl + lane);
             if (lane + 64 < D) gran_clear(gdl + lane + 64);
-            if (lane == 0) stu_sc1(a.cnt, 0u);
+            if (lane == 0) stu_sc1(cnt, 0u);
         }
         const ActBuf act = lds_act(smem, act_fmt_for(WD), D);
         if (lane < D) emit32(act, 0, lane, v[0]);  // lanes 0..31 / 32..63: whole quantization blocks
@@ -263,12 +272,12 @@ __global__ __launch_bounds__(320) void k_v6_att_fused(Att6Fused a) {
         const float d = x - mean;
         const double s2 = group_tree_sum_d((double)(d * d), S);
         const float var = (float)div_count(s2, S);
-        const float scale = 1.0f / sqrtf(var + at.eps);
+        const float scale = 1.0f / sqrtf(var + eps);
         float o = d * scale;
         o = o * lnw_c;
         o = o + lnb_c;
         o = o * sg[lane];
-        emit32(at.yq, 0, c0 + lane, o);
+        emit32(yq, 0, c0 + lane, o);
     }
     STAMP_END(6);
 }

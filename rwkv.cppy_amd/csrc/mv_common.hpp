@@ -359,15 +359,14 @@ __device__ __forceinline__ float decay_row_thread(const DMat & W, int row, const
     return one ? tree_wave32(p) + tree_wave32(p2) : tree_wave32(p) + 0.0f;
 }
 
-// One workgroup = NW waves x R rows (RW = NW*R rows per row block).  E == 0: the input is an
-// activation buffer in global memory (SRC_ACT, NW = 4); E > 0: the prologue builds it in LDS
-// (SRC_F32 / SRC_LNMIX, K <= 64*NW*E; NW = 16 so the per-wave prologue work is short).
-// stride > 0: the workgroup walks row blocks wgi, wgi+stride, ... with one prologue.
-// Workgroup roles: waves 0..NW-1 stream the weights and do the dots (R rows each); for
-// prologue sources NW more waves build the activation image (LayerNorm statistics each for
-// itself, one 512-element chunk each, ...).  Separate waves keep the two load streams apart:
-// vmcnt is in order per wave, so a prologue wave never waits behind the weight stream and a
-// dot wave's weights are in flight from its first instruction.
+// One workgroup = NW waves (SRC_ACT) or 2 NW waves (prologue sources) x R rows each; RW rows per
+// row block.  stride > 0: the workgroup walks row blocks wgi, wgi+stride, ... with one prologue.
+// Prologue sources (SRC_F32 / SRC_LNMIX): waves NW..2NW-1 also build the activation image in LDS
+// (LayerNorm statistics, one 512-element chunk each, token shift, quantization); their input
+// loads go out first (issue-order barrier), their weight loads right behind them -- vmcnt is in
+// order per wave, so the LayerNorm waits only for the inputs -- and after the image is ready
+// every wave dots its own R rows: the rows of a block are spread over all 2 NW waves, so the
+// per-wave dot and reduction chains are half as long as with the image waves idle.
 template <int WF, int R, int U, int SRCK, int FORM, bool EMIT, int NW, int LNP>
 __device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, int b0, int stride, char * smem, float * red,
                                         unsigned long long * stamp_mid = nullptr,
@@ -375,43 +374,69 @@ __device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, int b0, in
     constexpr bool PRO = SRCK != MVK_ACT;
     // LayerNorm chunks per prologue wave held in registers: LNP 32 -> K <= 2048, 64 -> K <= 4096
     constexpr int LCW = LNP > 32 ? 2 : 1;
-    constexpr int RW = NW * R;
+    constexpr int NWT = PRO ? 2 * NW : NW;  // waves with rows
+    constexpr int RW = NWT * R;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const DMat & W = Ent.W;
     const int M = W.M, K = W.K;
     const int nblk = (M + RW - 1) / RW;
     const int units = mv_units(WF, K);
     PROBE(0);
+    // every scalar the epilogue needs, in SGPRs before anything waits: a kernarg field first read
+    // after the dots is a scalar-cache round trip on the kernel's critical path
+    const int epi = Ent.epi;
+    float * const ey = Ent.y;
+    ActBuf ao = Ent.act_out;
+    const bool emit_on = EMIT && Ent.emit && ao.fmt >= 0;
+    asm volatile("" ::"s"(epi), "s"(ey));
+    if constexpr (EMIT) pin_act(ao);
     ActBuf a;
+    const bool pro_wave = PRO && wave >= NW;
+    const int pw = wave - NW, nch = (K + LN_CHUNK - 1) / LN_CHUNK;
+    const bool write_carry = PRO && Ent.carry_out && (int)blockIdx.x == b0;  // one writer per entry
+    ChunkIn ci[LCW];
+    int kc[LCW];
+    float mean = 0.0f, scale = 0.0f;
     if constexpr (PRO) {
         a = lds_act(smem, act_fmt_for(WF), K);
-        if (wave >= NW) {
-            // ---- prologue wave: chunks pw, pw + NW (512 elements each, 8 per lane)
-            const int pw = wave - NW, nch = (K + LN_CHUNK - 1) / LN_CHUNK;
-            const bool write_carry = Ent.carry_out && wgi == (int)blockIdx.x - b0;
-            ChunkIn ci[LCW];
-            int kc[LCW];
+        if (pro_wave) {
+            // the image wave's inputs: chunks pw, pw + NW (512 elements each, 8 per lane)
 #pragma unroll
             for (int q = 0; q < LCW; q++) {
                 kc[q] = (pw + q * NW) * LN_CHUNK + lane * 8;
                 chunk_load<SRCK, FORM>(Ent, min(kc[q], K - 8), ci[q]);
             }
-
-            // issue order: the input loads above go out before the dot waves start the weight
-            // stream (they wait at this barrier), so they are not queued behind megabytes of
-            // weights in the memory system; no wait on the loads themselves here
-            asm volatile("s_barrier" ::: "memory");
+        } else {
+            // the weight pointers reach SGPRs before the issue-order barrier, so the stream starts
+            // right after it (a kernarg scalar load behind the barrier is a round trip in the path)
+            asm volatile("" ::"s"(W.qs), "s"(W.sc), "s"(W.qh));
+        }
+        // issue order: the image inputs go out before any weight stream starts, so they are not
+        // queued behind megabytes of weights in the memory system; no wait on them here
+        asm volatile("s_barrier" ::: "memory");
 #ifdef RWKV_STAMP
-            if (pw == 0 && stamp_x) {
-                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-                if (lane == 0) stamp_x[0] = __builtin_amdgcn_s_memrealtime();
-            }
+        if (pw == 0 && stamp_x) {
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            if (lane == 0) stamp_x[0] = __builtin_amdgcn_s_memrealtime();
+        }
 #endif
-            float mean = 0.0f, scale = 0.0f;
+    }
+    // ---- this wave's weight units (HBM), all in flight before anything waits
+    int row0 = wgi * RW + wave * R;
+    int rows[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) rows[r] = min(row0 + r, M - 1);
+    WBlk w[R][U];
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+        for (int r = 0; r < R; r++) w[r][u] = load_unit<WF>(W, rows[r], u, lane);
+    if constexpr (PRO) {
+        if (pro_wave) {
             if constexpr (SRCK == MVK_LN) {
-                // LayerNorm statistics in the chunk association (device_common.hpp, one pass):
-                // each wave sums its chunks and their squares, the chunk sums meet in LDS (one
-                // barrier the dot waves join)
+                // LayerNorm statistics in the chunk association (device_common.hpp, one pass): each
+                // image wave sums its chunks and their squares, the chunk sums meet in LDS (one
+                // barrier every wave joins)
                 __shared__ double ln_part[2][8];
 #pragma unroll
                 for (int q = 0; q < LCW; q++)
@@ -444,57 +469,13 @@ __device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, int b0, in
             }
 #ifdef RWKV_STAMP
             if (pw == 0 && stamp_x) {
-                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 if (lane == 0) stamp_x[2] = __builtin_amdgcn_s_memrealtime();
             }
 #endif
-            __syncthreads();
-            if constexpr (SRCK == MVK_LN && FORM != 2) {
-                // the entry's first workgroup: the same LayerNorm output mixed with mu2 into a
-                // global activation row (the channel-mix receptance input of k_mvsig), while the
-                // dot waves stream the weights
-                if (Ent.mu2 && wgi == (int)blockIdx.x - b0) {
-                    MVEntry E2 = Ent;
-                    E2.mu = Ent.mu2;
-#pragma unroll
-                    for (int q = 0; q < LCW; q++)
-                        if (pw + q * NW < nch) {
-                            ld8(ci[q].m, Ent.mu2 + min(kc[q], K - 8));
-                            chunk_store<WF, SRCK, FORM>(E2, Ent.act2_out, ci[q], mean, scale, false, kc[q], kc[q] < K,
-                                                        lane);
-                        }
-                }
-            }
-            // take part in the dot waves' barriers, then leave (to the kernel's common end)
-            for (;;) {
-                if constexpr (EMIT) __syncthreads();
-                wgi += stride;
-                if (stride <= 0 || wgi >= nblk) break;
-                if constexpr (EMIT) __syncthreads();
-            }
-            return;  // returns from mv_body only
+        } else if constexpr (SRCK == MVK_LN) {
+            asm volatile("s_barrier" ::: "memory");  // the image waves' statistics exchange
         }
-    }
-    // ---- dot wave: this wave's weight units (HBM) and the epilogue operands
-    if constexpr (PRO) {
-        // the weight pointers reach SGPRs before the issue-order barrier, so the stream starts
-        // right after it (a kernarg scalar load behind the barrier is a round trip in the path)
-        asm volatile("" ::"s"(W.qs), "s"(W.sc), "s"(W.qh));
-        asm volatile("s_barrier" ::: "memory");  // after the prologue's input loads
-    }
-    int row0 = wgi * RW + wave * R;
-    int rows[R];
-#pragma unroll
-    for (int r = 0; r < R; r++) rows[r] = min(row0 + r, M - 1);
-    WBlk w[R][U];
-#pragma unroll
-    for (int u = 0; u < U; u++)
-#pragma unroll
-        for (int r = 0; r < R; r++) w[r][u] = load_unit<WF>(W, rows[r], u, lane);
-    if constexpr (SRCK == MVK_LN) {
-        // the prologue's statistics barrier, right after the weight issue (no wait on this
-        // wave's loads; the epilogue operands are fetched after it)
-        asm volatile("s_barrier" ::: "memory");
     }
     // epilogue operands: !EMIT lane r < R runs row row0 + r's epilogue; EMIT thread tid < RW row tid
     EpiIn ep;
@@ -544,8 +525,8 @@ __device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, int b0, in
             if (s[0] == 1.2345f) g_probe[0] = 0;  // orders the stamp after the dots
 #endif
             PROBE(2);
-            const float v = epi_apply(Ent.epi, lane_row_sum<R>(s, lane), ep);
-            if (lane < R && row0 + lane < M) Ent.y[row0 + lane] = v;
+            const float v = epi_apply(epi, lane_row_sum<R>(s, lane), ep);
+            if (lane < R && row0 + lane < M) ey[row0 + lane] = v;
         } else {
             // RW rows per block (a multiple of 32): apply the epilogue and emit each 32 rows as
             // one quantization block of the next matmul's input (ggml Q8 / fp16 / fp32)
@@ -561,10 +542,10 @@ __device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, int b0, in
                 const int row = wgi * RW + tid;
                 float vv = 0.0f;
                 if (row < M) {
-                    vv = epi_apply(Ent.epi, red[tid], ep);
-                    if (Ent.y) Ent.y[row] = vv;
+                    vv = epi_apply(epi, red[tid], ep);
+                    if (ey) ey[row] = vv;
                 }
-                if (Ent.act_out.fmt >= 0 && Ent.emit) emit32(Ent.act_out, 0, row, vv);
+                if (emit_on) emit32(ao, 0, row, vv);
             }
         }
         PROBE(3);
@@ -581,6 +562,20 @@ __device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, int b0, in
         if constexpr (!EMIT) ep = epi_load(Ent, min(row0 + min(lane, R - 1), M - 1));
         else ep = epi_load(Ent, min(wgi * RW + (tid < RW ? tid : 0), M - 1));
     }
+    if constexpr (SRCK == MVK_LN && FORM != 2) {
+        // the entry's first workgroup, after its rows: the same LayerNorm output mixed with mu2
+        // into a global activation row (the channel-mix receptance input of k_mvsig)
+        if (pro_wave && Ent.mu2 && (int)blockIdx.x == b0) {
+            MVEntry E2 = Ent;
+            E2.mu = Ent.mu2;
+#pragma unroll
+            for (int q = 0; q < LCW; q++)
+                if (pw + q * NW < nch) {
+                    ld8(ci[q].m, Ent.mu2 + min(kc[q], K - 8));
+                    chunk_store<WF, SRCK, FORM>(E2, Ent.act2_out, ci[q], mean, scale, false, kc[q], kc[q] < K, lane);
+                }
+        }
+    }
 }
 
 // WFIX >= 0: every entry of the group has weight type WFIX (one body, fewer registers);
@@ -596,7 +591,7 @@ template <int R, int U, int SRCK, int FORM, bool EMIT, int WFIX, int LNP>
 __global__ __launch_bounds__(512) void k_mv(int b1, int b2, int b3, int b4, int b5, int b6, int b7, MVGroup g) {
     constexpr int NW = 4;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    __shared__ float red[NW * R];
+    __shared__ float red[(SRCK == MVK_ACT ? NW : 2 * NW) * R];
     const int bx = (int)blockIdx.x;
     const int e = (bx >= b1) + (bx >= b2) + (bx >= b3) + (bx >= b4) + (bx >= b5) + (bx >= b6) + (bx >= b7);
     const int b0 = e == 0 ? 0 : e == 1 ? b1 : e == 2 ? b2 : e == 3 ? b3 : e == 4 ? b4 : e == 5 ? b5 : e == 6 ? b6 : b7;
@@ -832,8 +827,8 @@ bool launch_mv_shape(hipStream_t st, MVGroup & g, int U, int srck, int form, boo
         return true;
     }
     if (srck == MVK_F32) {
-        if (U == 1) MV_L(2, 1, MVK_F32, 0, false, 0);
-        else MV_L(2, 4, MVK_F32, 0, false, 0);
+        if (U == 1) MV_L(1, 1, MVK_F32, 0, false, 0);
+        else MV_L(1, 4, MVK_F32, 0, false, 0);
         return true;
     }
     for (int i = 1; i < g.n; i++)
@@ -845,6 +840,8 @@ bool launch_mv_shape(hipStream_t st, MVGroup & g, int U, int srck, int form, boo
         fprintf(stderr, "rwkv: LayerNorm matvec prologue needs K <= 4096 (K=%d)\n", K);
         return false;
     }
+    // prologue groups: the rows of a block over all 8 waves (image waves included), so R here is
+    // half of launch_mv_group's rows per wave (g.rows, which counts the 4 streaming waves)
 #define MV_PR(Rv, S, F, E)                                    \
     do {                                                      \
         if (K <= 2048) {                                      \
@@ -857,15 +854,15 @@ bool launch_mv_shape(hipStream_t st, MVGroup & g, int U, int srck, int form, boo
             else MV_L(Rv, 4, S, F, E, 64);                    \
         }                                                     \
     } while (0)
-    // not emitting: g.rows rows per wave (2, or 4 for large LayerNorm groups); emitting: 8
+    // not emitting: g.rows rows per streaming wave (2, or 4 for large LayerNorm groups); emitting: 8
 #define MV_P(S, F, E)                                         \
     do {                                                      \
-        if (g.rows == 4) MV_PR(4, S, F, false);               \
-        else MV_PR(2, S, F, false);                           \
+        if (g.rows == 4) MV_PR(2, S, F, false);               \
+        else MV_PR(1, S, F, false);                           \
     } while (0)
     if (emit) {
-        if (form == 0) MV_PR(8, MVK_LN, 0, true);
-        else MV_PR(8, MVK_LN, 1, true);
+        if (form == 0) MV_PR(4, MVK_LN, 0, true);
+        else MV_PR(4, MVK_LN, 1, true);
     } else {
         if (form == 0) MV_P(MVK_LN, 0, false);
         else if (form == 1) MV_P(MVK_LN, 1, false);

@@ -28,92 +28,26 @@ struct MaaDec {
     int xa_off;                 // LDS byte offset of the fp32 xa image
 };
 
-// 512 threads.  Waves 0..3: W1 rows (R each, D <= 4R), then the mix of one channel per thread
-// (its W2 column prefetched with the weights).  Waves 4..7: the activation image (LayerNorm +
-// token shift + quantization, one 512-element chunk per wave per pass) and the fp32 xa image.
-// Each wave keeps well under 63 loads in flight, so none stalls on the vmcnt limit.
+// 512 threads.  Waves 4..7 build the activation image (LayerNorm + token shift + quantization,
+// one 512-element chunk per wave per pass) and the fp32 xa image; then every wave dots R rows of
+// W1 (D <= 8R: the image waves issue their weight loads right behind their input loads, so the
+// rows stream while the LayerNorm runs), and waves 0..3 mix one channel per thread (its W2 column
+// prefetched).  Each wave keeps well under 63 loads in flight, so none stalls on the vmcnt limit.
 template <int WF, int R, int U, int LNP, int DM, int CPW>
 __global__ __launch_bounds__(512) void k_v6_maa_dec(MaaDec a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ float s_lora[64];
     const int n = blockIdx.y, C = a.C, D = a.D, K = C;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const bool pro = wave >= 4;
+    const int pw = wave - 4;
     const ActBuf act = lds_act(smem, act_fmt_for(WF), K);
     float * s_xa = (float *)(smem + a.xa_off);
     STAMP_BEGIN();
-    if (wave < 4) {
-        // ---- dot wave: rows n*D + wave*R + r of W1
-        asm volatile("" ::"s"(a.w1.qs), "s"(a.w1.sc), "s"(a.w1.qh));  // pointers before the barrier
-        asm volatile("s_barrier" ::: "memory");  // after the prologue waves' input loads
-        const DMat & W = a.w1;
-        const int units = mv_units(WF, K);
-        const int row0 = n * D + wave * R, rlast = n * D + D - 1;
-        int rows[R];
-#pragma unroll
-        for (int r = 0; r < R; r++) rows[r] = min(row0 + r, rlast);
-        WBlk w[R][U];
-#pragma unroll
-        for (int u = 0; u < U; u++)
-#pragma unroll
-            for (int r = 0; r < R; r++) w[r][u] = load_unit<WF, false>(W, rows[r], u, lane);
-        // the prologue's LayerNorm statistics barrier, right after the weight issue
-        asm volatile("s_barrier" ::: "memory");
-        // this thread's mix channel: W2 column, carry, maa
-        const int c = blockIdx.x * CPW + tid;
-        const bool cval = tid < CPW && (int)(blockIdx.x * CPW + (tid & ~31)) < C;  // half-wave uniform
-        const int cc = min(c, C - 1);
-        float w2v[DM];
-        const float * w2 = a.w2t + (size_t)n * D * C + cc;
-#pragma unroll
-        for (int i = 0; i < DM; i++) {
-            const float t = w2[(size_t)min(i, D - 1) * C];
-            w2v[i] = (i < D) ? t : 0.0f;
-        }
-        const float carry_c = a.carry[cc], mu_c = a.maa[n][cc];
-        __syncthreads();  // (1) activation image ready
-        STAMP_MID();
-        float acc[R], acc2[R];
-#pragma unroll
-        for (int r = 0; r < R; r++) acc[r] = acc2[r] = 0.0f;
-        for (int u0 = 0; u0 < units; u0 += U) {
-            if (u0 > 0) {
-#pragma unroll
-                for (int u = 0; u < U; u++)
-#pragma unroll
-                    for (int r = 0; r < R; r++) w[r][u] = load_unit<WF, false>(W, rows[r], u0 + u, lane);
-            }
-            AUnit xu[U];
-#pragma unroll
-            for (int u = 0; u < U; u++) xu[u] = load_act_unit<WF, true>(act, u0 + u, lane);
-#pragma unroll
-            for (int u = 0; u < U; u++) {
-                if (unit_valid<WF>(K, u0 + u, lane)) {
-#pragma unroll
-                    for (int r = 0; r < R; r++) dot_unit<WF>(w[r][u], xu[u], acc[r], acc2[r]);
-                }
-            }
-        }
-        constexpr bool one = WF == W_Q4_1 || WF == W_Q5_1;
-        float s[R];
-#pragma unroll
-        for (int r = 0; r < R; r++) s[r] = one ? wave_sum63(acc[r]) + wave_sum63(acc2[r]) : wave_sum63(acc[r]) + 0.0f;
-        const float t = rk_tanhf(lane_row_sum<R>(s, lane));  // EPI_TANH, lane r for row r
-        if (lane < R && wave * R + lane < D) s_lora[wave * R + lane] = t;
-        __syncthreads();  // (2) lora_n ready
-        if (wave == 0) STAMP_X(3);
-        // k_v6_mix5_dec's arithmetic: m = fma chain over i in order
-        const float xa = s_xa[cc];
-        const float sx = carry_c - xa;
-        float m = 0.0f;
-#pragma unroll
-        for (int i = 0; i < DM; i++)
-            if (i < D) m = fmaf(w2v[i], s_lora[i], m);
-        if (cval) emit32(a.out[n], 0, c, (m + mu_c) * sx + xa);
-        STAMP_END_NS(4 + 16 * blockIdx.y);
-        return;
-    }
-    // ---- prologue wave
-    const int pw = wave - 4;
+    // the emission target's fields in SGPRs now, not a scalar round trip after the mix
+    const ActBuf ao = a.out[n];
+    pin_act(ao);
+    const DMat & W = a.w1;
     MVEntry E;
     E.x = a.x;
     E.carry = a.carry;
@@ -122,52 +56,125 @@ __global__ __launch_bounds__(512) void k_v6_maa_dec(MaaDec a) {
     E.mu = a.maa_x;
     E.carry_out = a.carry_out;
     E.f = nullptr;
-    // chunks pw, pw + 4 of the LayerNorm input (512 elements each, 8 per lane)
     constexpr int LCW = LNP > 32 ? 2 : 1;
     const int nch = (K + LN_CHUNK - 1) / LN_CHUNK;
     ChunkIn ci[LCW];
     int kc[LCW];
+    if (pro) {
+        // chunks pw, pw + 4 of the LayerNorm input (512 elements each, 8 per lane)
 #pragma unroll
-    for (int q = 0; q < LCW; q++) {
-        kc[q] = (pw + 4 * q) * LN_CHUNK + lane * 8;
-        chunk_load<MVK_LN, 1>(E, min(kc[q], K - 8), ci[q]);
+        for (int q = 0; q < LCW; q++) {
+            kc[q] = (pw + 4 * q) * LN_CHUNK + lane * 8;
+            chunk_load<MVK_LN, 1>(E, min(kc[q], K - 8), ci[q]);
+        }
+    } else {
+        asm volatile("" ::"s"(a.w1.qs), "s"(a.w1.sc), "s"(a.w1.qh));  // pointers before the barrier
     }
-    asm volatile("s_barrier" ::: "memory");  // input loads issued ahead of the weight stream
+    asm volatile("s_barrier" ::: "memory");  // image inputs issued ahead of the weight stream
     if (pw == 0) STAMP_X(0);
-    // LayerNorm statistics, chunk association, one pass (device_common.hpp); the dot waves join
-    // the exchange barrier
-    __shared__ double ln_part[2][8];
+    // ---- rows n*D + wave*R + r of W1 (all waves)
+    const int units = mv_units(WF, K);
+    const int row0 = n * D + wave * R, rlast = n * D + D - 1;
+    int rows[R];
 #pragma unroll
-    for (int q = 0; q < LCW; q++)
-        if (pw + 4 * q < nch) {
-            double c1, c2;
-            ln_chunk_sums(ci[q].x, kc[q] < K, c1, c2);
-            if (lane == 0) {
-                ln_part[0][pw + 4 * q] = c1;
-                ln_part[1][pw + 4 * q] = c2;
+    for (int r = 0; r < R; r++) rows[r] = min(row0 + r, rlast);
+    WBlk w[R][U];
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+        for (int r = 0; r < R; r++) w[r][u] = load_unit<WF, false>(W, rows[r], u, lane);
+    // this thread's mix channel (waves 0..3): W2 column, carry, maa
+    const int c = blockIdx.x * CPW + tid;
+    const bool cval = tid < CPW && (int)(blockIdx.x * CPW + (tid & ~31)) < C;  // half-wave uniform
+    const int cc = min(c, C - 1);
+    float w2v[DM];
+    float carry_c = 0.0f, mu_c = 0.0f;
+    if (pro) {
+        // LayerNorm statistics, chunk association, one pass (device_common.hpp); every wave joins
+        // the exchange barrier
+        __shared__ double ln_part[2][8];
+#pragma unroll
+        for (int q = 0; q < LCW; q++)
+            if (pw + 4 * q < nch) {
+                double c1, c2;
+                ln_chunk_sums(ci[q].x, kc[q] < K, c1, c2);
+                if (lane == 0) {
+                    ln_part[0][pw + 4 * q] = c1;
+                    ln_part[1][pw + 4 * q] = c2;
+                }
+            }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        double s1 = 0.0, s2 = 0.0;
+        for (int q = 0; q < nch; q++) s1 += ln_part[0][q], s2 += ln_part[1][q];
+        float mean, scale;
+        ln_finish(s1, s2, K, 1e-5f, mean, scale);
+#ifdef RWKV_STAMP
+        if (pw == 0 && lane == 0) stamp_x_[1] = __builtin_amdgcn_s_memrealtime() + (scale == 1.2345f);
+#endif
+        const bool write_carry = blockIdx.x == 0 && n == 0;
+#pragma unroll
+        for (int q = 0; q < LCW; q++) {
+            if (pw + 4 * q >= nch) continue;
+            if (kc[q] < K) {
+#pragma unroll
+                for (int j = 0; j < 8; j++) s_xa[kc[q] + j] = ln_apply(ci[q].x[j], mean, scale, ci[q].w[j], ci[q].b[j]);
+            }
+            chunk_store<WF, MVK_LN, 1>(E, act, ci[q], mean, scale, write_carry, kc[q], kc[q] < K, lane);
+        }
+        if (pw == 0) STAMP_X(2);
+    } else {
+        const float * w2 = a.w2t + (size_t)n * D * C + cc;
+#pragma unroll
+        for (int i = 0; i < DM; i++) {
+            const float t = w2[(size_t)min(i, D - 1) * C];
+            w2v[i] = (i < D) ? t : 0.0f;
+        }
+        carry_c = a.carry[cc];
+        mu_c = a.maa[n][cc];
+        asm volatile("s_barrier" ::: "memory");  // the image waves' statistics exchange
+    }
+    __syncthreads();  // (1) activation image ready
+    if (wave == 0) STAMP_MID();
+    float acc[R], acc2[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) acc[r] = acc2[r] = 0.0f;
+    for (int u0 = 0; u0 < units; u0 += U) {
+        if (u0 > 0) {
+#pragma unroll
+            for (int u = 0; u < U; u++)
+#pragma unroll
+                for (int r = 0; r < R; r++) w[r][u] = load_unit<WF, false>(W, rows[r], u0 + u, lane);
+        }
+        AUnit xu[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) xu[u] = load_act_unit<WF, true>(act, u0 + u, lane);
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            if (unit_valid<WF>(K, u0 + u, lane)) {
+#pragma unroll
+                for (int r = 0; r < R; r++) dot_unit<WF>(w[r][u], xu[u], acc[r], acc2[r]);
             }
         }
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    double s1 = 0.0, s2 = 0.0;
-    for (int c = 0; c < nch; c++) s1 += ln_part[0][c], s2 += ln_part[1][c];
-    float mean, scale;
-    ln_finish(s1, s2, K, 1e-5f, mean, scale);
-#ifdef RWKV_STAMP
-    if (pw == 0 && lane == 0) stamp_x_[1] = __builtin_amdgcn_s_memrealtime() + (scale == 1.2345f);
-#endif
-    const bool write_carry = blockIdx.x == 0 && n == 0;
-#pragma unroll
-    for (int q = 0; q < LCW; q++) {
-        if (pw + 4 * q >= nch) continue;
-        if (kc[q] < K) {
-#pragma unroll
-            for (int j = 0; j < 8; j++) s_xa[kc[q] + j] = ln_apply(ci[q].x[j], mean, scale, ci[q].w[j], ci[q].b[j]);
-        }
-        chunk_store<WF, MVK_LN, 1>(E, act, ci[q], mean, scale, write_carry, kc[q], kc[q] < K, lane);
     }
-    if (pw == 0) STAMP_X(2);
-    __syncthreads();  // (1)
-    __syncthreads();  // (2)
+    constexpr bool one = WF == W_Q4_1 || WF == W_Q5_1;
+    float sr[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) sr[r] = one ? wave_sum63(acc[r]) + wave_sum63(acc2[r]) : wave_sum63(acc[r]) + 0.0f;
+    const float t = rk_tanhf(lane_row_sum<R>(sr, lane));  // EPI_TANH, lane r for row r
+    if (lane < R && wave * R + lane < D) s_lora[wave * R + lane] = t;
+    __syncthreads();  // (2) lora_n ready
+    if (wave == 0) STAMP_X(3);
+    if (!pro) {
+        // k_v6_mix5_dec's arithmetic: m = fma chain over i in order
+        const float xa = s_xa[cc];
+        const float sx = carry_c - xa;
+        float m = 0.0f;
+#pragma unroll
+        for (int i = 0; i < DM; i++)
+            if (i < D) m = fmaf(w2v[i], s_lora[i], m);
+        if (cval) emit32(ao, 0, c, (m + mu_c) * sx + xa);
+    }
+    STAMP_END_NS(4 + 16 * blockIdx.y);
 }
 
 // Channels mixed per workgroup (CPW): the workgroups of one mix each recompute its D rows of W1
@@ -188,17 +195,18 @@ static bool launch_maa_t(hipStream_t st, const MaaDec & a, int lds, int units) {
     const dim3 grid((a.C + cpw - 1) / cpw, 5);
 #define MAA_L(Rv, Uv, P)                                                                                           \
     do {                                                                                                           \
-        if (cpw == 64) RK_LAUNCH((k_v6_maa_dec<WF, Rv, Uv, P, (Rv) * 4, 64>), grid, dim3(512), lds, st, a); \
-        else if (cpw == 128) RK_LAUNCH((k_v6_maa_dec<WF, Rv, Uv, P, (Rv) * 4, 128>), grid, dim3(512), lds, st, a); \
-        else RK_LAUNCH((k_v6_maa_dec<WF, Rv, Uv, P, (Rv) * 4, 256>), grid, dim3(512), lds, st, a);      \
+        if (cpw == 64) RK_LAUNCH((k_v6_maa_dec<WF, Rv, Uv, P, (Rv) * 8, 64>), grid, dim3(512), lds, st, a); \
+        else if (cpw == 128) RK_LAUNCH((k_v6_maa_dec<WF, Rv, Uv, P, (Rv) * 8, 128>), grid, dim3(512), lds, st, a); \
+        else RK_LAUNCH((k_v6_maa_dec<WF, Rv, Uv, P, (Rv) * 8, 256>), grid, dim3(512), lds, st, a);      \
     } while (0)
 #define MAA_P(Rv, Uv) \
     do { if (a.C <= 2048) MAA_L(Rv, Uv, 32); else MAA_L(Rv, Uv, 64); } while (0)
     const bool u1 = units <= 1;
+    // rows per wave over all 8 waves (D <= 8R)
     if (a.D <= 32) {
-        if (u1) MAA_P(8, 1); else MAA_P(8, 2);
+        if (u1) MAA_P(4, 1); else MAA_P(4, 2);
     } else {
-        if (u1) MAA_P(16, 1); else MAA_P(16, 2);
+        if (u1) MAA_P(8, 1); else MAA_P(8, 2);
     }
 #undef MAA_P
 #undef MAA_L

@@ -143,13 +143,23 @@ struct QGOps {
     float dx[2];
 };
 
+// The 8-byte operand reads stay single ds_read_b64 (2 LDS cycles, 64 banks): the compiler would
+// otherwise pair reads of consecutive steps into ds_read2st64_b64, which the LDS serves as two
+// 16-lane-group accesses over 32 banks (8 cycles per pair, and tokens t / t + 8 of the activation
+// record then share banks).  QG_MERGED_READS restores the compiler's pairing (A/B builds).
+#ifdef QG_MERGED_READS
+typedef const long qg_op_t;
+#else
+typedef __attribute__((address_space(3))) const volatile long qg_op_t;
+#endif
+
 template <int WF>
 __device__ __forceinline__ void qg_read_ops(const char * sp, QGOps<QGLayout<WF>::TI> & o, int wr, int wt, int r16,
                                             int h) {
     using Lt = QGLayout<WF>;
 #pragma unroll
     for (int i = 0; i < Lt::TI; i++) {
-        o.af[i] = *(const long *)(sp + qg_w_off(wr + 16 * i + r16, h * 8));  // int8 row, k = 8h..8h+7
+        o.af[i] = *(qg_op_t *)(sp + qg_w_off(wr + 16 * i + r16, h * 8));  // int8 row, k = 8h..8h+7
         const int ro = wr + 16 * i + 4 * h;
         o.sd[i] = *(const float4 *)(sp + qg_w_d(WF) + ro * 4);
     }
@@ -157,7 +167,7 @@ __device__ __forceinline__ void qg_read_ops(const char * sp, QGOps<QGLayout<WF>:
 #pragma unroll
     for (int j = 0; j < 2; j++) {
         const int tl = wt + 16 * j + r16;
-        o.xf[j] = *(const long *)(ap + (h >> 1) * QG_TOK * 16 + tl * 16 + (h & 1) * 8);
+        o.xf[j] = *(qg_op_t *)(ap + (h >> 1) * QG_TOK * 16 + tl * 16 + (h & 1) * 8);
         o.dx[j] = *(const float *)(ap + QG_A_D + tl * 4);
     }
 }

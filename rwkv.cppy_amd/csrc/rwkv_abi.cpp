@@ -11,12 +11,14 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <vector>
 #include <tuple>
 
 #include "../../include/rwkv.h"
 #include "../../include/rwkv_mi355x.h"
 #include "engine.hpp"
 #include "model_file.hpp"
+#include "pipeline.hpp"
 
 using namespace rwkvmi;
 
@@ -43,6 +45,10 @@ struct rwkv_context {
     uint32_t n_threads = 1;
     enum rwkv_error_flags last_error = RWKV_ERROR_NONE;
     bool print_errors = true;
+    // layer pipeline (RWKV_MI355X_PIPELINE / rwkv_mi355x_init_pipeline): this context is stage 0;
+    // stages[i] (i >= 1) are owned stage contexts on their own GPUs
+    LayerPipeline * pipe = nullptr;
+    std::vector<rwkv_context *> stages;
 };
 
 static std::mutex g_model_mutex;
@@ -100,7 +106,7 @@ static struct rwkv_context * new_context(SharedModel * sm, uint32_t n_threads) {
 }
 
 static struct rwkv_context * init_from_file(const char * path, const uint32_t n_threads, uint32_t layer_begin = 0,
-                                            uint32_t layer_end = UINT32_MAX) {
+                                            uint32_t layer_end = UINT32_MAX, int device = -1) {
     int ndev = 0;
     const hipError_t de = hipGetDeviceCount(&ndev);
     RWKV_CHECK(RWKV_ERROR_CTX | RWKV_ERROR_UNSUPPORTED, nullptr, de == hipSuccess && ndev > 0,
@@ -111,7 +117,7 @@ static struct rwkv_context * init_from_file(const char * path, const uint32_t n_
                "Bad layer range [%u, %u) for %u layers", layer_begin, layer_end, mf.header.n_layer);
     SharedModel * sm = new (std::nothrow) SharedModel();
     RWKV_CHECK(RWKV_ERROR_CTX | RWKV_ERROR_ALLOC, nullptr, sm != nullptr, "Failed to allocate model");
-    sm->dm.device = pick_device();
+    sm->dm.device = device >= 0 ? device : pick_device();
     if (sm->dm.device >= ndev) sm->dm.device = 0;
     if (hipSetDevice(sm->dm.device) != hipSuccess || !upload_model(mf, sm->dm, layer_begin, layer_end)) {
         free_model(sm->dm);
@@ -137,16 +143,108 @@ static struct rwkv_context * init_from_file(const char * path, const uint32_t n_
 // may sit on different GPUs: rwkv_mi355x_clone_context_on).
 static void use_device(const rwkv_context * ctx) { (void)hipSetDevice(ctx->model->dm.device); }
 
+static void free_context(struct rwkv_context * ctx);
+
+// The layer pipeline behind the reference entry points: P stage contexts, stage i
+// on devices[i] holding layers stage_layers(n_layer, P, i) (earlier stages take the extra layers,
+// as rwkv_cpp/pipeline.py stage_layers), driven from this process by LayerPipeline.  The returned
+// context is stage 0; it reports the whole model's dimensions and accepts rwkv_eval /
+// rwkv_eval_sequence[_in_chunks] with host buffers, bit-identical to a single-GPU context.
+static struct rwkv_context * init_pipeline(const char * path, uint32_t n_threads, int P, const int * devices) {
+    int ndev = 0;
+    RWKV_CHECK(RWKV_ERROR_CTX | RWKV_ERROR_UNSUPPORTED, nullptr, hipGetDeviceCount(&ndev) == hipSuccess && ndev > 0,
+               "No HIP device available");
+    FileHeader h{};
+    {
+        FILE * f = fopen(path, "rb");
+        RWKV_CHECK(RWKV_ERROR_FILE | RWKV_ERROR_FILE_OPEN, nullptr, f != nullptr, "Failed to open %s", path);
+        const bool ok = read_file_header(f, h);
+        fclose(f);
+        if (!ok) return nullptr;
+    }
+    RWKV_CHECK(RWKV_ERROR_ARGS, nullptr, P >= 2 && (uint32_t)P <= h.n_layer, "Pipeline of %d stages for %u layers", P,
+               h.n_layer);
+    std::vector<rwkv_context *> st;
+    std::vector<LayerPipeline::StageSpec> specs;
+    const uint32_t base = h.n_layer / (uint32_t)P, extra = h.n_layer % (uint32_t)P;
+    for (int i = 0; i < P; i++) {
+        const uint32_t l0 = (uint32_t)i * base + std::min<uint32_t>((uint32_t)i, extra);
+        const uint32_t l1 = l0 + base + ((uint32_t)i < extra ? 1u : 0u);
+        const int dev = devices ? devices[i] : i % ndev;
+        rwkv_context * c = (dev >= 0 && dev < ndev) ? init_from_file(path, n_threads, l0, l1, dev) : nullptr;
+        if (!c) {
+            for (rwkv_context * q : st) free_context(q);
+            RWKV_CHECK(RWKV_ERROR_CTX | RWKV_ERROR_ALLOC, nullptr, false, "Failed to create pipeline stage %d on device %d",
+                       i, dev);
+        }
+        st.push_back(c);
+        specs.push_back(LayerPipeline::StageSpec{c->engine, c->model->dm.device, l0, l1});
+    }
+    LayerPipeline * p = new (std::nothrow) LayerPipeline();
+    if (!p || !p->init(specs, h.n_embed, st[0]->model->dm.major == 7)) {
+        delete p;
+        for (rwkv_context * q : st) free_context(q);
+        RWKV_CHECK(RWKV_ERROR_CTX | RWKV_ERROR_ALLOC, nullptr, false, "Failed to set up the layer pipeline");
+    }
+    rwkv_context * head = st[0];
+    head->pipe = p;
+    head->stages.assign(st.begin() + 1, st.end());
+    return head;
+}
+
+static int env_pipeline_stages() {
+    const char * e = getenv("RWKV_MI355X_PIPELINE");
+    return e && *e ? atoi(e) : 0;
+}
+
+static std::vector<int> env_pipeline_devices(int P) {
+    std::vector<int> d;
+    const char * e = getenv("RWKV_MI355X_PIPELINE_DEVICES");  // "0,1,2,3"; default i % device count
+    if (!e || !*e) return d;
+    std::string v(e);
+    size_t pos = 0;
+    while ((int)d.size() < P && pos <= v.size()) {
+        const size_t q = v.find(',', pos);
+        d.push_back(atoi(v.substr(pos, q == std::string::npos ? std::string::npos : q - pos).c_str()));
+        if (q == std::string::npos) break;
+        pos = q + 1;
+    }
+    if ((int)d.size() != P) d.clear();
+    return d;
+}
+
 // No C++ exception crosses the C ABI: a failed host allocation (std::bad_alloc from a corrupt
 // file's sizes, say) becomes RWKV_ERROR_ALLOC and a NULL context.
+// n_gpu_layers is accepted and ignored: the whole model always runs on the GPU(s).  With the
+// additive setting RWKV_MI355X_PIPELINE=P (P >= 2) the context is a P-stage layer pipeline
+// (devices RWKV_MI355X_PIPELINE_DEVICES="d0,d1,..." or 0..P-1 modulo the device count).
 RWKV_API struct rwkv_context * rwkv_init_from_file(const char * path, const uint32_t n_threads, const uint32_t n_gpu_layers) {
     (void)n_gpu_layers;
     g_last_error = RWKV_ERROR_NONE;
     try {
+        const int P = env_pipeline_stages();
+        if (P >= 2) {
+            const std::vector<int> devs = env_pipeline_devices(P);
+            return init_pipeline(path, n_threads, P, devs.empty() ? nullptr : devs.data());
+        }
         return init_from_file(path, n_threads);
     } catch (const std::exception & e) {
         RWKV_CHECK(RWKV_ERROR_CTX | RWKV_ERROR_ALLOC, nullptr, false, "Failed to load %s: %s", path, e.what());
     }
+}
+
+RWKV_API struct rwkv_context * rwkv_mi355x_init_pipeline(const char * path, const uint32_t n_threads, const int n_stages,
+                                                         const int * devices) {
+    g_last_error = RWKV_ERROR_NONE;
+    try {
+        return init_pipeline(path, n_threads, n_stages, devices);
+    } catch (const std::exception & e) {
+        RWKV_CHECK(RWKV_ERROR_CTX | RWKV_ERROR_ALLOC, nullptr, false, "Failed to load %s: %s", path, e.what());
+    }
+}
+
+RWKV_API int rwkv_mi355x_pipeline_stages(const struct rwkv_context * ctx) {
+    return ctx && ctx->pipe ? (int)ctx->pipe->stages() : (ctx ? 1 : 0);
 }
 
 RWKV_API struct rwkv_context * rwkv_mi355x_init_from_file_layers(const char * path, const uint32_t n_threads,
@@ -161,6 +259,38 @@ RWKV_API struct rwkv_context * rwkv_mi355x_init_from_file_layers(const char * pa
 
 RWKV_API struct rwkv_context * rwkv_clone_context(struct rwkv_context * ctx, const uint32_t n_threads) {
     if (!ctx) return nullptr;
+    if (ctx->pipe) {
+        // a pipeline clone: the same stages on the same GPUs, each with its own engine (fresh
+        // state) sharing the stage's uploaded weights
+        std::vector<rwkv_context *> st;
+        std::vector<LayerPipeline::StageSpec> specs;
+        std::vector<rwkv_context *> src = {ctx};
+        src.insert(src.end(), ctx->stages.begin(), ctx->stages.end());
+        for (rwkv_context * s : src) {
+            rwkv_context * c = nullptr;
+            {
+                std::lock_guard<std::mutex> lk(g_model_mutex);
+                c = new_context(s->model, n_threads);
+            }
+            if (!c) {
+                for (rwkv_context * q : st) free_context(q);
+                return nullptr;
+            }
+            c->print_errors = ctx->print_errors;
+            st.push_back(c);
+            specs.push_back(LayerPipeline::StageSpec{c->engine, c->model->dm.device, s->model->dm.layer_lo,
+                                                     s->model->dm.layer_hi});
+        }
+        LayerPipeline * p = new (std::nothrow) LayerPipeline();
+        if (!p || !p->init(specs, ctx->model->dm.n_embed, ctx->model->dm.major == 7)) {
+            delete p;
+            for (rwkv_context * q : st) free_context(q);
+            return nullptr;
+        }
+        st[0]->pipe = p;
+        st[0]->stages.assign(st.begin() + 1, st.end());
+        return st[0];
+    }
     std::lock_guard<std::mutex> lk(g_model_mutex);
     rwkv_context * c = new_context(ctx->model, n_threads);
     if (c) c->print_errors = ctx->print_errors;
@@ -226,11 +356,20 @@ RWKV_API struct rwkv_context * rwkv_mi355x_clone_context_on(struct rwkv_context 
 
 RWKV_API int rwkv_mi355x_context_device(const struct rwkv_context * ctx) { return ctx ? ctx->model->dm.device : -1; }
 
+static bool pipe_eval(struct rwkv_context * ctx, const uint32_t * tokens, size_t T, const float * state_in,
+                      float * state_out, float * logits_out) {
+    CTX_CHECK(ctx, RWKV_ERROR_CTX, false,
+              ctx->pipe->eval(tokens, T, state_in, state_out, logits_out, ctx->engine->layer_state_len()),
+              "GPU evaluation failed (layer pipeline)");
+    return true;
+}
+
 RWKV_API bool rwkv_eval(struct rwkv_context * ctx, const uint32_t token, const float * state_in, float * state_out,
                         float * logits_out) {
     ctx->last_error = RWKV_ERROR_NONE;
     const size_t n_vocab = ctx->model->dm.n_vocab;
     CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, token < n_vocab, "Token (%" PRIu32 ") is out of range (0 .. %zu)", token, n_vocab - 1);
+    if (ctx->pipe) return pipe_eval(ctx, &token, 1, state_in, state_out, logits_out);
     CTX_CHECK(ctx, RWKV_ERROR_CTX | RWKV_ERROR_UNSUPPORTED, false, !ctx->model->dm.partial(),
               "This context holds layers [%u, %u) only (a pipeline stage): use rwkv_mi355x_eval_layers",
               ctx->model->dm.layer_lo, ctx->model->dm.layer_hi);
@@ -245,6 +384,13 @@ RWKV_API bool rwkv_eval_sequence(struct rwkv_context * ctx, const uint32_t * tok
     CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, T > 0, "Sequence length is 0");
     if (!tokens) return true;  // build/cache only (rwkv_eval_inc:102,122): workspace is allocated lazily
     if (T == 1) return rwkv_eval(ctx, tokens[0], state_in, state_out, logits_out);
+    if (ctx->pipe) {
+        const size_t nv = ctx->model->dm.n_vocab;
+        for (size_t i = 0; i < T; i++)
+            CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, tokens[i] < nv, "Token at index %zu (%" PRIu32 ") is out of range (0 .. %zu)",
+                      i, tokens[i], nv - 1);
+        return pipe_eval(ctx, tokens, T, state_in, state_out, logits_out);
+    }
     CTX_CHECK(ctx, RWKV_ERROR_CTX | RWKV_ERROR_UNSUPPORTED, false, !ctx->model->dm.partial(),
               "This context holds layers [%u, %u) only (a pipeline stage): use rwkv_mi355x_eval_layers",
               ctx->model->dm.layer_lo, ctx->model->dm.layer_hi);
@@ -287,8 +433,14 @@ RWKV_API void rwkv_init_state(const struct rwkv_context * ctx, float * state) {
         for (size_t i = 4 * C; i < 5 * C; i++) state[l * 5 * C + i] = -1e30f;
 }
 
-RWKV_API void rwkv_free(struct rwkv_context * ctx) {
+RWKV_API void rwkv_free(struct rwkv_context * ctx) { free_context(ctx); }
+
+static void free_context(struct rwkv_context * ctx) {
     if (!ctx) return;
+    delete ctx->pipe;  // before the stage engines it drives
+    ctx->pipe = nullptr;
+    for (rwkv_context * s : ctx->stages) free_context(s);
+    ctx->stages.clear();
     delete ctx->engine;
     SharedModel * sm = ctx->model;
     delete ctx;

@@ -121,6 +121,10 @@ class RWKVSharedLibrary:
         L.rwkv_mi355x_clone_context_on.restype = vp
         L.rwkv_mi355x_context_device.argtypes = [vp]
         L.rwkv_mi355x_context_device.restype = ctypes.c_int
+        L.rwkv_mi355x_init_pipeline.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p]
+        L.rwkv_mi355x_init_pipeline.restype = vp
+        L.rwkv_mi355x_pipeline_stages.argtypes = [vp]
+        L.rwkv_mi355x_pipeline_stages.restype = ctypes.c_int
 
         self.nullptr = ctypes.cast(0, ctypes.c_void_p)
 

@@ -255,20 +255,25 @@ __device__ __forceinline__ T ldw(const T * p) {
     else return *p;
 }
 
+// Offsets in 32 bits (a weight tensor is far below 4 GiB): base (SGPR) + 32-bit offset is the
+// saddr load form, whose offset register is not the destination -- with 64-bit per-lane addresses
+// the compiler reuses an address register as a later load's destination and must wait for the
+// earlier load to return before issuing the next (waits inside the weight stream's issue).
 template <int WF, bool NT = false>
-__device__ __forceinline__ WBlk load_wblk(const DMat & W, size_t bi) {
+__device__ __forceinline__ WBlk load_wblk(const DMat & W, size_t bi_) {
     WBlk w;
+    const uint32_t bi = (uint32_t)bi_;
     if constexpr (WF == W_Q8_0) {
-        const int4 * p = (const int4 *)(W.qs + bi * 32);
+        const int4 * p = (const int4 *)(W.qs + bi * 32u);
         w.q0 = ld16w<NT>(p);
-        w.q1 = ld16w<NT>(p + 1);
+        w.q1 = ld16w<NT>((const int4 *)(W.qs + (bi * 32u + 16u)));
     } else {
-        w.q0 = ld16w<NT>(W.qs + bi * 16);
+        w.q0 = ld16w<NT>(W.qs + bi * 16u);
         w.q1 = make_int4(0, 0, 0, 0);
     }
-    w.qh = (WF == W_Q5_0 || WF == W_Q5_1) ? ldw<NT>(W.qh + bi) : 0u;
-    if constexpr (WF == W_Q4_1 || WF == W_Q5_1) w.sc = ldw<NT>((const uint32_t *)W.sc + bi);
-    else w.sc = ldw<NT>((const uint16_t *)W.sc + bi);
+    w.qh = (WF == W_Q5_0 || WF == W_Q5_1) ? ldw<NT>((const uint32_t *)((const char *)W.qh + bi * 4u)) : 0u;
+    if constexpr (WF == W_Q4_1 || WF == W_Q5_1) w.sc = ldw<NT>((const uint32_t *)((const char *)W.sc + bi * 4u));
+    else w.sc = ldw<NT>((const uint16_t *)((const char *)W.sc + bi * 2u));
     return w;
 }
 

@@ -401,7 +401,7 @@ bool Engine::init() {
     ws_allocs_.push_back(hcnt_);
     HIP_OK(hipMemset(hcnt_, 0, kHandoffWords * 4));
     {
-        const size_t ng = 4 * (size_t)m_->n_embed + 128;  // k_v6_att_fused granules (4 C + D)
+        const size_t ng = 6 * (size_t)m_->n_embed;  // k_v6_att_fused granules: 4 C + H D (D <= 128, H = C / 64)
         HIP_OK(hipMalloc(&hgran_, ng * 8));
         ws_allocs_.push_back(hgran_);
         HIP_OK(hipMemset(hgran_, 0, ng * 8));
@@ -1288,18 +1288,39 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits, uint32
         };
         // ---------------- time mixing ----------------
         if (m_->major == 4) {
-            MV b;
-            src_lnmix(b.add(L.att_r, r_, EPI_SIGMOID), x_, si + C, L.ln1_w, L.ln1_b, L.att_mix_r, 0, so + C);
-            src_lnmix(b.add(L.att_k, k_, EPI_STORE), x_, si + C, L.ln1_w, L.ln1_b, L.att_mix_k, 0);
-            src_lnmix(b.add(L.att_v, v_, EPI_STORE), x_, si + C, L.ln1_w, L.ln1_b, L.att_mix_v, 0);
-            if (!mv(b.g)) return false;
             ActBuf o = A(0, L.att_o);
-            if (!launch_wkv4(stream_, 1, C, r_, k_, v_, L.att_first, L.att_decay, si, so, o)) return false;
-            MV c;
-            MVEntry & e = c.add(L.att_o, x_, EPI_ADD);
-            e.src = SRC_ACT;
-            e.act = o;
-            if (!mv(c.g)) return false;
+            if (v4_att_fused_supported(C, L.att_r, L.att_k, L.att_v, o)) {
+                // LN + r, k, v rows + WKV-4 in one launch, v4_att_fused_cpw() channels per workgroup (mv_att4f.hip)
+                if (timing_) {
+                    kt_bytes_ = 3 * wbytes(L.att_r) + 9.0 * C * 4 + 6.0 * C * 4 + C * 4.0 + act_bytes(o, 1);
+                    kt_flops_ = 6.0 * C * C;
+                }
+                if (!launch_v4_att_fused(stream_, C, L.att_r, L.att_k, L.att_v, x_, si + C, so + C, L.ln1_w, L.ln1_b,
+                                         L.att_mix_r, L.att_mix_k, L.att_mix_v, L.att_first, L.att_decay, si, so, o, y_))
+                    return false;
+                if (v4_att_fused_cpw() != 32) {
+                    // y fp32: Wo quantizes it in its own prologue (the same Q8 bits as the emission)
+                    MV c;
+                    src_f32(c.add(L.att_o, x_, EPI_ADD), y_);
+                    if (!mv(c.g)) return false;
+                    goto v4_att_done;
+                }
+            } else {
+                MV b;
+                src_lnmix(b.add(L.att_r, r_, EPI_SIGMOID), x_, si + C, L.ln1_w, L.ln1_b, L.att_mix_r, 0, so + C);
+                src_lnmix(b.add(L.att_k, k_, EPI_STORE), x_, si + C, L.ln1_w, L.ln1_b, L.att_mix_k, 0);
+                src_lnmix(b.add(L.att_v, v_, EPI_STORE), x_, si + C, L.ln1_w, L.ln1_b, L.att_mix_v, 0);
+                if (!mv(b.g)) return false;
+                if (!launch_wkv4(stream_, 1, C, r_, k_, v_, L.att_first, L.att_decay, si, so, o)) return false;
+            }
+            {
+                MV c;
+                MVEntry & e = c.add(L.att_o, x_, EPI_ADD);
+                e.src = SRC_ACT;
+                e.act = o;
+                if (!mv(c.g)) return false;
+            }
+        v4_att_done:;
         } else if (m_->major == 5) {
             const bool v52 = m_->minor >= 2;
             MV b;
@@ -1806,7 +1827,7 @@ long long Engine::debug_copy(const char * name, void * out, size_t bytes) {
     if (n == "bonus") src = bonus_, cap_bytes = cap * (size_t)std::max<int64_t>(1, m_->H) * 4;
     if (n == "logits") src = logits_, cap_bytes = (size_t)m_->n_vocab * 4;
     if (n == "handoff") src = hcnt_, cap_bytes = kHandoffWords * 4;  // in-launch counters, [last] = timeout flag
-    if (n == "granules") src = hgran_, cap_bytes = (4 * C + 128) * 8;  // k_v6_att_fused hand-off granules
+    if (n == "granules") src = hgran_, cap_bytes = 6 * C * 8;  // k_v6_att_fused hand-off granules
     if (!src && n.rfind("slot", 0) == 0) {
         const size_t dot = n.find('.');
         const int i = atoi(n.c_str() + 4);

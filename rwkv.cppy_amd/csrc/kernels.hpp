@@ -144,7 +144,13 @@ struct MVGroup {
     int grid;                // set by launch_mv_group: workgroups launched
     int units_max;           // set by launch_mv_group: max 16-byte units per lane over entries
     int rows;                // set by launch_mv_group: rows per wave of the launched shape
+    int late;                // set by launch_mv_group: weights issued after the image inputs land
 };
+
+// Prologue matvecs: the streaming waves issue their weights only after the image waves' inputs
+// have landed (RWKV_MI355X_LATE_W, default 1): inputs queued behind a weight flood arrive late,
+// and the image gates every row.
+int mv_late_weights();
 
 // Busy-waits about `us` microseconds on the device (kernel timing: lets the host queue a whole
 // decode step before the GPU starts it, so event pairs time kernels, not host submission).
@@ -214,6 +220,15 @@ struct Att6Fused {
 };
 bool v6_att_fused_supported(const Att6Fused & a);
 bool launch_v6_att_fused(hipStream_t st, const Att6Fused & a);
+// v4 decode: LN + token shift, r / k / v rows and WKV-4 in one launch, 32 channels per workgroup
+// (mv_att4f.hip); the two-launch k_mv + k_wkv4 pair gives the same bits
+// (channels per workgroup v4_att_fused_cpw(): 32 emits Wo's Q8 input, 8 / 16 write it as fp32 y)
+int v4_att_fused_cpw();
+bool v4_att_fused_supported(int C, const DMat & Wr, const DMat & Wk, const DMat & Wv, const ActBuf & out);
+bool launch_v4_att_fused(hipStream_t st, int C, const DMat & Wr, const DMat & Wk, const DMat & Wv, const float * x,
+                         const float * carry, float * carry_out, const float * lnw, const float * lnb,
+                         const float * mix_r, const float * mix_k, const float * mix_v, const float * first,
+                         const float * decay, const float * sin, float * sout, const ActBuf & out, float * y);
 
 // Sequence v6 decay LoRA tail (T >= 2): w[t][c] = exp(-exp(Wd2[c] . Q8(dl[t]) + decay[c])) with
 // k_att6_dec's per-row arithmetic; dl fp32 [T][D].  Quantized Wd2 with D <= 512 only.

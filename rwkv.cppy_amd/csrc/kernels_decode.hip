@@ -40,7 +40,16 @@ void set_mv_device_cus(int n) {
     kQgCUs = g_mv_cus;
 }
 
+int mv_late_weights() {
+    static const int v = [] {
+        const char * e = getenv("RWKV_MI355X_LATE_W");
+        return e ? atoi(e) : 1;
+    }();
+    return v;
+}
+
 bool launch_mv_group(hipStream_t st, MVGroup & g) {
+    g.late = mv_late_weights();
     bool emit = false;
     for (int i = 0; i < g.n; i++) emit |= g.e[i].emit != 0;
     const int src = g.e[0].src, form = g.e[0].form;

@@ -1,0 +1,266 @@
+// mv_att4f.hip -- v4 decode: LayerNorm + token shift, the r, k, v matvecs and the WKV-4
+// recurrence (rwkv_graph.inc:253-304) in ONE launch.
+//
+// Before: one k_mv launch over the 3 C rows of r, k, v (LN prologue), then k_wkv4 (a second
+// launch that waits at the kernel boundary for every row although channel c only needs r[c],
+// k[c], v[c]).  WKV-4 is per channel, so workgroup b takes channels [32 b, 32 b + 32): it builds
+// the three token-shifted LayerNorm images itself (the k_mv prologue, once per workgroup), dots
+// its 32 rows of each matrix (8 waves x 4 rows x 3 matrices, exactly k_mv's lane/unit order,
+// wave_sum63 tree and epilogues, so r, k, v are bit-identical), runs k_wkv4's per-channel
+// arithmetic and emits the 32 outputs -- one quantization block of Wo's input -- with no
+// hand-off between workgroups at all.  Small models are launch-bound (v4-169M: 12 layers at
+// C = 768), so this removes one dependent launch per layer.
+#include "mv_common.hpp"
+
+#include <stdlib.h>
+#include <string.h>
+
+namespace rwkvmi {
+
+struct Att4Fused {
+    int C;
+    DMat W[3];                  // r, k, v (M = K = C)
+    const float * x;            // residual stream [C]
+    const float * carry;        // previous att_xx [C]
+    float * carry_out;          // new att_xx [C] (= LN(x)), written by workgroup 0
+    const float * lnw, * lnb;
+    const float * mix[3];       // time_mix_r, _k, _v [C]
+    const float * first, * decay;
+    const float * sin;          // layer state in: [aa | bb | pp] at 2C, 3C, 4C
+    float * sout;               // layer state out (same layout)
+    ActBuf out;                 // Wo's input (CPW = 32: emitted as Q8 blocks)
+    float * y;                  // Wo's input as fp32 (CPW < 32: Wo quantizes it in its prologue)
+    int img;                    // LDS bytes per activation image (16-aligned)
+};
+
+// 512 threads = 8 waves, CPW channels per workgroup.  Waves 4..7 build the three images (LayerNorm
+// statistics in the chunk association, one 512-element chunk per wave, token shift per mix,
+// quantization); every wave dots rows R w .. R w + R - 1 (R = CPW / 8) of each matrix within the
+// workgroup's channels; wave 0 (CPW lanes) runs the recurrence.  CPW = 32 emits Wo's input as one
+// Q8 block; smaller CPW (more workgroups streaming the rows) write it as fp32.
+template <int WF, int U, int CPW>
+__global__ __launch_bounds__(512) void k_v4_att_fused(Att4Fused a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    __shared__ float sr[CPW], sk[CPW], sv[CPW];
+    constexpr int R = CPW / 8, LCW = 1;
+    const int C = a.C, K = C, c0 = blockIdx.x * CPW;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool pro = wave >= 4;
+    const int pw = wave - 4, nch = (K + LN_CHUNK - 1) / LN_CHUNK;
+    STAMP_BEGIN();
+    const ActBuf ao = a.out;
+    pin_act(ao);
+    MVEntry E;
+    E.x = a.x;
+    E.carry = a.carry;
+    E.lnw = a.lnw;
+    E.lnb = a.lnb;
+    E.mu = a.mix[0];
+    E.carry_out = a.carry_out;
+    E.f = nullptr;
+    // image inputs (chunk pw of x, carry, LN weights, mix r) and mixes k, v: every wave issues
+    // the loads without a branch (chunk_load_all), the dot waves' are empty
+    ChunkIn ci[LCW];
+    float mk[8], mv[8];
+    const int kc = max(min(pw * LN_CHUNK + lane * 8, K - 8), 0);
+    const bool kval = pro && pw * LN_CHUNK + lane * 8 < K;
+    chunk_load_all<MVK_LN, 0>(E, kc, ci[0], pro);
+    ld8_buf(mk, a.mix[1], kc, pro);
+    ld8_buf(mv, a.mix[2], kc, pro);
+    asm volatile("" ::"s"(a.W[0].qs), "s"(a.W[1].qs), "s"(a.W[2].qs));
+    asm volatile("s_barrier" ::: "memory");  // image inputs issued ahead of the weight stream
+    // ---- rows c0 + 4 wave + r of r, k, v (all waves)
+    WBlk w[3][R][U];
+#pragma unroll
+    for (int m = 0; m < 3; m++)
+#pragma unroll
+        for (int u = 0; u < U; u++)
+#pragma unroll
+            for (int r = 0; r < R; r++) w[m][r][u] = load_unit<WF>(a.W[m], min(c0 + R * wave + r, C - 1), u, lane);
+    // the recurrence's operands (wave 0, lane = channel)
+    float aa = 0.0f, bb = 0.0f, pp = 0.0f, fi = 0.0f, de = 0.0f;
+    if (wave == 0 && lane < CPW) {
+        const int c = min(c0 + lane, C - 1);
+        aa = a.sin[2 * C + c];
+        bb = a.sin[3 * C + c];
+        pp = a.sin[4 * C + c];
+        fi = a.first[c];
+        de = a.decay[c];
+    }
+    ActBuf img[3];
+#pragma unroll
+    for (int m = 0; m < 3; m++) img[m] = lds_act(smem + m * a.img, act_fmt_for(WF), K);
+    if (pro) {
+        // LayerNorm statistics (chunk association, one pass); the chunk sums meet in LDS
+        __shared__ double ln_part[2][8];
+        if (pw < nch) {
+            double c1, c2;
+            ln_chunk_sums(ci[0].x, kval, c1, c2);
+            if (lane == 0) {
+                ln_part[0][pw] = c1;
+                ln_part[1][pw] = c2;
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        double s1 = 0.0, s2 = 0.0;
+        for (int q = 0; q < nch; q++) s1 += ln_part[0][q], s2 += ln_part[1][q];
+        float mean, scale;
+        ln_finish(s1, s2, K, 1e-5f, mean, scale);
+        if (pw < nch) {
+            const bool wc = blockIdx.x == 0;
+            chunk_store<WF, MVK_LN, 0>(E, img[0], ci[0], mean, scale, wc, kc, kval, lane);
+#pragma unroll
+            for (int j = 0; j < 8; j++) ci[0].m[j] = mk[j];
+            chunk_store<WF, MVK_LN, 0>(E, img[1], ci[0], mean, scale, false, kc, kval, lane);
+#pragma unroll
+            for (int j = 0; j < 8; j++) ci[0].m[j] = mv[j];
+            chunk_store<WF, MVK_LN, 0>(E, img[2], ci[0], mean, scale, false, kc, kval, lane);
+        }
+    } else {
+        asm volatile("s_barrier" ::: "memory");  // the image waves' statistics exchange
+    }
+    __syncthreads();  // (1) images ready
+    if (wave == 0) STAMP_MID();
+    const int units = mv_units(WF, K);
+    constexpr bool one = WF == W_Q4_1 || WF == W_Q5_1;
+#pragma unroll
+    for (int m = 0; m < 3; m++) {
+        float acc[R], acc2[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) acc[r] = acc2[r] = 0.0f;
+        for (int u0 = 0; u0 < units; u0 += U) {
+            if (u0 > 0) {
+#pragma unroll
+                for (int u = 0; u < U; u++)
+#pragma unroll
+                    for (int r = 0; r < R; r++) w[m][r][u] = load_unit<WF>(a.W[m], min(c0 + R * wave + r, C - 1), u0 + u, lane);
+            }
+            AUnit xu[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) xu[u] = load_act_unit<WF, true>(img[m], u0 + u, lane);
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                if (unit_valid<WF>(K, u0 + u, lane)) {
+#pragma unroll
+                    for (int r = 0; r < R; r++) dot_unit<WF>(w[m][r][u], xu[u], acc[r], acc2[r]);
+                }
+            }
+        }
+        float s[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) s[r] = one ? wave_sum63(acc[r]) + wave_sum63(acc2[r]) : wave_sum63(acc[r]) + 0.0f;
+        const float v = lane_row_sum<R>(s, lane);  // lane r: row R wave + r
+        float * dst = m == 0 ? sr : m == 1 ? sk : sv;
+        if (lane < R) dst[R * wave + lane] = m == 0 ? sigmoidf_(v) : v;  // r: EPI_SIGMOID
+    }
+    __syncthreads();  // (2) r, k, v of the workgroup's channels ready
+    if (wave == 0) {
+        STAMP_X(0);
+        if (lane < CPW) {
+            // k_wkv4's arithmetic, in its order
+            const int c = c0 + lane;
+            const float kt = sk[lane], vt = sv[lane];
+            float ww = fi + kt;
+            float qq = fmaxf(pp, ww);
+            float e1 = rk_expf(pp - qq), e2 = rk_expf(ww - qq);
+            const float an = e1 * aa + e2 * vt;
+            const float bn = e1 * bb + e2;
+            ww = pp + de;
+            qq = fmaxf(ww, kt);
+            e1 = rk_expf(ww - qq);
+            e2 = rk_expf(kt - qq);
+            aa = e1 * aa + e2 * vt;
+            bb = e1 * bb + e2;
+            pp = qq;
+            const float y = sr[lane] * (an / bn);
+            if constexpr (CPW == 32) emit32(ao, 0, c, y);  // lanes 0..31: one quantization block
+            else a.y[c] = y;
+            if (c < C) {
+                a.sout[2 * C + c] = aa;
+                a.sout[3 * C + c] = bb;
+                a.sout[4 * C + c] = pp;
+            }
+        }
+    }
+    STAMP_END(8);
+}
+
+// channels per workgroup: RWKV_MI355X_ATT4_FUSED = 32 / 16 / 8, 0 = the two-launch form
+int v4_att_fused_cpw() {
+    static const int v = [] {
+        const char * e = getenv("RWKV_MI355X_ATT4_FUSED");
+        const int c = e ? atoi(e) : 8;
+        return c == 32 || c == 16 || c == 8 ? c : 0;
+    }();
+    return v;
+}
+
+bool v4_att_fused_supported(int C, const DMat & Wr, const DMat & Wk, const DMat & Wv, const ActBuf & out) {
+    const int cpw = v4_att_fused_cpw();
+    if (!cpw || C % 32 || C > 2048 || (cpw == 32 && (out.fmt < 0 || out.tiled))) return false;
+    const int t = Wr.type;
+    if (t < 0 || Wk.type != t || Wv.type != t || mv_units(t, C) > 2) return false;
+    for (const DMat * W : {&Wr, &Wk, &Wv})
+        if ((int)W->M != C || (int)W->K != C) return false;
+    return true;
+}
+
+template <int WF, int CPW>
+static void launch_att4_c(hipStream_t st, const Att4Fused & a, int units) {
+    const int lds = 3 * a.img;
+    if (units <= 1) RK_LAUNCH((k_v4_att_fused<WF, 1, CPW>), dim3(a.C / CPW), dim3(512), lds, st, a);
+    else RK_LAUNCH((k_v4_att_fused<WF, 2, CPW>), dim3(a.C / CPW), dim3(512), lds, st, a);
+}
+template <int WF>
+static void launch_att4_t(hipStream_t st, const Att4Fused & a, int units) {
+    const int cpw = v4_att_fused_cpw();
+    if (cpw == 32) launch_att4_c<WF, 32>(st, a, units);
+    else if (cpw == 16) launch_att4_c<WF, 16>(st, a, units);
+    else launch_att4_c<WF, 8>(st, a, units);
+}
+
+bool launch_v4_att_fused(hipStream_t st, int C, const DMat & Wr, const DMat & Wk, const DMat & Wv, const float * x,
+                         const float * carry, float * carry_out, const float * lnw, const float * lnb,
+                         const float * mix_r, const float * mix_k, const float * mix_v, const float * first,
+                         const float * decay, const float * sin, float * sout, const ActBuf & out, float * y) {
+    if (!v4_att_fused_supported(C, Wr, Wk, Wv, out)) {
+        fprintf(stderr, "rwkv: fused v4 attention decode: unsupported shape (C %d)\n", C);
+        return false;
+    }
+    Att4Fused a;
+    memset(&a, 0, sizeof(a));
+    a.C = C;
+    a.W[0] = Wr;
+    a.W[1] = Wk;
+    a.W[2] = Wv;
+    a.x = x;
+    a.carry = carry;
+    a.carry_out = carry_out;
+    a.lnw = lnw;
+    a.lnb = lnb;
+    a.mix[0] = mix_r;
+    a.mix[1] = mix_k;
+    a.mix[2] = mix_v;
+    a.first = first;
+    a.decay = decay;
+    a.sin = sin;
+    a.sout = sout;
+    a.out = out;
+    a.y = y;
+    a.img = (lds_bytes_for(act_fmt_for(Wr.type), C) + 15) & ~15;
+    const int units = mv_units(Wr.type, C);
+    switch (Wr.type) {
+        case W_F32: launch_att4_t<W_F32>(st, a, units); break;
+        case W_F16: launch_att4_t<W_F16>(st, a, units); break;
+        case W_Q4_0: launch_att4_t<W_Q4_0>(st, a, units); break;
+        case W_Q4_1: launch_att4_t<W_Q4_1>(st, a, units); break;
+        case W_Q5_0: launch_att4_t<W_Q5_0>(st, a, units); break;
+        case W_Q5_1: launch_att4_t<W_Q5_1>(st, a, units); break;
+        case W_Q8_0: launch_att4_t<W_Q8_0>(st, a, units); break;
+        default: return false;
+    }
+    HIP_OK(hipGetLastError());
+    return true;
+}
+
+}  // namespace rwkvmi

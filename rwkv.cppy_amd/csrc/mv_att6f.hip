@@ -6,16 +6,15 @@
 // own 64 channels of r, k, v, g -- plus the D decay-LoRA values every head shares).  Here the
 // grid is 8 workgroups per head: workgroup (h, s) computes 32 of head h's 256 r/k/v/g rows (4
 // waves x 8 rows, exactly k_mva's lane/unit order, wave_sum63 tree and epilogues, so the values
-// are bit-identical) and, on a fifth wave, the decay-LoRA rows of its slot (non-reducers first).  The rows are
-// published write-through (sc1 stores, every storing wave drained, then one agent-scope counter
-// add per workgroup: MI355X_MICROARCH.md "Valid forms", row 1), and workgroup (h, 0) -- which
-// loaded the head's state, decay-tail weights and per-channel operands while its own rows
-// streamed -- waits for its head's 8 arrivals and the D decay rows, reads them with sc1 loads and
-// runs k_att6_dec's arithmetic (decay tail, wkv6, GroupNorm, gate, Q8 emission of Wo's input).
-// The waiting workgroups are producers first, so the wait can never hold a slot a producer
-// needs; every spin is bounded (a timeout sets *err and the results are garbage, never a hang).
-// Counters are re-armed inside the launch by their last readers, so a replayed graph needs no
-// memset node.
+// are bit-identical) and, on a fifth wave, the decay-LoRA rows of its slot (non-reducers first).
+// Every row is published as a granule (value + tag in one 8-byte write-through store, below); a
+// decay-LoRA value once per head, so each head owns its copy.  Workgroup (h, 0) -- which loaded
+// the head's state, decay-tail weights and per-channel operands while its own rows streamed --
+// sweeps its head's granules and runs k_att6_dec's arithmetic (decay tail, wkv6, GroupNorm, gate,
+// Q8 emission of Wo's input).  The waiting workgroups are producers first, so the wait can never
+// hold a slot a producer needs; every spin is bounded (a timeout sets *err and the results are
+// garbage, never a hang).  Each granule has exactly one reader, which clears it right after
+// reading: no counters, no atomics, and a replayed graph needs no memset node.
 //
 // The state update uses 16-byte accesses: wave g owns keys 16g..16g+15, lane (kk, jq) keys
 // 16g + 4kk + q (q < 4) of value columns 4jq..4jq+3.  Each output column's sum keeps
@@ -135,7 +134,7 @@ __global__ __launch_bounds__(320) void k_v6_att_fused(Att6Fused a) {
     __shared__ __attribute__((aligned(16))) float part[16][64];
     constexpr int S = 64;
     const int wg = (int)blockIdx.x, h = wg / AF_P, sidx = wg % AF_P, H = a.H, C = a.C, D = a.D;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform branches
     const bool red = sidx == 0;
     const int c0 = h * S;
     const Att6Dec & at = a.att;
@@ -145,12 +144,11 @@ __global__ __launch_bounds__(320) void k_v6_att_fused(Att6Fused a) {
     STAMP_BEGIN();
     // the reducer's late scalars (Wo input record, hand-off words, eps) in SGPRs now
     const ActBuf yq = at.yq;
-    unsigned * const cnt = a.cnt;
     unsigned * const err = a.err;
     const float eps = at.eps;
     if (red) {
         pin_act(yq);
-        asm volatile("" ::"s"(cnt), "s"(err), "s"(eps));
+        asm volatile("" ::"s"(err), "s"(eps));
     }
     // ---- the reducer's head operands first (state rows, per-channel vectors, decay-tail weights):
     // they stream in with this workgroup's own weight rows
@@ -186,8 +184,9 @@ __global__ __launch_bounds__(320) void k_v6_att_fused(Att6Fused a) {
         if (lane < AF_R) gran_put(a.gran + (size_t)m * C + row0 + lane, v);
     } else {
         for (int d = af_slot(sidx, h, H); d < D; d += AF_P * H) {
-            const float v = af_rows<WF, 1, U>(a.wd1, a.xw, d, EPI_TANH, lane);
-            if (lane == 0) gran_put(gdl + d, v);
+            const float v = af_rows<WF, 1, U>(a.wd1, a.xw, d, EPI_TANH, lane);  // in lane 0
+            const float v0 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+            if (lane < H) gran_put(gdl + (size_t)lane * D + d, v0);  // one copy per head
         }
     }
     if (!red) {
@@ -211,16 +210,10 @@ __global__ __launch_bounds__(320) void k_v6_att_fused(Att6Fused a) {
     } else {
         bool live[2] = {lane < D, lane + 64 < D};
         float v[2];
-        gran_sweep<2>(gdl + lane, 64, live, v, err);
-        // every head reads the decay values: the last reader clears them
-        unsigned n = 0;
-        if (lane == 0) n = addu(cnt, 1u);
-        n = (unsigned)__shfl((int)n, 0);
-        if (n == (unsigned)H - 1) {
-            if (lane < D) gran_clear(gdl + lane);
-            if (lane + 64 < D) gran_clear(gdl + lane + 64);
-            if (lane == 0) stu_sc1(cnt, 0u);
-        }
+        unsigned long long * const own = gdl + (size_t)h * D + lane;  // this head's copy
+        gran_sweep<2>(own, 64, live, v, err);
+        if (live[0]) gran_clear(own);
+        if (live[1]) gran_clear(own + 64);
         const ActBuf act = lds_act(smem, act_fmt_for(WD), D);
         if (lane < D) emit32(act, 0, lane, v[0]);  // lanes 0..31 / 32..63: whole quantization blocks
         if (lane + 64 < D) emit32(act, 0, lane + 64, v[1]);
@@ -298,7 +291,7 @@ bool v6_att_fused_supported(const Att6Fused & a) {
     if (!wtype_quantized(a.att.wd2.type) || a.att.wd2.M != a.C || a.att.wd2.K != a.D) return false;
     // the decay tail's PF = 4 units per row and one emission half-wave per 32 decay rows
     if (a.D % 32 || a.D > 128) return false;  // two granules per lane of the sweeping wave
-    return a.cnt && a.err;
+    return a.H <= 64 && a.err;  // one decay-value copy per head: a lane per head
 }
 
 template <int WF, int U>

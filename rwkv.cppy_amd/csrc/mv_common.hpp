@@ -212,6 +212,34 @@ __device__ __forceinline__ void chunk_load(const MVEntry & E, int kc, ChunkIn & 
     }
 }
 
+// chunk_load for a whole workgroup without a branch: every wave issues the same raw buffer
+// loads, and the waves that do not build the image (on = false, wave-uniform) get descriptors
+// with no records, so their loads return zeros without touching memory.  A branch around the
+// loads would make the compiler copy the loaded registers at the join -- copies that wait for
+// the loads to ARRIVE, ahead of the issue-order barrier that releases the weight stream.
+__device__ __forceinline__ void ld8_buf(float (&v)[8], const float * p, int kc, bool on) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)p, 0, on ? 0x7fffffff : 0, 0x00020000);
+    typedef float v4f_t __attribute__((ext_vector_type(4)));
+    const v4f_t t0 = __builtin_amdgcn_raw_buffer_load_b128(r, kc * 4, 0, 0);
+    const v4f_t t1 = __builtin_amdgcn_raw_buffer_load_b128(r, kc * 4 + 16, 0, 0);
+    v[0] = t0.x, v[1] = t0.y, v[2] = t0.z, v[3] = t0.w, v[4] = t1.x, v[5] = t1.y, v[6] = t1.z, v[7] = t1.w;
+}
+
+template <int SRCK, int FORM>
+__device__ __forceinline__ void chunk_load_all(const MVEntry & E, int kc, ChunkIn & ci, bool on) {
+    if constexpr (SRCK == MVK_F32) {
+        ld8_buf(ci.x, E.f, kc, on);
+    } else {
+        ld8_buf(ci.x, E.x, kc, on);
+        ld8_buf(ci.w, E.lnw, kc, on);
+        ld8_buf(ci.b, E.lnb, kc, on);
+        if constexpr (FORM != 2) {
+            ld8_buf(ci.c, E.carry, kc, on);
+            ld8_buf(ci.m, E.mu, kc, on);
+        }
+    }
+}
+
 template <int WF, int SRCK, int FORM>
 __device__ __forceinline__ void chunk_store(const MVEntry & E, const ActBuf & a, const ChunkIn & ci, float mean,
                                             float scale, bool write_carry, int k0, bool valid, int lane) {
@@ -359,24 +387,25 @@ __device__ __forceinline__ float decay_row_thread(const DMat & W, int row, const
     return one ? tree_wave32(p) + tree_wave32(p2) : tree_wave32(p) + 0.0f;
 }
 
-// One workgroup = NW waves (SRC_ACT) or 2 NW waves (prologue sources) x R rows each; RW rows per
-// row block.  stride > 0: the workgroup walks row blocks wgi, wgi+stride, ... with one prologue.
-// Prologue sources (SRC_F32 / SRC_LNMIX): waves NW..2NW-1 also build the activation image in LDS
+// One workgroup = NW waves (SRC_ACT) or 2 NW waves (prologue sources); RW rows per row block.
+// stride > 0: the workgroup walks row blocks wgi, wgi+stride, ... with one prologue.
+// Prologue sources (SRC_F32 / SRC_LNMIX): waves NW..2NW-1 build the activation image in LDS
 // (LayerNorm statistics, one 512-element chunk each, token shift, quantization); their input
-// loads go out first (issue-order barrier), their weight loads right behind them -- vmcnt is in
-// order per wave, so the LayerNorm waits only for the inputs -- and after the image is ready
-// every wave dots its own R rows: the rows of a block are spread over all 2 NW waves, so the
-// per-wave dot and reduction chains are half as long as with the image waves idle.
+// loads go out first (issue-order barrier) and the streaming waves' weight loads right behind
+// them, then the streaming waves dot the block's rows once the image is ready.
 template <int WF, int R, int U, int SRCK, int FORM, bool EMIT, int NW, int LNP>
 __device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, int b0, int stride, char * smem, float * red,
-                                        unsigned long long * stamp_mid = nullptr,
+                                        int late, unsigned long long * stamp_mid = nullptr,
                                         unsigned long long * stamp_x = nullptr) {
     constexpr bool PRO = SRCK != MVK_ACT;
     // LayerNorm chunks per prologue wave held in registers: LNP 32 -> K <= 2048, 64 -> K <= 4096
     constexpr int LCW = LNP > 32 ? 2 : 1;
+    // Prologue groups: the rows of a block over all 2 NW waves (the image waves too: the per-wave
+    // dot and reduction chains are half as long as with the image waves idle).
     constexpr int NWT = PRO ? 2 * NW : NW;  // waves with rows
-    constexpr int RW = NWT * R;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    constexpr int RR = R;                   // rows per wave
+    constexpr int RW = NWT * RR;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform branches
     const DMat & W = Ent.W;
     const int M = W.M, K = W.K;
     const int nblk = (M + RW - 1) / RW;
@@ -399,38 +428,36 @@ __device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, int b0, in
     float mean = 0.0f, scale = 0.0f;
     if constexpr (PRO) {
         a = lds_act(smem, act_fmt_for(WF), K);
-        if (pro_wave) {
-            // the image wave's inputs: chunks pw, pw + NW (512 elements each, 8 per lane)
+        // the image waves' inputs: chunks pw, pw + NW (512 elements each, 8 per lane); issued
+        // by every wave without a branch (chunk_load_all: the dot waves' loads are empty)
 #pragma unroll
-            for (int q = 0; q < LCW; q++) {
-                kc[q] = (pw + q * NW) * LN_CHUNK + lane * 8;
-                chunk_load<SRCK, FORM>(Ent, min(kc[q], K - 8), ci[q]);
-            }
-        } else {
-            // the weight pointers reach SGPRs before the issue-order barrier, so the stream starts
-            // right after it (a kernarg scalar load behind the barrier is a round trip in the path)
-            asm volatile("" ::"s"(W.qs), "s"(W.sc), "s"(W.qh));
+        for (int q = 0; q < LCW; q++) {
+            kc[q] = (pw + q * NW) * LN_CHUNK + lane * 8;
+            chunk_load_all<SRCK, FORM>(Ent, max(min(kc[q], K - 8), 0), ci[q], pro_wave);
         }
-        // issue order: the image inputs go out before any weight stream starts, so they are not
-        // queued behind megabytes of weights in the memory system; no wait on them here
+        // the weight pointers reach SGPRs before the issue-order barrier, so the stream starts
+        // right after it (a kernarg scalar load behind the barrier is a round trip in the path)
+        asm volatile("" ::"s"(W.qs), "s"(W.sc), "s"(W.qh));
+        // issue order: the image inputs go out before any weight stream starts, and (late) have
+        // landed before it starts: measured, a weight stream issued right behind them delays the
+        // image by more than the late start costs the rows (v6-1B6 decode 691.7 vs 700 us/token)
+        if (late && pro_wave) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         asm volatile("s_barrier" ::: "memory");
-#ifdef RWKV_STAMP
-        if (pw == 0 && stamp_x) {
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-            if (lane == 0) stamp_x[0] = __builtin_amdgcn_s_memrealtime();
-        }
-#endif
     }
     // ---- this wave's weight units (HBM), all in flight before anything waits
-    int row0 = wgi * RW + wave * R;
-    int rows[R];
+    constexpr bool has_rows = true;
+    int row0 = wgi * RW + wave * RR;
+    int rows[RR];
 #pragma unroll
-    for (int r = 0; r < R; r++) rows[r] = min(row0 + r, M - 1);
-    WBlk w[R][U];
+    for (int r = 0; r < RR; r++) rows[r] = min(row0 + r, M - 1);
+    WBlk w[RR][U];
+    auto issue_w = [&]() {
 #pragma unroll
-    for (int u = 0; u < U; u++)
+        for (int u = 0; u < U; u++)
 #pragma unroll
-        for (int r = 0; r < R; r++) w[r][u] = load_unit<WF>(W, rows[r], u, lane);
+            for (int r = 0; r < RR; r++) w[r][u] = load_unit<WF>(W, rows[r], u, lane);
+    };
+    issue_w();
     if constexpr (PRO) {
         if (pro_wave) {
             if constexpr (SRCK == MVK_LN) {
@@ -479,7 +506,7 @@ __device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, int b0, in
     }
     // epilogue operands: !EMIT lane r < R runs row row0 + r's epilogue; EMIT thread tid < RW row tid
     EpiIn ep;
-    if constexpr (!EMIT) ep = epi_load(Ent, min(row0 + min(lane, R - 1), M - 1));
+    if constexpr (!EMIT) ep = epi_load(Ent, min(row0 + min(lane, RR - 1), M - 1));
     else ep = epi_load(Ent, min(wgi * RW + (tid < RW ? tid : 0), M - 1));
     if constexpr (PRO) __syncthreads();  // activation image ready
     else a = Ent.act;
@@ -492,47 +519,51 @@ __device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, int b0, in
 #endif
 
     for (;;) {
-        // dots
-        float acc[R], acc2[R];
+        // dots (the waves with rows)
+        constexpr bool one = WF == W_Q4_1 || WF == W_Q5_1;
+        float s[RR];
+        if (has_rows) {
+            float acc[RR], acc2[RR];
 #pragma unroll
-        for (int r = 0; r < R; r++) acc[r] = acc2[r] = 0.0f;
-        for (int u0 = 0; u0 < units; u0 += U) {
-            if (u0 > 0) {
+            for (int r = 0; r < RR; r++) acc[r] = acc2[r] = 0.0f;
+            for (int u0 = 0; u0 < units; u0 += U) {
+                if (u0 > 0) {
 #pragma unroll
-                for (int u = 0; u < U; u++)
+                    for (int u = 0; u < U; u++)
 #pragma unroll
-                    for (int r = 0; r < R; r++) w[r][u] = load_unit<WF>(W, rows[r], u0 + u, lane);
-            }
-            AUnit x[U];
+                        for (int r = 0; r < RR; r++) w[r][u] = load_unit<WF>(W, rows[r], u0 + u, lane);
+                }
+                AUnit x[U];
 #pragma unroll
-            for (int u = 0; u < U; u++) x[u] = load_act_unit<WF, PRO>(a, u0 + u, lane);
+                for (int u = 0; u < U; u++) x[u] = load_act_unit<WF, PRO>(a, u0 + u, lane);
 #pragma unroll
-            for (int u = 0; u < U; u++) {
-                if (unit_valid<WF>(K, u0 + u, lane)) {
+                for (int u = 0; u < U; u++) {
+                    if (unit_valid<WF>(K, u0 + u, lane)) {
 #pragma unroll
-                    for (int r = 0; r < R; r++) dot_unit<WF>(w[r][u], x[u], acc[r], acc2[r]);
+                        for (int r = 0; r < RR; r++) dot_unit<WF>(w[r][u], x[u], acc[r], acc2[r]);
+                    }
                 }
             }
-        }
-
-        // reduce + epilogue
-        constexpr bool one = WF == W_Q4_1 || WF == W_Q5_1;
-        float s[R];
+            // reduce
 #pragma unroll
-        for (int r = 0; r < R; r++) s[r] = one ? wave_sum63(acc[r]) + wave_sum63(acc2[r]) : wave_sum63(acc[r]) + 0.0f;
+            for (int r = 0; r < RR; r++) s[r] = one ? wave_sum63(acc[r]) + wave_sum63(acc2[r]) : wave_sum63(acc[r]) + 0.0f;
+        } else {
+#pragma unroll
+            for (int r = 0; r < RR; r++) s[r] = 0.0f;
+        }
         if constexpr (!EMIT) {
 #ifdef MV_PROBE
             if (s[0] == 1.2345f) g_probe[0] = 0;  // orders the stamp after the dots
 #endif
             PROBE(2);
-            const float v = epi_apply(epi, lane_row_sum<R>(s, lane), ep);
-            if (lane < R && row0 + lane < M) ey[row0 + lane] = v;
+            const float v = epi_apply(epi, lane_row_sum<RR>(s, lane), ep);
+            if (has_rows && lane < RR && row0 + lane < M) ey[row0 + lane] = v;
         } else {
             // RW rows per block (a multiple of 32): apply the epilogue and emit each 32 rows as
             // one quantization block of the next matmul's input (ggml Q8 / fp16 / fp32)
 #pragma unroll
-            for (int r = 0; r < R; r++)
-                if (lane == 63) red[wave * R + r] = s[r];
+            for (int r = 0; r < RR; r++)
+                if (has_rows && lane == 63) red[wave * RR + r] = s[r];
 #ifdef RWKV_STAMP
             if (wave == 0 && stamp_x && lane == 0) stamp_x[3] = __builtin_amdgcn_s_memrealtime() + (s[0] == 1.2345f);
 #endif
@@ -552,14 +583,11 @@ __device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, int b0, in
         wgi += stride;
         if (stride <= 0 || wgi >= nblk) break;
         if constexpr (EMIT) __syncthreads();  // red[] reuse
-        row0 = wgi * RW + wave * R;
+        row0 = wgi * RW + wave * RR;
 #pragma unroll
-        for (int r = 0; r < R; r++) rows[r] = min(row0 + r, M - 1);
-#pragma unroll
-        for (int u = 0; u < U; u++)
-#pragma unroll
-            for (int r = 0; r < R; r++) w[r][u] = load_unit<WF>(W, rows[r], u, lane);
-        if constexpr (!EMIT) ep = epi_load(Ent, min(row0 + min(lane, R - 1), M - 1));
+        for (int r = 0; r < RR; r++) rows[r] = min(row0 + r, M - 1);
+        if (has_rows) issue_w();
+        if constexpr (!EMIT) ep = epi_load(Ent, min(row0 + min(lane, RR - 1), M - 1));
         else ep = epi_load(Ent, min(wgi * RW + (tid < RW ? tid : 0), M - 1));
     }
     if constexpr (SRCK == MVK_LN && FORM != 2) {
@@ -606,16 +634,16 @@ __global__ __launch_bounds__(512) void k_mv(int b1, int b2, int b3, int b4, int 
     unsigned long long * sx = nullptr;
 #endif
     if constexpr (WFIX >= 0) {
-        mv_body<WFIX, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red, smid, sx);
+        mv_body<WFIX, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red, g.late, smid, sx);
     } else {
         switch (Ent.W.type) {
-            case W_F32: mv_body<W_F32, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red); break;
-            case W_F16: mv_body<W_F16, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red); break;
-            case W_Q4_0: mv_body<W_Q4_0, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red); break;
-            case W_Q4_1: mv_body<W_Q4_1, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red); break;
-            case W_Q5_0: mv_body<W_Q5_0, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red); break;
-            case W_Q5_1: mv_body<W_Q5_1, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red); break;
-            case W_Q8_0: mv_body<W_Q8_0, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red); break;
+            case W_F32: mv_body<W_F32, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red, g.late); break;
+            case W_F16: mv_body<W_F16, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red, g.late); break;
+            case W_Q4_0: mv_body<W_Q4_0, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red, g.late); break;
+            case W_Q4_1: mv_body<W_Q4_1, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red, g.late); break;
+            case W_Q5_0: mv_body<W_Q5_0, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red, g.late); break;
+            case W_Q5_1: mv_body<W_Q5_1, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red, g.late); break;
+            case W_Q8_0: mv_body<W_Q8_0, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red, g.late); break;
             default: break;
         }
     }

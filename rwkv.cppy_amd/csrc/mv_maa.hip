@@ -26,6 +26,7 @@ struct MaaDec {
     const float * maa[5];       // time_maa_{w,k,v,r,g} [C]
     ActBuf out[5];
     int xa_off;                 // LDS byte offset of the fp32 xa image
+    int late;                   // mv_late_weights(): W1 rows issued after the image inputs land
 };
 
 // 512 threads.  Waves 4..7 build the activation image (LayerNorm + token shift + quantization,
@@ -38,7 +39,7 @@ __global__ __launch_bounds__(512) void k_v6_maa_dec(MaaDec a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ float s_lora[64];
     const int n = blockIdx.y, C = a.C, D = a.D, K = C;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform branches
     const bool pro = wave >= 4;
     const int pw = wave - 4;
     const ActBuf act = lds_act(smem, act_fmt_for(WF), K);
@@ -60,18 +61,15 @@ __global__ __launch_bounds__(512) void k_v6_maa_dec(MaaDec a) {
     const int nch = (K + LN_CHUNK - 1) / LN_CHUNK;
     ChunkIn ci[LCW];
     int kc[LCW];
-    if (pro) {
-        // chunks pw, pw + 4 of the LayerNorm input (512 elements each, 8 per lane)
+    // chunks pw, pw + 4 of the LayerNorm input (512 elements each, 8 per lane); issued by every
+    // wave without a branch (chunk_load_all: the mix waves' loads are empty)
 #pragma unroll
-        for (int q = 0; q < LCW; q++) {
-            kc[q] = (pw + 4 * q) * LN_CHUNK + lane * 8;
-            chunk_load<MVK_LN, 1>(E, min(kc[q], K - 8), ci[q]);
-        }
-    } else {
-        asm volatile("" ::"s"(a.w1.qs), "s"(a.w1.sc), "s"(a.w1.qh));  // pointers before the barrier
+    for (int q = 0; q < LCW; q++) {
+        kc[q] = (pw + 4 * q) * LN_CHUNK + lane * 8;
+        chunk_load_all<MVK_LN, 1>(E, max(min(kc[q], K - 8), 0), ci[q], pro);
     }
+    asm volatile("" ::"s"(a.w1.qs), "s"(a.w1.sc), "s"(a.w1.qh));  // pointers before the barrier
     asm volatile("s_barrier" ::: "memory");  // image inputs issued ahead of the weight stream
-    if (pw == 0) STAMP_X(0);
     // ---- rows n*D + wave*R + r of W1 (all waves)
     const int units = mv_units(WF, K);
     const int row0 = n * D + wave * R, rlast = n * D + D - 1;
@@ -83,12 +81,28 @@ __global__ __launch_bounds__(512) void k_v6_maa_dec(MaaDec a) {
     for (int u = 0; u < U; u++)
 #pragma unroll
         for (int r = 0; r < R; r++) w[r][u] = load_unit<WF, false>(W, rows[r], u, lane);
-    // this thread's mix channel (waves 0..3): W2 column, carry, maa
+    if (pw == 0) STAMP_XN(0);  // weights issued
+    // this thread's mix channel (waves 0..3): W2 column, carry, maa.  Issued by every wave without
+    // a branch, the image waves' descriptors empty (as chunk_load_all): loads on one side of a
+    // branch make the compiler's wait counts at the join conservative -- the image waves would
+    // wait for their whole weight stream before the LayerNorm statistics.  Rows i >= D of the
+    // column repeat row D - 1; the mix chain skips them.
     const int c = blockIdx.x * CPW + tid;
     const bool cval = tid < CPW && (int)(blockIdx.x * CPW + (tid & ~31)) < C;  // half-wave uniform
     const int cc = min(c, C - 1);
     float w2v[DM];
-    float carry_c = 0.0f, mu_c = 0.0f;
+    float carry_c, mu_c;
+    {
+        const int on = pro ? 0 : 0x7fffffff;
+        const __amdgpu_buffer_rsrc_t r2 = __builtin_amdgcn_make_buffer_rsrc((void *)(a.w2t + (size_t)n * D * C), 0, on, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < DM; i++)
+            w2v[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r2, (min(i, D - 1) * C + cc) * 4, 0, 0));
+        const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc((void *)a.carry, 0, on, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc((void *)a.maa[n], 0, on, 0x00020000);
+        carry_c = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rc, cc * 4, 0, 0));
+        mu_c = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rm, cc * 4, 0, 0));
+    }
     if (pro) {
         // LayerNorm statistics, chunk association, one pass (device_common.hpp); every wave joins
         // the exchange barrier
@@ -121,16 +135,8 @@ __global__ __launch_bounds__(512) void k_v6_maa_dec(MaaDec a) {
             }
             chunk_store<WF, MVK_LN, 1>(E, act, ci[q], mean, scale, write_carry, kc[q], kc[q] < K, lane);
         }
-        if (pw == 0) STAMP_X(2);
+        if (pw == 0) STAMP_XN(2);
     } else {
-        const float * w2 = a.w2t + (size_t)n * D * C + cc;
-#pragma unroll
-        for (int i = 0; i < DM; i++) {
-            const float t = w2[(size_t)min(i, D - 1) * C];
-            w2v[i] = (i < D) ? t : 0.0f;
-        }
-        carry_c = a.carry[cc];
-        mu_c = a.maa[n][cc];
         asm volatile("s_barrier" ::: "memory");  // the image waves' statistics exchange
     }
     __syncthreads();  // (1) activation image ready
@@ -177,6 +183,147 @@ __global__ __launch_bounds__(512) void k_v6_maa_dec(MaaDec a) {
     STAMP_END_NS(4 + 16 * blockIdx.y);
 }
 
+// D <= 32: the image waves have no rows.  The two roles run as separate straight paths that meet
+// only at the barriers: waves 4..7 load the image inputs, compute the LayerNorm statistics (no
+// weight load ahead of them in their instruction stream: a load's issue blocks the wave once the
+// CU's share of the memory system is saturated) and store the images; waves 0..3 issue their
+// R = 8 W1 rows and their W2 columns at once, dot the rows after the image barrier and mix.
+// Same arithmetic and association as k_v6_maa_dec (bit-identical).
+template <int WF, int U, int LNP, int CPW>
+__global__ __launch_bounds__(512) void k_v6_maa_dec4(MaaDec a) {
+    constexpr int R = 8, DM = 32;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    __shared__ float s_lora[64];
+    __shared__ double ln_part[2][8];
+    const int n = blockIdx.y, C = a.C, D = a.D, K = C;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const ActBuf act = lds_act(smem, act_fmt_for(WF), K);
+    float * s_xa = (float *)(smem + a.xa_off);
+    STAMP_BEGIN();
+    constexpr int LCW = LNP > 32 ? 2 : 1;
+    const int nch = (K + LN_CHUNK - 1) / LN_CHUNK;
+    if (wave >= 4) {
+        const int pw = wave - 4;
+        MVEntry E;
+        E.x = a.x;
+        E.carry = a.carry;
+        E.lnw = a.lnw;
+        E.lnb = a.lnb;
+        E.mu = a.maa_x;
+        E.carry_out = a.carry_out;
+        E.f = nullptr;
+        ChunkIn ci[LCW];
+        int kc[LCW];
+#pragma unroll
+        for (int q = 0; q < LCW; q++) {
+            kc[q] = (pw + 4 * q) * LN_CHUNK + lane * 8;
+            chunk_load<MVK_LN, 1>(E, min(kc[q], K - 8), ci[q]);
+        }
+        if (a.late) {
+            // the inputs land before the mix waves' weight stream starts (mv_late_weights)
+            asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        }
+        // LayerNorm statistics (chunk association, one pass); the chunk sums meet in LDS
+#pragma unroll
+        for (int q = 0; q < LCW; q++)
+            if (pw + 4 * q < nch) {
+                double c1, c2;
+                ln_chunk_sums(ci[q].x, kc[q] < K, c1, c2);
+                if (lane == 0) {
+                    ln_part[0][pw + 4 * q] = c1;
+                    ln_part[1][pw + 4 * q] = c2;
+                }
+            }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        double s1 = 0.0, s2 = 0.0;
+        for (int q = 0; q < nch; q++) s1 += ln_part[0][q], s2 += ln_part[1][q];
+        float mean, scale;
+        ln_finish(s1, s2, K, 1e-5f, mean, scale);
+        if (pw == 0) STAMP_XN(1);
+        const bool write_carry = blockIdx.x == 0 && n == 0;
+#pragma unroll
+        for (int q = 0; q < LCW; q++) {
+            if (pw + 4 * q >= nch) continue;
+            if (kc[q] < K) {
+#pragma unroll
+                for (int j = 0; j < 8; j++) s_xa[kc[q] + j] = ln_apply(ci[q].x[j], mean, scale, ci[q].w[j], ci[q].b[j]);
+            }
+            chunk_store<WF, MVK_LN, 1>(E, act, ci[q], mean, scale, write_carry, kc[q], kc[q] < K, lane);
+        }
+        if (pw == 0) STAMP_XN(2);
+        __syncthreads();  // (1) activation image ready
+        __syncthreads();  // (2) lora_n ready
+    } else {
+        const ActBuf ao = a.out[n];
+        pin_act(ao);
+        const DMat & W = a.w1;
+        asm volatile("" ::"s"(W.qs), "s"(W.sc), "s"(W.qh));
+        if (a.late) asm volatile("s_barrier" ::: "memory");  // the image inputs have landed
+        // ---- rows n*D + wave*R + r of W1 and this thread's mix channel: W2 column, carry, maa
+        const int units = mv_units(WF, K);
+        const int row0 = n * D + wave * R, rlast = n * D + D - 1;
+        int rows[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) rows[r] = min(row0 + r, rlast);
+        WBlk w[R][U];
+#pragma unroll
+        for (int u = 0; u < U; u++)
+#pragma unroll
+            for (int r = 0; r < R; r++) w[r][u] = load_unit<WF, false>(W, rows[r], u, lane);
+        const int c = blockIdx.x * CPW + tid;
+        const bool cval = tid < CPW && (int)(blockIdx.x * CPW + (tid & ~31)) < C;  // half-wave uniform
+        const int cc = min(c, C - 1);
+        float w2v[DM];
+        const float * w2 = a.w2t + (size_t)n * D * C + cc;
+#pragma unroll
+        for (int i = 0; i < DM; i++) w2v[i] = w2[(size_t)min(i, D - 1) * C];  // rows >= D: skipped below
+        const float carry_c = a.carry[cc];
+        const float mu_c = a.maa[n][cc];
+        if (wave == 0) STAMP_XN(0);  // weights issued
+        asm volatile("s_barrier" ::: "memory");  // the image waves' statistics exchange
+        __syncthreads();  // (1) activation image ready
+        if (wave == 0) STAMP_MID();
+        float acc[R], acc2[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) acc[r] = acc2[r] = 0.0f;
+        for (int u0 = 0; u0 < units; u0 += U) {
+            if (u0 > 0) {
+#pragma unroll
+                for (int u = 0; u < U; u++)
+#pragma unroll
+                    for (int r = 0; r < R; r++) w[r][u] = load_unit<WF, false>(W, rows[r], u0 + u, lane);
+            }
+            AUnit xu[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) xu[u] = load_act_unit<WF, true>(act, u0 + u, lane);
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                if (unit_valid<WF>(K, u0 + u, lane)) {
+#pragma unroll
+                    for (int r = 0; r < R; r++) dot_unit<WF>(w[r][u], xu[u], acc[r], acc2[r]);
+                }
+            }
+        }
+        constexpr bool one = WF == W_Q4_1 || WF == W_Q5_1;
+        float sr[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) sr[r] = one ? wave_sum63(acc[r]) + wave_sum63(acc2[r]) : wave_sum63(acc[r]) + 0.0f;
+        const float t = rk_tanhf(lane_row_sum<R>(sr, lane));  // EPI_TANH, lane r for row r
+        if (lane < R && wave * R + lane < D) s_lora[wave * R + lane] = t;
+        __syncthreads();  // (2) lora_n ready
+        if (wave == 0) STAMP_X(3);
+        // k_v6_mix5_dec's arithmetic: m = fma chain over i in order
+        const float xa = s_xa[cc];
+        const float sx = carry_c - xa;
+        float m = 0.0f;
+#pragma unroll
+        for (int i = 0; i < DM; i++)
+            if (i < D) m = fmaf(w2v[i], s_lora[i], m);
+        if (cval) emit32(ao, 0, c, (m + mu_c) * sx + xa);
+    }
+    STAMP_END_NS(4 + 16 * blockIdx.y);
+}
+
 // Channels mixed per workgroup (CPW): the workgroups of one mix each recompute its D rows of W1
 // (37 KB of L2 reads for v6-1B6) and stream CPW columns of W2 from HBM; 64 gives 32 x 5 = 160
 // workgroups for C = 2048 (256: 40), so the W2 stream is spread over more CUs.
@@ -202,10 +349,22 @@ static bool launch_maa_t(hipStream_t st, const MaaDec & a, int lds, int units) {
 #define MAA_P(Rv, Uv) \
     do { if (a.C <= 2048) MAA_L(Rv, Uv, 32); else MAA_L(Rv, Uv, 64); } while (0)
     const bool u1 = units <= 1;
-    // rows per wave over all 8 waves (D <= 8R)
     if (a.D <= 32) {
-        if (u1) MAA_P(4, 1); else MAA_P(4, 2);
+        // rows on the 4 mix waves only (k_v6_maa_dec4)
+#define MAA4_L(Uv, P)                                                                                   \
+    do {                                                                                                \
+        if (cpw == 64) RK_LAUNCH((k_v6_maa_dec4<WF, Uv, P, 64>), grid, dim3(512), lds, st, a);          \
+        else if (cpw == 128) RK_LAUNCH((k_v6_maa_dec4<WF, Uv, P, 128>), grid, dim3(512), lds, st, a);   \
+        else RK_LAUNCH((k_v6_maa_dec4<WF, Uv, P, 256>), grid, dim3(512), lds, st, a);                   \
+    } while (0)
+        if (a.C <= 2048) {
+            if (u1) MAA4_L(1, 32); else MAA4_L(2, 32);
+        } else {
+            if (u1) MAA4_L(1, 64); else MAA4_L(2, 64);
+        }
+#undef MAA4_L
     } else {
+        // rows per wave over all 8 waves (D <= 8R)
         if (u1) MAA_P(8, 1); else MAA_P(8, 2);
     }
 #undef MAA_P
@@ -227,6 +386,7 @@ bool launch_v6_maa_dec(hipStream_t st, int C, int D, const DMat & w1, const floa
         return false;
     }
     MaaDec a;
+    a.late = 0;  // measured: the W1 rows (37 KB per workgroup, L2) are better streamed at once
     a.C = C;
     a.D = D;
     a.w1 = w1;

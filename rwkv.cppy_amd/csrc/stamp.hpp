@@ -53,6 +53,11 @@ __device__ __forceinline__ unsigned stamp_cu() {
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   \
         if ((threadIdx.x & 63) == 0) stamp_x_[i] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
+// STAMP_XN: the time this wave got here, without waiting for its outstanding loads
+#define STAMP_XN(i)                                                                  \
+    do {                                                                             \
+        if ((threadIdx.x & 63) == 0) stamp_x_[i] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
 #define STAMP_MID()                                          \
     do {                                                     \
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); \
@@ -78,6 +83,9 @@ __device__ __forceinline__ unsigned stamp_cu() {
 #else
 #define STAMP_X(i) \
     do {           \
+    } while (0)
+#define STAMP_XN(i) \
+    do {            \
     } while (0)
 #define STAMP_BEGIN()
 #define STAMP_MID() \

@@ -176,7 +176,7 @@ def test_v6_decode_handoff_many_tokens(cfg_dir):
     assert n == words.nbytes
     assert not words.any(), f'hand-off words not re-armed / timeout: {np.nonzero(words)[0][:8]}'
     C = 2048
-    gran = np.ones(4 * C + 128, np.uint64)
+    gran = np.ones(6 * C, np.uint64)  # r, k, v, g rows + one decay-LoRA copy per head
     n = library().library.rwkv_mi355x_debug_buffer(m._ctx.ptr, b'granules', gran.ctypes.data_as(ctypes.c_void_p),
                                                    gran.nbytes)
     assert n == gran.nbytes

@@ -243,12 +243,11 @@ __device__ __forceinline__ void chunk_load_all(const MVEntry & E, int kc, ChunkI
 template <int WF, int SRCK, int FORM>
 __device__ __forceinline__ void chunk_store(const MVEntry & E, const ActBuf & a, const ChunkIn & ci, float mean,
                                             float scale, bool write_carry, int k0, bool valid, int lane) {
-    float v[8];
+    float v[8], xa[8];
     if constexpr (SRCK == MVK_F32) {
 #pragma unroll
         for (int j = 0; j < 8; j++) v[j] = ci.x[j];
     } else {
-        float xa[8];
 #pragma unroll
         for (int j = 0; j < 8; j++) {
             xa[j] = ln_apply(ci.x[j], mean, scale, ci.w[j], ci.b[j]);
@@ -256,22 +255,31 @@ __device__ __forceinline__ void chunk_store(const MVEntry & E, const ActBuf & a,
             else if constexpr (FORM == 0) v[j] = xa[j] * ci.m[j] + (ci.c[j] - ci.c[j] * ci.m[j]);
             else v[j] = (ci.c[j] - xa[j]) * ci.m[j] + xa[j];
         }
-        if (write_carry && valid) {
-            *(float4 *)(E.carry_out + k0) = make_float4(xa[0], xa[1], xa[2], xa[3]);
-            *(float4 *)(E.carry_out + k0 + 4) = make_float4(xa[4], xa[5], xa[6], xa[7]);
-        }
     }
+    // The carry (LayerNorm output) is stored last: vmcnt counts loads and stores in one order, so a
+    // global store issued before the last use of the inputs makes the waits for those inputs also
+    // wait for weight loads issued after them (measured: the carry-writing workgroup ended last).
+    auto store_carry = [&]() {
+        if constexpr (SRCK != MVK_F32) {
+            if (write_carry && valid) {
+                *(float4 *)(E.carry_out + k0) = make_float4(xa[0], xa[1], xa[2], xa[3]);
+                *(float4 *)(E.carry_out + k0 + 4) = make_float4(xa[4], xa[5], xa[6], xa[7]);
+            }
+        }
+    };
     if constexpr (WF == W_F32) {
         if (valid) {
             *(float4 *)(a.f + k0) = make_float4(v[0], v[1], v[2], v[3]);
             *(float4 *)(a.f + k0 + 4) = make_float4(v[4], v[5], v[6], v[7]);
         }
+        store_carry();
     } else if constexpr (WF == W_F16) {
         int p[4];
 #pragma unroll
         for (int j = 0; j < 4; j++)
             p[j] = __builtin_bit_cast(int, __halves2half2(to_half(v[2 * j]), to_half(v[2 * j + 1])));
         if (valid) *(int4 *)(a.h + k0) = make_int4(p[0], p[1], p[2], p[3]);
+        store_carry();
     } else {
         // ggml quantize_row_q8_0 / q8_1 (x86): d = amax/127, q = rint(x*127/amax)
         float am = 0.0f;
@@ -300,6 +308,7 @@ __device__ __forceinline__ void chunk_store(const MVEntry & E, const ActBuf & a,
                 if (a.fmt == A_Q8_1) a.s[bi] = f16_round(d * (float)sum);
             }
         }
+        store_carry();
     }
 }
 
@@ -485,7 +494,7 @@ __device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, int b0, in
 #endif
 #pragma unroll
             for (int q = 0; q < LCW; q++)
-                if (pw + q * NW < nch) chunk_store<WF, SRCK, FORM>(Ent, a, ci[q], mean, scale, write_carry, kc[q], kc[q] < K, lane);
+                if (pw + q * NW < nch) chunk_store<WF, SRCK, FORM>(Ent, a, ci[q], mean, scale, false, kc[q], kc[q] < K, lane);
             if constexpr (SRCK == MVK_F32) {
                 // plain fp32 input: any K, further chunks streamed
                 for (int c = pw + LCW * NW; c < nch; c += NW) {
@@ -590,9 +599,27 @@ __device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, int b0, in
         if constexpr (!EMIT) ep = epi_load(Ent, min(row0 + min(lane, RR - 1), M - 1));
         else ep = epi_load(Ent, min(wgi * RW + (tid < RW ? tid : 0), M - 1));
     }
+    if constexpr (SRCK == MVK_LN) {
+        // the carry (this LayerNorm output, the next token's shift input) after the rows: vmcnt
+        // counts loads and stores in one order, so a store ahead of the dots would make waits
+        // for earlier loads also wait for the weight stream behind it
+        if (pro_wave && write_carry) {
+#pragma unroll
+            for (int q = 0; q < LCW; q++)
+                if (pw + q * NW < nch && kc[q] < K) {
+                    float xa[8];
+#pragma unroll
+                    for (int j = 0; j < 8; j++) xa[j] = ln_apply(ci[q].x[j], mean, scale, ci[q].w[j], ci[q].b[j]);
+                    *(float4 *)(Ent.carry_out + kc[q]) = make_float4(xa[0], xa[1], xa[2], xa[3]);
+                    *(float4 *)(Ent.carry_out + kc[q] + 4) = make_float4(xa[4], xa[5], xa[6], xa[7]);
+                }
+        }
+    }
     if constexpr (SRCK == MVK_LN && FORM != 2) {
         // the entry's first workgroup, after its rows: the same LayerNorm output mixed with mu2
-        // into a global activation row (the channel-mix receptance input of k_mvsig)
+        // into a global activation row (the channel-mix receptance input of k_mvsig).  (Spread
+        // block-interleaved over all workgroups instead: 704 vs 695 us/token -- every workgroup's
+        // image waves then pay the reload and quantization pass.)
         if (pro_wave && Ent.mu2 && (int)blockIdx.x == b0) {
             MVEntry E2 = Ent;
             E2.mu = Ent.mu2;

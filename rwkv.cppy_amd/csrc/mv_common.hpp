@@ -409,10 +409,12 @@ __device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, int b0, in
     constexpr bool PRO = SRCK != MVK_ACT;
     // LayerNorm chunks per prologue wave held in registers: LNP 32 -> K <= 2048, 64 -> K <= 4096
     constexpr int LCW = LNP > 32 ? 2 : 1;
-    // Prologue groups: the rows of a block over all 2 NW waves (the image waves too: the per-wave
-    // dot and reduction chains are half as long as with the image waves idle).
-    constexpr int NWT = PRO ? 2 * NW : NW;  // waves with rows
-    constexpr int RR = R;                   // rows per wave
+    // Prologue groups with K <= 2048 (one LayerNorm chunk per image wave; larger K: mv_body_split):
+    // the rows of a block go over all 2 NW waves -- the image waves too, so the per-wave dot and
+    // reduction chains are half as long.
+    constexpr bool IMGR = PRO;
+    constexpr int NWT = (PRO && IMGR) ? 2 * NW : NW;  // waves with rows
+    constexpr int RR = (PRO && !IMGR) ? 2 * R : R;    // rows per wave with rows
     constexpr int RW = NWT * RR;
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform branches
     const DMat & W = Ent.W;
@@ -454,7 +456,7 @@ __device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, int b0, in
         asm volatile("s_barrier" ::: "memory");
     }
     // ---- this wave's weight units (HBM), all in flight before anything waits
-    constexpr bool has_rows = true;
+    const bool has_rows = !pro_wave || IMGR;
     int row0 = wgi * RW + wave * RR;
     int rows[RR];
 #pragma unroll
@@ -466,7 +468,7 @@ __device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, int b0, in
 #pragma unroll
             for (int r = 0; r < RR; r++) w[r][u] = load_unit<WF>(W, rows[r], u, lane);
     };
-    issue_w();
+    if (has_rows) issue_w();
     if constexpr (PRO) {
         if (pro_wave) {
             if constexpr (SRCK == MVK_LN) {
@@ -633,6 +635,190 @@ __device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, int b0, in
     }
 }
 
+// Prologue groups with K > 2048: the image waves hold two LayerNorm chunks of inputs, so they stay
+// rowless (the NW streaming waves take 2 R rows each), and the two roles run as separate straight
+// paths that meet only at barriers.  With both roles in one path the compiler keeps the streaming
+// waves' weight registers live through the image waves' statistics (it cannot tell the two wave
+// conditions apart), the kernel needs 145-235 VGPRs -- one workgroup per CU -- and the multi-round
+// LayerNorm groups of the 2.9B / 7B models ran 10-14 % slower.  Same arithmetic and association as
+// mv_body (bit-identical); the barrier sequence of both paths matches one for one.
+template <int WF, int R, int U, int SRCK, int FORM, bool EMIT, int NW, int LNP>
+__device__ __forceinline__ void mv_body_split(const MVEntry & Ent, int wgi, int b0, int stride, char * smem,
+                                              float * red, int late) {
+    constexpr int LCW = LNP > 32 ? 2 : 1;
+    constexpr int RR = 2 * R, RW = NW * RR;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const DMat & W = Ent.W;
+    const int M = W.M, K = W.K;
+    const int nblk = (M + RW - 1) / RW;
+    const int units = mv_units(WF, K);
+    const int nch = (K + LN_CHUNK - 1) / LN_CHUNK;
+    const ActBuf a = lds_act(smem, act_fmt_for(WF), K);
+    if (wave >= NW) {
+        // ---- image waves: inputs, statistics, the image; then only the barriers of the rows
+        const int pw = wave - NW;
+        const bool write_carry = Ent.carry_out && (int)blockIdx.x == b0;
+        ChunkIn ci[LCW];
+        int kc[LCW];
+#pragma unroll
+        for (int q = 0; q < LCW; q++) {
+            kc[q] = (pw + q * NW) * LN_CHUNK + lane * 8;
+            chunk_load<SRCK, FORM>(Ent, min(kc[q], K - 8), ci[q]);
+        }
+        if (late) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_barrier" ::: "memory");  // issue order: the image inputs ahead of the weights
+        float mean = 0.0f, scale = 0.0f;
+        if constexpr (SRCK == MVK_LN) {
+            __shared__ double ln_part[2][8];
+#pragma unroll
+            for (int q = 0; q < LCW; q++)
+                if (pw + q * NW < nch) {
+                    double c1, c2;
+                    ln_chunk_sums(ci[q].x, kc[q] < K, c1, c2);
+                    if (lane == 0) {
+                        ln_part[0][pw + q * NW] = c1;
+                        ln_part[1][pw + q * NW] = c2;
+                    }
+                }
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            double s1 = 0.0, s2 = 0.0;
+            for (int c = 0; c < nch; c++) s1 += ln_part[0][c], s2 += ln_part[1][c];
+            ln_finish(s1, s2, K, 1e-5f, mean, scale);
+        }
+#pragma unroll
+        for (int q = 0; q < LCW; q++)
+            if (pw + q * NW < nch) chunk_store<WF, SRCK, FORM>(Ent, a, ci[q], mean, scale, false, kc[q], kc[q] < K, lane);
+        if constexpr (SRCK == MVK_F32) {
+            for (int c = pw + LCW * NW; c < nch; c += NW) {
+                const int kk = c * LN_CHUNK + lane * 8;
+                chunk_load<SRCK, FORM>(Ent, min(kk, K - 8), ci[0]);
+                chunk_store<WF, SRCK, FORM>(Ent, a, ci[0], mean, scale, false, kk, kk < K, lane);
+            }
+        }
+        __syncthreads();  // activation image ready
+        for (;;) {
+            if constexpr (EMIT) __syncthreads();  // the streaming waves' row sums in red[]
+            wgi += stride;
+            if (stride <= 0 || wgi >= nblk) break;
+            if constexpr (EMIT) __syncthreads();  // red[] reuse
+        }
+        if constexpr (SRCK == MVK_LN) {
+            if (write_carry) {  // after the rows (see mv_body)
+#pragma unroll
+                for (int q = 0; q < LCW; q++)
+                    if (pw + q * NW < nch && kc[q] < K) {
+                        float xa[8];
+#pragma unroll
+                        for (int j = 0; j < 8; j++) xa[j] = ln_apply(ci[q].x[j], mean, scale, ci[q].w[j], ci[q].b[j]);
+                        *(float4 *)(Ent.carry_out + kc[q]) = make_float4(xa[0], xa[1], xa[2], xa[3]);
+                        *(float4 *)(Ent.carry_out + kc[q] + 4) = make_float4(xa[4], xa[5], xa[6], xa[7]);
+                    }
+            }
+        }
+        if constexpr (SRCK == MVK_LN && FORM != 2) {
+            if (Ent.mu2 && (int)blockIdx.x == b0) {
+                MVEntry E2 = Ent;
+                E2.mu = Ent.mu2;
+#pragma unroll
+                for (int q = 0; q < LCW; q++)
+                    if (pw + q * NW < nch) {
+                        ld8(ci[q].m, Ent.mu2 + min(kc[q], K - 8));
+                        chunk_store<WF, SRCK, FORM>(E2, Ent.act2_out, ci[q], mean, scale, false, kc[q], kc[q] < K, lane);
+                    }
+            }
+        }
+    } else {
+        // ---- streaming waves: weights at once, the rows after the image
+        const int epi = Ent.epi;
+        float * const ey = Ent.y;
+        ActBuf ao = Ent.act_out;
+        const bool emit_on = EMIT && Ent.emit && ao.fmt >= 0;
+        asm volatile("" ::"s"(epi), "s"(ey));
+        if constexpr (EMIT) pin_act(ao);
+        asm volatile("" ::"s"(W.qs), "s"(W.sc), "s"(W.qh));
+        asm volatile("s_barrier" ::: "memory");  // issue order (late: the image inputs have landed)
+        int row0 = wgi * RW + wave * RR;
+        int rows[RR];
+#pragma unroll
+        for (int r = 0; r < RR; r++) rows[r] = min(row0 + r, M - 1);
+        WBlk w[RR][U];
+#pragma unroll
+        for (int u = 0; u < U; u++)
+#pragma unroll
+            for (int r = 0; r < RR; r++) w[r][u] = load_unit<WF>(W, rows[r], u, lane);
+        if constexpr (SRCK == MVK_LN) asm volatile("s_barrier" ::: "memory");  // the statistics exchange
+        EpiIn ep;
+        if constexpr (!EMIT) ep = epi_load(Ent, min(row0 + min(lane, RR - 1), M - 1));
+        else ep = epi_load(Ent, min(wgi * RW + (tid < RW ? tid : 0), M - 1));
+        __syncthreads();  // activation image ready
+        for (;;) {
+            constexpr bool one = WF == W_Q4_1 || WF == W_Q5_1;
+            float acc[RR], acc2[RR];
+#pragma unroll
+            for (int r = 0; r < RR; r++) acc[r] = acc2[r] = 0.0f;
+            for (int u0 = 0; u0 < units; u0 += U) {
+                if (u0 > 0) {
+#pragma unroll
+                    for (int u = 0; u < U; u++)
+#pragma unroll
+                        for (int r = 0; r < RR; r++) w[r][u] = load_unit<WF>(W, rows[r], u0 + u, lane);
+                }
+                AUnit x[U];
+#pragma unroll
+                for (int u = 0; u < U; u++) x[u] = load_act_unit<WF, true>(a, u0 + u, lane);
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    if (unit_valid<WF>(K, u0 + u, lane)) {
+#pragma unroll
+                        for (int r = 0; r < RR; r++) dot_unit<WF>(w[r][u], x[u], acc[r], acc2[r]);
+                    }
+                }
+            }
+            float s[RR];
+#pragma unroll
+            for (int r = 0; r < RR; r++) s[r] = one ? wave_sum63(acc[r]) + wave_sum63(acc2[r]) : wave_sum63(acc[r]) + 0.0f;
+            if constexpr (!EMIT) {
+                const float v = epi_apply(epi, lane_row_sum<RR>(s, lane), ep);
+                if (lane < RR && row0 + lane < M) ey[row0 + lane] = v;
+            } else {
+#pragma unroll
+                for (int r = 0; r < RR; r++)
+                    if (lane == 63) red[wave * RR + r] = s[r];
+                __syncthreads();
+                if (tid < RW) {
+                    const int row = wgi * RW + tid;
+                    float vv = 0.0f;
+                    if (row < M) {
+                        vv = epi_apply(epi, red[tid], ep);
+                        if (ey) ey[row] = vv;
+                    }
+                    if (emit_on) emit32(ao, 0, row, vv);
+                }
+            }
+            wgi += stride;
+            if (stride <= 0 || wgi >= nblk) break;
+            if constexpr (EMIT) __syncthreads();  // red[] reuse
+            row0 = wgi * RW + wave * RR;
+#pragma unroll
+            for (int r = 0; r < RR; r++) rows[r] = min(row0 + r, M - 1);
+#pragma unroll
+            for (int u = 0; u < U; u++)
+#pragma unroll
+                for (int r = 0; r < RR; r++) w[r][u] = load_unit<WF>(W, rows[r], u, lane);
+            if constexpr (!EMIT) ep = epi_load(Ent, min(row0 + min(lane, RR - 1), M - 1));
+            else ep = epi_load(Ent, min(wgi * RW + (tid < RW ? tid : 0), M - 1));
+        }
+    }
+}
+
+// mv_body, or mv_body_split for the prologue groups with K > 2048
+template <int WF, int R, int U, int SRCK, int FORM, bool EMIT, int NW, int LNP>
+__device__ __forceinline__ void mv_run(const MVEntry & Ent, int wgi, int b0, int stride, char * smem, float * red,
+                                       int late, unsigned long long * stamp_mid, unsigned long long * stamp_x) {
+    if constexpr (SRCK != MVK_ACT && LNP > 32) mv_body_split<WF, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, stride, smem, red, late);
+    else mv_body<WF, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, stride, smem, red, late, stamp_mid, stamp_x);
+}
+
 // WFIX >= 0: every entry of the group has weight type WFIX (one body, fewer registers);
 // WFIX < 0: per-entry switch.  SRCK / FORM: the group's input source and token-shift form
 // (compile-time, so the prologue has no data-independent branches).
@@ -661,16 +847,16 @@ __global__ __launch_bounds__(512) void k_mv(int b1, int b2, int b3, int b4, int 
     unsigned long long * sx = nullptr;
 #endif
     if constexpr (WFIX >= 0) {
-        mv_body<WFIX, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red, g.late, smid, sx);
+        mv_run<WFIX, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red, g.late, smid, sx);
     } else {
         switch (Ent.W.type) {
-            case W_F32: mv_body<W_F32, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red, g.late); break;
-            case W_F16: mv_body<W_F16, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red, g.late); break;
-            case W_Q4_0: mv_body<W_Q4_0, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red, g.late); break;
-            case W_Q4_1: mv_body<W_Q4_1, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red, g.late); break;
-            case W_Q5_0: mv_body<W_Q5_0, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red, g.late); break;
-            case W_Q5_1: mv_body<W_Q5_1, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red, g.late); break;
-            case W_Q8_0: mv_body<W_Q8_0, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red, g.late); break;
+            case W_F32: mv_run<W_F32, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red, g.late, nullptr, nullptr); break;
+            case W_F16: mv_run<W_F16, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red, g.late, nullptr, nullptr); break;
+            case W_Q4_0: mv_run<W_Q4_0, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red, g.late, nullptr, nullptr); break;
+            case W_Q4_1: mv_run<W_Q4_1, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red, g.late, nullptr, nullptr); break;
+            case W_Q5_0: mv_run<W_Q5_0, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red, g.late, nullptr, nullptr); break;
+            case W_Q5_1: mv_run<W_Q5_1, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red, g.late, nullptr, nullptr); break;
+            case W_Q8_0: mv_run<W_Q8_0, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, g.stride, smem, red, g.late, nullptr, nullptr); break;
             default: break;
         }
     }

@@ -815,7 +815,14 @@ __device__ __forceinline__ void mv_body_split(const MVEntry & Ent, int wgi, int 
 template <int WF, int R, int U, int SRCK, int FORM, bool EMIT, int NW, int LNP>
 __device__ __forceinline__ void mv_run(const MVEntry & Ent, int wgi, int b0, int stride, char * smem, float * red,
                                        int late, unsigned long long * stamp_mid, unsigned long long * stamp_x) {
-    if constexpr (SRCK != MVK_ACT && LNP > 32) mv_body_split<WF, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, stride, smem, red, late);
+    // every prologue group in the split form (K <= 2048 too: v6-1B6 decode 686-692 vs 696-698 us per
+    // token with the image waves carrying rows in mv_body, v4-169M 244 vs 251); MV_IMG_ROWS: mv_body
+#ifdef MV_IMG_ROWS
+    constexpr int LNS = 32;
+#else
+    constexpr int LNS = 0;
+#endif
+    if constexpr (SRCK != MVK_ACT && LNP > LNS) mv_body_split<WF, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, stride, smem, red, late);
     else mv_body<WF, R, U, SRCK, FORM, EMIT, NW, LNP>(Ent, wgi, b0, stride, smem, red, late, stamp_mid, stamp_x);
 }
 

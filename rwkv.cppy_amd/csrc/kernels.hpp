@@ -147,9 +147,8 @@ struct MVGroup {
     int late;                // set by launch_mv_group: weights issued after the image inputs land
 };
 
-// Prologue matvecs: the streaming waves issue their weights only after the image waves' inputs
-// have landed (RWKV_MI355X_LATE_W, default 1): inputs queued behind a weight flood arrive late,
-// and the image gates every row.
+// Prologue matvecs: RWKV_MI355X_LATE_W=1 makes the streaming waves issue their weights only after
+// the image waves' inputs have landed (default 0: measured slower in the split form).
 int mv_late_weights();
 
 // Busy-waits about `us` microseconds on the device (kernel timing: lets the host queue a whole

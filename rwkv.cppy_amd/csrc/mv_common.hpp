@@ -449,9 +449,8 @@ __device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, int b0, in
         // the weight pointers reach SGPRs before the issue-order barrier, so the stream starts
         // right after it (a kernarg scalar load behind the barrier is a round trip in the path)
         asm volatile("" ::"s"(W.qs), "s"(W.sc), "s"(W.qh));
-        // issue order: the image inputs go out before any weight stream starts, and (late) have
-        // landed before it starts: measured, a weight stream issued right behind them delays the
-        // image by more than the late start costs the rows (v6-1B6 decode 691.7 vs 700 us/token)
+        // issue order: the image inputs go out before any weight stream starts (late: they have
+        // landed before it starts)
         if (late && pro_wave) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         asm volatile("s_barrier" ::: "memory");
     }

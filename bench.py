@@ -7,7 +7,8 @@ logits produced) of RWKV-v6-World-1B6 Q4_0 with the recurrent state resident in 
 value = tokens decoded by all ranks / max-over-ranks wall time of the K timed steps.
 Multi-GPU: decode does not shard -- each rank runs an independent replica
 ("scaling": "weak").  Sequence evaluation is reported both ways: independent replicas, and one
-sequence through a layer pipeline over all ranks (rwkv_cpp/pipeline.py, RCCL point-to-point).
+sequence through the in-library layer pipeline over all N GPUs (rwkv_mi355x_init_pipeline, driven by
+rank 0; peer copies over xGMI).  At N = 1 the same pipeline runs with every stage on GPU 0.
 
 Also reported (same run): 1024-token rwkv_eval_sequence throughput, ABI-level decode
 (13 MB of host state in and out per token, the reference's contract), the dominant kernel's
@@ -47,6 +48,23 @@ CONFIGS = {
 
 def log(*a):
     print('[bench]', *a, file=sys.stderr, flush=True)
+
+
+def physical_cores():
+    """Physical cores of this host: distinct (physical id, core id) pairs in /proc/cpuinfo."""
+    try:
+        cores, phys = set(), '0'
+        with open('/proc/cpuinfo') as f:
+            for line in f:
+                k, _, v = line.partition(':')
+                k = k.strip()
+                if k == 'physical id':
+                    phys = v.strip()
+                elif k == 'core id':
+                    cores.add((phys, v.strip()))
+        return len(cores) or None
+    except OSError:
+        return None
 
 
 def decode_parity(L, ctx, om, tokens, olg0, ost0, n_vocab, state_len, tok_arr, P_F):
@@ -121,7 +139,8 @@ def main():
     ap.add_argument('--seq-len', type=int, default=1024)
     ap.add_argument('--seq-reps', type=int, default=3)
     ap.add_argument('--abi-steps', type=int, default=32)
-    ap.add_argument('--pipe-chunk', type=int, default=0, help='pipeline chunk (0: max(64, T / (2 N)))')
+    ap.add_argument('--pipe-stages', type=int, default=-1,
+                    help='N = 1: stages of the one-GPU pipeline run (-1: 4; 0: skip the pipeline leg); N > 1: N')
     ap.add_argument('--timing-steps', type=int, default=8)
     ap.add_argument('--cpu-seconds', type=float, default=12.0)
     ap.add_argument('--skip-cpu', action='store_true')
@@ -218,9 +237,13 @@ def main():
     elapsed = time.perf_counter() - t0
     if world > 1:
         elapsed = allmax(elapsed)
-    ms_per_step = elapsed * 1e3 / args.steps
-    value = world * args.steps / elapsed
-    log(f'decode: {ms_per_step * 1e3:.1f} us/token, {value:.1f} tok/s aggregate over {world} GPU(s)')
+    if args.roofline_only:
+        # no timed decode steps ran: this line carries the roofline pass only (profiles/), never a rate
+        ms_per_step, value = None, None
+    else:
+        ms_per_step = elapsed * 1e3 / args.steps
+        value = world * args.steps / elapsed
+        log(f'decode: {ms_per_step * 1e3:.1f} us/token, {value:.1f} tok/s aggregate over {world} GPU(s)')
     if args.decode_only or args.roofline_only:
         args.batch, args.seq_reps, args.abi_steps, args.skip_cpu = '', 0, 0, True
 
@@ -282,45 +305,67 @@ def main():
     seq_tps = args.seq_len / seq_s if ts else 0.0
     log(f'seq-eval T={args.seq_len}: {seq_s * 1e3:.1f} ms, {seq_tps:.0f} tok/s')
 
-    # ---------------- sequence eval as a layer pipeline over all ranks ----------------
+    # ---------------- sequence eval through the in-library layer pipeline ----------------
+    # rwkv_mi355x_init_pipeline: ONE process drives P stage contexts (stage s on GPU devices[s], layers
+    # [s*L/P, (s+1)*L/P)); rwkv_eval_sequence on it cuts the tokens into chunks of >= 256 and forwards
+    # each chunk's residual stream stage to stage by a peer copy over xGMI (csrc/pipeline.cpp) -- the
+    # path rwkv_eval_sequence ships.  N > 1: rank 0 drives all N GPUs while the other ranks wait at a
+    # barrier (strong scaling of one sequence).  N = 1: the same schedule with every stage on GPU 0,
+    # so its own overhead against one context is a number.
     pipe = None
-    if world > 1 and args.seq_reps > 0:
-        try:
-            from rwkv_cpp.pipeline import LibraryStage, pipeline_eval_sequence, stage_layers
-            # a stage context holding only this rank's layers (and the head on the last rank),
-            # computing on its own stream with no host wait between chunks
-            stage = LibraryStage.from_file(lib, path, rank, world, async_=True)
-            chunk = args.pipe_chunk or max(64, args.seq_len // (2 * world))
-            pseq = np.random.default_rng(4321).integers(0, n_vocab, size=args.seq_len)  # same on every rank
-            dev = torch.device('cuda', gpu)
+    if args.seq_reps > 0 and args.pipe_stages != 0:
+        P = world if world > 1 else (args.pipe_stages if args.pipe_stages > 0 else 4)
+        P = max(2, min(P, NL))
+        if rank == 0:
+            try:
+                ndev = torch.cuda.device_count()
+                devices = [d % max(1, ndev) for d in range(P)] if world > 1 else [gpu] * P
+                devs = (ctypes.c_int * P)(*devices)
+                t = time.time()
+                pctx = L.rwkv_mi355x_init_pipeline(path.encode(), 1, P, devs)
+                if not pctx:
+                    raise RuntimeError('rwkv_mi355x_init_pipeline failed')
+                log(f'pipeline: {P} stages on devices {devices} loaded in {time.time() - t:.1f}s')
+                pseq = np.random.default_rng(4321).integers(0, n_vocab, size=args.seq_len)
+                pa, pp_ = tok_arr(pseq)
+                plg = np.zeros(n_vocab, np.float32)
 
-            def run_pipe():
-                stage.reset_state()
-                return pipeline_eval_sequence(stage, pseq, chunk, NL, C, stage.planes, rank, world, dev,
-                                              wire_device=wire)
+                def run_pipe():
+                    if not L.rwkv_eval_sequence(pctx, pp_, len(pseq), None, None, plg.ctypes.data_as(P_F)):
+                        raise RuntimeError('pipeline rwkv_eval_sequence failed')
 
-            run_pipe()  # warm-up: P2P communicators, workspaces
-            pts = []
-            for _ in range(args.seq_reps):
-                torch.cuda.synchronize()
-                barrier()
-                t1 = time.perf_counter()
-                run_pipe()
-                torch.cuda.synchronize()
-                barrier()
-                pts.append(allmax(time.perf_counter() - t1))
-            l0, l1 = stage_layers(NL, world, rank)
-            pipe = {'tokens_per_s': round(args.seq_len / min(pts), 1), 'ms_per_sequence': round(min(pts) * 1e3, 3),
-                    'parallelism': f'layer pipeline x{world}', 'scaling': 'strong', 'chunk': chunk,
-                    'transport': f'torch.distributed {backend} isend/irecv of x [chunk, C] fp32',
-                    'stage_weight_gb_rank0': round(L.rwkv_mi355x_weight_bytes(stage.ctx.ptr, True) / 1e9, 4),
-                    'model_weight_gb': round(L.rwkv_mi355x_weight_bytes(ctx.ptr, True) / 1e9, 4)}
-            lib.rwkv_free(stage.ctx)
-            log(f'pipeline seq-eval over {world} stages (rank {rank}: layers [{l0}, {l1})): '
-                f'{min(pts) * 1e3:.1f} ms, {args.seq_len / min(pts):.0f} tok/s, chunk {chunk}')
-        except Exception as e:  # the decode line is still printed; the run exits non-zero
-            errors.append(f'pipeline: {e!r}')
-            log(f'pipeline seq-eval failed: {e!r}')
+                run_pipe()  # warm-up: workspaces, staging buffers
+                pts = []
+                for _ in range(args.seq_reps):
+                    t1 = time.perf_counter()
+                    run_pipe()
+                    pts.append(time.perf_counter() - t1)
+                # the same sequence through one context: pipeline logits must be bit-identical
+                slg = np.zeros(n_vocab, np.float32)
+                assert L.rwkv_eval_sequence(ctx.ptr, pp_, len(pseq), None, None, slg.ctypes.data_as(P_F))
+                chunk = -(-args.seq_len // (2 * P))  # LayerPipeline::pick_chunk: ceil(T / 2P) in whole 64-token
+                chunk = min(args.seq_len, max(256, -(-chunk // 64) * 64))  # tiles, at least 256, at most T
+                pairs = L.rwkv_mi355x_pipeline_peer_pairs(pctx)
+                pipe = {'tokens_per_s': round(args.seq_len / min(pts), 1), 'ms_per_sequence': round(min(pts) * 1e3, 3),
+                        'stages': P, 'devices': devices, 'peer_pairs': pairs, 'chunk': chunk, 'T': args.seq_len,
+                        'parallelism': f'layer pipeline x{P} (one process, rwkv_mi355x_init_pipeline)',
+                        'scaling': 'strong',
+                        'transport': ('hipMemcpyPeerAsync over xGMI, peer access enabled' if pairs else
+                                      'device-local copies (every stage on one GPU)'),
+                        'bit_exact_vs_single_context': bool(np.array_equal(plg.view(np.uint32), slg.view(np.uint32))),
+                        'single_context_ms_per_sequence': round(seq_s * 1e3, 3),
+                        'overhead_vs_single_context': round(min(pts) / seq_s, 4) if world == 1 else None,
+                        'stage_weight_gb': round(L.rwkv_mi355x_weight_bytes(ctx.ptr, True) / 1e9 / P, 4)}
+                L.rwkv_free(pctx)
+                log(f'pipeline seq-eval, {P} stages on {devices}: {min(pts) * 1e3:.1f} ms ({args.seq_len / min(pts):.0f} '
+                    f'tok/s, chunk {chunk}, peer pairs {pairs}); one context {seq_s * 1e3:.1f} ms; bit-exact '
+                    f'{pipe["bit_exact_vs_single_context"]}')
+                if not pipe['bit_exact_vs_single_context']:
+                    errors.append('pipeline: logits differ from one context')
+            except Exception as e:  # the decode line is still printed; the run exits non-zero
+                errors.append(f'pipeline: {e!r}')
+                log(f'pipeline seq-eval failed: {e!r}')
+        barrier()
 
     # ---------------- ABI-level decode (host state, reference contract) ----------------
     state = np.zeros(state_len, np.float32)
@@ -421,8 +466,9 @@ def main():
                            for k in kstats},
             'kernel_time_us_per_token': round(all_ms / timing_steps * 1e3, 1),
             'decode_bytes_per_token': round(dbytes),
-            'decode_GBps_end_to_end': round(dbytes / (ms_per_step * 1e-3) / 1e9, 1),
-            'decode_frac_end_to_end': round(dbytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            'decode_GBps_end_to_end': round(dbytes / (ms_per_step * 1e-3) / 1e9, 1) if ms_per_step else None,
+            'decode_frac_end_to_end': (round(dbytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                                       if ms_per_step else None),
         }
     except StopIteration:
         pass
@@ -486,11 +532,13 @@ def main():
             cpu_s = time.perf_counter() - t4
             cpu = {'value': round(ntok / cpu_s, 3), 'unit': 'tokens/s', 'cores': olib().oracle_get_threads(),
                    'threads': olib().oracle_get_threads(), 'host_cpus': os.cpu_count(),
+                   'host_physical_cores': physical_cores(),
                    'kind': 'port',
                    'sample': f'{label} single-token decode (logits on), {ntok} tokens from a fresh state, '
                              f'{cpu_s:.1f}s; oracle/ C restatement of the reference CPU arithmetic '
                              f'(ggml Q8 activation quantization + int8 block dots), OpenMP over rows; cores = OpenMP '
-                             f'threads used (OMP_NUM_THREADS, else min(16, host CPUs)), host_cpus = os.cpu_count()'}
+                             f'threads used (OMP_NUM_THREADS, else min(16, host CPUs)), host_cpus = os.cpu_count() '
+                             f'(logical), host_physical_cores = distinct (package, core) pairs in /proc/cpuinfo'}
             log(f'cpu baseline: {cpu["value"]} tok/s on {cpu["cores"]} threads (load {load_s:.1f}s)')
         except Exception as e:
             errors.append(f'cpu_baseline: {e!r}')
@@ -506,8 +554,10 @@ def main():
     L.rwkv_free(ctx.ptr)
     if rank == 0:
         out = {
-            'metric': METRIC, 'value': round(value, 2), 'unit': 'tokens/s', 'n_gpus': world, 'steps': args.steps,
-            'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 5), 'higher_is_better': True,
+            'metric': METRIC, 'value': round(value, 2) if value is not None else None, 'unit': 'tokens/s',
+            'n_gpus': world, 'steps': args.steps,
+            'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 5) if ms_per_step is not None else None,
+            'higher_is_better': True,
             'scaling': 'weak', 'vs_baseline': None, 'dtype': 'i8 (q4 x q8 int8 dot) + f32', 'data': 'synthetic',
             'config': {'workload': f'{label} single-token decode (rwkv_eval semantics, logits on), '
                                    f'state resident in HBM', 'n_embed': C, 'n_layer': NL, 'n_vocab': V,
@@ -537,8 +587,10 @@ def main():
             errors.append('roofline missing')
         if args.seq_reps > 0 and seq_roofline is None:
             errors.append('seq_roofline missing')
-        if world > 1 and args.seq_reps > 0 and pipe is None:
+        if args.seq_reps > 0 and args.pipe_stages != 0 and pipe is None:
             errors.append('seq_eval.pipeline missing')
+        if args.roofline_only:
+            out['not_a_measurement'] = 'roofline-only pass: no timed decode steps; value / ms_per_step are null'
         if errors:
             out['errors'] = errors
         print(json.dumps(out), flush=True)

@@ -58,6 +58,11 @@ RWKV_API bool rwkv_mi355x_sync(struct rwkv_context * ctx);
  * (names: x xa sx r k v g w y a nb bb vfirst fr lora bonus logits, slot<i>.<q|d|s|qsum|h|f>).
  * Returns the bytes copied, or -1 (unknown name / copy failure).  Not part of rwkv.h. */
 RWKV_API long long rwkv_mi355x_debug_buffer(struct rwkv_context * ctx, const char * name, void * out, size_t bytes);
+/* Test hooks (not part of rwkv.h): "skip_granule" = index of a k_v6_att_fused producer workgroup that
+ * publishes nothing (-1: off), so the in-launch hand-off times out and the next synchronising call
+ * fails with RWKV_ERROR_CTX; "spin_max" = the hand-off sweep bound in passes (<= 0: the default
+ * 2^20).  Returns false for an unknown name or a NULL context. */
+RWKV_API bool rwkv_mi355x_debug_set(struct rwkv_context * ctx, const char * name, long long value);
 
 /* One stage of the layer pipeline (the reference has no such entry point -- it is
  * the unit the multi-GPU sequence evaluation is built from, rwkv.cppy_amd/python/rwkv_cpp/pipeline.py).
@@ -101,11 +106,18 @@ RWKV_API struct rwkv_context * rwkv_mi355x_init_from_file_layers(const char * pa
  * chunk c+1; results are bit-identical to a single-GPU context.  rwkv_clone_context clones the
  * pipeline (same stages and GPUs, weights shared).  The same context is what rwkv_init_from_file
  * returns when RWKV_MI355X_PIPELINE=P (P >= 2) is set (devices: RWKV_MI355X_PIPELINE_DEVICES, a
- * comma list).  The device-resident entry points refuse a pipeline context (it is partial). */
+ * comma list).  Adjacent stages on different GPUs get peer access enabled at init (a GPU pair
+ * without it fails the init).  rwkv_eval_sequence_in_chunks passes chunk_size to the pipeline as
+ * its chunk (the results do not depend on it).  rwkv_mi355x_state_upload / _download / sync act on
+ * every stage; the other device-resident entry points (eval_device, eval_batch*, stream,
+ * device_state, clone_context_on) refuse a pipeline context with RWKV_ERROR_UNSUPPORTED. */
 RWKV_API struct rwkv_context * rwkv_mi355x_init_pipeline(const char * path, uint32_t n_threads, int n_stages,
                                                          const int * devices);
 /* Stages of a context: P for a pipeline context, 1 otherwise (0 for NULL). */
 RWKV_API int rwkv_mi355x_pipeline_stages(const struct rwkv_context * ctx);
+/* Adjacent stage pairs of a pipeline context that sit on different GPUs (their hop is a peer copy
+ * over xGMI, peer access enabled at init); 0 when every stage shares one GPU or for a non-pipeline. */
+RWKV_API int rwkv_mi355x_pipeline_peer_pairs(const struct rwkv_context * ctx);
 
 /* Batched decode (multi-context serving): n_contexts independent sequences of this
  * model advance ONE token each in one pass -- the rwkv_eval of each context, with every weight byte

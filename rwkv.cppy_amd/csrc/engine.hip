@@ -373,6 +373,7 @@ Engine::~Engine() {
     if (m2_) (void)hipFree(m2_);
     for (void * p : ws_allocs_) (void)hipFree(p);
     if (htokens_) (void)hipHostFree(htokens_);
+    if (herr_h_) (void)hipHostFree(herr_h_);
     collect_timing();
     for (hipEvent_t e : event_pool_) (void)hipEventDestroy(e);
     if (tok_event_) (void)hipEventDestroy(tok_event_);
@@ -396,15 +397,16 @@ bool Engine::init() {
     }
     HIP_OK(hipMalloc(&logits_, (size_t)m_->n_vocab * sizeof(float) + 16));
     ws_allocs_.push_back(logits_);
-    // in-launch hand-off counters (k_v6_att_fused): zero once here, re-armed by the kernels
-    HIP_OK(hipMalloc(&hcnt_, kHandoffWords * 4));
-    ws_allocs_.push_back(hcnt_);
-    HIP_OK(hipMemset(hcnt_, 0, kHandoffWords * 4));
+    // in-launch hand-off (k_v6_att_fused): granules zeroed once here and re-armed by their readers;
+    // the timeout flag is a host-mapped word, so checking it costs the host one load after a sync
+    HIP_OK(hipHostMalloc((void **)&herr_h_, 64, hipHostMallocMapped | hipHostMallocCoherent));
+    *(volatile unsigned *)herr_h_ = 0;
+    HIP_OK(hipHostGetDevicePointer((void **)&herr_d_, herr_h_, 0));
     {
-        const size_t ng = 6 * (size_t)m_->n_embed;  // k_v6_att_fused granules: 4 C + H D (D <= 128, H = C / 64)
-        HIP_OK(hipMalloc(&hgran_, ng * 8));
+        hgran_n_ = 6 * (size_t)m_->n_embed;  // k_v6_att_fused granules: 4 C + H D (D <= 128, H = C / 64)
+        HIP_OK(hipMalloc(&hgran_, hgran_n_ * 8));
         ws_allocs_.push_back(hgran_);
-        HIP_OK(hipMemset(hgran_, 0, ng * 8));
+        HIP_OK(hipMemset(hgran_, 0, hgran_n_ * 8));
     }
     const char * g = getenv("RWKV_MI355X_NO_GRAPH");
     use_graphs_ = !(g && g[0] == '1');
@@ -442,7 +444,7 @@ bool Engine::ensure_workspace(int T) {
     // keep state and logits, drop the rest; until every allocation below has succeeded the
     // workspace counts as absent (tcap_ = 0, pointers null), so a failed grow can never leave a
     // capacity that points at freed or missing buffers
-    std::vector<void *> keep = {dstate_[0], dstate_[1], logits_, hcnt_, hgran_};
+    std::vector<void *> keep = {dstate_[0], dstate_[1], logits_, hgran_};
     for (void * p : ws_allocs_) {
         bool k = false;
         for (void * q : keep) k |= (p == q);
@@ -1405,8 +1407,9 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits, uint32
             f.xw = outs[mats[4]];
             f.att = a;
             f.gran = hgran_;
-            f.cnt = hcnt_;
-            f.err = hcnt_ + kHandoffWords - 1;
+            f.err = herr_d_;
+            f.spin_max = spin_max_;
+            f.skip_wg = dbg_skip_gran_;
             if (v6_att_fused_supported(f)) {
                 if (timing_) {
                     // r, k, v, g, Wd1, Wd2 weights, their 5 Q8 inputs, the head state in and out,
@@ -1622,7 +1625,7 @@ bool Engine::state_download(float * state) {
     HIP_OK(hipMemcpyAsync(state, dstate_[cur_], m_->state_len * 4, hipMemcpyDeviceToHost, stream_));
     HIP_OK(hipStreamSynchronize(stream_));
     io_d2h_ += m_->state_len * 4.0;
-    return true;
+    return handoff_check();
 }
 
 // The host layout is per layer contiguous (rwkv_graph.inc:545-606), so layers [l0, l1) are one
@@ -1642,11 +1645,39 @@ bool Engine::state_download_layers(float * slice, uint32_t l0, uint32_t l1) {
     HIP_OK(hipMemcpyAsync(slice, dstate_[cur_] + off, n * 4, hipMemcpyDeviceToHost, stream_));
     HIP_OK(hipStreamSynchronize(stream_));
     io_d2h_ += n * 4.0;
-    return true;
+    return handoff_check();
 }
 
 bool Engine::sync() {
     HIP_OK(hipStreamSynchronize(stream_));
+    return handoff_check();
+}
+
+// k_v6_att_fused's reducer gives up after spin_max_ sweep passes and sets the host-mapped flag
+// (mv_att6f.hip).  Every call that synchronises the stream reads it: a set flag fails that call
+// (the reference's error convention: false + RWKV_ERROR_CTX, rwkv_error_handling.inc:1-54).  A
+// producer that arrives after the timeout leaves its granule tagged, which the next launch would
+// read as its own value, so every granule is cleared before the flag is re-armed.
+bool Engine::handoff_check() {
+    if (*(volatile unsigned *)herr_h_ == 0) return true;
+    (void)hipStreamSynchronize(stream_);
+    (void)hipMemsetAsync(hgran_, 0, hgran_n_ * 8, stream_);
+    (void)hipStreamSynchronize(stream_);
+    *(volatile unsigned *)herr_h_ = 0;
+    fprintf(stderr, "rwkv: in-launch hand-off timed out (k_v6_att_fused): the evaluation's results are invalid\n");
+    return false;
+}
+
+bool Engine::debug_set(const char * name, long long value) {
+    if (!name) return false;
+    const std::string n(name);
+    if (n == "skip_granule") dbg_skip_gran_ = (int)value;
+    else if (n == "spin_max") spin_max_ = value > 0 ? (unsigned)std::min<long long>(value, 0xffffffffLL) : (1u << 20);
+    else return false;
+    // the decode graphs captured the old values
+    (void)hipStreamSynchronize(stream_);
+    drop_graphs();
+    drop_io_graphs();
     return true;
 }
 
@@ -1741,6 +1772,7 @@ bool Engine::eval_host_chunked(uint32_t token, const float * state_in, float * s
     HIP_OK(hipStreamSynchronize(io_stream_[1]));
     HIP_OK(hipStreamSynchronize(io_stream_[0]));
     HIP_OK(hipStreamSynchronize(stream_));
+    if (!handoff_check()) return false;
     cur_ ^= 1;
     return true;
 }
@@ -1766,6 +1798,7 @@ bool Engine::eval(const uint32_t * tokens, size_t T, const float * state_in, flo
         return false;
     }
     if (!state_upload(state_in)) return false;
+    const int cur0 = cur_;
     if (!run_tokens(tokens, T, logits_out != nullptr)) return false;
     if (logits_out)
         HIP_OK(hipMemcpyAsync(logits_out, logits_, (size_t)m_->n_vocab * 4, hipMemcpyDeviceToHost, stream_));
@@ -1774,6 +1807,10 @@ bool Engine::eval(const uint32_t * tokens, size_t T, const float * state_in, flo
         io_d2h_ += m_->state_len * 4.0;
     }
     HIP_OK(hipStreamSynchronize(stream_));
+    if (!handoff_check()) {
+        cur_ = cur0;
+        return false;
+    }
     return true;
 }
 
@@ -1805,8 +1842,11 @@ bool Engine::eval_layers(const uint32_t * tokens, size_t T, uint32_t l0, uint32_
     if (vfirst_io && m_->major == 7) HIP_OK(hipMemcpyAsync(vfirst_io, vfirst_, bytes, hipMemcpyDeviceToDevice, stream_));
     if (lg && logits_out)
         HIP_OK(hipMemcpyAsync(logits_out, logits_, (size_t)m_->n_vocab * 4, hipMemcpyDeviceToHost, stream_));
-    if (sync) HIP_OK(hipStreamSynchronize(stream_));  // async: the caller orders on stream() (pipeline.py)
-    return true;
+    if (sync) {
+        HIP_OK(hipStreamSynchronize(stream_));
+        return handoff_check();
+    }
+    return true;  // async: the caller orders on stream() (pipeline.py) and synchronises (sync())
 }
 
 // Names: x xa sx r k v g w y a nb bb vfirst fr lora bonus logits, slot<i>.<q|d|s|qsum|h|f>.
@@ -1826,7 +1866,6 @@ long long Engine::debug_copy(const char * name, void * out, size_t bytes) {
     if (n == "lora") src = lora_, cap_bytes = cap * kmax * 4;
     if (n == "bonus") src = bonus_, cap_bytes = cap * (size_t)std::max<int64_t>(1, m_->H) * 4;
     if (n == "logits") src = logits_, cap_bytes = (size_t)m_->n_vocab * 4;
-    if (n == "handoff") src = hcnt_, cap_bytes = kHandoffWords * 4;  // in-launch counters, [last] = timeout flag
     if (n == "granules") src = hgran_, cap_bytes = 6 * C * 8;  // k_v6_att_fused hand-off granules
     if (!src && n.rfind("slot", 0) == 0) {
         const size_t dot = n.find('.');
@@ -1966,6 +2005,7 @@ bool Engine::eval_batch(const uint32_t * tokens, size_t B, const float * state_i
         if (logits_out) HIP_OK(hipMemcpyAsync(logits_out, lout, B * V * 4, hipMemcpyDeviceToHost, stream_));
         if (state_out) HIP_OK(hipMemcpyAsync(state_out, sout, B * n * 4, hipMemcpyDeviceToHost, stream_));
         HIP_OK(hipStreamSynchronize(stream_));
+        return handoff_check();
     }
     return true;
 }
@@ -1980,7 +2020,10 @@ bool Engine::eval_device(const uint32_t * tokens, size_t T, bool want_logits, fl
     if (!run_tokens(tokens, T, want_logits || logits_out != nullptr)) return false;
     if (logits_out)
         HIP_OK(hipMemcpyAsync(logits_out, logits_, (size_t)m_->n_vocab * 4, hipMemcpyDeviceToHost, stream_));
-    if (sync_after || logits_out) HIP_OK(hipStreamSynchronize(stream_));
+    if (sync_after || logits_out) {
+        HIP_OK(hipStreamSynchronize(stream_));
+        return handoff_check();
+    }
     return true;
 }
 

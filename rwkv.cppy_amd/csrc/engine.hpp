@@ -113,6 +113,12 @@ class Engine : public KLaunchTimer {
     float * device_state() const { return dstate_[cur_]; }
     // debugging aid (rwkv_mi355x_debug_buffer): copies a workspace buffer of the last evaluation
     long long debug_copy(const char * name, void * out, size_t bytes);
+    // test hooks (rwkv_mi355x_debug_set): "skip_granule" = producer workgroup of k_v6_att_fused that
+    // publishes nothing (-1 off), "spin_max" = the hand-off sweep bound; returns false for unknown names
+    bool debug_set(const char * name, long long value);
+    // false when an in-launch hand-off of the work completed so far timed out: reports it, clears the
+    // granules and the flag (the caller fails the evaluation with RWKV_ERROR_CTX)
+    bool handoff_check();
 
   private:
     bool ensure_workspace(int T);
@@ -146,9 +152,12 @@ class Engine : public KLaunchTimer {
     ActSlot slots_[kSlots];
     float * dstate_[2] = {nullptr, nullptr};
     int cur_ = 0;
-    static constexpr int kHandoffWords = 256;  // in-launch hand-off counters; the last word = timeout flag
-    unsigned * hcnt_ = nullptr;
+    unsigned * herr_h_ = nullptr;  // hand-off timeout flag, host-mapped (herr_d_ = its device address)
+    unsigned * herr_d_ = nullptr;
     unsigned long long * hgran_ = nullptr;  // in-launch hand-off granules (k_v6_att_fused)
+    size_t hgran_n_ = 0;
+    int dbg_skip_gran_ = -1;
+    unsigned spin_max_ = 1u << 20;
     hipGraphExec_t graphs_[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // [cur][logits]
     bool use_graphs_ = true;
     bool split_maa_ = false;       // RWKV_MI355X_SPLIT_MAA=1: v6 decode W1 + mix as two launches

@@ -213,9 +213,11 @@ struct Att6Fused {
     DMat wd1;        // time_decay_w1 (M = D, K = C)
     ActBuf xw;       // its input
     Att6Dec att;     // wd2, decay, u, sin, sout, lnx_w, lnx_b, eps, yq
-    unsigned long long * gran;  // 4 C + D zeroed 8-byte granules: r, k, v, silu(g), tanh(Wd1 . xw)
-    unsigned * cnt;  // one zeroed word: heads that have read the decay granules
-    unsigned * err;  // set on a hand-off timeout
+    unsigned long long * gran;  // 4 C + H D zeroed 8-byte granules: r, k, v, silu(g), tanh(Wd1 . xw)
+    unsigned * err;  // set (system scope) on a hand-off timeout: a host-mapped word the engine reads
+                     // after every synchronising call (Engine::handoff_check)
+    unsigned spin_max;  // sweep bound (passes) before a timeout
+    int skip_wg;     // test hook: this producer workgroup publishes nothing (-1: none)
 };
 bool v6_att_fused_supported(const Att6Fused & a);
 bool launch_v6_att_fused(hipStream_t st, const Att6Fused & a);

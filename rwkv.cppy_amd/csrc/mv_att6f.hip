@@ -12,8 +12,9 @@
 // the head's state, decay-tail weights and per-channel operands while its own rows streamed --
 // sweeps its head's granules and runs k_att6_dec's arithmetic (decay tail, wkv6, GroupNorm, gate,
 // Q8 emission of Wo's input).  The waiting workgroups are producers first, so the wait can never
-// hold a slot a producer needs; every spin is bounded (a timeout sets *err and the results are
-// garbage, never a hang).  Each granule has exactly one reader, which clears it right after
+// hold a slot a producer needs; every spin is bounded: a timeout sets *err (a host-mapped word) and
+// the engine fails the evaluation that synchronises next, then clears every granule (a late
+// producer may have left one tagged) -- never a hang, never a silently wrong result.  Each granule has exactly one reader, which clears it right after
 // reading: no counters, no atomics, and a replayed graph needs no memset node.
 //
 // The state update uses 16-byte accesses: wave g owns keys 16g..16g+15, lane (kk, jq) keys
@@ -104,10 +105,11 @@ __device__ __forceinline__ void gran_clear(unsigned long long * g) {
     __hip_atomic_store((gu64_t *)g, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// One wave sweeps N granules per lane (stride S) until every tag is set; bounded (timeout: *err).
+// One wave sweeps N granules per lane (stride S) until every tag is set; bounded (timeout: *err, a
+// host-mapped word, stored at system scope so the host sees it after the stream synchronises).
 template <int N>
 __device__ __forceinline__ void gran_sweep(const unsigned long long * g, int stride, bool (&live)[N], float (&v)[N],
-                                           unsigned * err) {
+                                           unsigned * err, unsigned spin_max) {
     for (unsigned it = 0;; it++) {
         bool ok = true;
         unsigned long long x[N];
@@ -119,8 +121,8 @@ __device__ __forceinline__ void gran_sweep(const unsigned long long * g, int str
             ok = ok && (x[k] >> 32) == 1ull;
         }
         if (__all(ok)) return;
-        if (it >= (1u << 20)) {
-            stu_sc1(err, 1u);
+        if (it >= spin_max) {
+            __hip_atomic_store((gunsigned_t *)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             return;
         }
         __builtin_amdgcn_s_sleep(1);
@@ -145,11 +147,13 @@ __global__ __launch_bounds__(320) void k_v6_att_fused(Att6Fused a) {
     // the reducer's late scalars (Wo input record, hand-off words, eps) in SGPRs now
     const ActBuf yq = at.yq;
     unsigned * const err = a.err;
+    const unsigned spin_max = a.spin_max;
     const float eps = at.eps;
     if (red) {
         pin_act(yq);
-        asm volatile("" ::"s"(err), "s"(eps));
+        asm volatile("" ::"s"(err), "s"(eps), "s"(spin_max));
     }
+    const bool publish = wg != a.skip_wg;  // test hook (Engine debug knob "skip_granule")
     // ---- the reducer's head operands first (state rows, per-channel vectors, decay-tail weights):
     // they stream in with this workgroup's own weight rows
     float4 st[4];
@@ -181,12 +185,12 @@ __global__ __launch_bounds__(320) void k_v6_att_fused(Att6Fused a) {
         const DMat W = m == 0 ? a.W[0] : m == 1 ? a.W[1] : m == 2 ? a.W[2] : a.W[3];
         const ActBuf x = m == 0 ? a.x[0] : m == 1 ? a.x[1] : m == 2 ? a.x[2] : a.x[3];
         const float v = af_rows<WF, AF_R, U>(W, x, row0, m == 3 ? EPI_SILU : EPI_STORE, lane);
-        if (lane < AF_R) gran_put(a.gran + (size_t)m * C + row0 + lane, v);
+        if (lane < AF_R && publish) gran_put(a.gran + (size_t)m * C + row0 + lane, v);
     } else {
         for (int d = af_slot(sidx, h, H); d < D; d += AF_P * H) {
             const float v = af_rows<WF, 1, U>(a.wd1, a.xw, d, EPI_TANH, lane);  // in lane 0
             const float v0 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
-            if (lane < H) gran_put(gdl + (size_t)lane * D + d, v0);  // one copy per head
+            if (lane < H && publish) gran_put(gdl + (size_t)lane * D + d, v0);  // one copy per head
         }
     }
     if (!red) {
@@ -199,7 +203,7 @@ __global__ __launch_bounds__(320) void k_v6_att_fused(Att6Fused a) {
         unsigned long long * g = a.gran + (size_t)wave * C + c0 + lane;
         bool live[1] = {true};
         float v[1];
-        gran_sweep<1>(g, 0, live, v, err);
+        gran_sweep<1>(g, 0, live, v, err, spin_max);
         float * dst = wave == 0 ? sr : wave == 1 ? sk : wave == 2 ? sv : sg;
         dst[lane] = v[0];
         gran_clear(g);
@@ -211,7 +215,7 @@ __global__ __launch_bounds__(320) void k_v6_att_fused(Att6Fused a) {
         bool live[2] = {lane < D, lane + 64 < D};
         float v[2];
         unsigned long long * const own = gdl + (size_t)h * D + lane;  // this head's copy
-        gran_sweep<2>(own, 64, live, v, err);
+        gran_sweep<2>(own, 64, live, v, err, spin_max);
         if (live[0]) gran_clear(own);
         if (live[1]) gran_clear(own + 64);
         const ActBuf act = lds_act(smem, act_fmt_for(WD), D);

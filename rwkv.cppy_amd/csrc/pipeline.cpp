@@ -50,7 +50,43 @@ bool LayerPipeline::init(const std::vector<StageSpec> & specs, size_t n_embed, b
             HIP_OK(hipEventCreateWithFlags(&s.consumed[b], hipEventDisableTiming));
         }
     }
+    // The hop between adjacent stages on different GPUs is a peer copy issued on the producer's
+    // stream: with peer access enabled both ways it is one DMA over xGMI; without it the runtime
+    // would stage it through host memory, so a pair without peer access fails the init.
+    for (size_t i = 0; i + 1 < st_.size(); i++) {
+        const int a = st_[i].device, b = st_[i + 1].device;
+        if (a == b) continue;
+        int ab = 0, ba = 0;
+        HIP_OK(hipDeviceCanAccessPeer(&ab, a, b));
+        HIP_OK(hipDeviceCanAccessPeer(&ba, b, a));
+        if (!ab || !ba) {
+            fprintf(stderr, "rwkv: layer pipeline: GPUs %d and %d have no peer access (stages %zu, %zu)\n", a, b, i,
+                    i + 1);
+            return false;
+        }
+        for (int k = 0; k < 2; k++) {
+            HIP_OK(hipSetDevice(k ? b : a));
+            const hipError_t e = hipDeviceEnablePeerAccess(k ? a : b, 0);
+            if (e == hipErrorPeerAccessAlreadyEnabled) {
+                (void)hipGetLastError();
+            } else if (e != hipSuccess) {
+                fprintf(stderr, "rwkv: layer pipeline: enabling peer access %d -> %d failed: %s\n", k ? b : a, k ? a : b,
+                        hipGetErrorString(e));
+                return false;
+            }
+        }
+        peer_pairs_++;
+    }
     return true;
+}
+
+// Drains every stage stream (after an error: no copy or kernel of this call may still touch the
+// staging buffers when the next call reuses or frees them).
+void LayerPipeline::drain() {
+    for (Stage & s : st_) {
+        (void)hipSetDevice(s.device);
+        (void)hipStreamSynchronize(s.eng->stream());
+    }
 }
 
 bool LayerPipeline::ensure_buffers(size_t chunk) {
@@ -91,6 +127,20 @@ bool LayerPipeline::eval(const uint32_t * tokens, size_t T, const float * state_
     if (!chunk) chunk = pick_chunk(T);
     chunk = std::min(chunk, T);
     if (!ensure_buffers(chunk)) return false;
+    if (!eval_impl(tokens, T, state_in, state_out, logits_out, layer_len, chunk)) {
+        drain();
+        // a failure may have been an in-launch hand-off timeout: clear every stage's flag
+        for (Stage & s : st_) {
+            (void)hipSetDevice(s.device);
+            (void)s.eng->handoff_check();
+        }
+        return false;
+    }
+    return true;
+}
+
+bool LayerPipeline::eval_impl(const uint32_t * tokens, size_t T, const float * state_in, float * state_out,
+                              float * logits_out, size_t layer_len, size_t chunk) {
     const size_t P = st_.size();
     // state in: each stage uploads its own slice (NULL = fresh)
     for (Stage & s : st_) {
@@ -123,16 +173,15 @@ bool LayerPipeline::eval(const uint32_t * tokens, size_t T, const float * state_
             HIP_OK(hipEventRecord(s.consumed[b], sst));
         }
     }
-    // state out: each stage's slice (synchronous per stage); otherwise wait for every stage
+    // state out: each stage's slice (synchronous per stage); otherwise wait for every stage.  Both
+    // read each stage's hand-off flag (Engine::handoff_check).
+    bool ok = true;
     for (Stage & s : st_) {
         HIP_OK(hipSetDevice(s.device));
-        if (state_out) {
-            if (!s.eng->state_download_layers(state_out + (size_t)s.l0 * layer_len, s.l0, s.l1)) return false;
-        } else {
-            HIP_OK(hipStreamSynchronize(s.eng->stream()));
-        }
+        if (state_out) ok = s.eng->state_download_layers(state_out + (size_t)s.l0 * layer_len, s.l0, s.l1) && ok;
+        else ok = s.eng->sync() && ok;
     }
-    return true;
+    return ok;
 }
 
 }  // namespace rwkvmi

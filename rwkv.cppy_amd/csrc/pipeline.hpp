@@ -23,6 +23,7 @@ class LayerPipeline {
               size_t layer_len, size_t chunk = 0);
     size_t stages() const { return st_.size(); }
     size_t pick_chunk(size_t T) const;
+    int peer_pairs() const { return peer_pairs_; }  // adjacent stage pairs on different GPUs (peer access on)
 
   private:
     struct Stage {
@@ -35,6 +36,10 @@ class LayerPipeline {
         hipEvent_t consumed[2] = {nullptr, nullptr};  // this stage is done with buffer b
     };
     bool ensure_buffers(size_t chunk);
+    bool eval_impl(const uint32_t * tokens, size_t T, const float * state_in, float * state_out, float * logits_out,
+                   size_t layer_len, size_t chunk);
+    void drain();
+    int peer_pairs_ = 0;
     std::vector<Stage> st_;
     size_t C_ = 0, cap_ = 0;
     bool v7_ = false;

@@ -595,6 +595,254 @@ __global__ __launch_bounds__(256) void k_qgemm(MMGroup g) {
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// k_qg32 (round 5): the same arithmetic as k_qgemm on the 32 x 32 MFMA shapes.
+//
+// A wave owns a 32-row x 32-token tile of the workgroup's 64 x 64 (as before); per step (block):
+//   * ONE v_mfma_i32_32x32x32_i8 gives the 32 x 32 integer block dots (k_qgemm issued four
+//     16x16x32, each holding the SIMD's vector issue as long as this one does);
+//   * ONE v_mfma_f32_32x32x2_f32 gives p = d_w * d_x for the 32 x 32 outputs as an outer product
+//     (k = 0: d_w of row i times d_x of token j onto C = 0; k = 1: 0 x 0).  d_w and d_x are fp16
+//     values, so d_w * d_x is exact in f32 and the MFMA's fma reproduces the VALU product bit for
+//     bit (a product of -0 becomes +0, which no chain can see: every class chain starts with
+//     fma(p, s, +0)).  The VALU epilogue is then s = sumi (bias trick) and acc = fma(p, s, acc):
+//     two ops per output and block instead of three, and the operands of a step are three LDS
+//     reads (row fragment, token fragment, one d each) instead of k_qgemm's eight;
+//   * lane l holds token (l & 31) and rows 8g + 4 (l >> 5) + q (g, q < 4) -- the 32x32 D layout.
+// The class walk, the binary-counter folds, the LDS-DMA ring of CH-step chunks, the epilogue
+// stores / fused Q8 emission / split-K partials are k_qgemm's, so y is bit-identical.
+typedef int qg_v16i_t __attribute__((ext_vector_type(16)));
+typedef float qg_v16f_t __attribute__((ext_vector_type(16)));
+
+struct Q32Ops {
+    v4i_t a, b;  // row fragment (16 int8 of row l & 31, half l >> 5), token fragment (same half)
+    float dw, dx;  // lanes < 32: d of row l / token l (k = 0 of the outer product); lanes >= 32: 0 (k = 1)
+};
+
+template <int WF>
+__device__ __forceinline__ void q32_read(const char * sp, Q32Ops & o, int wr, int wt, int lane) {
+    using Lt = QGLayout<WF>;
+    const int r = wr + (lane & 31), hh = lane >> 5, t = wt + (lane & 31);
+    o.a = *(const v4i_t *)(sp + qg_w_off(r, hh * 16));
+    const char * ap = sp + Lt::WB;
+    o.b = *(const v4i_t *)(ap + hh * QG_TOK * 16 + t * 16);
+    const float dw = *(const float *)(sp + qg_w_d(WF) + r * 4);
+    const float dx = *(const float *)(ap + QG_A_D + t * 4);
+    o.dw = hh ? 0.0f : dw;
+    o.dx = hh ? 0.0f : dx;
+}
+
+// y[t][m] for the lane's 16 outputs (token tok0 + wt + (l & 31), rows row0 + wr + 8g + 4(l >> 5) + q)
+__device__ __forceinline__ void q32_store(const MMEntry & E, const float * m2, int T, int M, int tok0, int row0, int wt,
+                                          int wr, int lane, const float (&tot)[16]) {
+    const int t = tok0 + wt + (lane & 31), hh = lane >> 5;
+    if (E.fuse_emit) {
+        // the wave's 32 rows of token t are one quantization block of the next matmul's input: 16 in
+        // this lane, 16 in lane l ^ 32.  quant32 / store32's values: amax over the block (order-free),
+        // d = amax / 127 (fp16-rounded), q = rint(v * 127 / amax).
+        const int tc = min(t, T - 1);
+        float v[16];
+        float am = 0.0f;
+#pragma unroll
+        for (int g = 0; g < 4; g++)
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int m = row0 + wr + 8 * g + 4 * hh + q;
+                const float t2 = m2 ? m2[(size_t)m * T + tc] : 0.0f;
+                v[4 * g + q] = apply_epi_v(E, m, tot[4 * g + q] + t2, 0.0f, 0.0f);
+                am = fmaxf(am, fabsf(v[4 * g + q]));
+            }
+        am = fmaxf(am, __shfl_xor(am, 32));
+        const float d = am / 127.f;
+        const float id = (am != 0.0f) ? 127.f / am : 0.0f;
+        if (t < T) {
+            uint8_t * rec = E.out.tq + ((size_t)(t / QG_TOK) * (M >> 5) + ((row0 + wr) >> 5)) * qg_a_bytes(false);
+            const int tl = t % QG_TOK;
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                uint32_t packed = 0;
+#pragma unroll
+                for (int q = 0; q < 4; q++) packed |= ((uint32_t)(int)rintf(v[4 * g + q] * id) & 0xffu) << (8 * q);
+                // block element e = 8g + 4hh + q: half e >> 4 = g >> 1, byte (8 (g & 1) + 4 hh + q)
+                *(uint32_t *)(rec + (g >> 1) * QG_TOK * 16 + tl * 16 + 8 * (g & 1) + 4 * hh) = packed;
+            }
+            if (hh == 0) ((float *)(rec + QG_A_D))[tl] = f16_round(d);
+        }
+        return;
+    }
+    if (t >= T) return;
+    const bool vec = ((E.ldy | M) & 3) == 0 && (((uintptr_t)E.y | (uintptr_t)E.aux) & 15) == 0;
+#pragma unroll
+    for (int g = 0; g < 4; g++) {
+        const int m0 = row0 + wr + 8 * g + 4 * hh;
+        if (m0 >= M) continue;
+        float acc[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) acc[q] = tot[4 * g + q] + (m2 && m0 + q < M ? m2[(size_t)(m0 + q) * T + t] : 0.0f);
+        float * yp = E.y + (size_t)t * E.ldy + m0;
+        if (vec) {
+            float4 yv = make_float4(0.f, 0.f, 0.f, 0.f), av = yv;
+            if (epi_reads_y(E.epi)) yv = *(const float4 *)yp;
+            if (epi_reads_aux(E.epi)) av = *(const float4 *)(E.aux + (size_t)t * E.ldy + m0);
+            float4 o;
+            o.x = apply_epi_v(E, m0, acc[0], yv.x, av.x);
+            o.y = apply_epi_v(E, m0 + 1, acc[1], yv.y, av.y);
+            o.z = apply_epi_v(E, m0 + 2, acc[2], yv.z, av.z);
+            o.w = apply_epi_v(E, m0 + 3, acc[3], yv.w, av.w);
+            *(float4 *)yp = o;
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                if (m0 + q < M) yp[q] = apply_epi(E, t, m0 + q, acc[q]);
+        }
+    }
+}
+
+__device__ __forceinline__ void q32_store_part(float * part, int sidx, int T, int M, int tok0, int row0, int wt, int wr,
+                                               int lane, const float (&sub)[16]) {
+    const int t = tok0 + wt + (lane & 31), hh = lane >> 5;
+    if (t >= T) return;
+#pragma unroll
+    for (int g = 0; g < 4; g++) {
+        const int m0 = row0 + wr + 8 * g + 4 * hh;
+        float * pp = part + ((size_t)sidx * T + t) * M + m0;
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            if (m0 + q < M) pp[q] = sub[4 * g + q];
+    }
+}
+
+// This wave's share of chunk c of CH steps: steps CH c + wave + 4 h2 (the walk is at the first of
+// them and is left at CH (c + 1) + wave).
+template <int WF, int CH>
+__device__ __forceinline__ void q32_load_chunk(v4i_t rw, v4i_t ra, unsigned lds_buf, int c, QGWalk & wk, int nsteps,
+                                               int wave, int lane) {
+    using Lt = QGLayout<WF>;
+#pragma unroll
+    for (int h2 = 0; h2 < CH / 4; h2++) {
+        const int k = wave + 4 * h2;
+        if (c * CH + k < nsteps) {
+            const int b = wk.block();
+            const unsigned m = lds_buf + k * Lt::STEP;
+            qg_record<Lt::WB>(rw, (unsigned)(b * Lt::WB), m, lane);
+            qg_record<Lt::AC>(ra, (unsigned)(b * Lt::AB), m + Lt::WB, lane);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++) wk.next();
+    }
+}
+
+template <int WF, int SPLIT, int CH>
+__global__ __launch_bounds__(256) void k_qg32(MMGroup g) {
+    using Lt = QGLayout<WF>;
+    constexpr bool ONE = Lt::ONE;
+    constexpr int CPS = 64 / SPLIT;  // classes per split
+    constexpr int BUF = Lt::STEP * CH;
+    __shared__ __attribute__((aligned(16))) char smem[2][BUF];
+    int e = 0;
+#pragma unroll 1
+    while (e + 1 < g.n && (int)blockIdx.x >= g.e[e + 1].block0) e++;
+    const MMEntry & E = g.e[e];
+    const int M = E.W.M, K = E.W.K, T = g.T, nb = K >> 5;
+    const int tilesT = (T + QG_TOK - 1) / QG_TOK;
+    const int local0 = (int)blockIdx.x - E.block0;
+    const int sidx = local0 % SPLIT, local = local0 / SPLIT, l0 = sidx * CPS;
+    const int mtile = local / tilesT, ttile = local % tilesT;
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int row0 = mtile * Lt::ROWS, tok0 = ttile * QG_TOK;
+    const int wr = (wave & 1) * 32, wt = (wave >> 1) * 32;  // this wave's tile-local rows / tokens
+    const v4i_t rw = qg_rsrc(E.W.gt + (size_t)mtile * nb * Lt::WB);
+    const v4i_t ra = qg_rsrc(E.in.tq + (size_t)ttile * nb * Lt::AB);
+    const unsigned lds0 = __builtin_amdgcn_readfirstlane((unsigned)(unsigned long)(lds_void_t *)&smem[0][0]);
+    const int cq = nb >> 6, crem = nb & 63;
+    const int nsteps = CPS * cq + min(max(crem - l0, 0), CPS);
+    QGWalk ld;
+    ld.init(nb, l0);
+    for (int i = 0; i < wave; i++) ld.next();
+
+    float st[6][16];
+    float tot[16];
+    float c[16];
+    const int nchunks = (nsteps + CH - 1) / CH;
+    int k = 0, cb = 0, cn = 1;
+    Q32Ops cur;
+    const qg_v16i_t bias = {QG_BIAS, QG_BIAS, QG_BIAS, QG_BIAS, QG_BIAS, QG_BIAS, QG_BIAS, QG_BIAS,
+                            QG_BIAS, QG_BIAS, QG_BIAS, QG_BIAS, QG_BIAS, QG_BIAS, QG_BIAS, QG_BIAS};
+    const qg_v16f_t fzero = {};
+    auto step = [&](auto first, float (&acc)[16]) {
+        constexpr bool FIRST = decltype(first)::value;
+        if (k == CH) {
+            k = 0;
+            qg_chunk_done();
+            if (cn < nchunks) q32_load_chunk<WF, CH>(rw, ra, lds0 + cb * BUF, cn, ld, nsteps, wave, lane);
+            cn++;
+            cb ^= 1;
+            q32_read<WF>(smem[cb], cur, wr, wt, lane);
+        }
+        const qg_v16i_t sv = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.a, cur.b, bias, 0, 0, 0);
+        const qg_v16f_t p = __builtin_amdgcn_mfma_f32_32x32x2f32(cur.dw, cur.dx, fzero, 0, 0, 0);
+        Q32Ops nxt = cur;
+        if (k + 1 < CH) q32_read<WF>(smem[cb] + (k + 1) * Lt::STEP, nxt, wr, wt, lane);
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+            const qf2_t si = qf2_t{__int_as_float(sv[r]), __int_as_float(sv[r + 1])} + qf2_t{-QG_BIAS_F, -QG_BIAS_F};
+            const qf2_t a0 = FIRST ? qf2_t{0.0f, 0.0f} : qf2_t{acc[r], acc[r + 1]};
+            const qf2_t a = __builtin_elementwise_fma(qf2_t{p[r], p[r + 1]}, si, a0);
+            acc[r] = a.x;
+            acc[r + 1] = a.y;
+        }
+        cur = nxt;
+        k++;
+    };
+    using T1 = std::integral_constant<bool, true>;
+    using T0 = std::integral_constant<bool, false>;
+    auto run_class = [&](int l, float (&acc)[16]) {
+        const int n = cq + (l < crem ? 1 : 0);
+        if (n == 0) {
+#pragma unroll
+            for (int r = 0; r < 16; r++) acc[r] = 0.0f;
+            return;
+        }
+        step(T1{}, acc);
+        for (int u = 1; u < n; u++) step(T0{}, acc);
+    };
+#define Q32_CASE(N, DST)                                                          \
+    case N: {                                                                     \
+        _Pragma("unroll") for (int r = 0; r < 16; r++) {                          \
+            float v = c[r];                                                       \
+            for (int kk = 0; kk < N; kk++) v = st[kk][r] + v;                     \
+            DST[r] = v;                                                           \
+        }                                                                         \
+        break;                                                                    \
+    }
+    if (nchunks > 0) q32_load_chunk<WF, CH>(rw, ra, lds0, 0, ld, nsteps, wave, lane);
+    qg_chunk_done();
+    if (nchunks > 1) q32_load_chunk<WF, CH>(rw, ra, lds0 + BUF, 1, ld, nsteps, wave, lane);
+    cn = 2;
+    q32_read<WF>(smem[0], cur, wr, wt, lane);
+    for (int pr = 0; pr < CPS / 2; pr++) {
+        run_class(l0 + 2 * pr, st[0]);
+        run_class(l0 + 2 * pr + 1, c);
+        switch (__builtin_ctz(~(2 * pr + 1))) {
+            Q32_CASE(1, st[1])
+            Q32_CASE(2, st[2])
+            Q32_CASE(3, st[3])
+            Q32_CASE(4, st[4])
+            Q32_CASE(5, st[5])
+            default:
+            Q32_CASE(6, tot)
+        }
+    }
+#undef Q32_CASE
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (SPLIT == 1) {
+        q32_store(E, ONE ? g.m2 + E.moff : nullptr, T, M, tok0, row0, wt, wr, lane, tot);
+    } else {
+        constexpr int LEV = SPLIT == 8 ? 3 : SPLIT == 4 ? 4 : 5;
+        q32_store_part(g.part + E.poff, sidx, T, M, tok0, row0, wt, wr, lane, st[LEV]);
+    }
+}
+
 // The _1 formats' m*s chains, in the matvec's association: for class l (= b mod 64) the chain
 // acc = acc + m_w[b] * s_x[b] over b = l + 64 u ascending, from 0; the 64 class sums folded by
 // wave_sum63's tree (the binary counter of the GEMM).  Independent of the int8 dot, so it runs as

@@ -247,6 +247,10 @@ RWKV_API int rwkv_mi355x_pipeline_stages(const struct rwkv_context * ctx) {
     return ctx && ctx->pipe ? (int)ctx->pipe->stages() : (ctx ? 1 : 0);
 }
 
+RWKV_API int rwkv_mi355x_pipeline_peer_pairs(const struct rwkv_context * ctx) {
+    return ctx && ctx->pipe ? ctx->pipe->peer_pairs() : 0;
+}
+
 RWKV_API struct rwkv_context * rwkv_mi355x_init_from_file_layers(const char * path, const uint32_t n_threads,
                                                                  const uint32_t layer_begin, const uint32_t layer_end) {
     g_last_error = RWKV_ERROR_NONE;
@@ -301,6 +305,8 @@ RWKV_API struct rwkv_context * rwkv_mi355x_clone_context_on(struct rwkv_context 
                                                             const int device) {
     if (!ctx) return nullptr;
     ctx->last_error = RWKV_ERROR_NONE;
+    CTX_CHECK(ctx, RWKV_ERROR_CTX | RWKV_ERROR_UNSUPPORTED, nullptr, ctx->pipe == nullptr,
+              "A layer pipeline context cannot be replicated onto one device (use rwkv_clone_context)");
     int ndev = 0;
     (void)hipGetDeviceCount(&ndev);
     CTX_CHECK(ctx, RWKV_ERROR_ARGS, nullptr, device >= 0 && device < ndev, "Device %d out of range (0 .. %d)", device,
@@ -357,9 +363,9 @@ RWKV_API struct rwkv_context * rwkv_mi355x_clone_context_on(struct rwkv_context 
 RWKV_API int rwkv_mi355x_context_device(const struct rwkv_context * ctx) { return ctx ? ctx->model->dm.device : -1; }
 
 static bool pipe_eval(struct rwkv_context * ctx, const uint32_t * tokens, size_t T, const float * state_in,
-                      float * state_out, float * logits_out) {
+                      float * state_out, float * logits_out, size_t chunk = 0) {
     CTX_CHECK(ctx, RWKV_ERROR_CTX, false,
-              ctx->pipe->eval(tokens, T, state_in, state_out, logits_out, ctx->engine->layer_state_len()),
+              ctx->pipe->eval(tokens, T, state_in, state_out, logits_out, ctx->engine->layer_state_len(), chunk),
               "GPU evaluation failed (layer pipeline)");
     return true;
 }
@@ -378,8 +384,16 @@ RWKV_API bool rwkv_eval(struct rwkv_context * ctx, const uint32_t token, const f
     return true;
 }
 
+static bool eval_sequence(struct rwkv_context * ctx, const uint32_t * tokens, const size_t T, const float * state_in,
+                          float * state_out, float * logits_out, size_t pipe_chunk);
+
 RWKV_API bool rwkv_eval_sequence(struct rwkv_context * ctx, const uint32_t * tokens, const size_t T, const float * state_in,
                                  float * state_out, float * logits_out) {
+    return eval_sequence(ctx, tokens, T, state_in, state_out, logits_out, 0);
+}
+
+static bool eval_sequence(struct rwkv_context * ctx, const uint32_t * tokens, const size_t T, const float * state_in,
+                          float * state_out, float * logits_out, size_t pipe_chunk) {
     ctx->last_error = RWKV_ERROR_NONE;
     CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, T > 0, "Sequence length is 0");
     if (!tokens) return true;  // build/cache only (rwkv_eval_inc:102,122): workspace is allocated lazily
@@ -389,7 +403,7 @@ RWKV_API bool rwkv_eval_sequence(struct rwkv_context * ctx, const uint32_t * tok
         for (size_t i = 0; i < T; i++)
             CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, tokens[i] < nv, "Token at index %zu (%" PRIu32 ") is out of range (0 .. %zu)",
                       i, tokens[i], nv - 1);
-        return pipe_eval(ctx, tokens, T, state_in, state_out, logits_out);
+        return pipe_eval(ctx, tokens, T, state_in, state_out, logits_out, pipe_chunk);
     }
     CTX_CHECK(ctx, RWKV_ERROR_CTX | RWKV_ERROR_UNSUPPORTED, false, !ctx->model->dm.partial(),
               "This context holds layers [%u, %u) only (a pipeline stage): use rwkv_mi355x_eval_layers",
@@ -411,8 +425,9 @@ RWKV_API bool rwkv_eval_sequence_in_chunks(struct rwkv_context * ctx, const uint
     CTX_CHECK(ctx, RWKV_ERROR_ARGS, false, chunk_size > 0, "Chunk size is 0");
     // The per-token arithmetic of this engine does not depend on how a sequence is cut, so the
     // chunked call is one device-resident pass (state never returns to the host in between);
-    // results are bit-identical to the reference's chunk loop (rwkv_eval.inc:158-221).
-    return rwkv_eval_sequence(ctx, tokens, T, state_in, state_out, logits_out);
+    // results are bit-identical to the reference's chunk loop (rwkv_eval.inc:158-221).  A layer
+    // pipeline context takes chunk_size as its chunk (the unit that moves between stages).
+    return eval_sequence(ctx, tokens, T, state_in, state_out, logits_out, chunk_size);
 }
 
 RWKV_API size_t rwkv_get_n_vocab(const struct rwkv_context * ctx) { return ctx->model->dm.n_vocab; }
@@ -476,13 +491,46 @@ RWKV_API const char * rwkv_get_system_info_string(void) {
 
 // ------------------------------------------------------------------ additive extensions
 
+// Every stage of a pipeline context holds its own layers' slice: the whole-state calls move each
+// stage's slice (state + l0 * layer_len) on that stage's GPU.
+static std::vector<rwkv_context *> all_stages(rwkv_context * ctx) {
+    std::vector<rwkv_context *> v = {ctx};
+    v.insert(v.end(), ctx->stages.begin(), ctx->stages.end());
+    return v;
+}
+
 RWKV_API bool rwkv_mi355x_state_upload(struct rwkv_context * ctx, const float * state) {
     if (!ctx || !ctx->engine) return false;
+    if (ctx->pipe) {
+        const size_t per = ctx->engine->layer_state_len();
+        for (rwkv_context * s : all_stages(ctx)) {
+            use_device(s);
+            const DeviceModel & dm = s->model->dm;
+            CTX_CHECK(ctx, RWKV_ERROR_CTX, false,
+                      s->engine->state_upload_layers(state ? state + (size_t)dm.layer_lo * per : nullptr, dm.layer_lo,
+                                                     dm.layer_hi),
+                      "State upload failed (pipeline stage on device %d)", dm.device);
+        }
+        use_device(ctx);
+        return true;
+    }
     use_device(ctx);
     return ctx->engine->state_upload(state);
 }
 RWKV_API bool rwkv_mi355x_state_download(struct rwkv_context * ctx, float * state) {
     if (!ctx || !ctx->engine || !state) return false;
+    if (ctx->pipe) {
+        const size_t per = ctx->engine->layer_state_len();
+        for (rwkv_context * s : all_stages(ctx)) {
+            use_device(s);
+            const DeviceModel & dm = s->model->dm;
+            CTX_CHECK(ctx, RWKV_ERROR_CTX, false,
+                      s->engine->state_download_layers(state + (size_t)dm.layer_lo * per, dm.layer_lo, dm.layer_hi),
+                      "State download failed (pipeline stage on device %d)", dm.device);
+        }
+        use_device(ctx);
+        return true;
+    }
     use_device(ctx);
     return ctx->engine->state_download(state);
 }
@@ -616,17 +664,39 @@ RWKV_API bool rwkv_mi355x_eval_batch_device(struct rwkv_context * ctx, const uin
 
 RWKV_API bool rwkv_mi355x_sync(struct rwkv_context * ctx) {
     if (!ctx || !ctx->engine) return false;
+    bool ok = true;
+    for (rwkv_context * s : all_stages(ctx)) {
+        use_device(s);
+        ok = s->engine->sync() && ok;
+    }
     use_device(ctx);
-    return ctx->engine->sync();
+    CTX_CHECK(ctx, RWKV_ERROR_CTX, false, ok, "GPU evaluation failed (reported at synchronisation)");
+    return true;
 }
 RWKV_API long long rwkv_mi355x_debug_buffer(struct rwkv_context * ctx, const char * name, void * out, size_t bytes) {
     return ctx && ctx->engine ? ctx->engine->debug_copy(name, out, bytes) : -1;
 }
+RWKV_API bool rwkv_mi355x_debug_set(struct rwkv_context * ctx, const char * name, long long value) {
+    if (!ctx || !ctx->engine) return false;
+    bool ok = true;
+    for (rwkv_context * s : all_stages(ctx)) {
+        use_device(s);
+        ok = s->engine->debug_set(name, value) && ok;
+    }
+    use_device(ctx);
+    return ok;
+}
 RWKV_API void * rwkv_mi355x_stream(struct rwkv_context * ctx) {
-    return ctx && ctx->engine ? (void *)ctx->engine->stream() : nullptr;
+    if (!ctx || !ctx->engine) return nullptr;
+    CTX_CHECK(ctx, RWKV_ERROR_CTX | RWKV_ERROR_UNSUPPORTED, nullptr, ctx->pipe == nullptr,
+              "A layer pipeline context has one stream per stage");
+    return (void *)ctx->engine->stream();
 }
 RWKV_API float * rwkv_mi355x_device_state(struct rwkv_context * ctx) {
-    return ctx && ctx->engine ? ctx->engine->device_state() : nullptr;
+    if (!ctx || !ctx->engine) return nullptr;
+    CTX_CHECK(ctx, RWKV_ERROR_CTX | RWKV_ERROR_UNSUPPORTED, nullptr, ctx->pipe == nullptr,
+              "A layer pipeline context's state is split over its stages");
+    return ctx->engine->device_state();
 }
 
 RWKV_API double rwkv_mi355x_weight_bytes(const struct rwkv_context * ctx, bool with_head) {

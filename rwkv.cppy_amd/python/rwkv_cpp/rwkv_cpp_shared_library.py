@@ -125,6 +125,10 @@ class RWKVSharedLibrary:
         L.rwkv_mi355x_init_pipeline.restype = vp
         L.rwkv_mi355x_pipeline_stages.argtypes = [vp]
         L.rwkv_mi355x_pipeline_stages.restype = ctypes.c_int
+        L.rwkv_mi355x_pipeline_peer_pairs.argtypes = [vp]
+        L.rwkv_mi355x_pipeline_peer_pairs.restype = ctypes.c_int
+        L.rwkv_mi355x_debug_set.argtypes = [vp, ctypes.c_char_p, ctypes.c_longlong]
+        L.rwkv_mi355x_debug_set.restype = ctypes.c_bool
 
         self.nullptr = ctypes.cast(0, ctypes.c_void_p)
 

@@ -160,8 +160,8 @@ def test_v6_1b6_width_1024_tokens(cfg_dir):
 def test_v6_decode_handoff_many_tokens(cfg_dir):
     """The fused v6 decode launch (mv_att6f.hip: r, k, v, g and decay-LoRA rows + per-head attention,
     an in-launch granule hand-off per head) at the v6-1B6 width over many tokens: serial decode equals
-    one sequence evaluation bit for bit (the sequence path has no hand-off), and afterwards every
-    granule is cleared, the reader counter re-armed and the timeout flag clear."""
+    one sequence evaluation bit for bit (the sequence path has no hand-off), every rwkv_eval
+    succeeded (no hand-off timed out) and afterwards every granule is cleared."""
     import ctypes
     path = cfg_model(cfg_dir, 'v6-1b6-q4_0')
     toks = [int(t) for t in np.random.default_rng(12).integers(0, VOCAB, 48)]
@@ -170,11 +170,6 @@ def test_v6_decode_handoff_many_tokens(cfg_dir):
     slg, sst = m.eval_sequence(toks, None, use_numpy=True)
     assert_bits_equal(lg, slg, 'decode vs sequence logits')
     assert_bits_equal(st, sst, 'decode vs sequence state')
-    words = np.ones(256, np.uint32)
-    n = library().library.rwkv_mi355x_debug_buffer(m._ctx.ptr, b'handoff', words.ctypes.data_as(ctypes.c_void_p),
-                                                   words.nbytes)
-    assert n == words.nbytes
-    assert not words.any(), f'hand-off words not re-armed / timeout: {np.nonzero(words)[0][:8]}'
     C = 2048
     gran = np.ones(6 * C, np.uint64)  # r, k, v, g rows + one decay-LoRA copy per head
     n = library().library.rwkv_mi355x_debug_buffer(m._ctx.ptr, b'granules', gran.ctypes.data_as(ctypes.c_void_p),
@@ -182,3 +177,47 @@ def test_v6_decode_handoff_many_tokens(cfg_dir):
     assert n == gran.nbytes
     assert not gran.any(), f'hand-off granules not cleared: {np.nonzero(gran)[0][:8]}'
     m.free()
+
+
+@pytest.mark.parametrize('skip_wg', [9, 8 * 31 + 7])
+def test_v6_decode_handoff_timeout_fails_the_call(cfg_dir, skip_wg):
+    """A hand-off that times out must fail the evaluation, never return garbage with success
+    (reference error convention: false + RWKV_ERROR_CTX, rwkv_error_handling.inc:1-54).  The test hook
+    makes one producer workgroup of k_v6_att_fused publish nothing (9: head 1's slot 1 -- r, k, v, g
+    rows; 255: the last head's slot 7 -- decay-LoRA rows) with a short sweep bound.  rwkv_eval (host
+    state, the chunked graphs) and rwkv_mi355x_eval_device + rwkv_mi355x_sync both fail with
+    RWKV_ERROR_CTX; with the hook off the same context then decodes bit-exactly again (the granules
+    were cleared and the flag re-armed)."""
+    import ctypes
+    L = library().library
+    path = cfg_model(cfg_dir, 'v6-1b6-q4_0')
+    toks = [int(t) for t in np.random.default_rng(13).integers(0, VOCAB, 4)]
+    ctx = L.rwkv_init_from_file(path.encode(), 1, 99)
+    assert ctx
+    L.rwkv_set_print_errors(ctx, False)
+    n_state, n_vocab = L.rwkv_get_state_len(ctx), L.rwkv_get_n_vocab(ctx)
+    fp = ctypes.POINTER(ctypes.c_float)
+    ref_lg, ref_st = gpu_variant(path, toks)
+    E_CTX = 6 << 8  # RWKV_ERROR_CTX (reference rwkv.h:50; flags = category | code)
+    assert L.rwkv_mi355x_debug_set(ctx, b'spin_max', 2048)
+    assert L.rwkv_mi355x_debug_set(ctx, b'skip_granule', skip_wg)
+    st = np.zeros(n_state, np.float32)
+    lg = np.zeros(n_vocab, np.float32)
+    L.rwkv_init_state(ctx, st.ctypes.data_as(fp))
+    assert not L.rwkv_eval(ctx, toks[0], st.ctypes.data_as(fp), st.ctypes.data_as(fp), lg.ctypes.data_as(fp))
+    assert (L.rwkv_get_last_error(ctx) & 0xff00) == E_CTX
+    # the device-resident path: enqueue without waiting, the synchronising call reports it
+    arr = (ctypes.c_int32 * 1)(toks[0])
+    assert L.rwkv_mi355x_state_upload(ctx, None)
+    assert L.rwkv_mi355x_eval_device(ctx, arr, 1, True, None, False)
+    assert not L.rwkv_mi355x_sync(ctx)
+    assert (L.rwkv_get_last_error(ctx) & 0xff00) == E_CTX
+    # hook off: the context decodes correctly again
+    assert L.rwkv_mi355x_debug_set(ctx, b'skip_granule', -1)
+    assert L.rwkv_mi355x_debug_set(ctx, b'spin_max', 0)
+    L.rwkv_init_state(ctx, st.ctypes.data_as(fp))
+    for t in toks:
+        assert L.rwkv_eval(ctx, t, st.ctypes.data_as(fp), st.ctypes.data_as(fp), lg.ctypes.data_as(fp))
+    assert_bits_equal(lg, ref_lg, 'logits after a timed-out hand-off')
+    assert_bits_equal(st, ref_st, 'state after a timed-out hand-off')
+    L.rwkv_free(ctx)

@@ -4,7 +4,8 @@ stage by peer copies while the previous stage starts chunk c + 1.  On the one-GP
 on device 0 (the same code path; the peer copy is then a device-local copy).  rwkv_eval_sequence /
 rwkv_eval on the pipeline context must equal a single-GPU context bit for bit -- logits and state,
 fresh and carried state -- at the BASELINE config-4 width (v7-2.9B: C 2560, H 40, Q5_1) over several
-256-token chunks, and on the tiny v6 checkpoint through the environment switch."""
+256-token chunks, at BASELINE config 5's partition (v5-7B width, 8 stages, 4096 tokens in chunks of
+1024), and on the tiny v6 checkpoint through the environment switch."""
 import ctypes
 import os
 
@@ -12,7 +13,7 @@ import numpy as np
 import pytest
 import torch  # noqa: F401  (torch's HIP runtime before the library's)
 
-from oracle_ctypes import assert_bits_equal
+from oracle_ctypes import assert_bits_equal, gpu_variant
 from rwkv_lib import library
 
 pytestmark = pytest.mark.gpu
@@ -105,3 +106,52 @@ def test_pipeline_env_switch_and_clone(monkeypatch):
     L.rwkv_free(clone)
     L.rwkv_free(pipe)
     L.rwkv_free(single)
+
+
+def _seq_chunks(L, ctx, toks, chunk):
+    n_vocab, n_state = L.rwkv_get_n_vocab(ctx), L.rwkv_get_state_len(ctx)
+    t = np.ascontiguousarray(np.asarray(toks, np.int32))
+    lg = np.zeros(n_vocab, np.float32)
+    st = np.zeros(n_state, np.float32)
+    assert L.rwkv_eval_sequence_in_chunks(ctx, t.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), len(t), chunk, None,
+                                          st.ctypes.data_as(P_F), lg.ctypes.data_as(P_F))
+    return lg, st
+
+
+def test_pipeline_v5_width_eight_stages(tmp_path):
+    """BASELINE config 5's partition: 8 stages at the v5-7B width (C 4096, FFN 14336, 64 heads, Q4_1),
+    one layer per stage, 4096 tokens through rwkv_eval_sequence_in_chunks(chunk_size = 1024), which a
+    pipeline context takes as its chunk: equal to one single-GPU context bit for bit.  The oracle
+    (GPU association) pins the same 8-stage pipeline on 160 tokens in chunks of 64 (64, 64, 32:
+    ragged), the CPU-affordable length at this width.  Every stage sits on device 0 of the one-GPU
+    test box; init reports no peer pairs then."""
+    L = library().library
+    p = str(tmp_path / 'v5-7b-q4_1-L8.bin')
+    assert L.rwkv_mi355x_write_synthetic_model(p.encode(), 5, 4096, 4096, 8, 14336, b'Q4_1', 33)
+    toks = [int(t) for t in np.random.default_rng(43).integers(0, 4096, 4096)]
+    devs = (ctypes.c_int * 8)(*([0] * 8))
+    pipe = L.rwkv_mi355x_init_pipeline(p.encode(), 1, 8, devs)
+    assert pipe and L.rwkv_mi355x_pipeline_stages(pipe) == 8
+    assert L.rwkv_mi355x_pipeline_peer_pairs(pipe) == 0
+    plg, pst = _seq_chunks(L, pipe, toks, 1024)
+    single = L.rwkv_init_from_file(p.encode(), 1, 99)
+    assert single
+    slg, sst = _seq_chunks(L, single, toks, 1024)
+    L.rwkv_free(single)
+    assert_bits_equal(plg, slg, '8-stage pipeline logits, T = 4096')
+    assert_bits_equal(pst, sst, '8-stage pipeline state, T = 4096')
+    short = toks[:160]
+    olg, ost = gpu_variant(p, short, sequence=True)
+    plg, pst = _seq_chunks(L, pipe, short, 64)
+    assert_bits_equal(plg, olg, '8-stage pipeline logits vs oracle')
+    assert_bits_equal(pst, ost, '8-stage pipeline state vs oracle')
+    # the whole-state entry points act on every stage
+    st = np.zeros(L.rwkv_get_state_len(pipe), np.float32)
+    assert L.rwkv_mi355x_state_download(pipe, st.ctypes.data_as(P_F))
+    assert_bits_equal(st, ost, 'pipeline rwkv_mi355x_state_download')
+    assert L.rwkv_mi355x_sync(pipe)
+    L.rwkv_set_print_errors(pipe, False)
+    assert not L.rwkv_mi355x_stream(pipe)
+    assert not L.rwkv_mi355x_device_state(pipe)
+    assert not L.rwkv_mi355x_clone_context_on(pipe, 1, 0)
+    L.rwkv_free(pipe)

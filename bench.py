@@ -486,15 +486,15 @@ def main():
             assert L.rwkv_mi355x_eval_device(ctx.ptr, sp, len(seq), True, None, True)
             sstats = read_stats()
             L.rwkv_mi355x_set_kernel_timing(ctx.ptr, False)
-            g = [k for k in sstats if k['name'].startswith('k_qgemm')]
+            g = [k for k in sstats if k['name'].startswith(('k_qgemm', 'k_qg32'))]
             if not g:
                 raise RuntimeError('no k_qgemm timings recorded')
             ms = sum(k['ms'] for k in g)
             flops = sum(k['flops'] for k in g)
             tops = flops / (ms * 1e-3) / 1e12
-            other = [k for k in sstats if not k['name'].startswith('k_qgemm')]
+            other = [k for k in sstats if not k['name'].startswith(('k_qgemm', 'k_qg32'))]
             seq_roofline = {
-                'kernel': 'k_qgemm (all int8-MFMA sequence GEMM launches)', 'bound': 'mfma',
+                'kernel': 'k_qgemm / k_qg32 (all int8-MFMA sequence GEMM launches)', 'bound': 'mfma',
                 'achieved': round(tops, 1), 'peak': INT8_MFMA_PEAK_TOPS, 'unit': 'TOP/s',
                 'frac': round(tops / INT8_MFMA_PEAK_TOPS, 4), 'launches': sum(k['launches'] for k in g),
                 'ms_per_sequence': round(ms, 3), 'algorithmic_ops': flops,

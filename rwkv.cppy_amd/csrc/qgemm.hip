@@ -76,6 +76,21 @@ __device__ __forceinline__ void qg_chunk_done() {
 }
 
 constexpr int QG_STEPS = 8;  // blocks per chunk
+#ifndef QG32_PK
+#define QG32_PK 0  // k_qg32 epilogue in packed f32 (1) or scalar f32 (0)
+#endif
+#ifndef QG32_PROBE
+#define QG32_PROBE 0  // tools: 1 = copies only, 2 = compute only (stale LDS after the first chunks)
+#endif
+#ifndef QG32_PMUL
+#define QG32_PMUL 0  // 1: p = d_w * d_x on the VALU instead of the f32 outer-product MFMA
+#endif
+#ifndef QG32_PIPE
+#define QG32_PIPE 0  // 1: MFMAs of step k + 1 issued before step k's epilogue
+#endif
+#ifndef QG32_RT
+#define QG32_RT 1  // k_qg32 workgroup rows in 64-row tiles (2: 128 x 64 tiles, 8 waves)
+#endif
 
 template <int WF>
 struct QGLayout {
@@ -619,12 +634,15 @@ struct Q32Ops {
     float dw, dx;  // lanes < 32: d of row l / token l (k = 0 of the outer product); lanes >= 32: 0 (k = 1)
 };
 
-template <int WF>
-__device__ __forceinline__ void q32_read(const char * sp, Q32Ops & o, int wr, int wt, int lane) {
+// sp: the step's LDS base ([RT weight records][activation record]); wr: the wave's first row in the
+// workgroup's RT x 64 rows (its 32 rows sit in weight record wr / 64)
+template <int WF, int RT = 1>
+__device__ __forceinline__ void q32_read(const char * sp0, Q32Ops & o, int wr, int wt, int lane) {
     using Lt = QGLayout<WF>;
-    const int r = wr + (lane & 31), hh = lane >> 5, t = wt + (lane & 31);
+    const char * sp = sp0 + (wr >> 6) * Lt::WB;
+    const int r = (wr & 63) + (lane & 31), hh = lane >> 5, t = wt + (lane & 31);
     o.a = *(const v4i_t *)(sp + qg_w_off(r, hh * 16));
-    const char * ap = sp + Lt::WB;
+    const char * ap = sp0 + RT * Lt::WB;
     o.b = *(const v4i_t *)(ap + hh * QG_TOK * 16 + t * 16);
     const float dw = *(const float *)(sp + qg_w_d(WF) + r * 4);
     const float dx = *(const float *)(ap + QG_A_D + t * 4);
@@ -714,31 +732,46 @@ __device__ __forceinline__ void q32_store_part(float * part, int sidx, int T, in
 
 // This wave's share of chunk c of CH steps: steps CH c + wave + 4 h2 (the walk is at the first of
 // them and is left at CH (c + 1) + wave).
-template <int WF, int CH>
-__device__ __forceinline__ void q32_load_chunk(v4i_t rw, v4i_t ra, unsigned lds_buf, int c, QGWalk & wk, int nsteps,
-                                               int wave, int lane) {
+// RT weight records per step (row tiles of the workgroup; rw2 = the second one's descriptor, used
+// when it exists) and one activation record; NW = 4 RT waves, wave w copies steps w, w + NW, ...
+template <int WF, int CH, int RT = 1>
+__device__ __forceinline__ void q32_load_chunk(v4i_t rw, v4i_t rw2, bool two, v4i_t ra, unsigned lds_buf, int c,
+                                               QGWalk & wk, int nsteps, int wave, int lane) {
     using Lt = QGLayout<WF>;
+    constexpr int NW = 4 * RT, STEP = RT * Lt::WB + Lt::AC;
 #pragma unroll
-    for (int h2 = 0; h2 < CH / 4; h2++) {
-        const int k = wave + 4 * h2;
-        if (c * CH + k < nsteps) {
+    for (int h2 = 0; h2 < (CH + NW - 1) / NW; h2++) {
+        const int k = wave + NW * h2;
+        if (k < CH && c * CH + k < nsteps) {
             const int b = wk.block();
-            const unsigned m = lds_buf + k * Lt::STEP;
+            const unsigned m = lds_buf + k * STEP;
             qg_record<Lt::WB>(rw, (unsigned)(b * Lt::WB), m, lane);
-            qg_record<Lt::AC>(ra, (unsigned)(b * Lt::AB), m + Lt::WB, lane);
+            if (RT == 2 && two) qg_record<Lt::WB>(rw2, (unsigned)(b * Lt::WB), m + Lt::WB, lane);
+            qg_record<Lt::AC>(ra, (unsigned)(b * Lt::AB), m + RT * Lt::WB, lane);
         }
 #pragma unroll
-        for (int i = 0; i < 4; i++) wk.next();
+        for (int i = 0; i < NW; i++) wk.next();
     }
 }
 
-template <int WF, int SPLIT, int CH>
-__global__ __launch_bounds__(256) void k_qg32(MMGroup g) {
+// SPILL (SPLIT == 1): tree level 5 (the sum of classes 0..31, written once and read once per tile)
+// lives in LDS instead of 16 VGPRs per lane
+#ifndef QG32_LB
+#define QG32_LB 1  // __launch_bounds__ minimum waves per SIMD (3: <= 168 VGPRs)
+#endif
+// RT = 2: 128-row x 64-token workgroup tiles (8 waves, 4 x 2 wave tiles of 32 x 32): every token
+// record feeds twice the rows, so the operand bytes per output and block drop from 1.125 to 0.84.
+template <int WF, int SPLIT, int CH, bool K64 = false, bool SPILL = false, int RT = 1>
+__global__ __launch_bounds__(256 * RT, QG32_LB) void k_qg32(MMGroup g) {
     using Lt = QGLayout<WF>;
     constexpr bool ONE = Lt::ONE;
     constexpr int CPS = 64 / SPLIT;  // classes per split
-    constexpr int BUF = Lt::STEP * CH;
+    constexpr int STEP = RT * Lt::WB + Lt::AC;
+    constexpr int BUF = STEP * CH;
+    constexpr int NW = 4 * RT;
+    static_assert(!SPILL || SPLIT == 1, "k_qg32 spill: unsplit tiles only");
     __shared__ __attribute__((aligned(16))) char smem[2][BUF];
+    __shared__ __attribute__((aligned(16))) float sp5[SPILL ? NW : 1][16][64];
     int e = 0;
 #pragma unroll 1
     while (e + 1 < g.n && (int)blockIdx.x >= g.e[e + 1].block0) e++;
@@ -749,9 +782,12 @@ __global__ __launch_bounds__(256) void k_qg32(MMGroup g) {
     const int sidx = local0 % SPLIT, local = local0 / SPLIT, l0 = sidx * CPS;
     const int mtile = local / tilesT, ttile = local % tilesT;
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int row0 = mtile * Lt::ROWS, tok0 = ttile * QG_TOK;
-    const int wr = (wave & 1) * 32, wt = (wave >> 1) * 32;  // this wave's tile-local rows / tokens
-    const v4i_t rw = qg_rsrc(E.W.gt + (size_t)mtile * nb * Lt::WB);
+    const int row0 = mtile * Lt::ROWS * RT, tok0 = ttile * QG_TOK;
+    // this wave's tile-local rows / tokens
+    const int wr = (wave & (2 * RT - 1)) * 32, wt = (wave / (2 * RT)) * 32;
+    const v4i_t rw = qg_rsrc(E.W.gt + (size_t)mtile * RT * nb * Lt::WB);
+    const bool two = RT == 2 && (mtile * RT + 1) * Lt::ROWS < M;  // the second row tile exists
+    const v4i_t rw2 = qg_rsrc(E.W.gt + (size_t)(mtile * RT + (two ? 1 : 0)) * nb * Lt::WB);
     const v4i_t ra = qg_rsrc(E.in.tq + (size_t)ttile * nb * Lt::AB);
     const unsigned lds0 = __builtin_amdgcn_readfirstlane((unsigned)(unsigned long)(lds_void_t *)&smem[0][0]);
     const int cq = nb >> 6, crem = nb & 63;
@@ -766,34 +802,116 @@ __global__ __launch_bounds__(256) void k_qg32(MMGroup g) {
     const int nchunks = (nsteps + CH - 1) / CH;
     int k = 0, cb = 0, cn = 1;
     Q32Ops cur;
-    const qg_v16i_t bias = {QG_BIAS, QG_BIAS, QG_BIAS, QG_BIAS, QG_BIAS, QG_BIAS, QG_BIAS, QG_BIAS,
-                            QG_BIAS, QG_BIAS, QG_BIAS, QG_BIAS, QG_BIAS, QG_BIAS, QG_BIAS, QG_BIAS};
+    // C = 0 (an inline constant: a bias vector in C would be re-materialised into 16 VGPRs before
+    // every MFMA, whose D overwrites it); sumi -> f32 by v_cvt_f32_i32 (exact: |sumi| < 2^24)
+    const qg_v16i_t izero = {};
     const qg_v16f_t fzero = {};
+#if QG32_PIPE
+    // Software-pipelined: step k's epilogue runs beside the MFMAs of step k + 1 (issued first from
+    // operands read one step earlier) and the LDS reads of step k + 2.  A chunk's buffer is
+    // released two steps before its end (all its operands are in registers by then).
+    Q32Ops nx;                    // operands of step k + 1
+    qg_v16i_t sv_c;               // MFMA results of step k
+    qg_v16f_t p_c;
+    auto mfma = [&](const Q32Ops & o, qg_v16i_t & sv, qg_v16f_t & pp) {
+        sv = __builtin_amdgcn_mfma_i32_32x32x32_i8(o.a, o.b, izero, 0, 0, 0);
+        pp = __builtin_amdgcn_mfma_f32_32x32x2f32(o.dw, o.dx, fzero, 0, 0, 0);
+    };
+    auto step = [&](auto first, float (&acc)[16]) {
+        constexpr bool FIRST = decltype(first)::value;
+        if (k == CH - 2) {
+            qg_chunk_done();  // the next chunk has landed; every wave holds this chunk's operands
+            if (cn < nchunks) q32_load_chunk<WF, CH, RT>(rw, rw2, two, ra, lds0 + cb * BUF, cn, ld, nsteps, wave, lane);
+            cn++;
+        }
+        Q32Ops nn;
+        if (k + 2 < CH) q32_read<WF, RT>(smem[cb] + (k + 2) * STEP, nn, wr, wt, lane);
+        else q32_read<WF, RT>(smem[cb ^ 1] + (k + 2 - CH) * STEP, nn, wr, wt, lane);
+        qg_v16i_t sv_n;
+        qg_v16f_t p_n;
+        mfma(nx, sv_n, p_n);
+        // keep the epilogue below the MFMAs (the scheduler would hoist it above them, and the next
+        // epilogue would then wait on MFMAs issued just before it)
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+            const float si = (float)sv_c[r];
+            acc[r] = __builtin_fmaf(p_c[r], si, FIRST ? 0.0f : acc[r]);
+        }
+        sv_c = sv_n;
+        p_c = p_n;
+        nx = nn;
+        if (++k == CH) {
+            k = 0;
+            cb ^= 1;
+        }
+        // straight-line (K64) chunks: no MFMA of a later step above this step's epilogue (the
+        // scheduler would hoist all of them and hold every result: 256 VGPRs)
+        if constexpr (K64) __builtin_amdgcn_sched_barrier(0);
+    };
+#else
     auto step = [&](auto first, float (&acc)[16]) {
         constexpr bool FIRST = decltype(first)::value;
         if (k == CH) {
             k = 0;
             qg_chunk_done();
-            if (cn < nchunks) q32_load_chunk<WF, CH>(rw, ra, lds0 + cb * BUF, cn, ld, nsteps, wave, lane);
+#if QG32_PROBE == 2
+            if (cn < nchunks && cn < 2)  // probe: compute only (stale LDS after the first chunks)
+#else
+            if (cn < nchunks)
+#endif
+                q32_load_chunk<WF, CH, RT>(rw, rw2, two, ra, lds0 + cb * BUF, cn, ld, nsteps, wave, lane);
             cn++;
             cb ^= 1;
-            q32_read<WF>(smem[cb], cur, wr, wt, lane);
+            q32_read<WF, RT>(smem[cb], cur, wr, wt, lane);
         }
-        const qg_v16i_t sv = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.a, cur.b, bias, 0, 0, 0);
+#if QG32_PROBE == 1
+        if (0)  // probe: copies only
+#endif
+        {
+        const qg_v16i_t sv = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.a, cur.b, izero, 0, 0, 0);
+#if QG32_PMUL
+        // p = d_w * d_x on the VALU: d_w of the lane's 16 rows (4 broadcast b128 reads), d_x of its token
+        qg_v16f_t p;
+        {
+            const char * sp = smem[cb] + k * STEP;
+            const float dxv = *(const float *)(sp + RT * Lt::WB + QG_A_D + (wt + (lane & 31)) * 4);
+#pragma unroll
+            for (int g4 = 0; g4 < 4; g4++) {
+                const float4 dw4 = *(const float4 *)(sp + (wr >> 6) * Lt::WB + qg_w_d(WF) + ((wr & 63) + 8 * g4 + 4 * (lane >> 5)) * 4);
+                p[4 * g4 + 0] = dw4.x * dxv;
+                p[4 * g4 + 1] = dw4.y * dxv;
+                p[4 * g4 + 2] = dw4.z * dxv;
+                p[4 * g4 + 3] = dw4.w * dxv;
+            }
+        }
+#else
         const qg_v16f_t p = __builtin_amdgcn_mfma_f32_32x32x2f32(cur.dw, cur.dx, fzero, 0, 0, 0);
+#endif
         Q32Ops nxt = cur;
-        if (k + 1 < CH) q32_read<WF>(smem[cb] + (k + 1) * Lt::STEP, nxt, wr, wt, lane);
+        if (k + 1 < CH) q32_read<WF, RT>(smem[cb] + (k + 1) * STEP, nxt, wr, wt, lane);
+#if QG32_PK
 #pragma unroll
         for (int r = 0; r < 16; r += 2) {
-            const qf2_t si = qf2_t{__int_as_float(sv[r]), __int_as_float(sv[r + 1])} + qf2_t{-QG_BIAS_F, -QG_BIAS_F};
+            const qf2_t si = qf2_t{(float)sv[r], (float)sv[r + 1]};
             const qf2_t a0 = FIRST ? qf2_t{0.0f, 0.0f} : qf2_t{acc[r], acc[r + 1]};
             const qf2_t a = __builtin_elementwise_fma(qf2_t{p[r], p[r + 1]}, si, a0);
             acc[r] = a.x;
             acc[r + 1] = a.y;
         }
+#else
+        // scalar f32 (packed f32 VALU beside MFMAs costs extra issue cycles: MI355X_MICROARCH.md)
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+            const float si = (float)sv[r];
+            acc[r] = __builtin_fmaf(p[r], si, FIRST ? 0.0f : acc[r]);
+        }
+#endif
         cur = nxt;
+        }
         k++;
     };
+#endif
     using T1 = std::integral_constant<bool, true>;
     using T0 = std::integral_constant<bool, false>;
     auto run_class = [&](int l, float (&acc)[16]) {
@@ -815,15 +933,66 @@ __global__ __launch_bounds__(256) void k_qg32(MMGroup g) {
         }                                                                         \
         break;                                                                    \
     }
-    if (nchunks > 0) q32_load_chunk<WF, CH>(rw, ra, lds0, 0, ld, nsteps, wave, lane);
+    if (nchunks > 0) q32_load_chunk<WF, CH, RT>(rw, rw2, two, ra, lds0, 0, ld, nsteps, wave, lane);
     qg_chunk_done();
-    if (nchunks > 1) q32_load_chunk<WF, CH>(rw, ra, lds0 + BUF, 1, ld, nsteps, wave, lane);
+    if (nchunks > 1) q32_load_chunk<WF, CH, RT>(rw, rw2, two, ra, lds0 + BUF, 1, ld, nsteps, wave, lane);
     cn = 2;
-    q32_read<WF>(smem[0], cur, wr, wt, lane);
+#if QG32_PIPE
+    {
+        Q32Ops o0;
+        q32_read<WF, RT>(smem[0], o0, wr, wt, lane);
+        q32_read<WF, RT>(smem[0] + STEP, nx, wr, wt, lane);
+        mfma(o0, sv_c, p_c);
+    }
+#else
+    q32_read<WF, RT>(smem[0], cur, wr, wt, lane);
+#endif
+    if constexpr (K64) {
+        // K = 2048: every class is one block, the walk is block order, chunk ch = classes CH ch ..
+        // CH ch + CH - 1 (of this split): the folds after the odd steps are known at compile time
+        // except the chunk's last, which closes log2(CH) + ctz(~ch) levels
+        static_assert(CH == 8 || CH == 4, "k_qg32 K64 chunk");
+        constexpr int LCH = CH == 8 ? 3 : 2;
+#pragma unroll 1
+        for (int ch = 0; ch < CPS / CH; ch++) {
+#pragma unroll
+            for (int kk = 0; kk < CH; kk++) {
+                if (kk & 1) {
+                    step(T1{}, c);
+                    constexpr int N0 = 0;
+                    (void)N0;
+                    const int nf = kk + 1 < CH ? __builtin_ctz(~kk) : LCH + __builtin_ctz(~ch);
+                    switch (nf) {
+                        Q32_CASE(1, st[1])
+                        Q32_CASE(2, st[2])
+                        Q32_CASE(3, st[3])
+                        Q32_CASE(4, st[4])
+                        Q32_CASE(5, st[5])
+                        default:
+                        Q32_CASE(6, tot)
+                    }
+                } else {
+                    step(T1{}, st[0]);
+                }
+            }
+        }
+    } else
     for (int pr = 0; pr < CPS / 2; pr++) {
         run_class(l0 + 2 * pr, st[0]);
         run_class(l0 + 2 * pr + 1, c);
-        switch (__builtin_ctz(~(2 * pr + 1))) {
+        const int nf = __builtin_ctz(~(2 * pr + 1));
+        if (SPILL && nf >= 5) {
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                float v = c[r];
+#pragma unroll
+                for (int kk = 0; kk < 5; kk++) v = st[kk][r] + v;
+                if (nf == 5) sp5[SPILL ? wave : 0][r][lane] = v;
+                else tot[r] = sp5[SPILL ? wave : 0][r][lane] + v;
+            }
+            continue;
+        }
+        switch (nf) {
             Q32_CASE(1, st[1])
             Q32_CASE(2, st[2])
             Q32_CASE(3, st[3])
@@ -1192,10 +1361,30 @@ bool launch_qg_combine(hipStream_t st, MMGroup & g, int split) {
 // next matmul's activation format is a separate launch_act_from_f32 pass by the caller.  The
 // weights need their tile records (upload_mat) and the activations must be token tiles.
 int g_qgemm_generic = 0;  // 1: K = 2048 through the generic kernel too (tools, comparison)
+#ifndef QG32_CH
+#define QG32_CH 8
+#endif
+#ifndef QG32_PK
+#define QG32_PK 0
+#endif
+#ifndef QG32_SPILL
+#define QG32_SPILL 0
+#endif
+// RWKV_MI355X_QG32=1: the 32x32-MFMA GEMM (k_qg32); g_qg32 < 0 = read the environment
+int g_qg32 = -1;
+static bool qg32_on() {
+    if (g_qg32 < 0) {
+        const char * v = getenv("RWKV_MI355X_QG32");
+        g_qg32 = v && v[0] == '1' ? 1 : 0;
+    }
+    return g_qg32 == 1;
+}
+
 int kQgCUs = 256;          // compute units of the device (set_mv_device_cus): the split-K threshold
 
 bool launch_qgemm(hipStream_t st, MMGroup & g, int wtype) {
-    const int rows = qg_rows(wtype);
+    const int RTv = qg32_on() ? QG32_RT : 1;  // k_qg32: RT row tiles of 64 per workgroup
+    const int rows = qg_rows(wtype) * RTv;
     const int tilesT = (g.T + QG_TOK - 1) / QG_TOK;
     int blocks = 0;
     for (int i = 0; i < g.n; i++) {
@@ -1254,7 +1443,7 @@ bool launch_qgemm(hipStream_t st, MMGroup & g, int wtype) {
                       e.W.M % 64 == 0 && e.ldy == e.W.M && e.epi != EPI_ADD && e.epi != EPI_SIGMUL_ADD &&
                       e.epi != EPI_VMIX7 && e.epi != EPI_DECAY6 && e.epi != EPI_DECAY7 && e.epi != EPI_SIGMOID_BIAS;
     }
-    const dim3 grid(blocks), block(256);
+    const dim3 grid(blocks), block(256), qblock(256 * RTv);
     bool k64 = true;
     for (int i = 0; i < g.n; i++) k64 = k64 && g.e[i].W.K == 2048;
     // split-K when the group has few tiles (batched decode's 64-context tiles, small-M entries such
@@ -1266,8 +1455,10 @@ bool launch_qgemm(hipStream_t st, MMGroup & g, int wtype) {
         const char * v = getenv("RWKV_MI355X_QG_SPLIT2");
         return v && v[0] == '1';
     }();
-    if (split == 0)
-        split = blocks >= 2 * kQgCUs ? 1 : (split2 && blocks >= kQgCUs) ? 2 : blocks * 4 >= 2 * kQgCUs ? 4 : 8;
+    if (split == 0) {
+        const int wb = blocks * RTv;  // in 4-wave units
+        split = wb >= 2 * kQgCUs ? 1 : (split2 && wb >= kQgCUs) ? 2 : wb * 4 >= 2 * kQgCUs ? 4 : 8;
+    }
     if (split != 1 && split != 2 && split != 4 && split != 8) split = 1;
     size_t pfl = 0;
     if (split > 1) {
@@ -1285,7 +1476,8 @@ bool launch_qgemm(hipStream_t st, MMGroup & g, int wtype) {
         const dim3 sgrid(blocks * split);
 #define QG_SPLIT_L(WFv, SP)                                                                    \
     do {                                                                                       \
-        if (k64) RK_LAUNCH((k_qgemm_k64<WFv, SP>), sgrid, block, 0, st, g);           \
+        if (qg32_on()) RK_LAUNCH((k_qg32<WFv, SP, QG32_CH, false, false, QG32_RT>), sgrid, qblock, 0, st, g);  \
+        else if (k64) RK_LAUNCH((k_qgemm_k64<WFv, SP>), sgrid, block, 0, st, g);      \
         else RK_LAUNCH((k_qgemm<WFv, SP>), sgrid, block, 0, st, g);                   \
     } while (0)
 #define QG_SPLIT_T(SP)                                                                         \
@@ -1322,6 +1514,23 @@ bool launch_qgemm(hipStream_t st, MMGroup & g, int wtype) {
             if (one) RK_LAUNCH((k_qg_combine<8, true>), dim3(cblocks), block, 0, st, g);
             else RK_LAUNCH((k_qg_combine<8, false>), dim3(cblocks), block, 0, st, g);
         }
+        HIP_OK(hipGetLastError());
+        return true;
+    }
+    if (qg32_on()) {
+#define QG32_T(WFv)                                                                                      \
+    case WFv:                                                                                            \
+        RK_LAUNCH((k_qg32<WFv, 1, QG32_CH, false, QG32_SPILL, QG32_RT>), grid, qblock, 0, st, g);                \
+        break;
+        switch (wtype) {
+            QG32_T(W_Q4_0)
+            QG32_T(W_Q4_1)
+            QG32_T(W_Q5_0)
+            QG32_T(W_Q5_1)
+            QG32_T(W_Q8_0)
+            default: fprintf(stderr, "rwkv: qgemm type %d unsupported\n", wtype); return false;
+        }
+#undef QG32_T
         HIP_OK(hipGetLastError());
         return true;
     }

@@ -388,7 +388,16 @@ bool Engine::init() {
         HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, m_->device));
         set_mv_device_cus(cus);
     }
-    HIP_OK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    {
+        // RWKV_MI355X_STREAM_PRIO=1: the compute stream on a high-priority queue (A/B)
+        const char * pr = getenv("RWKV_MI355X_STREAM_PRIO");
+        int lo = 0, hi = 0;
+        if (pr && pr[0] == '1' && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess) {
+            HIP_OK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi));
+        } else {
+            HIP_OK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+        }
+    }
     HIP_OK(hipEventCreateWithFlags(&tok_event_, hipEventDisableTiming));
     HIP_OK(hipEventRecord(tok_event_, stream_));
     for (int i = 0; i < 2; i++) {
@@ -1690,12 +1699,54 @@ bool Engine::debug_set(const char * name, long long value) {
 // works for ordinary pageable buffers too: a pageable hipMemcpyAsync holds the HOST until its
 // bytes are staged, but the chunk graphs are already queued, so the GPU keeps computing.  The
 // bytes moved and every result are exactly those of the one-graph path.
+// Both caller state buffers page-locked (registered with / allocated by the HIP runtime)?  NULL
+// buffers count as page-locked (no copy).
+static bool host_pinned(const void * p) {
+    if (!p) return true;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+bool Engine::pinned_io(const float * state_in, const float * state_out) {
+    static const int mode = [] {
+        const char * v = getenv("RWKV_MI355X_IO_ORDER");  // "interleaved" / "upfront" (A/B)
+        return !v ? 0 : (v[0] == 'i' ? 1 : v[0] == 'u' ? 2 : 0);
+    }();
+    if (mode) return mode == 2;
+    return host_pinned(state_in) && host_pinned(state_out);
+}
+
 bool Engine::eval_host_chunked(uint32_t token, const float * state_in, float * state_out, float * logits_out) {
     const uint32_t NL = m_->n_layer, K = (uint32_t)io_chunk_, NC = (NL + K - 1) / K;
     const size_t C = m_->n_embed, per_layer = m_->major >= 5 ? C * (2 + (size_t)m_->S) : 5 * C;
     if (!ensure_workspace(1)) return false;
     if (!io_stream_[0]) {
-        for (auto & st : io_stream_) HIP_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        // The host->device slices must not share a hardware queue with the compute stream (a
+        // rocprofv3 trace showed them on the same queue, each copy then waiting for the previous
+        // chunk's kernels): RWKV_MI355X_IO_PRIO=1 puts the copy streams on high-priority queues
+        const char * ip = getenv("RWKV_MI355X_IO_PRIO");
+        int plo = 0, phi = 0;
+        if (ip && ip[0] == '1' && hipDeviceGetStreamPriorityRange(&plo, &phi) == hipSuccess) {
+            HIP_OK(hipStreamCreateWithPriority(&io_stream_[0], hipStreamNonBlocking, phi));
+        } else {
+            HIP_OK(hipStreamCreateWithFlags(&io_stream_[0], hipStreamNonBlocking));
+        }
+        // The device->host slices run as the runtime's blit kernels (__amd_rocclr_copyBuffer) on
+        // compute units; RWKV_MI355X_IO_CUMASK=N confines their stream's queue to N compute units
+        // so they stop taking slots from the decode kernels (A/B; 0 = unmasked)
+        const char * cm = getenv("RWKV_MI355X_IO_CUMASK");
+        const int ncu = cm ? atoi(cm) : 0;
+        if (ncu > 0) {
+            uint32_t mask[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            for (int i = 0; i < ncu && i < 256; i++) mask[i / 32] |= 1u << (i % 32);
+            HIP_OK(hipExtStreamCreateWithCUMask(&io_stream_[1], 8, mask));
+        } else {
+            HIP_OK(hipStreamCreateWithFlags(&io_stream_[1], hipStreamNonBlocking));
+        }
         HIP_OK(hipEventCreateWithFlags(&io_entry_ev_, hipEventDisableTiming));
     }
     // the copy streams start behind everything already queued on stream_ (an earlier
@@ -1736,36 +1787,49 @@ bool Engine::eval_host_chunked(uint32_t token, const float * state_in, float * s
     hipEvent_t * in_ev = io_ev_.data(), * done_ev = io_ev_.data() + NC;
     size_t off, bytes;
     HIP_OK(hipStreamWriteValue32(stream_, dtokens_, token, 0));
-    if (state_in) {
-        slice(0, off, bytes);
+    if (!state_in && !init_state(din)) return false;
+    auto upload = [&](uint32_t c) -> bool {
+        slice(c, off, bytes);
         HIP_OK(hipMemcpyAsync(din + off, state_in + off, bytes, hipMemcpyHostToDevice, io_stream_[0]));
-        HIP_OK(hipEventRecord(in_ev[0], io_stream_[0]));
+        HIP_OK(hipEventRecord(in_ev[c], io_stream_[0]));
         io_h2d_ += (double)bytes;
-    } else if (!init_state(din)) {
-        return false;
-    }
-    for (uint32_t c = 0; c < NC; c++) {
+        return true;
+    };
+    auto download = [&](uint32_t c) -> bool {
+        slice(c, off, bytes);
+        HIP_OK(hipStreamWaitEvent(io_stream_[1], done_ev[c], 0));
+        HIP_OK(hipMemcpyAsync(state_out + off, dout + off, bytes, hipMemcpyDeviceToHost, io_stream_[1]));
+        io_d2h_ += (double)bytes;
+        return true;
+    };
+    auto launch = [&](uint32_t c) -> bool {
         if (state_in) HIP_OK(hipStreamWaitEvent(stream_, in_ev[c], 0));
         HIP_OK(hipGraphLaunch(gs[c], stream_));
         HIP_OK(hipEventRecord(done_ev[c], stream_));
-        if (state_in && c + 1 < NC) {
-            slice(c + 1, off, bytes);
-            HIP_OK(hipMemcpyAsync(din + off, state_in + off, bytes, hipMemcpyHostToDevice, io_stream_[0]));
-            HIP_OK(hipEventRecord(in_ev[c + 1], io_stream_[0]));
-            io_h2d_ += (double)bytes;
+        return true;
+    };
+    // Page-locked caller buffers: every copy call returns at once, so all uploads are queued first
+    // (they only read din, which no chunk graph writes), then the graphs, then the downloads.  A
+    // rocprofv3 memory-copy trace of the interleaved order showed each upload starting only when
+    // the previous chunk's kernels ended: the download call issued between them held the host
+    // until its chunk had finished.  Pageable buffers: a copy call returns once the runtime has
+    // staged the bytes, so the interleaved order keeps the GPU fed; downloads lag two chunks.
+    if (pinned_io(state_in, state_out)) {
+        for (uint32_t c = 0; state_in && c < NC; c++)
+            if (!upload(c)) return false;
+        for (uint32_t c = 0; c < NC; c++)
+            if (!launch(c)) return false;
+        for (uint32_t c = 0; state_out && c < NC; c++)
+            if (!download(c)) return false;
+    } else {
+        if (state_in && !upload(0)) return false;
+        for (uint32_t c = 0; c < NC; c++) {
+            if (!launch(c)) return false;
+            if (state_in && c + 1 < NC && !upload(c + 1)) return false;
+            if (state_out && c >= 2 && !download(c - 2)) return false;
         }
-        if (state_out && c >= 1) {
-            slice(c - 1, off, bytes);
-            HIP_OK(hipStreamWaitEvent(io_stream_[1], done_ev[c - 1], 0));
-            HIP_OK(hipMemcpyAsync(state_out + off, dout + off, bytes, hipMemcpyDeviceToHost, io_stream_[1]));
-            io_d2h_ += (double)bytes;
-        }
-    }
-    if (state_out) {
-        slice(NC - 1, off, bytes);
-        HIP_OK(hipStreamWaitEvent(io_stream_[1], done_ev[NC - 1], 0));
-        HIP_OK(hipMemcpyAsync(state_out + off, dout + off, bytes, hipMemcpyDeviceToHost, io_stream_[1]));
-        io_d2h_ += (double)bytes;
+        for (uint32_t c = NC >= 2 ? NC - 2 : 0; state_out && c < NC; c++)
+            if (!download(c)) return false;
     }
     if (logits_out)
         HIP_OK(hipMemcpyAsync(logits_out, logits_, (size_t)m_->n_vocab * 4, hipMemcpyDeviceToHost, stream_));

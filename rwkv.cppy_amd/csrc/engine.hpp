@@ -209,6 +209,7 @@ class Engine : public KLaunchTimer {
     hipEvent_t io_entry_ev_ = nullptr;  // work already queued on stream_ at entry (copy streams wait)
     std::vector<hipGraphExec_t> io_graphs_[2][2];  // [cur][logits] per chunk
     bool eval_host_chunked(uint32_t token, const float * state_in, float * state_out, float * logits_out);
+    bool pinned_io(const float * state_in, const float * state_out);
     void drop_io_graphs();
     void drop_graphs();
     std::vector<Pending> pending_;

@@ -377,6 +377,9 @@ Engine::~Engine() {
     collect_timing();
     for (hipEvent_t e : event_pool_) (void)hipEventDestroy(e);
     if (tok_event_) (void)hipEventDestroy(tok_event_);
+    for (hipEvent_t e : fork_ev_)
+        if (e) (void)hipEventDestroy(e);
+    if (side_) (void)hipStreamDestroy(side_);
     if (stream_) (void)hipStreamDestroy(stream_);
 }
 
@@ -431,6 +434,12 @@ bool Engine::init() {
     io_chunk_ = ic ? std::max(1, atoi(ic)) : 4;
     const char * sm = getenv("RWKV_MI355X_SPLIT_MAA");  // v6 decode: W1 and mix as two launches (comparison)
     split_maa_ = sm && sm[0] == '1';
+    const char * vf = getenv("RWKV_MI355X_V7_FORK");
+    v7_fork_ = vf && vf[0] == '1' && m_->major == 7;
+    if (v7_fork_) {
+        HIP_OK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
+        for (auto & e : fork_ev_) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
     // the fused decode prologues hold LayerNorm inputs in registers up to n_embed 4096
     if (m_->n_embed > 4096 || m_->n_embed % 64) generic_decode_ = true;
     return ensure_workspace(1) && init_state(dstate_[0]);
@@ -1185,7 +1194,7 @@ bool Engine::forward_range(int T, const float * sin, float * sout, uint32_t l0, 
     return true;
 }
 
-bool Engine::mv(MVGroup & g) {
+bool Engine::mv(MVGroup & g, hipStream_t st) {
     if (timing_) {
         // the group's single launch is timed by its own dispatch events (RK_LAUNCH, g_klt)
         double bytes = 0, flops = 0;
@@ -1199,7 +1208,7 @@ bool Engine::mv(MVGroup & g) {
         kt_bytes_ = bytes;
         kt_flops_ = flops;
     }
-    return launch_mv_group(stream_, g);
+    return launch_mv_group(st ? st : stream_, g);
 }
 
 // KLaunchTimer (common.hpp): while a decode step is timed, every RK_LAUNCH takes an event pair
@@ -1455,15 +1464,21 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits, uint32
             src_lnmix(bl.add(L.a1, dsmall_[1], EPI_STORE), x_, si + C, L.ln1_w, L.ln1_b, mu + 4 * (size_t)C, 1);
             src_lnmix(bl.add(L.g1, dsmall_[2], EPI_SIGMOID), x_, si + C, L.ln1_w, L.ln1_b, mu + 5 * (size_t)C, 1);
             if (l != 0) src_lnmix(bl.add(L.v1, dsmall_[3], EPI_STORE), x_, si + C, L.ln1_w, L.ln1_b, mu + 3 * (size_t)C, 1);
+            // RWKV_MI355X_V7_FORK=1: the LoRA first stages (their own launch when their weight type
+            // differs) on a second stream forked from the first -- both only read x, so the two
+            // launches may run side by side (a graph branch when captured); joined before the
+            // attention launch.  Eager timing keeps them serial.
+            const bool fork = v7_fork_ && lb.g.n && !timing_;
+            if (fork) {
+                HIP_OK(hipEventRecord(fork_ev_[0], stream_));
+                HIP_OK(hipStreamWaitEvent(side_, fork_ev_[0], 0));
+                if (!mv(lb.g, side_)) return false;
+                HIP_OK(hipEventRecord(fork_ev_[1], side_));
+            }
             if (!mv(b.g)) return false;
-            if (lb.g.n && !mv(lb.g)) return false;
+            if (!fork && lb.g.n && !mv(lb.g)) return false;
+            if (fork) HIP_OK(hipStreamWaitEvent(stream_, fork_ev_[1], 0));
             if (l == 0) HIP_OK(hipMemcpyAsync(vfirst_, v_, (size_t)C * 4, hipMemcpyDeviceToDevice, stream_));
-            MV c;
-            src_f32(c.add(L.w2, w_, EPI_DECAY7, nullptr, L.w0), dsmall_[0]);
-            src_f32(c.add(L.a2, a_, EPI_SIGMOID_BIAS, nullptr, L.a0), dsmall_[1]);
-            src_f32(c.add(L.g2, g_, EPI_STORE), dsmall_[2]);
-            if (l != 0) src_f32(c.add(L.v2, v_, EPI_VMIX7, vfirst_, L.v0), dsmall_[3]);
-            if (!mv(c.g)) return false;
             Att7Dec a;
             memset(&a, 0, sizeof(a));
             a.H = H;
@@ -1482,7 +1497,38 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits, uint32
             a.lnx_w = L.att_lnx_w;
             a.lnx_b = L.att_lnx_b;
             if (!att_out(a, c_wo, L.att_o)) return false;
-            if (!launch_att7_dec(stream_, a)) return false;
+            // LoRA second stages + attention in one launch (mv_att7f.hip), else the LoRA-out matvec
+            // group + k_att7_dec (the same bits)
+            Att7Lora f;
+            memset(&f, 0, sizeof(f));
+            f.att = a;
+            f.W2[0] = L.w2;
+            f.W2[1] = L.a2;
+            f.W2[2] = L.g2;
+            f.W2[3] = L.v2;
+            for (int i = 0; i < 4; i++) f.lin[i] = dsmall_[i];
+            f.bias[0] = L.w0;
+            f.bias[1] = L.a0;
+            f.bias[2] = nullptr;
+            f.bias[3] = L.v0;
+            f.vfirst = vfirst_;
+            f.has_v = l != 0;
+            if (att7_lora_supported(f)) {
+                if (timing_) {
+                    double lb = wbytes(L.w2) + wbytes(L.a2) + wbytes(L.g2) + (l ? wbytes(L.v2) : 0.0);
+                    kt_bytes_ = lb + 2.0 * H * S * S * 4 + 12.0 * C * 4 + act_bytes(a.yq, 1);
+                    kt_flops_ = 2.0 * (L.w2.K + L.a2.K + L.g2.K + (l ? L.v2.K : 0)) * C;
+                }
+                if (!launch_att7_lora(stream_, f)) return false;
+            } else {
+                MV c;
+                src_f32(c.add(L.w2, w_, EPI_DECAY7, nullptr, L.w0), dsmall_[0]);
+                src_f32(c.add(L.a2, a_, EPI_SIGMOID_BIAS, nullptr, L.a0), dsmall_[1]);
+                src_f32(c.add(L.g2, g_, EPI_STORE), dsmall_[2]);
+                if (l != 0) src_f32(c.add(L.v2, v_, EPI_VMIX7, vfirst_, L.v0), dsmall_[3]);
+                if (!mv(c.g)) return false;
+                if (!launch_att7_dec(stream_, a)) return false;
+            }
             if (!mv(c_wo.g)) return false;
         }
         // ---------------- channel mixing ----------------

@@ -126,7 +126,7 @@ class Engine : public KLaunchTimer {
     bool forward(int T, const float * sin, float * sout, bool logits);
     bool forward_range(int T, const float * sin, float * sout, uint32_t l0, uint32_t l1, bool logits);
     bool forward_decode(const float * sin, float * sout, bool logits, uint32_t l0 = 0, uint32_t l1 = UINT32_MAX);
-    bool mv(MVGroup & g);
+    bool mv(MVGroup & g, hipStream_t st = nullptr);
     bool run_tokens(const uint32_t * tokens, size_t T, bool want_logits);
     bool run_tokens_impl(const uint32_t * tokens, size_t T, bool want_logits);
     bool layer_v4(int l, int T, const float * si, float * so);
@@ -163,6 +163,9 @@ class Engine : public KLaunchTimer {
     bool split_maa_ = false;       // RWKV_MI355X_SPLIT_MAA=1: v6 decode W1 + mix as two launches
     bool generic_decode_ = false;  // RWKV_MI355X_GENERIC_DECODE=1: decode through the T>1 kernels
     hipEvent_t tok_event_ = nullptr;
+    bool v7_fork_ = false;             // RWKV_MI355X_V7_FORK=1 (v7 decode LoRA-in on side_)
+    hipStream_t side_ = nullptr;
+    hipEvent_t fork_ev_[2] = {nullptr, nullptr};
     bool timing_ = false;
     struct Pending {
         int stat;

@@ -253,4 +253,17 @@ struct Att7Dec {
 };
 bool launch_att7_dec(hipStream_t st, const Att7Dec & a);
 
+// v7 decode: the LoRA second stages (w, a, g, v: F16 / F32, K <= 512) and the per-head attention
+// core in one launch (mv_att7f.hip); bit-identical to the LoRA-out matvec + k_att7_dec pair.
+struct Att7Lora {
+    Att7Dec att;            // r, k, v (pre-mix), k_k, k_a, r_k, state, ln_x, yq (w, a, g unused)
+    DMat W2[4];             // time_w2, time_a2, time_g2, time_v2 (M = C, K = the LoRA widths)
+    const float * lin[4];   // their inputs: the LoRA first-stage outputs (fp32 [K])
+    const float * bias[4];  // w0, a0, none, v0
+    const float * vfirst;   // layer 0's v (the v mix's aux)
+    int has_v;              // layers > 0 mix v with v_first
+};
+bool att7_lora_supported(const Att7Lora & a);
+bool launch_att7_lora(hipStream_t st, const Att7Lora & a);
+
 }  // namespace rwkvmi

@@ -419,6 +419,10 @@ bool Engine::init() {
         HIP_OK(hipMalloc(&hgran_, hgran_n_ * 8));
         ws_allocs_.push_back(hgran_);
         HIP_OK(hipMemset(hgran_, 0, hgran_n_ * 8));
+        // the head outputs handed to the fused Wo rows: tagged per (layer, state parity), never cleared
+        HIP_OK(hipMalloc(&ygran_, (size_t)m_->n_embed * 8));
+        ws_allocs_.push_back(ygran_);
+        HIP_OK(hipMemset(ygran_, 0, (size_t)m_->n_embed * 8));
     }
     const char * g = getenv("RWKV_MI355X_NO_GRAPH");
     use_graphs_ = !(g && g[0] == '1');
@@ -462,7 +466,7 @@ bool Engine::ensure_workspace(int T) {
     // keep state and logits, drop the rest; until every allocation below has succeeded the
     // workspace counts as absent (tcap_ = 0, pointers null), so a failed grow can never leave a
     // capacity that points at freed or missing buffers
-    std::vector<void *> keep = {dstate_[0], dstate_[1], logits_, hgran_};
+    std::vector<void *> keep = {dstate_[0], dstate_[1], logits_, hgran_, ygran_};
     for (void * p : ws_allocs_) {
         bool k = false;
         for (void * q : keep) k |= (p == q);
@@ -1428,6 +1432,21 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits, uint32
             f.err = herr_d_;
             f.spin_max = spin_max_;
             f.skip_wg = dbg_skip_gran_;
+            // Wo inside the same launch (the head outputs handed to the non-reducer workgroups as
+            // granules tagged by layer and state parity); else Wo is its own k_mva launch below
+            bool wo_in = false;
+            if (v6_wo_fused_enabled()) {
+                f.wo = L.att_o;
+                f.xres = x_;
+                f.ygran = ygran_;
+                f.ytag = (unsigned)(l + 1) | ((unsigned)(cur_ + 1) << 16);
+                wo_in = v6_att_fused_supported(f);
+                if (!wo_in) {
+                    memset(&f.wo, 0, sizeof(f.wo));
+                    f.xres = nullptr;
+                    f.ygran = nullptr;
+                }
+            }
             if (v6_att_fused_supported(f)) {
                 if (timing_) {
                     // r, k, v, g, Wd1, Wd2 weights, their 5 Q8 inputs, the head state in and out,
@@ -1435,6 +1454,11 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits, uint32
                     kt_bytes_ = 4 * wbytes(L.att_r) + wbytes(L.decay_w1) + wbytes(L.decay_w2) + 5 * act_bytes(outs[0], 1) +
                                 2.0 * H * S * S * 4 + 4.0 * C * 4 + 2.0 * (4.0 * C + f.D) * 4 + act_bytes(a.yq, 1);
                     kt_flops_ = 2.0 * (4.0 * C + f.D) * C + 2.0 * C * f.D;
+                    if (wo_in) {
+                        // Wo weights, the y granules written and gathered, x read and written
+                        kt_bytes_ += wbytes(L.att_o) + 2.0 * C * 8 + 2.0 * C * 4 - act_bytes(a.yq, 1);
+                        kt_flops_ += 2.0 * C * C;
+                    }
                 }
                 if (!launch_v6_att_fused(stream_, f)) return false;
             } else {
@@ -1447,7 +1471,7 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits, uint32
                 if (!mv(c.g)) return false;
                 if (!launch_att6_dec(stream_, a)) return false;
             }
-            if (!mv(c_wo.g)) return false;
+            if (!wo_in && !mv(c_wo.g)) return false;
         } else {
             // v7, order r, w, k, v, a, g of x_rwkvag (rwkv_graph.inc:404-413)
             MV b;
@@ -1609,6 +1633,9 @@ bool Engine::run_tokens(const uint32_t * tokens, size_t T, bool want_logits) {
     const int cur0 = cur_;
     if (!run_tokens_impl(tokens, T, want_logits)) {
         (void)hipStreamSynchronize(stream_);
+        // the call's tagged Wo-input granules must not satisfy a replay of the same parity
+        (void)hipMemsetAsync(ygran_, 0, (size_t)m_->n_embed * 8, stream_);
+        (void)hipStreamSynchronize(stream_);
         cur_ = cur0;
         return false;
     }
@@ -1717,6 +1744,7 @@ bool Engine::handoff_check() {
     if (*(volatile unsigned *)herr_h_ == 0) return true;
     (void)hipStreamSynchronize(stream_);
     (void)hipMemsetAsync(hgran_, 0, hgran_n_ * 8, stream_);
+    (void)hipMemsetAsync(ygran_, 0, (size_t)m_->n_embed * 8, stream_);
     (void)hipStreamSynchronize(stream_);
     *(volatile unsigned *)herr_h_ = 0;
     fprintf(stderr, "rwkv: in-launch hand-off timed out (k_v6_att_fused): the evaluation's results are invalid\n");

@@ -155,6 +155,7 @@ class Engine : public KLaunchTimer {
     unsigned * herr_h_ = nullptr;  // hand-off timeout flag, host-mapped (herr_d_ = its device address)
     unsigned * herr_d_ = nullptr;
     unsigned long long * hgran_ = nullptr;  // in-launch hand-off granules (k_v6_att_fused)
+    unsigned long long * ygran_ = nullptr;  // head outputs -> fused Wo rows (tagged granules, [C])
     size_t hgran_n_ = 0;
     int dbg_skip_gran_ = -1;
     unsigned spin_max_ = 1u << 20;

@@ -218,8 +218,17 @@ struct Att6Fused {
                      // after every synchronising call (Engine::handoff_check)
     unsigned spin_max;  // sweep bound (passes) before a timeout
     int skip_wg;     // test hook: this producer workgroup publishes nothing (-1: none)
+    // Wo fused (wo.qs != null): the reducers publish the head outputs y as granules tagged ytag
+    // (unique per layer and state parity, so they need no clearing) instead of emitting Wo's Q8
+    // input; the non-reducer workgroups then gather y, quantize it (the matvec prologue's
+    // arithmetic) and run Wo's rows with x += Wo . y (EPI_ADD) -- the Wo launch disappears
+    DMat wo;
+    float * xres;                 // the residual stream x [C]
+    unsigned long long * ygran;   // C granules
+    unsigned ytag;
 };
 bool v6_att_fused_supported(const Att6Fused & a);
+bool v6_wo_fused_enabled();  // RWKV_MI355X_WO_FUSED (default on)
 bool launch_v6_att_fused(hipStream_t st, const Att6Fused & a);
 // v4 decode: LN + token shift, r / k / v rows and WKV-4 in one launch, 32 channels per workgroup
 // (mv_att4f.hip); the two-launch k_mv + k_wkv4 pair gives the same bits

@@ -25,6 +25,8 @@
 
 #include <stdlib.h>
 
+#include <algorithm>
+
 namespace rwkvmi {
 
 typedef __attribute__((address_space(1))) float gfloat_t;
@@ -98,6 +100,10 @@ __device__ __forceinline__ void gran_put(unsigned long long * g, float v) {
     __hip_atomic_store((gu64_t *)g, (1ull << 32) | (unsigned long long)__float_as_uint(v), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ __forceinline__ void gran_put_tag(unsigned long long * g, float v, unsigned tag) {
+    __hip_atomic_store((gu64_t *)g, ((unsigned long long)tag << 32) | (unsigned long long)__float_as_uint(v),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 __device__ __forceinline__ unsigned long long gran_get(const unsigned long long * g) {
     return __hip_atomic_load((gu64_t *)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -129,7 +135,9 @@ __device__ __forceinline__ void gran_sweep(const unsigned long long * g, int str
     }
 }
 
-template <int WF, int U, int WD>
+constexpr int AF_WOR = 3;  // Wo rows per non-reducer wave: ceil(C / (28 H)) with C = 64 H
+
+template <int WF, int U, int WD, bool WO>
 __global__ __launch_bounds__(320) void k_v6_att_fused(Att6Fused a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];  // Q8 image of dl (decay tail input)
     __shared__ __attribute__((aligned(16))) float sr[64], sk[64], sv[64], sg[64], sw[64], su[64];
@@ -194,6 +202,91 @@ __global__ __launch_bounds__(320) void k_v6_att_fused(Att6Fused a) {
         }
     }
     if (!red) {
+        if constexpr (WO) {
+            // ---- Wo (rwkv_graph.inc:382-384, x += Wo . y) on the 7 H non-reducer workgroups: wave
+            // gw owns rows gw, gw + 28 H, gw + 56 H (k_mva's per-row arithmetic does not depend on
+            // which wave computes a row).  Its units are loaded now, under the reducers' attention.
+            const int nwo = 28 * H, gw = ((sidx - 1) * H + h) * 4 + wave;
+            WBlk wo[AF_WOR][U];
+            float xr = 0.0f;
+            if (wave < 4) {
+#pragma unroll
+                for (int u = 0; u < U; u++)
+#pragma unroll
+                    for (int j = 0; j < AF_WOR; j++) wo[j][u] = load_unit<WF>(a.wo, min(gw + nwo * j, C - 1), u, lane);
+                xr = a.xres[min(gw + nwo * min(lane, AF_WOR - 1), C - 1)];
+            }
+            // Wait for every head: wave 0 polls ONE granule per head (its last channel, lane h)
+            // with a sleep between polls -- the other waves park at the barrier, so the 7 H waiting
+            // workgroups add little L2 traffic beside the reducers' own sweeps
+            if (wave == 0) {
+                for (unsigned it = 0;; it++) {
+                    const unsigned long long x = lane < H ? gran_get(a.ygran + (size_t)lane * S + S - 1)
+                                                          : ((unsigned long long)a.ytag << 32);
+                    if (__all((unsigned)(x >> 32) == a.ytag)) break;
+                    if (it >= spin_max) {
+                        __hip_atomic_store((gunsigned_t *)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(4);
+                }
+            }
+            __syncthreads();
+            // y: 512-element chunks, 8 consecutive channels per lane (a quad = one 32-block), each
+            // granule's tag checked; then the matvec prologue's Q8 quantization into LDS
+            const ActBuf xq = lds_act(smem, act_fmt_for(WF), C);
+            MVEntry dummy{};
+            for (int ck = wave; ck * 512 < C; ck += 5) {
+                const int k0 = ck * 512 + lane * 8;
+                const bool valid = k0 < C;
+                const unsigned long long * g = a.ygran + min(k0, C - 8);
+                ChunkIn ci;
+                for (unsigned it = 0;; it++) {
+                    unsigned long long x[8];
+#pragma unroll
+                    for (int j = 0; j < 8; j++) x[j] = gran_get(g + j);
+                    bool ok = true;
+#pragma unroll
+                    for (int j = 0; j < 8; j++) {
+                        ci.x[j] = __uint_as_float((unsigned)x[j]);
+                        ok = ok && (unsigned)(x[j] >> 32) == a.ytag;
+                    }
+                    if (__all(ok || !valid)) break;
+                    if (it >= spin_max) {
+                        __hip_atomic_store((gunsigned_t *)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                chunk_store<WF, MVK_F32, 0>(dummy, xq, ci, 0.0f, 1.0f, false, k0, valid, lane);
+            }
+            __syncthreads();
+            if (wave < 4) {
+                float acc[AF_WOR], acc2[AF_WOR];
+#pragma unroll
+                for (int j = 0; j < AF_WOR; j++) acc[j] = acc2[j] = 0.0f;
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    const AUnit xu = load_act_unit<WF, true>(xq, u, lane);
+                    const bool uv = unit_valid<WF>(C, u, lane);
+#pragma unroll
+                    for (int j = 0; j < AF_WOR; j++) {
+                        float t = acc[j], t2 = acc2[j];
+                        dot_unit<WF>(wo[j][u], xu, t, t2);
+                        acc[j] = uv ? t : acc[j];
+                        acc2[j] = uv ? t2 : acc2[j];
+                    }
+                }
+                constexpr bool one = WF == W_Q4_1 || WF == W_Q5_1;
+                float sr_[AF_WOR];
+#pragma unroll
+                for (int j = 0; j < AF_WOR; j++)
+                    sr_[j] = one ? wave_sum63(acc[j]) + wave_sum63(acc2[j]) : wave_sum63(acc[j]) + 0.0f;
+                const float s = lane_row_sum<AF_WOR>(sr_, lane);
+                const int row = gw + nwo * lane;
+                if (lane < AF_WOR && row < C) a.xres[row] = xr + s;  // EPI_ADD
+            }
+        }
         STAMP_END_NS(6);
         return;
     }
@@ -274,7 +367,8 @@ __global__ __launch_bounds__(320) void k_v6_att_fused(Att6Fused a) {
         o = o * lnw_c;
         o = o + lnb_c;
         o = o * sg[lane];
-        emit32(yq, 0, c0 + lane, o);
+        if constexpr (WO) gran_put_tag(a.ygran + c0 + lane, o, a.ytag);
+        else emit32(yq, 0, c0 + lane, o);
     }
     STAMP_END(6);
 }
@@ -295,18 +389,31 @@ bool v6_att_fused_supported(const Att6Fused & a) {
     if (!wtype_quantized(a.att.wd2.type) || a.att.wd2.M != a.C || a.att.wd2.K != a.D) return false;
     // the decay tail's PF = 4 units per row and one emission half-wave per 32 decay rows
     if (a.D % 32 || a.D > 128) return false;  // two granules per lane of the sweeping wave
+    if (a.wo.qs) {
+        // Wo fused: C x C of the same type, rows spread over the 28 H non-reducer waves
+        if (a.wo.type != t || a.wo.M != a.C || a.wo.K != a.C || !a.xres || !a.ygran || a.C % 512) return false;
+        if ((a.C + 28 * a.H - 1) / (28 * a.H) > AF_WOR) return false;
+    }
     return a.H <= 64 && a.err;  // one decay-value copy per head: a lane per head
 }
 
-template <int WF, int U>
+bool v6_wo_fused_enabled() {
+    static const bool on = [] {
+        const char * v = getenv("RWKV_MI355X_WO_FUSED");  // 1: Wo inside the attention launch (A/B)
+        return v && v[0] == '1';
+    }();
+    return on;
+}
+
+template <int WF, int U, bool WO>
 static void launch_af_wd(hipStream_t st, const Att6Fused & a, int lds) {
     const dim3 grid(AF_P * a.H), block(320);
     switch (a.att.wd2.type) {
-        case W_Q4_0: RK_LAUNCH((k_v6_att_fused<WF, U, W_Q4_0>), grid, block, lds, st, a); break;
-        case W_Q4_1: RK_LAUNCH((k_v6_att_fused<WF, U, W_Q4_1>), grid, block, lds, st, a); break;
-        case W_Q5_0: RK_LAUNCH((k_v6_att_fused<WF, U, W_Q5_0>), grid, block, lds, st, a); break;
-        case W_Q5_1: RK_LAUNCH((k_v6_att_fused<WF, U, W_Q5_1>), grid, block, lds, st, a); break;
-        default: RK_LAUNCH((k_v6_att_fused<WF, U, W_Q8_0>), grid, block, lds, st, a); break;
+        case W_Q4_0: RK_LAUNCH((k_v6_att_fused<WF, U, W_Q4_0, WO>), grid, block, lds, st, a); break;
+        case W_Q4_1: RK_LAUNCH((k_v6_att_fused<WF, U, W_Q4_1, WO>), grid, block, lds, st, a); break;
+        case W_Q5_0: RK_LAUNCH((k_v6_att_fused<WF, U, W_Q5_0, WO>), grid, block, lds, st, a); break;
+        case W_Q5_1: RK_LAUNCH((k_v6_att_fused<WF, U, W_Q5_1, WO>), grid, block, lds, st, a); break;
+        default: RK_LAUNCH((k_v6_att_fused<WF, U, W_Q8_0, WO>), grid, block, lds, st, a); break;
     }
 }
 
@@ -315,12 +422,16 @@ bool launch_v6_att_fused(hipStream_t st, const Att6Fused & a) {
         fprintf(stderr, "rwkv: fused v6 attention decode: unsupported shape\n");
         return false;
     }
-    const int lds = lds_bytes_for(act_fmt_for(a.att.wd2.type), a.D);
+    const bool wo = a.wo.qs != nullptr;
+    int lds = lds_bytes_for(act_fmt_for(a.att.wd2.type), a.D);
+    if (wo) lds = std::max(lds, lds_bytes_for(act_fmt_for(a.W[0].type), a.C));
     const bool u1 = mv_units(a.W[0].type, a.C) <= 1;
 #define AF_T(WFv)                                                  \
     do {                                                           \
-        if (u1) launch_af_wd<WFv, 1>(st, a, lds);                  \
-        else launch_af_wd<WFv, 2>(st, a, lds);                     \
+        if (wo && u1) launch_af_wd<WFv, 1, true>(st, a, lds);      \
+        else if (wo) launch_af_wd<WFv, 2, true>(st, a, lds);       \
+        else if (u1) launch_af_wd<WFv, 1, false>(st, a, lds);      \
+        else launch_af_wd<WFv, 2, false>(st, a, lds);              \
     } while (0)
     switch (a.W[0].type) {
         case W_Q4_0: AF_T(W_Q4_0); break;

@@ -1319,9 +1319,25 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits, uint32
                     kt_bytes_ = 3 * wbytes(L.att_r) + 9.0 * C * 4 + 6.0 * C * 4 + C * 4.0 + act_bytes(o, 1);
                     kt_flops_ = 6.0 * C * C;
                 }
+                V4WoFused wf;
+                const bool wo_in = v4_wo_fused_enabled() && L.att_o.type == L.att_r.type;
+                if (wo_in) {
+                    wf.wo = L.att_o;
+                    wf.xres = x_;
+                    wf.ygran = ygran_;
+                    wf.ytag = (unsigned)(l + 1) | ((unsigned)(cur_ + 1) << 16);
+                    wf.err = herr_d_;
+                    wf.spin_max = spin_max_;
+                    if (timing_) {
+                        kt_bytes_ += wbytes(L.att_o) + 2.0 * C * 8 + 2.0 * C * 4;
+                        kt_flops_ += 2.0 * C * C;
+                    }
+                }
                 if (!launch_v4_att_fused(stream_, C, L.att_r, L.att_k, L.att_v, x_, si + C, so + C, L.ln1_w, L.ln1_b,
-                                         L.att_mix_r, L.att_mix_k, L.att_mix_v, L.att_first, L.att_decay, si, so, o, y_))
+                                         L.att_mix_r, L.att_mix_k, L.att_mix_v, L.att_first, L.att_decay, si, so, o, y_,
+                                         wo_in ? &wf : nullptr))
                     return false;
+                if (wo_in) goto v4_att_done;
                 if (v4_att_fused_cpw() != 32) {
                     // y fp32: Wo quantizes it in its own prologue (the same Q8 bits as the emission)
                     MV c;

@@ -235,10 +235,23 @@ bool launch_v6_att_fused(hipStream_t st, const Att6Fused & a);
 // (channels per workgroup v4_att_fused_cpw(): 32 emits Wo's Q8 input, 8 / 16 write it as fp32 y)
 int v4_att_fused_cpw();
 bool v4_att_fused_supported(int C, const DMat & Wr, const DMat & Wk, const DMat & Wv, const ActBuf & out);
+// wf (RWKV_MI355X_WO4_FUSED=1, 8 channels per workgroup): Wo in the same launch -- every workgroup
+// publishes its channels' outputs as granules tagged ytag (per layer and state parity), gathers all
+// C of them, quantizes them as Wo's fp32-input prologue does and runs one Wo row per wave, x += Wo . y
+struct V4WoFused {
+    DMat wo;
+    float * xres;
+    unsigned long long * ygran;
+    unsigned ytag;
+    unsigned * err;
+    unsigned spin_max;
+};
+bool v4_wo_fused_enabled();
 bool launch_v4_att_fused(hipStream_t st, int C, const DMat & Wr, const DMat & Wk, const DMat & Wv, const float * x,
                          const float * carry, float * carry_out, const float * lnw, const float * lnb,
                          const float * mix_r, const float * mix_k, const float * mix_v, const float * first,
-                         const float * decay, const float * sin, float * sout, const ActBuf & out, float * y);
+                         const float * decay, const float * sin, float * sout, const ActBuf & out, float * y,
+                         const V4WoFused * wf = nullptr);
 
 // Sequence v6 decay LoRA tail (T >= 2): w[t][c] = exp(-exp(Wd2[c] . Q8(dl[t]) + decay[c])) with
 // k_att6_dec's per-row arithmetic; dl fp32 [T][D].  Quantized Wd2 with D <= 512 only.

@@ -31,14 +31,25 @@ struct Att4Fused {
     ActBuf out;                 // Wo's input (CPW = 32: emitted as Q8 blocks)
     float * y;                  // Wo's input as fp32 (CPW < 32: Wo quantizes it in its prologue)
     int img;                    // LDS bytes per activation image (16-aligned)
+    // Wo fused (WO): every workgroup publishes its channels' outputs as tagged granules, then
+    // gathers all C, quantizes them (the Wo prologue's arithmetic) and runs one Wo row per wave
+    DMat wo;
+    float * xres;
+    unsigned long long * ygran;
+    unsigned ytag;
+    unsigned * err;
+    unsigned spin_max;
 };
+
+typedef __attribute__((address_space(1))) unsigned long long a4_gu64_t;
+typedef __attribute__((address_space(1))) unsigned a4_gu32_t;
 
 // 512 threads = 8 waves, CPW channels per workgroup.  Waves 4..7 build the three images (LayerNorm
 // statistics in the chunk association, one 512-element chunk per wave, token shift per mix,
 // quantization); every wave dots rows R w .. R w + R - 1 (R = CPW / 8) of each matrix within the
 // workgroup's channels; wave 0 (CPW lanes) runs the recurrence.  CPW = 32 emits Wo's input as one
 // Q8 block; smaller CPW (more workgroups streaming the rows) write it as fp32.
-template <int WF, int U, int CPW>
+template <int WF, int U, int CPW, bool WO = false>
 __global__ __launch_bounds__(512) void k_v4_att_fused(Att4Fused a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ float sr[CPW], sk[CPW], sv[CPW];
@@ -77,6 +88,15 @@ __global__ __launch_bounds__(512) void k_v4_att_fused(Att4Fused a) {
         for (int u = 0; u < U; u++)
 #pragma unroll
             for (int r = 0; r < R; r++) w[m][r][u] = load_unit<WF>(a.W[m], min(c0 + R * wave + r, C - 1), u, lane);
+    // WO: this wave's Wo row (row blockIdx.x * 8 + wave: one per wave at CPW = 8) and its x
+    WBlk wo[U];
+    float xr = 0.0f;
+    const int worow = (int)blockIdx.x * 8 + wave;
+    if constexpr (WO) {
+#pragma unroll
+        for (int u = 0; u < U; u++) wo[u] = load_unit<WF>(a.wo, min(worow, C - 1), u, lane);
+        xr = a.xres[min(worow, C - 1)];
+    }
     // the recurrence's operands (wave 0, lane = channel)
     float aa = 0.0f, bb = 0.0f, pp = 0.0f, fi = 0.0f, de = 0.0f;
     if (wave == 0 && lane < CPW) {
@@ -173,7 +193,10 @@ __global__ __launch_bounds__(512) void k_v4_att_fused(Att4Fused a) {
             bb = e1 * bb + e2;
             pp = qq;
             const float y = sr[lane] * (an / bn);
-            if constexpr (CPW == 32) emit32(ao, 0, c, y);  // lanes 0..31: one quantization block
+            if constexpr (WO)
+                __hip_atomic_store((a4_gu64_t *)(a.ygran + c), ((unsigned long long)a.ytag << 32) | __float_as_uint(y),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else if constexpr (CPW == 32) emit32(ao, 0, c, y);  // lanes 0..31: one quantization block
             else a.y[c] = y;
             if (c < C) {
                 a.sout[2 * C + c] = aa;
@@ -181,6 +204,69 @@ __global__ __launch_bounds__(512) void k_v4_att_fused(Att4Fused a) {
                 a.sout[4 * C + c] = pp;
             }
         }
+    }
+    if constexpr (WO) {
+        // Every workgroup's outputs: wave 0 polls the last granule of each workgroup (lanes over
+        // the C / 8 producers), the other waves park at the barrier.  Every producer published
+        // before waiting, and all C / 8 workgroups are resident at once, so the wait ends.
+        const int nwg = C / CPW;
+        if (wave == 0) {
+            for (unsigned it = 0;; it++) {
+                bool ok = true;
+                for (int j = lane; j < nwg; j += 64) {
+                    const unsigned long long x = __hip_atomic_load((a4_gu64_t *)(a.ygran + (size_t)j * CPW + CPW - 1),
+                                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    ok = ok && (unsigned)(x >> 32) == a.ytag;
+                }
+                if (__all(ok)) break;
+                if (it >= a.spin_max) {
+                    __hip_atomic_store((a4_gu32_t *)a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(4);
+            }
+        }
+        __syncthreads();
+        // gather y (8 channels per lane, tags checked) and quantize it as Wo's SRC_F32 prologue does
+        const ActBuf xq = lds_act(smem, act_fmt_for(WF), K);
+        for (int ck = wave; ck * LN_CHUNK < C; ck += 8) {
+            const int k0 = ck * LN_CHUNK + lane * 8;
+            const bool valid = k0 < C;
+            const unsigned long long * g = a.ygran + max(min(k0, C - 8), 0);
+            ChunkIn cy;
+            for (unsigned it = 0;; it++) {
+                bool ok = true;
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    const unsigned long long x = __hip_atomic_load((a4_gu64_t *)(g + j), __ATOMIC_RELAXED,
+                                                                   __HIP_MEMORY_SCOPE_AGENT);
+                    cy.x[j] = __uint_as_float((unsigned)x);
+                    ok = ok && (unsigned)(x >> 32) == a.ytag;
+                }
+                if (__all(ok || !valid)) break;
+                if (it >= a.spin_max) {
+                    __hip_atomic_store((a4_gu32_t *)a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            chunk_store<WF, MVK_F32, 0>(E, xq, cy, 0.0f, 1.0f, false, k0, valid, lane);
+        }
+        __syncthreads();
+        float acc = 0.0f, acc2 = 0.0f;
+        for (int u0 = 0; u0 < units; u0 += U) {
+            if (u0 > 0) {
+#pragma unroll
+                for (int u = 0; u < U; u++) wo[u] = load_unit<WF>(a.wo, min(worow, C - 1), u0 + u, lane);
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const AUnit xu = load_act_unit<WF, true>(xq, u0 + u, lane);
+                if (unit_valid<WF>(K, u0 + u, lane)) dot_unit<WF>(wo[u], xu, acc, acc2);
+            }
+        }
+        const float sw_ = one ? wave_sum63(acc) + wave_sum63(acc2) : wave_sum63(acc) + 0.0f;
+        if (lane == 63 && worow < C) a.xres[worow] = xr + sw_;  // EPI_ADD (the sum is valid in lane 63)
     }
     STAMP_END(8);
 }
@@ -214,15 +300,34 @@ static void launch_att4_c(hipStream_t st, const Att4Fused & a, int units) {
 template <int WF>
 static void launch_att4_t(hipStream_t st, const Att4Fused & a, int units) {
     const int cpw = v4_att_fused_cpw();
+    if (a.wo.qs) {
+        const int lds = 3 * a.img;
+        if (units <= 1) RK_LAUNCH((k_v4_att_fused<WF, 1, 8, true>), dim3(a.C / 8), dim3(512), lds, st, a);
+        else RK_LAUNCH((k_v4_att_fused<WF, 2, 8, true>), dim3(a.C / 8), dim3(512), lds, st, a);
+        return;
+    }
     if (cpw == 32) launch_att4_c<WF, 32>(st, a, units);
     else if (cpw == 16) launch_att4_c<WF, 16>(st, a, units);
     else launch_att4_c<WF, 8>(st, a, units);
 }
 
+bool v4_wo_fused_enabled() {
+    static const bool on = [] {
+        const char * v = getenv("RWKV_MI355X_WO4_FUSED");  // 1: Wo inside the v4 attention launch (A/B)
+        return v && v[0] == '1';
+    }();
+    return on && v4_att_fused_cpw() == 8;
+}
+
 bool launch_v4_att_fused(hipStream_t st, int C, const DMat & Wr, const DMat & Wk, const DMat & Wv, const float * x,
                          const float * carry, float * carry_out, const float * lnw, const float * lnb,
                          const float * mix_r, const float * mix_k, const float * mix_v, const float * first,
-                         const float * decay, const float * sin, float * sout, const ActBuf & out, float * y) {
+                         const float * decay, const float * sin, float * sout, const ActBuf & out, float * y,
+                         const V4WoFused * wf) {
+    if (wf && (!v4_wo_fused_enabled() || wf->wo.type != Wr.type || wf->wo.M != C || wf->wo.K != C || C % 8)) {
+        fprintf(stderr, "rwkv: fused v4 attention + Wo decode: unsupported shape (C %d)\n", C);
+        return false;
+    }
     if (!v4_att_fused_supported(C, Wr, Wk, Wv, out)) {
         fprintf(stderr, "rwkv: fused v4 attention decode: unsupported shape (C %d)\n", C);
         return false;
@@ -247,6 +352,14 @@ bool launch_v4_att_fused(hipStream_t st, int C, const DMat & Wr, const DMat & Wk
     a.sout = sout;
     a.out = out;
     a.y = y;
+    if (wf) {
+        a.wo = wf->wo;
+        a.xres = wf->xres;
+        a.ygran = wf->ygran;
+        a.ytag = wf->ytag;
+        a.err = wf->err;
+        a.spin_max = wf->spin_max;
+    }
     a.img = (lds_bytes_for(act_fmt_for(Wr.type), C) + 15) & ~15;
     const int units = mv_units(Wr.type, C);
     switch (Wr.type) {

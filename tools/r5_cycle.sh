@@ -49,6 +49,21 @@ for s in $STEPS; do
       python3 tools/pmc_stream.py $O/r5_${TAG}_pmc_FETCH_SIZE $O/r5_${TAG}_pmc_WRITE_SIZE > $O/r5_${TAG}_pmc.json
       cat $O/r5_${TAG}_pmc.json | head -40
       ;;
+    configs)
+      # the other BASELINE configurations' lines (decode, seq-eval, batched B = 8 / 64, ABI decode)
+      for c in v4-169m-q8_0 v7-2b9-q5_1 v5-7b-q4_1; do
+        timeout -k 10 400 python3 bench.py --config $c --steps 64 --warmup 8 --batch "8,64" --seq-reps 2 --abi-steps 8 \
+          --skip-cpu --pipe-stages 0 > $O/r5_${TAG}_$c.log 2>&1 || { tail -5 $O/r5_${TAG}_$c.log; exit 1; }
+        grep '^{' $O/r5_${TAG}_$c.log > $O/r5_${TAG}_$c.json
+        grep -E "decode:|seq-eval" $O/r5_${TAG}_$c.log | sed "s/^/[$c] /" | cut -c1-160
+      done
+      ;;
+    pipe8)
+      # BASELINE config 5's pipeline: v5-7B, 8 stages on this box's one GPU, 4096 tokens
+      timeout -k 10 400 python3 bench.py --config v5-7b-q4_1 --steps 8 --warmup 2 --batch "" --seq-len 4096 --seq-reps 1 \
+        --abi-steps 0 --skip-cpu --timing-steps 1 --pipe-stages 8 > $O/r5_${TAG}_pipe8.log 2>&1 || { tail -5 $O/r5_${TAG}_pipe8.log; exit 1; }
+      grep -E "pipeline|seq-eval" $O/r5_${TAG}_pipe8.log | cut -c1-200
+      ;;
   esac
 done
 echo "cycle $TAG done"

@@ -228,14 +228,14 @@ struct Att6Fused {
     unsigned ytag;
 };
 bool v6_att_fused_supported(const Att6Fused & a);
-bool v6_wo_fused_enabled();  // RWKV_MI355X_WO_FUSED (default on)
+bool v6_wo_fused_enabled();  // RWKV_MI355X_WO_FUSED=0 turns it off (default on)
 bool launch_v6_att_fused(hipStream_t st, const Att6Fused & a);
 // v4 decode: LN + token shift, r / k / v rows and WKV-4 in one launch, 32 channels per workgroup
 // (mv_att4f.hip); the two-launch k_mv + k_wkv4 pair gives the same bits
 // (channels per workgroup v4_att_fused_cpw(): 32 emits Wo's Q8 input, 8 / 16 write it as fp32 y)
 int v4_att_fused_cpw();
 bool v4_att_fused_supported(int C, const DMat & Wr, const DMat & Wk, const DMat & Wv, const ActBuf & out);
-// wf (RWKV_MI355X_WO4_FUSED=1, 8 channels per workgroup): Wo in the same launch -- every workgroup
+// wf (default; RWKV_MI355X_WO4_FUSED=0 off; 8 channels per workgroup): Wo in the same launch -- every workgroup
 // publishes its channels' outputs as granules tagged ytag (per layer and state parity), gathers all
 // C of them, quantizes them as Wo's fp32-input prologue does and runs one Wo row per wave, x += Wo . y
 struct V4WoFused {

@@ -313,8 +313,8 @@ static void launch_att4_t(hipStream_t st, const Att4Fused & a, int units) {
 
 bool v4_wo_fused_enabled() {
     static const bool on = [] {
-        const char * v = getenv("RWKV_MI355X_WO4_FUSED");  // 1: Wo inside the v4 attention launch (A/B)
-        return v && v[0] == '1';
+        const char * v = getenv("RWKV_MI355X_WO4_FUSED");  // 0: Wo as its own launch (A/B)
+        return !(v && v[0] == '0');
     }();
     return on && v4_att_fused_cpw() == 8;
 }

@@ -399,8 +399,8 @@ bool v6_att_fused_supported(const Att6Fused & a) {
 
 bool v6_wo_fused_enabled() {
     static const bool on = [] {
-        const char * v = getenv("RWKV_MI355X_WO_FUSED");  // 1: Wo inside the attention launch (A/B)
-        return v && v[0] == '1';
+        const char * v = getenv("RWKV_MI355X_WO_FUSED");  // 0: Wo as its own k_mva launch (A/B)
+        return !(v && v[0] == '0');
     }();
     return on;
 }

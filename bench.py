@@ -305,6 +305,36 @@ def main():
     seq_tps = args.seq_len / seq_s if ts else 0.0
     log(f'seq-eval T={args.seq_len}: {seq_s * 1e3:.1f} ms, {seq_tps:.0f} tok/s')
 
+    # ---------------- sequence eval with the chunk-parallel wkv6 (v5/v6; off by default) ----------------
+    # csrc/wkv_chunk.hip re-associates the recurrence (not bit-exact), so it is a separate, labelled
+    # number; the headline seq_eval above is the serial, bit-exact path
+    wkvc = None
+    if args.seq_reps > 0 and arch in (5, 6):
+        try:
+            slg0 = np.zeros(n_vocab, np.float32)
+            clg = np.zeros(n_vocab, np.float32)
+            assert L.rwkv_eval_sequence(ctx.ptr, sp, len(seq), None, None, slg0.ctypes.data_as(P_F))
+            assert L.rwkv_mi355x_debug_set(ctx.ptr, b'wkv_chunk', 1)
+            assert L.rwkv_eval_sequence(ctx.ptr, sp, len(seq), None, None, clg.ctypes.data_as(P_F))
+            cts = []
+            for _ in range(args.seq_reps):
+                assert L.rwkv_mi355x_state_upload(ctx.ptr, None)
+                L.rwkv_mi355x_sync(ctx.ptr)
+                t1 = time.perf_counter()
+                assert L.rwkv_mi355x_eval_device(ctx.ptr, sp, len(seq), True, None, True)
+                cts.append(time.perf_counter() - t1)
+            assert L.rwkv_mi355x_debug_set(ctx.ptr, b'wkv_chunk', 0)
+            wkvc = {'tokens_per_s': round(args.seq_len / min(cts) * world, 1), 'ms_per_sequence': round(min(cts) * 1e3, 3),
+                    'what': 'seq_eval with RWKV_MI355X_WKV_CHUNK=1 (chunk-parallel wkv6, 16-token chunks, '
+                            're-associated: not bit-exact, off by default)',
+                    'max_abs_dlogit_vs_serial': float(np.abs(clg - slg0).max()),
+                    'max_abs_logit': float(np.abs(slg0).max())}
+            log(f"seq-eval, chunk-parallel wkv6: {min(cts) * 1e3:.1f} ms, {args.seq_len / min(cts):.0f} tok/s, "
+                f"max|dlogit| vs serial {wkvc['max_abs_dlogit_vs_serial']:.3g}")
+        except Exception as e:
+            log(f'chunked wkv seq-eval failed: {e!r}')
+            errors.append(f'chunked wkv seq-eval: {e!r}')
+
     # ---------------- sequence eval through the in-library layer pipeline ----------------
     # rwkv_mi355x_init_pipeline: ONE process drives P stage contexts (stage s on GPU devices[s], layers
     # [s*L/P, (s+1)*L/P)); rwkv_eval_sequence on it cuts the tokens into chunks of >= 256 and forwards
@@ -564,7 +594,7 @@ def main():
                        'weights': fmt, 'parallelism': f'replicas x{world}'},
             'seq_eval': {'tokens_per_s': round(seq_tps * world, 1), 'T': args.seq_len,
                          'ms_per_sequence': round(seq_s * 1e3, 3), 'parallelism': f'replicas x{world}',
-                         'pipeline': pipe},
+                         'pipeline': pipe, 'wkv_chunked': wkvc},
             'abi_decode_tokens_per_s': round(abi_tps * world, 2),
             'abi_decode_pinned_tokens_per_s': round(abi_pinned_tps * world, 2),
             'batched_decode': {'what': 'B independent contexts, one token each per step, weights read once per '

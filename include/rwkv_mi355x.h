@@ -192,6 +192,14 @@ RWKV_API bool rwkv_mi355x_selftest_gemm(int wtype, const void * W, int K, int M,
 RWKV_API bool rwkv_mi355x_selftest_gemm_split(int wtype, const void * W, int K, int M, const float * x, int T,
                                               float * y, int split);
 
+/* WKV-6 (v5 / v6 time mixing, head size 64) over T tokens of one context on host operands:
+ * chunked = 0 runs the serial kernel (bit-exact with decode), 1 the chunk-parallel form
+ * (RWKV_MI355X_WKV_CHUNK; re-associated sums).  k, v, r: [T][H*64]; w: [T][H*64] (w_per_token = 1,
+ * v6) or [H*64] (v5); u: [H*64]; state_in / state_out: [H][64 key][64 value]; y: [T][H*64]. */
+RWKV_API bool rwkv_mi355x_selftest_wkv6(int T, int H, int chunked, int w_per_token, const float * k, const float * v,
+                                       const float * r, const float * u, const float * w, const float * state_in,
+                                       float * state_out, float * y);
+
 #if defined(__cplusplus)
 }
 #endif

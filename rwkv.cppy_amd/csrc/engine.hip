@@ -371,6 +371,7 @@ Engine::~Engine() {
     if (gy_) (void)hipFree(gy_);
     if (part_) (void)hipFree(part_);
     if (m2_) (void)hipFree(m2_);
+    if (wkvc_) (void)hipFree(wkvc_);
     for (void * p : ws_allocs_) (void)hipFree(p);
     if (htokens_) (void)hipHostFree(htokens_);
     if (herr_h_) (void)hipHostFree(herr_h_);
@@ -438,6 +439,8 @@ bool Engine::init() {
     io_chunk_ = ic ? std::max(1, atoi(ic)) : 4;
     const char * sm = getenv("RWKV_MI355X_SPLIT_MAA");  // v6 decode: W1 and mix as two launches (comparison)
     split_maa_ = sm && sm[0] == '1';
+    const char * wc = getenv("RWKV_MI355X_WKV_CHUNK");  // 1: chunk-parallel wkv6 (not bit-exact)
+    wkv_chunk_ = wc && wc[0] == '1';
     const char * vf = getenv("RWKV_MI355X_V7_FORK");
     v7_fork_ = vf && vf[0] == '1' && m_->major == 7;
     if (v7_fork_) {
@@ -901,6 +904,30 @@ bool Engine::layer_v4(int l, int T, const float * si, float * so) {
     return ffn(l, T, si, so);
 }
 
+// v5/v6 sequence wkv: the serial recurrence (k_wkv6_s64, bit-exact with decode), or behind the
+// wkv_chunk_ switch the chunk-parallel form (RA / KB in the v7-only nb_ / bb_ buffers, free during a
+// v5/v6 layer; the chunk matrices and states in wkvc_, grown on demand)
+bool Engine::wkv6(int T, int H, int S, const float * u, const float * w, int wpt, const float * sin, float * sout) {
+    if (wkv_chunk_ && wkv6_chunked_supported(T, S, (int)bs_)) {
+        const size_t need = wkv6_chunked_scratch_floats(T, H);
+        if (need > wkvc_cap_) {
+            HIP_OK(hipStreamSynchronize(stream_));
+            if (wkvc_) (void)hipFree(wkvc_);
+            wkvc_ = nullptr;
+            wkvc_cap_ = 0;
+            if (hipMalloc(&wkvc_, need * 4 + 64) != hipSuccess) {
+                wkvc_ = nullptr;
+                (void)hipGetLastError();
+                fprintf(stderr, "rwkv: chunked wkv scratch (%zu MB) allocation failed\n", need * 4 >> 20);
+                return false;
+            }
+            wkvc_cap_ = need;
+        }
+        return launch_wkv6_chunked(stream_, T, H, k_, v_, r_, u, w, wpt, sin, sout, y_, nb_, bb_, wkvc_);
+    }
+    return launch_wkv6(stream_, T, H, S, k_, v_, r_, u, w, wpt, sin, sout, y_, (int)bs_);
+}
+
 bool Engine::layer_v5(int l, int T, const float * si, float * so) {
     const DLayer & L = m_->layers[l];
     const int C = (int)m_->n_embed, H = (int)m_->H, S = (int)m_->S;
@@ -958,7 +985,7 @@ bool Engine::layer_v5(int l, int T, const float * si, float * so) {
         if (!b.run(*this, T)) return false;
         return ffn(l, T, si, so);
     }
-    if (!launch_wkv6(stream_, T, H, S, k_, v_, r_, L.att_u, L.att_w, 0, si + 2 * C, so + 2 * C, y_, (int)bs_)) return false;
+    if (!wkv6(T, H, S, L.att_u, L.att_w, 0, si + 2 * C, so + 2 * C)) return false;
     ActBuf o = A(4, L.att_o);
     if (!launch_groupnorm(stream_, T, H, S, 1e-5f, y_, L.att_lnx_w, L.att_lnx_b, v52 ? 1 : 0, g_, nullptr, nullptr, o))
         return false;
@@ -1050,7 +1077,7 @@ bool Engine::layer_v6(int l, int T, const float * si, float * so) {
         b.add(L.decay_w2, dl, w_, C, EPI_DECAY6, nullptr, L.decay6);
         if (!b.run(*this, T)) return false;
     }
-    if (!launch_wkv6(stream_, T, H, S, k_, v_, r_, L.att_u, w_, 1, si + 2 * C, so + 2 * C, y_, (int)bs_)) return false;
+    if (!wkv6(T, H, S, L.att_u, w_, 1, si + 2 * C, so + 2 * C)) return false;
     ActBuf o = A(7, L.att_o);
     if (!launch_groupnorm(stream_, T, H, S, 64e-5f, y_, L.att_lnx_w, L.att_lnx_b, 1, g_, nullptr, nullptr, o)) return false;
     b.add(L.att_o, o, x_, C, EPI_ADD);
@@ -1772,6 +1799,7 @@ bool Engine::debug_set(const char * name, long long value) {
     const std::string n(name);
     if (n == "skip_granule") dbg_skip_gran_ = (int)value;
     else if (n == "spin_max") spin_max_ = value > 0 ? (unsigned)std::min<long long>(value, 0xffffffffLL) : (1u << 20);
+    else if (n == "wkv_chunk") wkv_chunk_ = value != 0;
     else return false;
     // the decode graphs captured the old values
     (void)hipStreamSynchronize(stream_);

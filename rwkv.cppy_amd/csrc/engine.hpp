@@ -130,6 +130,7 @@ class Engine : public KLaunchTimer {
     bool run_tokens(const uint32_t * tokens, size_t T, bool want_logits);
     bool run_tokens_impl(const uint32_t * tokens, size_t T, bool want_logits);
     bool layer_v4(int l, int T, const float * si, float * so);
+    bool wkv6(int T, int H, int S, const float * u, const float * w, int wpt, const float * sin, float * sout);
     bool layer_v5(int l, int T, const float * si, float * so);
     bool layer_v6(int l, int T, const float * si, float * so);
     bool layer_v7(int l, int T, const float * si, float * so);
@@ -159,6 +160,11 @@ class Engine : public KLaunchTimer {
     size_t hgran_n_ = 0;
     int dbg_skip_gran_ = -1;
     unsigned spin_max_ = 1u << 20;
+    // chunk-parallel wkv6 for sequences (wkv_chunk.hip; re-associated, not bit-exact): 0 = serial
+    // k_wkv6_s64 (default); RWKV_MI355X_WKV_CHUNK=1 or rwkv_mi355x_debug_set(ctx, "wkv_chunk", 1)
+    bool wkv_chunk_ = false;
+    float * wkvc_ = nullptr;  // its chunk matrices / chunk states
+    size_t wkvc_cap_ = 0;
     hipGraphExec_t graphs_[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // [cur][logits]
     bool use_graphs_ = true;
     bool split_maa_ = false;       // RWKV_MI355X_SPLIT_MAA=1: v6 decode W1 + mix as two launches

@@ -132,3 +132,32 @@ extern "C" RWKV_API bool rwkv_mi355x_selftest_gemm_split(int wtype, const void *
     if (wtype_quantized(wtype)) return T >= 2 && selftest_mm(wtype, W, K, M, x, T, y, true, split);
     return (wtype == W_F16 || wtype == W_F32) && T >= 16 && K >= 512 && selftest_mm(wtype, W, K, M, x, T, y, false, split);
 }
+
+// WKV-6 (v5 / v6) over T tokens of one context: chunked = 0 the serial k_wkv6_s64 (decode's
+// association), 1 the chunk-parallel form (wkv_chunk.hip).  k, v, r, w: [T][H*64] (w: [H*64] when
+// w_per_token = 0); u: [H*64]; state_in / state_out: [H][64][64]; y: [T][H*64]; all host.
+extern "C" RWKV_API bool rwkv_mi355x_selftest_wkv6(int T, int H, int chunked, int w_per_token, const float * k,
+                                                  const float * v, const float * r, const float * u, const float * w,
+                                                  const float * state_in, float * state_out, float * y) {
+    if (T < 1 || H < 1 || !k || !v || !r || !u || !w || !state_in || !state_out || !y) return false;
+    if (chunked && !wkv6_chunked_supported(T, 64, 0)) return false;
+    const size_t C = (size_t)H * 64, TC = (size_t)T * C, SN = C * 64, WN = w_per_token ? TC : C;
+    DevBufs b;
+    float *dk = (float *)b.alloc(TC * 4), *dv = (float *)b.alloc(TC * 4), *dr = (float *)b.alloc(TC * 4),
+          *du = (float *)b.alloc(C * 4), *dw = (float *)b.alloc(WN * 4), *dsi = (float *)b.alloc(SN * 4),
+          *dso = (float *)b.alloc(SN * 4), *dy = (float *)b.alloc(TC * 4), *ra = (float *)b.alloc(TC * 4),
+          *kb = (float *)b.alloc(TC * 4), *sc = (float *)b.alloc(wkv6_chunked_scratch_floats(T, H) * 4);
+    if (!dk || !dv || !dr || !du || !dw || !dsi || !dso || !dy || !ra || !kb || !sc) return false;
+    const std::pair<float *, const float *> up[] = {{dk, k}, {dv, v}, {dr, r}, {dy, y}};
+    for (const auto & p : up)
+        if (hipMemcpy(p.first, p.second, TC * 4, hipMemcpyHostToDevice) != hipSuccess) return false;
+    if (hipMemcpy(du, u, C * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(dw, w, WN * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(dsi, state_in, SN * 4, hipMemcpyHostToDevice) != hipSuccess)
+        return false;
+    const bool ok = chunked ? launch_wkv6_chunked(nullptr, T, H, dk, dv, dr, du, dw, w_per_token, dsi, dso, dy, ra, kb, sc)
+                            : launch_wkv6(nullptr, T, H, 64, dk, dv, dr, du, dw, w_per_token, dsi, dso, dy, 0);
+    if (!ok || hipDeviceSynchronize() != hipSuccess) return false;
+    return hipMemcpy(y, dy, TC * 4, hipMemcpyDeviceToHost) == hipSuccess &&
+           hipMemcpy(state_out, dso, SN * 4, hipMemcpyDeviceToHost) == hipSuccess;
+}

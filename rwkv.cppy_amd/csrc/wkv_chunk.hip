@@ -15,15 +15,18 @@
 // 1e-12: the terms it multiplies are below 1e-12 either way), and chunks are 16 tokens, so |la| stays
 // below 640 and the differences keep ~1e-5 relative accuracy in the worst case.
 //
-// Four launches per layer; only the third is serial, and only over chunks, elementwise:
+// Three launches per layer; only the second is serial, and only over chunks, elementwise:
 //   k_wkv6c_prep  (chunk, head): la, RA = r 2^la, KB = k 2^(la_L - la_{s+1}), the L x L matrix B and
 //                 AL = 2^la_L -- all the exp work;
-//   k_wkv6c_u     (chunk, head): U_c = KB_c^T V_c, the chunk's tokens carried to its end;
-//   k_wkv6c_carry (state element): S_{c+1} = AL_c S_c + U_c over the chunks, S_c stored over U_c --
-//                 64 dependent fmas per element at T = 1024 instead of 1024 token steps;
+//   k_wkv6c_carry (head, 4 key rows): S_{c+1} = AL_c S_c + KB_c^T V_c over the chunks, the chunk-start
+//                 states S_c stored -- 64 chunk steps at T = 1024 instead of 1024 token steps;
 //   k_wkv6c_out   (chunk, head): y = RA S_c + B V.
-// A first form with the chunk-serial loop doing the whole y product per chunk (one workgroup per
-// head and 8 columns) measured slower than the serial kernel (105 vs 90 us at T = 1024, H = 32).
+// Measured (v6-1B6 head count H = 32, rocprofv3 kernel trace of tools/wkv_chunk_time.py): T = 1024
+// 21.6 + 32.5 + 17.2 = 71 us against 90.9 us for k_wkv6_s64; T = 4096 64 + 128 + 53 = 245 us against
+// 350 us.  Earlier forms, not kept: the chunk-serial loop doing the whole y product per chunk (one
+// workgroup per head and 8 columns) 105 us; U_c as its own kernel with an elementwise carry through
+// memory 81 us.  The carry is bound by its S_c stores (32 MB at T = 1024) behind the loop-head
+// vmcnt(0) the compiler keeps.
 #include "device_common.hpp"
 #include "kernels.hpp"
 
@@ -87,72 +90,73 @@ __global__ __launch_bounds__(256) void k_wkv6c_prep(int T, int H, const float * 
     }
 }
 
-// Chunk state contributions U_c[i][j] = sum_s KB[s][i] v_s[j] (the chunk's own tokens carried to its
-// end), one workgroup per (chunk, head): thread (i = tid / 16 + 16 q, j = 4 (tid % 16) ..) 16 outputs.
-__global__ __launch_bounds__(256) void k_wkv6c_u(int T, int H, const float * KB, const float * v, float * US) {
-    constexpr int L = WKVC_L, S = WKVC_S;
-    __shared__ __attribute__((aligned(16))) float skb[L][S], sv[L][S];
-    const int c = blockIdx.x, h = blockIdx.y, tid = threadIdx.x, C = H * S, t0 = c * L;
-    {
-        const int tt = tid >> 4, i4 = (tid & 15) * 4;
-        const bool ok = t0 + tt < T;
-        const size_t o = (size_t)(t0 + tt) * C + (size_t)h * S + i4;
-        *(float4 *)&skb[tt][i4] = ok ? *(const float4 *)(KB + o) : make_float4(0.f, 0.f, 0.f, 0.f);
-        *(float4 *)&sv[tt][i4] = ok ? *(const float4 *)(v + o) : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    __syncthreads();
-    const int j4 = (tid & 15) * 4;
-    float * out = US + ((size_t)c * H + h) * S * S;
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-        const int i = (tid >> 4) + 16 * q;
-        float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-        for (int s = 0; s < L; s++) {
-            const float kb = skb[s][i];
-            const float4 vv = *(const float4 *)&sv[s][j4];
-            a.x = fmaf(kb, vv.x, a.x);
-            a.y = fmaf(kb, vv.y, a.y);
-            a.z = fmaf(kb, vv.z, a.z);
-            a.w = fmaf(kb, vv.w, a.w);
-        }
-        *(float4 *)(out + i * S + j4) = a;
-    }
-}
+// The chunk-serial part: S_{c+1} = AL_c S_c + U_c with U_c[i][j] = sum_s KB[s][i] v_s[j] formed on the
+// fly; the chunk-start states S_c go to SC for k_wkv6c_out.  Workgroup = (head, 4 key rows), thread
+// (row i = 4 blockIdx.y + tid / 64, column j = tid % 64).  Chunks go in groups of G: a group's operands
+// (v: 16 x 64, KB: 16 x 4, AL: 4 per chunk) are loaded global -> registers two groups ahead (one
+// chunk's work is far shorter than a load's latency), then into one half of an LDS ring; one barrier
+// per group, the G U_c products side by side, then the G dependent state steps.
+constexpr int WKVC_G = 4;
 
-// The chunk-serial part, elementwise: thread per state element (h, i, j), S <- AL_c[i] S + U_c[i][j]
-// over the chunks; the chunk-start states S_c replace U_c in place (read before the write).  The
-// U_c / AL_c loads do not depend on the recurrence: D chunks are kept in flight.
-__global__ __launch_bounds__(256) void k_wkv6c_carry(int nch, int H, const float * AL, float * US, const float * sin,
-                                                     float * sout) {
-    constexpr int S = WKVC_S, D = 8;
-    const int e = blockIdx.x * 256 + threadIdx.x;  // h * 4096 + i * 64 + j
-    const int h = e >> 12, i = (e >> 6) & 63, C = H * S;
-    const size_t cs = (size_t)H * S * S;  // one chunk's states
-    float * p = US + e;
-    const float * al = AL + h * S + i;
-    float st = sin[e];
-    float u[D], a[D];
+__global__ __launch_bounds__(256) void k_wkv6c_carry(int T, int H, const float * KB, const float * v, const float * AL,
+                                                     const float * sin, float * sout, float * SC) {
+    constexpr int L = WKVC_L, S = WKVC_S, G = WKVC_G, D = 2 * G;
+    __shared__ __attribute__((aligned(16))) float sv[2][G][L][S], skb[2][G][L][4], sal[2][G][4];
+    const int h = blockIdx.x, ib = blockIdx.y, tid = threadIdx.x, C = H * S;
+    const int r = tid >> 6, j = tid & 63, i = ib * 4 + r;
+    const int nch = (T + L - 1) / L;
+    const size_t hb = (size_t)h * S * S;
+    float st = sin[hb + (size_t)i * S + j];
+    // staging roles: v float4 (token tid / 16, columns 4 (tid % 16) ..); KB (tid < 64: token tid / 4,
+    // row tid % 4); AL (tid < 4: row tid)
+    const int vt = tid >> 4, vj = (tid & 15) * 4;
+    float4 rv[D];
+    float rk[D], ra[D];
+    // every load unconditional from a clamped address, zeroed (by a select) only when it is stored to
+    // LDS: a predicated load, or a select right behind it, makes the compiler wait for the load there
+    auto load = [&](int d, int c) __attribute__((always_inline)) {
+        const int cc = min(c, nch - 1), t0 = cc * L;
+        const int tv = min(t0 + vt, T - 1), tk = min(t0 + (tid >> 2), T - 1);
+        rv[d] = *(const float4 *)(v + (size_t)tv * C + (size_t)h * S + vj);
+        rk[d] = KB[(size_t)tk * C + (size_t)h * S + ib * 4 + (tid & 3)];
+        ra[d] = AL[(size_t)cc * C + (size_t)h * S + ib * 4 + (tid & 3)];
+    };
 #pragma unroll
-    for (int d = 0; d < D; d++) {
-        u[d] = d < nch ? p[d * cs] : 0.0f;
-        a[d] = d < nch ? al[(size_t)d * C] : 0.0f;
-    }
+    for (int d = 0; d < D; d++) load(d, d);
+    // straight-line groups (no early exit: chunks past the end compute zeros and are not stored), so
+    // the compiler's load counters stay exact across the loop
     for (int c0 = 0; c0 < nch; c0 += D) {
 #pragma unroll
-        for (int d = 0; d < D; d++) {
-            const int c = c0 + d;
-            if (c < nch) {
-                const float uc = u[d], ac = a[d];
-                const int cn = c + D;
-                u[d] = cn < nch ? p[cn * cs] : 0.0f;
-                a[d] = cn < nch ? al[(size_t)cn * C] : 0.0f;
-                p[c * cs] = st;
-                st = fmaf(ac, st, uc);
+        for (int half = 0; half < 2; half++) {
+            const int g0 = c0 + half * G;  // this group's first chunk
+#pragma unroll
+            for (int e = 0; e < G; e++) {
+                const int d = half * G + e;
+                const int t0 = (g0 + e) * L;  // token tails and chunks past the end: zeros
+                *(float4 *)&sv[half][e][vt][vj] = t0 + vt < T ? rv[d] : make_float4(0.f, 0.f, 0.f, 0.f);
+                if (tid < 64) skb[half][e][tid >> 2][tid & 3] = t0 + (tid >> 2) < T ? rk[d] : 0.0f;
+                if (tid < 4) sal[half][e][tid] = ra[d];
+                load(d, g0 + e + D);
+            }
+            __syncthreads();
+            float u[G];
+#pragma unroll
+            for (int e = 0; e < G; e++) u[e] = 0.0f;
+#pragma unroll
+            for (int s = 0; s < L; s++)
+#pragma unroll
+                for (int e = 0; e < G; e++) u[e] = fmaf(skb[half][e][s][r], sv[half][e][s][j], u[e]);
+#pragma unroll
+            for (int e = 0; e < G; e++) {
+                const int c = g0 + e;
+                const bool live = c < nch;
+                SC[(((size_t)c * H + h) * S + i) * S + j] = st;  // chunks past the end: padding slots
+                const float nst = fmaf(sal[half][e][r], st, u[e]);
+                st = live ? nst : st;
             }
         }
     }
-    sout[e] = st;
+    sout[hb + (size_t)i * S + j] = st;
 }
 
 // y of one (chunk, head): y[t][j] = sum_i RA[t][i] S_c[i][j] + sum_{s<=t} B[t][s] v_s[j]; thread
@@ -204,9 +208,9 @@ __global__ __launch_bounds__(256) void k_wkv6c_out(int T, int H, const float * R
 }
 
 size_t wkv6_chunked_scratch_floats(int T, int H) {
-    // B [nch][H][L][L], AL [nch][C], U / S_c [nch][H][64][64]
-    const size_t nch = ((size_t)T + WKVC_L - 1) / WKVC_L;
-    return nch * H * WKVC_L * WKVC_L + nch * H * WKVC_S + nch * H * WKVC_S * WKVC_S;
+    // B [nch][H][L][L], AL [nch][C], S_c [nch rounded up to 2 G][H][64][64]
+    const size_t nch = ((size_t)T + WKVC_L - 1) / WKVC_L, ncp = (nch + 2 * WKVC_G - 1) / (2 * WKVC_G) * (2 * WKVC_G);
+    return nch * H * WKVC_L * WKVC_L + nch * H * WKVC_S + ncp * H * WKVC_S * WKVC_S;
 }
 
 bool wkv6_chunked_supported(int T, int S, int bs) { return S == WKVC_S && bs == 0 && T >= 2; }
@@ -222,9 +226,7 @@ bool launch_wkv6_chunked(hipStream_t st, int T, int H, const float * k, const fl
     if (w_per_token) RK_LAUNCH((k_wkv6c_prep<true>), dim3(nch, H), dim3(256), 0, st, T, H, k, r, w, u, RA, KB, Bm, AL);
     else RK_LAUNCH((k_wkv6c_prep<false>), dim3(nch, H), dim3(256), 0, st, T, H, k, r, w, u, RA, KB, Bm, AL);
     HIP_OK(hipGetLastError());
-    RK_LAUNCH(k_wkv6c_u, dim3(nch, H), dim3(256), 0, st, T, H, KB, v, US);
-    HIP_OK(hipGetLastError());
-    RK_LAUNCH(k_wkv6c_carry, dim3(H * WKVC_S * WKVC_S / 256), dim3(256), 0, st, nch, H, AL, US, state_in, state_out);
+    RK_LAUNCH(k_wkv6c_carry, dim3(H, WKVC_S / 4), dim3(256), 0, st, T, H, KB, v, AL, state_in, state_out, US);
     HIP_OK(hipGetLastError());
     RK_LAUNCH(k_wkv6c_out, dim3(nch, H), dim3(256), 0, st, T, H, RA, Bm, v, US, y);
     HIP_OK(hipGetLastError());

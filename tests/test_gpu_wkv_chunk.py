@@ -7,7 +7,7 @@ matrix, carried state), so it is NOT bit-exact with the serial kernel (k_wkv6_s6
 association) and stays off by default.  The bar it is held to instead:
 
 * kernel level, against a float64 restatement of the recurrence (y_t = r_t (S + u k_t v_t^T),
-  S <- w_t S + k_t v_t^T): max |y - y64| <= 2e-5 * max |y64| and the same for the final state, over
+  S <- w_t S + k_t v_t^T): max |y - y64| <= 5e-6 * max |y64| and the same for the final state, over
   T = 2 .. 4096 (ragged chunk tails) with decays from 1 down to exact 0; for comparison the serial
   kernel's own fp32 error is printed beside it;
 * model level, v5 and v6 sequence evaluation with the switch on: logits within the oracle's noise
@@ -26,7 +26,7 @@ from rwkv_lib import RWKVModel, library
 
 pytestmark = pytest.mark.gpu
 
-TOL = 2e-5
+TOL = 5e-6
 P = ctypes.POINTER(ctypes.c_float)
 
 

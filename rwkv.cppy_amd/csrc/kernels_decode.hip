@@ -153,6 +153,13 @@ bool launch_mv_group(hipStream_t st, MVGroup & g) {
         return e ? atoi(e) : 1;
     }();
     if (emit_u1 && emit && U == 2 && blocks > g_mv_cus) U = 1;
+    // activation-input rows of 5..8 quantized units per lane (v7-2.9B FFN value, K = 10240): all
+    // units in one round of loads instead of 4 + the rest
+    static const int act_u8 = [] {
+        const char * e = getenv("RWKV_MI355X_ACT_U8");  // default on (0: off, A/B)
+        return e ? atoi(e) : 1;
+    }();
+    if (act_u8 && srck == MVK_ACT && !mva && umax > 4 && umax <= 8 && wfix >= 0 && wtype_quantized(wfix)) U = 8;
     bool ok = false;
     switch (wfix) {
         case W_F16: ok = launch_mv_shape<W_F16>(st, g, U, srck, form, emit, dim3(grid)); break;

@@ -1070,7 +1070,8 @@ bool launch_mv_shape(hipStream_t st, MVGroup & g, int U, int srck, int form, boo
     if (srck == MVK_ACT) {
         if (U == 1) MV_L(2, 1, MVK_ACT, 0, false, 0);
         else if (U == 2) MV_L(2, 2, MVK_ACT, 0, false, 0);
-        else MV_L(2, 4, MVK_ACT, 0, false, 0);
+        else if (U == 4) MV_L(2, 4, MVK_ACT, 0, false, 0);
+        else MV_L(2, 8, MVK_ACT, 0, false, 0);
         return true;
     }
     if (srck == MVK_F32) {

@@ -1050,7 +1050,7 @@ bool launch_mv_shape(hipStream_t st, MVGroup & g, int U, int srck, int form, boo
                        b[1], b[2], b[3], b[4], b[5], b[6], b[7], g)
     const int K = g.e[0].W.K;
     if constexpr (WFIX >= 0) {
-        if (srck == MVK_ACT && !emit && g.units_max <= U) {
+        if (srck == MVK_ACT && !emit && g.units_max <= U && U <= 4) {  // k_mva: <= 4 units per lane
 #define MVA_R(Rv, Uv) \
     RK_LAUNCH((k_mva<WFIX, Rv, Uv>), grid, dim3(256), 0, st, b[1], b[2], b[3], b[4], b[5], b[6], b[7], g)
 #define MVA_L(Uv)                          \

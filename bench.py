@@ -212,6 +212,27 @@ def main():
         a = np.ascontiguousarray(np.asarray(toks, dtype=np.int32))
         return a, a.ctypes.data_as(P_INT)
 
+    # ---------------- self-check (every config, before any timing) ----------------
+    # serial decode (the matvec kernels) and one sequence evaluation (the GEMM / sequence kernels) must
+    # give the same bits on the same tokens -- the library's invariant; a fast kernel that drops work
+    # breaks it, so no speed is reported from a build that fails it
+    # (skipped in the roofline-only profiling pass, whose kernel trace must hold the timed launches only)
+    sc_toks = [int(t) for t in np.random.default_rng(99).integers(0, n_vocab, 0 if args.roofline_only else 12)]
+    sc_st, sc_st2 = np.zeros(state_len, np.float32), np.zeros(state_len, np.float32)
+    sc_lg, sc_lg2 = np.zeros(n_vocab, np.float32), np.zeros(n_vocab, np.float32)
+    L.rwkv_init_state(ctx.ptr, sc_st.ctypes.data_as(P_F))
+    for t in sc_toks:
+        assert L.rwkv_eval(ctx.ptr, t, sc_st.ctypes.data_as(P_F), sc_st.ctypes.data_as(P_F), sc_lg.ctypes.data_as(P_F))
+    sca, scp = tok_arr(sc_toks)
+    if sc_toks:
+        assert L.rwkv_eval_sequence(ctx.ptr, scp, len(sc_toks), None, sc_st2.ctypes.data_as(P_F),
+                                    sc_lg2.ctypes.data_as(P_F))
+    self_check = {'decode_equals_sequence_bits': bool(np.array_equal(sc_lg.view(np.uint32), sc_lg2.view(np.uint32)) and
+                                                      np.array_equal(sc_st.view(np.uint32), sc_st2.view(np.uint32))),
+                  'tokens': len(sc_toks)}
+    log(f"self-check: serial decode == sequence eval bit for bit over {len(sc_toks)} tokens: "
+        f"{self_check['decode_equals_sequence_bits']}")
+
     assert L.rwkv_mi355x_state_upload(ctx.ptr, None)
 
     # ---------------- decode (device-resident state) ----------------
@@ -604,6 +625,7 @@ def main():
             'seq_roofline': seq_roofline,
             'cpu_baseline': cpu,
             'parity': parity,
+            'self_check': self_check,
         }
         # every requested field must be present: a missing one fails the run (after the line)
         if world == 1 and not args.skip_cpu:
@@ -613,6 +635,8 @@ def main():
                 errors.append('parity missing')
             elif not parity['bit_exact_vs_gpu_association_oracle']:
                 errors.append('parity: GPU decode not bit-exact to the GPU-association oracle')
+        if sc_toks and not self_check['decode_equals_sequence_bits']:
+            errors.append('self-check: serial decode and sequence evaluation differ')
         if roofline is None and not args.decode_only:
             errors.append('roofline missing')
         if args.seq_reps > 0 and seq_roofline is None:

@@ -366,26 +366,67 @@ bool launch_delay(hipStream_t st, int us) {
 
 // --------------------------------------------------------------------------- LayerNorm family
 
+// One token row per workgroup.  Every wave loads the embedding row straight into registers in the
+// LayerNorm chunk layout (lane l: elements 512 c + 8 l .. + 7) and computes the statistics itself
+// (ln_stats_regs: ln_stats_wave's association, the same bits as the sequence kernels); wave w then
+// normalizes and stores chunks w, w + 4, ...  The LayerNorm weights are loaded at kernel start, before
+// the token id returns: two dependent memory round trips (token, row) instead of a store / reload of
+// the row through L2 between them.
+constexpr int EMB_NC = 8;  // chunks held per lane: n_embed <= 4096
 __global__ __launch_bounds__(256) void k_embed_ln(const uint32_t * tokens, DMat emb, const float * w,
                                                   const float * b, float * x) {
-    __shared__ double sh[8];
     STAMP_BEGIN();
-    const int t = blockIdx.x, C = emb.K;
-    const size_t tok = tokens[t];
-    float * xr = x + (size_t)t * C;
-    for (int c = threadIdx.x; c < C; c += blockDim.x) {
-        xr[c] = emb.type == W_F16 ? __half2float(((const __half *)emb.qs)[tok * C + c])
-                                  : ((const float *)emb.qs)[tok * C + c];
+    const int t = blockIdx.x, C = emb.K, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int nc = (C + LN_CHUNK - 1) / LN_CHUNK;
+    float wv[2][8], bv[2][8];  // this wave's chunks w and w + 4
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+        const int c = wave + 4 * q;
+        if (c < nc) {
+            ln_load8(wv[q], w, c * LN_CHUNK + lane * 8, C);
+            ln_load8(bv[q], b, c * LN_CHUNK + lane * 8, C);
+        }
     }
-    __syncthreads();
+    const size_t tok = tokens[t];
+    float v[EMB_NC][8];
+#pragma unroll
+    for (int c = 0; c < EMB_NC; c++) {
+        if (c >= nc) break;
+        const int k = min(c * LN_CHUNK + lane * 8, C - 8);
+        if (emb.type == W_F16) {
+            const __half * p = (const __half *)emb.qs + tok * C + k;
+            const int4 raw = *(const int4 *)p;
+            const __half * h = (const __half *)&raw;
+#pragma unroll
+            for (int j = 0; j < 8; j++) v[c][j] = __half2float(h[j]);
+        } else {
+            ln_load8(v[c], (const float *)emb.qs + tok * C, k, C);
+        }
+    }
     float mean, scale;
-    ln_stats(xr, C, 1e-5f, mean, scale, sh);
-    for (int c = threadIdx.x; c < C; c += blockDim.x) xr[c] = ln_apply(xr[c], mean, scale, w[c], b[c]);
+    ln_stats_regs<EMB_NC>(v, nc, C, 1e-5f, mean, scale);
+    float * xr = x + (size_t)t * C;
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+        const int c = wave + 4 * q;
+        if (c >= nc) continue;
+        const int k = c * LN_CHUNK + lane * 8;
+        if (k >= C) continue;
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) o[j] = ln_apply(v[c][j], mean, scale, wv[q][j], bv[q][j]);
+        *(float4 *)(xr + k) = make_float4(o[0], o[1], o[2], o[3]);
+        *(float4 *)(xr + k + 4) = make_float4(o[4], o[5], o[6], o[7]);
+    }
     STAMP_END(5);
 }
 
 bool launch_embed_ln(hipStream_t st, const uint32_t * tokens, int T, const DMat & emb, const float * w,
                      const float * b, float * x) {
+    if (emb.K % 8 || emb.K > EMB_NC * LN_CHUNK || (emb.type != W_F16 && emb.type != W_F32)) {
+        fprintf(stderr, "rwkv: embedding row of %d elements (type %d) unsupported\n", emb.K, emb.type);
+        return false;
+    }
     RK_LAUNCH(k_embed_ln, dim3(T), dim3(256), 0, st, tokens, emb, w, b, x);
     HIP_OK(hipGetLastError());
     return true;
@@ -965,7 +1006,6 @@ typedef float f2_t __attribute__((ext_vector_type(2)));
 // and the 4 key groups are folded with fold_g4 ((s0 + s2) + (s1 + s3)): 8 dependent VALU ops per
 // token instead of a 16-add chain through the lanes.  Chunks of 64 tokens of k, r, w and v
 // are staged in LDS with coalesced loads, the next chunk in flight while this one runs.
-constexpr int WKV_TC = 32;
 
 // Sum over the four lane groups g = lane >> 4: partner g ^ 2 (permlane32 swap), then g ^ 1
 // (permlane16 swap) -- the (p0 + p2) + (p1 + p3) of group_sum(., 4) on adjacent lanes.

@@ -1022,6 +1022,34 @@ __global__ __launch_bounds__(256 * RT, QG32_LB) void k_qg32(MMGroup g) {
 // stage's in flight while this one is accumulated -- so a block costs a lane two b128 reads (4 rows'
 // m_w, 4 tokens' s_x) for 16 multiply-adds.
 // Output m2[row][token] (row-major over rows).
+// The m*s pass's arithmetic in packed f32 (v_pk_mul_f32 / v_pk_add_f32: per element the scalar
+// operations' bits, tools/pk_probe.hip; this file builds without the SLP vectorizer, so the packing
+// is spelled out): acc[j] = acc[j] + w * x[j] over pairs of outputs, and the class-tree folds.
+template <int N>
+__device__ __forceinline__ void qm_mac_row(float * acc, float w, const float (&x)[N]) {
+    const qf2_t w2 = {w, w};
+#pragma unroll
+    for (int j = 0; j < N; j += 2) {
+        qf2_t a = {acc[j], acc[j + 1]};
+        const qf2_t x2 = {x[j], x[j + 1]};
+        a = a + w2 * x2;
+        acc[j] = a.x;
+        acc[j + 1] = a.y;
+    }
+}
+// v = st[kk] + v for kk < NL, into st[NL] (NL < 6) or st[0] (NL = 6: the total), pairs of outputs
+template <int NL, int NO>
+__device__ __forceinline__ void qm_close(float (&st)[6][NO], const float (&acc)[NO]) {
+#pragma unroll
+    for (int k = 0; k < NO; k += 2) {
+        qf2_t v = {acc[k], acc[k + 1]};
+#pragma unroll
+        for (int kk = 0; kk < NL; kk++) v = qf2_t{st[kk][k], st[kk][k + 1]} + v;
+        st[NL < 6 ? NL : 0][k] = v.x;
+        st[NL < 6 ? NL : 0][k + 1] = v.y;
+    }
+}
+
 constexpr int QM_CLS = 8;  // classes per stage
 // NMAX = blocks per class rounded up to 1 / 2 / 4 / 8 (K <= 16384); slot (u, lc) at u * 8 + lc holds
 // m_w of the workgroup's 64 rows and s_x of its 32 tokens for block lc + 8 sg + 64 u
@@ -1078,11 +1106,7 @@ __global__ __launch_bounds__(256) void k_qg_msum(MMGroup g) {
     for (int k = 0; k < 16; k++) acc[k] = 0.0f;
 #define QM_CLOSE(N)                                                   \
     case N: {                                                         \
-        _Pragma("unroll") for (int k = 0; k < 16; k++) {              \
-            float v = acc[k];                                         \
-            for (int kk = 0; kk < N; kk++) v = st[kk][k] + v;         \
-            st[N < 6 ? N : 0][k] = v;  /* N = 6: the total */         \
-        }                                                             \
+        qm_close<N, 16>(st, acc);  /* N = 6: the total, into st[0] */ \
         break;                                                        \
     }
     gload(0);
@@ -1111,9 +1135,7 @@ __global__ __launch_bounds__(256) void k_qg_msum(MMGroup g) {
                 const float wv[4] = {o.w[u].x, o.w[u].y, o.w[u].z, o.w[u].w};
                 const float xv[4] = {o.x[u].x, o.x[u].y, o.x[u].z, o.x[u].w};
 #pragma unroll
-                for (int r = 0; r < 4; r++)
-#pragma unroll
-                    for (int c = 0; c < 4; c++) acc[4 * r + c] = acc[4 * r + c] + wv[r] * xv[c];
+                for (int r = 0; r < 4; r++) qm_mac_row<4>(acc + 4 * r, wv[r], xv);
             }
         };
         auto fold = [&](int l) {
@@ -1160,9 +1182,7 @@ __global__ __launch_bounds__(256) void k_qg_msum(MMGroup g) {
                         const float wv[4] = {w4[h][q].x, w4[h][q].y, w4[h][q].z, w4[h][q].w};
                         const float xv[4] = {x4[h][q].x, x4[h][q].y, x4[h][q].z, x4[h][q].w};
 #pragma unroll
-                        for (int r = 0; r < 4; r++)
-#pragma unroll
-                            for (int c = 0; c < 4; c++) acc[4 * r + c] = acc[4 * r + c] + wv[r] * xv[c];
+                        for (int r = 0; r < 4; r++) qm_mac_row<4>(acc + 4 * r, wv[r], xv);
                     }
                 };
                 rd4(0, 0);
@@ -1243,11 +1263,7 @@ __global__ __launch_bounds__(256) void k_qg_msum_rows(MMGroup g) {
     for (int k = 0; k < 8; k++) acc[k] = 0.0f;
 #define QM_CLOSE(N)                                                   \
     case N: {                                                         \
-        _Pragma("unroll") for (int k = 0; k < 8; k++) {               \
-            float v = acc[k];                                         \
-            for (int kk = 0; kk < N; kk++) v = st[kk][k] + v;         \
-            st[N < 6 ? N : 0][k] = v;  /* N = 6: the total */         \
-        }                                                             \
+        qm_close<N, 8>(st, acc);  /* N = 6: the total, into st[0] */  \
         break;                                                        \
     }
     gload(0);
@@ -1276,8 +1292,7 @@ __global__ __launch_bounds__(256) void k_qg_msum_rows(MMGroup g) {
             for (int u = 0; u < NMAX; u++) {
                 if (u >= n) break;  // uniform
                 const float sx[8] = {o.s0[u].x, o.s0[u].y, o.s0[u].z, o.s0[u].w, o.s1[u].x, o.s1[u].y, o.s1[u].z, o.s1[u].w};
-#pragma unroll
-                for (int k = 0; k < 8; k++) acc[k] = acc[k] + o.w[u] * sx[k];
+                qm_mac_row<8>(acc, o.w[u], sx);
             }
         };
         auto fold = [&](int l) {
@@ -1324,8 +1339,7 @@ __global__ __launch_bounds__(256) void k_qg_msum_rows(MMGroup g) {
                     for (int q = 0; q < 4; q++) {
                         if (u0 + q >= n) break;  // uniform
                         const float sx[8] = {a4[q].x, a4[q].y, a4[q].z, a4[q].w, b4[q].x, b4[q].y, b4[q].z, b4[q].w};
-#pragma unroll
-                        for (int k = 0; k < 8; k++) acc[k] = acc[k] + w4[q] * sx[k];
+                        qm_mac_row<8>(acc, w4[q], sx);
                     }
                 }
                 fold(l);

@@ -328,7 +328,8 @@ __device__ __forceinline__ void qg_store_part(float * part, int sidx, int T, int
 }
 
 // Class-pair fold: the odd class (in c) closes N >= 1 levels of the binary counter: v = c, then
-// v = st[k] + v for k < N, into st[N] (N < 6) or the total (N = 6)
+// v = st[k] + v for k < N, into st[N] (N < 6) or the total (N = 6).  Packed f32 over output pairs
+// (v_pk_add_f32: per element the scalar add's bits; this file builds without the SLP vectorizer).
 template <int TI, int N>
 __device__ __forceinline__ void qg_fold(float (&st)[6][TI][2][4], const float (&c)[TI][2][4], float (&tot)[TI][2][4]) {
 #pragma unroll
@@ -336,12 +337,17 @@ __device__ __forceinline__ void qg_fold(float (&st)[6][TI][2][4], const float (&
 #pragma unroll
         for (int j = 0; j < 2; j++)
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                float v = c[i][j][q];
+            for (int q = 0; q < 4; q += 2) {
+                qf2_t v = {c[i][j][q], c[i][j][q + 1]};
 #pragma unroll
-                for (int kk = 0; kk < N; kk++) v = st[kk][i][j][q] + v;
-                if constexpr (N < 6) st[N][i][j][q] = v;
-                else tot[i][j][q] = v;
+                for (int kk = 0; kk < N; kk++) v = qf2_t{st[kk][i][j][q], st[kk][i][j][q + 1]} + v;
+                if constexpr (N < 6) {
+                    st[N][i][j][q] = v.x;
+                    st[N][i][j][q + 1] = v.y;
+                } else {
+                    tot[i][j][q] = v.x;
+                    tot[i][j][q + 1] = v.y;
+                }
             }
 }
 
@@ -572,10 +578,12 @@ __global__ __launch_bounds__(256) void k_qgemm(MMGroup g) {
     case N: {                                                                     \
         _Pragma("unroll") for (int i = 0; i < TI; i++)                            \
         _Pragma("unroll") for (int j = 0; j < 2; j++)                             \
-        _Pragma("unroll") for (int q = 0; q < 4; q++) {                           \
-            float v = c[i][j][q];                                                 \
-            for (int kk = 0; kk < N; kk++) v = st[kk][i][j][q] + v;               \
-            DST[i][j][q] = v;                                                     \
+        _Pragma("unroll") for (int q = 0; q < 4; q += 2) {                        \
+            qf2_t v = {c[i][j][q], c[i][j][q + 1]};                               \
+            for (int kk = 0; kk < N; kk++)                                        \
+                v = qf2_t{st[kk][i][j][q], st[kk][i][j][q + 1]} + v;              \
+            DST[i][j][q] = v.x;                                                   \
+            DST[i][j][q + 1] = v.y;                                               \
         }                                                                         \
         break;                                                                    \
     }

@@ -87,7 +87,7 @@ def run(T, H, chunked, wpt, ops):
 
 
 @pytest.mark.parametrize('T,H,wpt', [(2, 1, True), (15, 2, True), (16, 1, True), (17, 2, True), (100, 2, False),
-                                     (1024, 2, True), (1024, 2, False), (4096, 1, True)])
+                                     (1024, 2, True), (1024, 2, False), (4096, 1, True), (1024, 32, True)])
 def test_chunked_wkv6_against_float64(T, H, wpt):
     ops = operands(T, H, wpt, seed=T * 7 + H)
     y64, s64 = recurrence64(*ops, wpt)

@@ -87,7 +87,17 @@ bool launch_mv_group(hipStream_t st, MVGroup & g) {
     for (int i = 0; i < g.n; i++) rows2 += (g.e[i].W.M + 7) / 8;
     const bool r4 = ln_r4 && prologue && !emit && srck == MVK_LN && (g.n > 1 || rows2 <= 8 * g_mv_cus) &&
                     rows2 > 2 * g_mv_cus;
-    const int R = emit ? 8 : mva ? mva_rows() : r4 ? 4 : 2, RW = 4 * R;
+    // ... and 8 rows per wave when even 4 leave more than four workgroups per CU (K > 2048, two units
+    // per lane: v5-7B r,k,v,g, 1024 -> 512 workgroups; decode 1557 -> 1535 us/token, bit-exact; v7's
+    // r,k,v at 480 workgroups measured neutral and stays at 4)
+    static const int ln_r8 = [] {
+        const char * e = getenv("RWKV_MI355X_LN_R8");  // default on (0: off, A/B)
+        return e ? atoi(e) : 1;
+    }();
+    int lnk = 0;
+    for (int i = 0; i < g.n; i++) lnk = std::max(lnk, g.e[i].W.K);
+    const bool r8 = ln_r8 && r4 && lnk > 2048 && umax0 == 2 && rows2 > 4 * g_mv_cus;
+    const int R = emit ? 8 : mva ? mva_rows() : r8 ? 8 : r4 ? 4 : 2, RW = 4 * R;
     g.rows = R;
     int blocks = 0, umax = 1, lds = 0;
     for (int i = 0; i < g.n; i++) {

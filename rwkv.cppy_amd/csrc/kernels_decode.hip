@@ -170,6 +170,12 @@ bool launch_mv_group(hipStream_t st, MVGroup & g) {
         return e ? atoi(e) : 1;
     }();
     if (act_u8 && srck == MVK_ACT && !mva && umax > 4 && umax <= 8 && wfix >= 0 && wtype_quantized(wfix)) U = 8;
+    // F16 LayerNorm groups of 5-8 units per lane (v7-2.9B LoRA first stages, K = 2560): one round
+    static const int f16_u8 = [] {
+        const char * e = getenv("RWKV_MI355X_F16_U8");  // A/B
+        return e ? atoi(e) : 1;
+    }();
+    if (f16_u8 && srck == MVK_LN && !emit && wfix == W_F16 && R == 2 && umax > 4 && umax <= 8 && lnk > 2048) U = 8;
     bool ok = false;
     switch (wfix) {
         case W_F16: ok = launch_mv_shape<W_F16>(st, g, U, srck, form, emit, dim3(grid)); break;

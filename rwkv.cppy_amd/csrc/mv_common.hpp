@@ -1105,6 +1105,12 @@ bool launch_mv_shape(hipStream_t st, MVGroup & g, int U, int srck, int form, boo
     // not emitting: g.rows rows per streaming wave (2, or 4 for large LayerNorm groups); emitting: 8
 #define MV_P(S, F, E)                                         \
     do {                                                      \
+        if constexpr (WFIX == W_F16) {                        \
+            if (U == 8 && K > 2048 && g.rows == 2) {          \
+                MV_L(1, 8, S, F, false, 64);                  \
+                break;                                        \
+            }                                                 \
+        }                                                     \
         if (g.rows == 8 && K > 2048 && U == 2) MV_L(4, 2, S, F, false, 64); \
         else if (g.rows == 4) MV_PR(2, S, F, false);          \
         else MV_PR(1, S, F, false);                           \

@@ -378,9 +378,6 @@ Engine::~Engine() {
     collect_timing();
     for (hipEvent_t e : event_pool_) (void)hipEventDestroy(e);
     if (tok_event_) (void)hipEventDestroy(tok_event_);
-    for (hipEvent_t e : fork_ev_)
-        if (e) (void)hipEventDestroy(e);
-    if (side_) (void)hipStreamDestroy(side_);
     if (stream_) (void)hipStreamDestroy(stream_);
 }
 
@@ -392,16 +389,7 @@ bool Engine::init() {
         HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, m_->device));
         set_mv_device_cus(cus);
     }
-    {
-        // RWKV_MI355X_STREAM_PRIO=1: the compute stream on a high-priority queue (A/B)
-        const char * pr = getenv("RWKV_MI355X_STREAM_PRIO");
-        int lo = 0, hi = 0;
-        if (pr && pr[0] == '1' && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess) {
-            HIP_OK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi));
-        } else {
-            HIP_OK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-        }
-    }
+    HIP_OK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     HIP_OK(hipEventCreateWithFlags(&tok_event_, hipEventDisableTiming));
     HIP_OK(hipEventRecord(tok_event_, stream_));
     for (int i = 0; i < 2; i++) {
@@ -420,33 +408,26 @@ bool Engine::init() {
         HIP_OK(hipMalloc(&hgran_, hgran_n_ * 8));
         ws_allocs_.push_back(hgran_);
         HIP_OK(hipMemset(hgran_, 0, hgran_n_ * 8));
-        // the head outputs handed to the fused Wo rows: tagged per (layer, state parity), never cleared
-        HIP_OK(hipMalloc(&ygran_, (size_t)m_->n_embed * 8));
+        // the tagged hand-offs (fused Wo, fused channel mix): tagged per (layer, state parity)
+        const size_t C = m_->n_embed, kg = (size_t)KG_STRIDE * ((size_t)std::max(m_->F, 32) / 32);
+        tgran_n_ = C + kg + C;
+        HIP_OK(hipMalloc(&ygran_, tgran_n_ * 8));
         ws_allocs_.push_back(ygran_);
-        HIP_OK(hipMemset(ygran_, 0, (size_t)m_->n_embed * 8));
+        HIP_OK(hipMemset(ygran_, 0, tgran_n_ * 8));
+        kgran_ = ygran_ + C;
+        rgran_ = kgran_ + kg;
     }
-    const char * g = getenv("RWKV_MI355X_NO_GRAPH");
-    use_graphs_ = !(g && g[0] == '1');
-    const char * gd = getenv("RWKV_MI355X_GENERIC_DECODE");
-    generic_decode_ = gd && gd[0] == '1';
-    const char * um = getenv("RWKV_MI355X_SEQ_MATVEC");  // sequence matmuls on k_mm (comparison)
-    use_mm_ = um && um[0] == '1';
-    const char * io = getenv("RWKV_MI355X_STATE_PIPELINE");  // 0: host state copied whole (comparison)
+    // Per-context switches read when the context is created (each arm tested):
+    const char * io = getenv("RWKV_MI355X_STATE_PIPELINE");  // 0: host state copied whole
     io_pipeline_ = !(io && io[0] == '0');
-    const char * bg = getenv("RWKV_MI355X_BATCH_GEMM_MIN");  // contexts from which batches use the GEMM
-    batch_gemm_min_ = bg ? std::max(2, atoi(bg)) : 16;
     const char * ic = getenv("RWKV_MI355X_IO_CHUNK");  // layers per chunk graph (host-state decode)
     io_chunk_ = ic ? std::max(1, atoi(ic)) : 4;
-    const char * sm = getenv("RWKV_MI355X_SPLIT_MAA");  // v6 decode: W1 and mix as two launches (comparison)
+    const char * sm = getenv("RWKV_MI355X_SPLIT_MAA");  // 1: v6 decode W1 and mix as two launches
     split_maa_ = sm && sm[0] == '1';
+    const char * df = getenv("RWKV_MI355X_DECODE_FUSION");  // mask of Engine::FUSE_* (default all)
+    fuse_ = df ? (unsigned)strtoul(df, nullptr, 0) & FUSE_ALL : FUSE_DEFAULT;
     const char * wc = getenv("RWKV_MI355X_WKV_CHUNK");  // 1: chunk-parallel wkv6 (not bit-exact)
     wkv_chunk_ = wc && wc[0] == '1';
-    const char * vf = getenv("RWKV_MI355X_V7_FORK");
-    v7_fork_ = vf && vf[0] == '1' && m_->major == 7;
-    if (v7_fork_) {
-        HIP_OK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
-        for (auto & e : fork_ev_) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    }
     // the fused decode prologues hold LayerNorm inputs in registers up to n_embed 4096
     if (m_->n_embed > 4096 || m_->n_embed % 64) generic_decode_ = true;
     return ensure_workspace(1) && init_state(dstate_[0]);
@@ -1191,6 +1172,7 @@ bool Engine::forward(int T, const float * sin, float * sout, bool logits) {
 // vfirst_) already hold the stream entering l0.  Head on the last token when l1 == n_layer.
 bool Engine::forward_range(int T, const float * sin, float * sout, uint32_t l0, uint32_t l1, bool logits) {
     const size_t C = m_->n_embed;
+    last_decode_ = false;
     if (l0 == 0 && !launch_embed_ln(stream_, dtokens_, T, m_->emb, m_->ln0_w, m_->ln0_b, x_)) return false;
     const size_t per_layer = m_->major >= 5 ? C * (2 + (size_t)m_->S) : 5 * C;
     // layer matmuls run over all T tokens: Q8 activations go straight into GEMM tiles
@@ -1316,6 +1298,7 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits, uint32
     const int C = (int)m_->n_embed, H = (int)m_->H, S = (int)m_->S;
     l1 = std::min(l1, m_->n_layer);
     if (l0 == 0 && !launch_embed_ln(stream_, dtokens_, 1, m_->emb, m_->ln0_w, m_->ln0_b, x_)) return false;
+    v7_fused_lora_ = false;
     const size_t per_layer = m_->major >= 5 ? (size_t)C * (2 + (size_t)S) : 5 * (size_t)C;
     for (uint32_t l = l0; l < l1; l++) {
         const DLayer & L = m_->layers[l];
@@ -1340,14 +1323,14 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits, uint32
         // ---------------- time mixing ----------------
         if (m_->major == 4) {
             ActBuf o = A(0, L.att_o);
-            if (v4_att_fused_supported(C, L.att_r, L.att_k, L.att_v, o)) {
-                // LN + r, k, v rows + WKV-4 in one launch, v4_att_fused_cpw() channels per workgroup (mv_att4f.hip)
+            if ((fuse_ & FUSE_ATT4) && v4_att_fused_supported(C, L.att_r, L.att_k, L.att_v, o)) {
+                // LN + r, k, v rows + WKV-4 in one launch, 8 channels per workgroup (mv_att4f.hip)
                 if (timing_) {
                     kt_bytes_ = 3 * wbytes(L.att_r) + 9.0 * C * 4 + 6.0 * C * 4 + C * 4.0 + act_bytes(o, 1);
                     kt_flops_ = 6.0 * C * C;
                 }
                 V4WoFused wf;
-                const bool wo_in = v4_wo_fused_enabled() && L.att_o.type == L.att_r.type;
+                const bool wo_in = (fuse_ & FUSE_WO4) && L.att_o.type == L.att_r.type && C % 8 == 0;
                 if (wo_in) {
                     wf.wo = L.att_o;
                     wf.xres = x_;
@@ -1365,7 +1348,7 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits, uint32
                                          wo_in ? &wf : nullptr))
                     return false;
                 if (wo_in) goto v4_att_done;
-                if (v4_att_fused_cpw() != 32) {
+                {
                     // y fp32: Wo quantizes it in its own prologue (the same Q8 bits as the emission)
                     MV c;
                     src_f32(c.add(L.att_o, x_, EPI_ADD), y_);
@@ -1478,11 +1461,13 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits, uint32
             // Wo inside the same launch (the head outputs handed to the non-reducer workgroups as
             // granules tagged by layer and state parity); else Wo is its own k_mva launch below
             bool wo_in = false;
-            if (v6_wo_fused_enabled()) {
+            if ((fuse_ & FUSE_WO6) && (fuse_ & FUSE_ATT6)) {
                 f.wo = L.att_o;
                 f.xres = x_;
                 f.ygran = ygran_;
                 f.ytag = (unsigned)(l + 1) | ((unsigned)(cur_ + 1) << 16);
+                f.wo_rows = wo_rows_;
+                f.wo_prepoll = wo_prepoll_;
                 wo_in = v6_att_fused_supported(f);
                 if (!wo_in) {
                     memset(&f.wo, 0, sizeof(f.wo));
@@ -1490,7 +1475,7 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits, uint32
                     f.ygran = nullptr;
                 }
             }
-            if (v6_att_fused_supported(f)) {
+            if ((fuse_ & FUSE_ATT6) && v6_att_fused_supported(f)) {
                 if (timing_) {
                     // r, k, v, g, Wd1, Wd2 weights, their 5 Q8 inputs, the head state in and out,
                     // u / decay / ln_x vectors, r / k / v / g / dl written (sc1) and read back, Wo's input out
@@ -1531,20 +1516,8 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits, uint32
             src_lnmix(bl.add(L.a1, dsmall_[1], EPI_STORE), x_, si + C, L.ln1_w, L.ln1_b, mu + 4 * (size_t)C, 1);
             src_lnmix(bl.add(L.g1, dsmall_[2], EPI_SIGMOID), x_, si + C, L.ln1_w, L.ln1_b, mu + 5 * (size_t)C, 1);
             if (l != 0) src_lnmix(bl.add(L.v1, dsmall_[3], EPI_STORE), x_, si + C, L.ln1_w, L.ln1_b, mu + 3 * (size_t)C, 1);
-            // RWKV_MI355X_V7_FORK=1: the LoRA first stages (their own launch when their weight type
-            // differs) on a second stream forked from the first -- both only read x, so the two
-            // launches may run side by side (a graph branch when captured); joined before the
-            // attention launch.  Eager timing keeps them serial.
-            const bool fork = v7_fork_ && lb.g.n && !timing_;
-            if (fork) {
-                HIP_OK(hipEventRecord(fork_ev_[0], stream_));
-                HIP_OK(hipStreamWaitEvent(side_, fork_ev_[0], 0));
-                if (!mv(lb.g, side_)) return false;
-                HIP_OK(hipEventRecord(fork_ev_[1], side_));
-            }
             if (!mv(b.g)) return false;
-            if (!fork && lb.g.n && !mv(lb.g)) return false;
-            if (fork) HIP_OK(hipStreamWaitEvent(stream_, fork_ev_[1], 0));
+            if (lb.g.n && !mv(lb.g)) return false;
             if (l == 0) HIP_OK(hipMemcpyAsync(vfirst_, v_, (size_t)C * 4, hipMemcpyDeviceToDevice, stream_));
             Att7Dec a;
             memset(&a, 0, sizeof(a));
@@ -1580,13 +1553,14 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits, uint32
             f.bias[3] = L.v0;
             f.vfirst = vfirst_;
             f.has_v = l != 0;
-            if (att7_lora_supported(f)) {
+            if ((fuse_ & FUSE_ATT7) && att7_lora_supported(f)) {
                 if (timing_) {
                     double lb = wbytes(L.w2) + wbytes(L.a2) + wbytes(L.g2) + (l ? wbytes(L.v2) : 0.0);
                     kt_bytes_ = lb + 2.0 * H * S * S * 4 + 12.0 * C * 4 + act_bytes(a.yq, 1);
                     kt_flops_ = 2.0 * (L.w2.K + L.a2.K + L.g2.K + (l ? L.v2.K : 0)) * C;
                 }
                 if (!launch_att7_lora(stream_, f)) return false;
+                v7_fused_lora_ = true;  // w, a, g and the mixed v never leave the launch (debug_copy)
             } else {
                 MV c;
                 src_f32(c.add(L.w2, w_, EPI_DECAY7, nullptr, L.w0), dsmall_[0]);
@@ -1600,8 +1574,33 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits, uint32
         }
         // ---------------- channel mixing ----------------
         if (m_->major == 7) {
-            MV b;
             ActBuf kin = A(0, L.ffn_v);
+            if (fuse_ & FUSE_FFN) {
+                FfnFused ff;
+                memset(&ff, 0, sizeof(ff));
+                MVEntry & fk = ff.e[0];
+                fk.W = L.ffn_k;
+                fk.epi = EPI_RELU_SQ;
+                src_lnmix(fk, x_, si, L.ln2_w, L.ln2_b, L.ffn_x_k, 1, so);
+                fk.emit = 1;
+                fk.act_out = kin;
+                ff.wv = L.ffn_v;
+                ff.x = x_;
+                ff.kg = kgran_;
+                ff.tag = (unsigned)(l + 1) | ((unsigned)(cur_ + 1) << 16);
+                ff.err = herr_d_;
+                ff.spin_max = spin_max_;
+                if (ffn_fused_supported(ff, 1, false)) {
+                    if (timing_) {
+                        kt_bytes_ = wbytes(L.ffn_k) + wbytes(L.ffn_v) + 5.0 * C * 4 + 2.0 * C * 4 +
+                                    (double)L.ffn_k.M / 32 * KG_STRIDE * 8 * 2;
+                        kt_flops_ = 2.0 * ((double)L.ffn_k.M * L.ffn_k.K + (double)L.ffn_v.M * L.ffn_v.K);
+                    }
+                    if (!launch_ffn_fused(stream_, ff, 1, false)) return false;
+                    continue;
+                }
+            }
+            MV b;
             MVEntry & ek = b.add(L.ffn_k, nullptr, EPI_RELU_SQ);
             src_lnmix(ek, x_, si, L.ln2_w, L.ln2_b, L.ffn_x_k, 1, so);
             ek.emit = 1;
@@ -1637,7 +1636,39 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits, uint32
             sr.src = SRC_ACT;
             sr.act = A(7, L.ffn_r);
             sr.epi = EPI_STORE;
-            const bool sig = L.ffn_r.type == L.ffn_k.type && mv_sigmul_supported(sv, sr);
+            // the whole channel mix in one launch (mv_ffnf.hpp), else the key group + k_mvsig
+            if (fuse_ & FUSE_FFN) {
+                FfnFused ff;
+                memset(&ff, 0, sizeof(ff));
+                MVEntry & fk = ff.e[0];
+                fk.W = L.ffn_k;
+                fk.epi = EPI_RELU_SQ;
+                src_lnmix(fk, x_, si, L.ln2_w, L.ln2_b, muk, form, so);
+                fk.emit = 1;
+                fk.act_out = kin;
+                MVEntry & fr = ff.e[1];
+                fr.W = L.ffn_r;
+                fr.epi = EPI_STORE;
+                src_lnmix(fr, x_, si, L.ln2_w, L.ln2_b, mur, form);
+                ff.wv = L.ffn_v;
+                ff.x = x_;
+                ff.kg = kgran_;
+                ff.rg = rgran_;
+                ff.tag = (unsigned)(l + 1) | ((unsigned)(cur_ + 1) << 16);
+                ff.err = herr_d_;
+                ff.spin_max = spin_max_;
+                if (ffn_fused_supported(ff, form, true)) {
+                    if (timing_) {
+                        kt_bytes_ = wbytes(L.ffn_k) + wbytes(L.ffn_r) + wbytes(L.ffn_v) + 5.0 * C * 4 + 2.0 * C * 4 +
+                                    (double)L.ffn_k.M / 32 * KG_STRIDE * 8 * 2 + 2.0 * C * 8 + C * 4.0;
+                        kt_flops_ = 2.0 * ((double)L.ffn_k.M * L.ffn_k.K + (double)L.ffn_r.M * L.ffn_r.K +
+                                           (double)L.ffn_v.M * L.ffn_v.K);
+                    }
+                    if (!launch_ffn_fused(stream_, ff, form, true)) return false;
+                    continue;
+                }
+            }
+            const bool sig = (fuse_ & FUSE_SIG) && L.ffn_r.type == L.ffn_k.type && mv_sigmul_supported(sv, sr);
             if (sig) {
                 ek.mu2 = mur;
                 ek.act2_out = sr.act;
@@ -1677,7 +1708,7 @@ bool Engine::run_tokens(const uint32_t * tokens, size_t T, bool want_logits) {
     if (!run_tokens_impl(tokens, T, want_logits)) {
         (void)hipStreamSynchronize(stream_);
         // the call's tagged Wo-input granules must not satisfy a replay of the same parity
-        (void)hipMemsetAsync(ygran_, 0, (size_t)m_->n_embed * 8, stream_);
+        (void)hipMemsetAsync(ygran_, 0, tgran_n_ * 8, stream_);
         (void)hipStreamSynchronize(stream_);
         cur_ = cur0;
         return false;
@@ -1703,6 +1734,7 @@ bool Engine::run_tokens_impl(const uint32_t * tokens, size_t T, bool want_logits
             HIP_OK(hipEventRecord(tok_event_, stream_));
         }
         const bool lg = last && want_logits;
+        last_decode_ = n == 1 && !generic_decode_;
         if (timing_) {
             // eager launches; a decode step's kernels each carry a dispatch-bound event pair
             // (RK_LAUNCH through g_klt), the sequence path's matmul groups an event pair around
@@ -1729,6 +1761,11 @@ bool Engine::run_tokens_impl(const uint32_t * tokens, size_t T, bool want_logits
         } else {
             if (!forward((int)n, dstate_[cur_], dstate_[cur_ ^ 1], lg)) return false;
         }
+        // The fused decode's Wo granules are tagged (layer, state parity) and never cleared by their
+        // readers.  A step that did not run the fused decode flips the parity without writing them,
+        // so the next decode would run at the parity of the decode before this step and could take
+        // a value that step left (one-layer engines: the same layer tag).  Clear them in stream order.
+        if (n > 1 || generic_decode_) HIP_OK(hipMemsetAsync(ygran_, 0, tgran_n_ * 8, stream_));
         // tokens buffer is reused by the next chunk: wait before overwriting the pinned copy
         if (!last) HIP_OK(hipStreamSynchronize(stream_));
         cur_ ^= 1;
@@ -1787,7 +1824,7 @@ bool Engine::handoff_check() {
     if (*(volatile unsigned *)herr_h_ == 0) return true;
     (void)hipStreamSynchronize(stream_);
     (void)hipMemsetAsync(hgran_, 0, hgran_n_ * 8, stream_);
-    (void)hipMemsetAsync(ygran_, 0, (size_t)m_->n_embed * 8, stream_);
+    (void)hipMemsetAsync(ygran_, 0, tgran_n_ * 8, stream_);
     (void)hipStreamSynchronize(stream_);
     *(volatile unsigned *)herr_h_ = 0;
     fprintf(stderr, "rwkv: in-launch hand-off timed out (k_v6_att_fused): the evaluation's results are invalid\n");
@@ -1800,11 +1837,19 @@ bool Engine::debug_set(const char * name, long long value) {
     if (n == "skip_granule") dbg_skip_gran_ = (int)value;
     else if (n == "spin_max") spin_max_ = value > 0 ? (unsigned)std::min<long long>(value, 0xffffffffLL) : (1u << 20);
     else if (n == "wkv_chunk") wkv_chunk_ = value != 0;
+    else if (n == "generic_decode") generic_decode_ = value != 0 || m_->n_embed > 4096;
+    else if (n == "graphs") use_graphs_ = value != 0;
+    else if (n == "decode_fusion") fuse_ = (unsigned)value & FUSE_ALL;
+    else if (n == "wo_rows" && (value == 4 || value == 8)) wo_rows_ = (int)value;
+    else if (n == "wo_prepoll") wo_prepoll_ = value != 0;
     else return false;
-    // the decode graphs captured the old values
+    // the decode graphs captured the old values; a decode program without the fused Wo flips the
+    // state parity without writing the Wo granules (see run_tokens_impl): clear them
     (void)hipStreamSynchronize(stream_);
     drop_graphs();
     drop_io_graphs();
+    (void)hipMemsetAsync(ygran_, 0, tgran_n_ * 8, stream_);
+    (void)hipStreamSynchronize(stream_);
     return true;
 }
 
@@ -1830,11 +1875,6 @@ static bool host_pinned(const void * p) {
 }
 
 bool Engine::pinned_io(const float * state_in, const float * state_out) {
-    static const int mode = [] {
-        const char * v = getenv("RWKV_MI355X_IO_ORDER");  // "interleaved" / "upfront" (A/B)
-        return !v ? 0 : (v[0] == 'i' ? 1 : v[0] == 'u' ? 2 : 0);
-    }();
-    if (mode) return mode == 2;
     return host_pinned(state_in) && host_pinned(state_out);
 }
 
@@ -1843,28 +1883,9 @@ bool Engine::eval_host_chunked(uint32_t token, const float * state_in, float * s
     const size_t C = m_->n_embed, per_layer = m_->major >= 5 ? C * (2 + (size_t)m_->S) : 5 * C;
     if (!ensure_workspace(1)) return false;
     if (!io_stream_[0]) {
-        // The host->device slices must not share a hardware queue with the compute stream (a
-        // rocprofv3 trace showed them on the same queue, each copy then waiting for the previous
-        // chunk's kernels): RWKV_MI355X_IO_PRIO=1 puts the copy streams on high-priority queues
-        const char * ip = getenv("RWKV_MI355X_IO_PRIO");
-        int plo = 0, phi = 0;
-        if (ip && ip[0] == '1' && hipDeviceGetStreamPriorityRange(&plo, &phi) == hipSuccess) {
-            HIP_OK(hipStreamCreateWithPriority(&io_stream_[0], hipStreamNonBlocking, phi));
-        } else {
-            HIP_OK(hipStreamCreateWithFlags(&io_stream_[0], hipStreamNonBlocking));
-        }
-        // The device->host slices run as the runtime's blit kernels (__amd_rocclr_copyBuffer) on
-        // compute units; RWKV_MI355X_IO_CUMASK=N confines their stream's queue to N compute units
-        // so they stop taking slots from the decode kernels (A/B; 0 = unmasked)
-        const char * cm = getenv("RWKV_MI355X_IO_CUMASK");
-        const int ncu = cm ? atoi(cm) : 0;
-        if (ncu > 0) {
-            uint32_t mask[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-            for (int i = 0; i < ncu && i < 256; i++) mask[i / 32] |= 1u << (i % 32);
-            HIP_OK(hipExtStreamCreateWithCUMask(&io_stream_[1], 8, mask));
-        } else {
-            HIP_OK(hipStreamCreateWithFlags(&io_stream_[1], hipStreamNonBlocking));
-        }
+        // copy streams (high-priority queues and CU-masked download queues measured no better)
+        HIP_OK(hipStreamCreateWithFlags(&io_stream_[0], hipStreamNonBlocking));
+        HIP_OK(hipStreamCreateWithFlags(&io_stream_[1], hipStreamNonBlocking));
         HIP_OK(hipEventCreateWithFlags(&io_entry_ev_, hipEventDisableTiming));
     }
     // the copy streams start behind everything already queued on stream_ (an earlier
@@ -1905,6 +1926,7 @@ bool Engine::eval_host_chunked(uint32_t token, const float * state_in, float * s
     hipEvent_t * in_ev = io_ev_.data(), * done_ev = io_ev_.data() + NC;
     size_t off, bytes;
     HIP_OK(hipStreamWriteValue32(stream_, dtokens_, token, 0));
+    last_decode_ = true;
     if (!state_in && !init_state(din)) return false;
     auto upload = [&](uint32_t c) -> bool {
         slice(c, off, bytes);
@@ -2045,6 +2067,9 @@ long long Engine::debug_copy(const char * name, void * out, size_t bytes) {
         {"fr", fr_}};
     for (const auto & p : fb)
         if (n == p.first) src = p.second, cap_bytes = cap * C * 4;
+    // the fused v7 decode (k_att7_lora) keeps w, a, g and the mixed v in LDS: those buffers hold
+    // another evaluation's values, so they are refused rather than returned stale
+    if (last_decode_ && v7_fused_lora_ && (n == "w" || n == "a" || n == "g" || n == "v")) return -1;
     if (n == "lora") src = lora_, cap_bytes = cap * kmax * 4;
     if (n == "bonus") src = bonus_, cap_bytes = cap * (size_t)std::max<int64_t>(1, m_->H) * 4;
     if (n == "logits") src = logits_, cap_bytes = (size_t)m_->n_vocab * 4;

@@ -156,7 +156,13 @@ class Engine : public KLaunchTimer {
     unsigned * herr_h_ = nullptr;  // hand-off timeout flag, host-mapped (herr_d_ = its device address)
     unsigned * herr_d_ = nullptr;
     unsigned long long * hgran_ = nullptr;  // in-launch hand-off granules (k_v6_att_fused)
-    unsigned long long * ygran_ = nullptr;  // head outputs -> fused Wo rows (tagged granules, [C])
+    // tagged granules (per layer and state parity, never cleared by their readers): ygran_ [C] head
+    // outputs -> fused Wo rows; kgran_ [KG_STRIDE F / 32] FFN key blocks and rgran_ [C] receptance
+    // rows -> fused FFN value rows.  One allocation of tgran_n_ granules, cleared as a whole.
+    unsigned long long * ygran_ = nullptr;
+    unsigned long long * kgran_ = nullptr;
+    unsigned long long * rgran_ = nullptr;
+    size_t tgran_n_ = 0;
     size_t hgran_n_ = 0;
     int dbg_skip_gran_ = -1;
     unsigned spin_max_ = 1u << 20;
@@ -168,11 +174,28 @@ class Engine : public KLaunchTimer {
     hipGraphExec_t graphs_[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // [cur][logits]
     bool use_graphs_ = true;
     bool split_maa_ = false;       // RWKV_MI355X_SPLIT_MAA=1: v6 decode W1 + mix as two launches
+    // Decode fusions (RWKV_MI355X_DECODE_FUSION, a mask read at init; rwkv_mi355x_debug_set
+    // "decode_fusion"): every fused launch has an unfused form of the same bits.
+    enum : unsigned {
+        FUSE_ATT6 = 1,   // k_v6_att_fused (r, k, v, g, decay-LoRA rows + per-head attention)
+        FUSE_WO6 = 2,    // + Wo in that launch
+        FUSE_ATT4 = 4,   // k_v4_att_fused (LN + r, k, v rows + WKV-4)
+        FUSE_WO4 = 8,    // + Wo in that launch
+        FUSE_ATT7 = 16,  // k_att7_lora (v7 LoRA second stages + attention)
+        FUSE_SIG = 32,   // k_mvsig (FFN value + receptance rows)
+        FUSE_FFN = 64,   // k_ffn_fused (the whole channel mix: key, receptance and value rows)
+        FUSE_ALL = 127,
+        // default: everything but the one-launch channel mix (measured slower: v6-1B6 708.9 vs
+        // 697.5 us/token, its 21 MB of weights streaming at once delay the key rows)
+        FUSE_DEFAULT = FUSE_ALL & ~FUSE_FFN,
+    };
+    unsigned fuse_ = FUSE_DEFAULT;
+    int wo_rows_ = 8;      // k_v6_att_fused: Wo rows per wave of a Wo workgroup (debug knob "wo_rows": 4 / 8)
+    int wo_prepoll_ = 1;   // k_v6_att_fused: one wave polls a granule per head before the gather ("wo_prepoll"; 0: 707.5 -> 708.9 us/token)
     bool generic_decode_ = false;  // RWKV_MI355X_GENERIC_DECODE=1: decode through the T>1 kernels
     hipEvent_t tok_event_ = nullptr;
-    bool v7_fork_ = false;             // RWKV_MI355X_V7_FORK=1 (v7 decode LoRA-in on side_)
-    hipStream_t side_ = nullptr;
-    hipEvent_t fork_ev_[2] = {nullptr, nullptr};
+    bool v7_fused_lora_ = false;  // the decode program runs k_att7_lora (w/a/g/v buffers not written)
+    bool last_decode_ = false;    // the last step ran the decode program (debug_copy)
     bool timing_ = false;
     struct Pending {
         int stat;

@@ -330,14 +330,10 @@ static bool launch_mm_small(hipStream_t st, MMGroup & g, int wtype) {
 }
 
 bool launch_mm_group(hipStream_t st, MMGroup & g, int wtype) {
-    static const bool small_on = [] {
-        const char * v = getenv("RWKV_MI355X_MM_SMALL");  // 0: small-K float matmuls on k_mm too
-        return !(v && v[0] == '0');
-    }();
     bool fmm = false;
     if (!launch_fmm_group(st, g, wtype, &fmm)) return false;
     if (fmm) return true;
-    if (small_on && launch_mm_small(st, g, wtype)) return true;
+    if (launch_mm_small(st, g, wtype)) return true;
     switch (wtype) {
         case W_F32: return launch_mm_wf<W_F32>(st, g);
         case W_F16: return launch_mm_wf<W_F16>(st, g);
@@ -421,13 +417,65 @@ __global__ __launch_bounds__(256) void k_embed_ln(const uint32_t * tokens, DMat 
     STAMP_END(5);
 }
 
+// Rows wider than EMB_NC chunks (n_embed > 4096, e.g. RWKV-4 14B at 5120): the same statistics
+// association (ln_stats_wave's chunk order, 4 chunks in flight) with the row re-read from HBM per
+// group of chunks, every wave on its own (no exchange), then wave w normalizes chunks w, w + 4, ...
+__device__ __forceinline__ void emb_load8(float (&v)[8], const DMat & emb, size_t tok, int k) {
+    const int C = emb.K;
+    if (emb.type == W_F16) {
+        const int4 raw = *(const int4 *)((const __half *)emb.qs + tok * C + min(k, C - 8));
+        const __half * h = (const __half *)&raw;
+#pragma unroll
+        for (int j = 0; j < 8; j++) v[j] = __half2float(h[j]);
+    } else {
+        ln_load8(v, (const float *)emb.qs + tok * C, k, C);
+    }
+}
+__global__ __launch_bounds__(256) void k_embed_ln_wide(const uint32_t * tokens, DMat emb, const float * w,
+                                                       const float * b, float * x) {
+    const int t = blockIdx.x, C = emb.K, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int nc = (C + LN_CHUNK - 1) / LN_CHUNK;
+    const size_t tok = tokens[t];
+    double s1 = 0.0, s2 = 0.0;
+    for (int c0 = 0; c0 < nc; c0 += 4) {
+        float v[4][8];
+#pragma unroll
+        for (int c = 0; c < 4; c++) emb_load8(v[c], emb, tok, min(c0 + c, nc - 1) * LN_CHUNK + lane * 8);
+        double c1[4], c2[4];
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            c1[c] = c2[c] = 0.0;
+            if (c0 + c < nc) ln_chunk_sums(v[c], (c0 + c) * LN_CHUNK + lane * 8 < C, c1[c], c2[c]);
+        }
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+            if (c0 + c < nc) s1 += c1[c], s2 += c2[c];
+    }
+    float mean, scale;
+    ln_finish(s1, s2, C, 1e-5f, mean, scale);
+    float * xr = x + (size_t)t * C;
+    for (int c = wave; c < nc; c += 4) {
+        const int k = c * LN_CHUNK + lane * 8;
+        if (k >= C) continue;
+        float v[8], wv[8], bv[8], o[8];
+        emb_load8(v, emb, tok, k);
+        ln_load8(wv, w, k, C);
+        ln_load8(bv, b, k, C);
+#pragma unroll
+        for (int j = 0; j < 8; j++) o[j] = ln_apply(v[j], mean, scale, wv[j], bv[j]);
+        *(float4 *)(xr + k) = make_float4(o[0], o[1], o[2], o[3]);
+        *(float4 *)(xr + k + 4) = make_float4(o[4], o[5], o[6], o[7]);
+    }
+}
+
 bool launch_embed_ln(hipStream_t st, const uint32_t * tokens, int T, const DMat & emb, const float * w,
                      const float * b, float * x) {
-    if (emb.K % 8 || emb.K > EMB_NC * LN_CHUNK || (emb.type != W_F16 && emb.type != W_F32)) {
+    if (emb.K % 8 || (emb.type != W_F16 && emb.type != W_F32)) {
         fprintf(stderr, "rwkv: embedding row of %d elements (type %d) unsupported\n", emb.K, emb.type);
         return false;
     }
-    RK_LAUNCH(k_embed_ln, dim3(T), dim3(256), 0, st, tokens, emb, w, b, x);
+    if (emb.K > EMB_NC * LN_CHUNK) RK_LAUNCH(k_embed_ln_wide, dim3(T), dim3(256), 0, st, tokens, emb, w, b, x);
+    else RK_LAUNCH(k_embed_ln, dim3(T), dim3(256), 0, st, tokens, emb, w, b, x);
     HIP_OK(hipGetLastError());
     return true;
 }
@@ -532,17 +580,12 @@ __global__ __launch_bounds__(1024) void k_ln_mix(LnMixArgs a) {
 }
 
 bool launch_ln_mix(hipStream_t st, const LnMixArgs & a) {
-    // long sequences: the channel blocks split over grid.y = ln_mix_y() (each workgroup computes
-    // its rows' LayerNorm statistics itself, so y > 1 repeats that work for a shorter store phase)
-    static const int ln_mix_y = [] {
-        const char * e = getenv("RWKV_MI355X_LNMIX_Y");
-        const int v = e ? atoi(e) : 1;
-        return v >= 1 && v <= 16 ? v : 1;
-    }();
+    // long sequences: one channel block row (grid.y = 1; each workgroup computes its rows' LayerNorm
+    // statistics itself, so splitting the channels repeats that work: y = 2 / 4 / 8 measured slower)
     // fewer token groups than ~2 per CU (short sequences, batched decode): the channel blocks over
     // grid.y until the grid holds about 512 workgroups
     const int tgs = (a.T + TOKS_PER_WG - 1) / TOKS_PER_WG, cbs = (a.C + 255) / 256;
-    const int gy = a.T <= 64 ? cbs : tgs < 256 ? std::min(cbs, (512 + tgs - 1) / tgs) : std::min(ln_mix_y, cbs);
+    const int gy = a.T <= 64 ? cbs : tgs < 256 ? std::min(cbs, (512 + tgs - 1) / tgs) : 1;
     const dim3 grid((a.T + TOKS_PER_WG - 1) / TOKS_PER_WG, gy), block(256 * TOKS_PER_WG);
     const int tq = tile_q(a.out, a.n_out, a.C);
     if (tq == 1) RK_LAUNCH(k_ln_mix<1>, grid, block, 0, st, a);
@@ -796,11 +839,7 @@ bool launch_v6_mix5(hipStream_t st, int T, int C, int D, const float * lora, con
         if (all) tq = outs[0].fmt == A_Q8_1 ? 2 : 1;
     }
     // the f32-MFMA form: tiled Q8 outputs, LoRA width 32 or 64, whole 32-channel blocks
-    static const bool mfma_on = [] {
-        const char * v = getenv("RWKV_MI355X_MIX5_MFMA");
-        return !(v && v[0] == '0');
-    }();
-    if (mfma_on && tq > 0 && (D == 32 || D == 64) && C % 32 == 0) {
+    if (tq > 0 && (D == 32 || D == 64) && C % 32 == 0) {
         const dim3 mgrid(C / 32, (T + 63) / 64);
         if (D == 32) {
             if (tq == 1) RK_LAUNCH((k_v6_mix5m<32, 1>), mgrid, dim3(320), 0, st, a);

@@ -235,18 +235,18 @@ struct Att6Fused {
     float * xres;                 // the residual stream x [C]
     unsigned long long * ygran;   // C granules
     unsigned ytag;
+    int wo_rows;                  // Wo rows per wave of a Wo workgroup: 4 or 8
+    int wo_prepoll;               // 1: one wave polls a granule per head before the gather
 };
 bool v6_att_fused_supported(const Att6Fused & a);
-bool v6_wo_fused_enabled();  // RWKV_MI355X_WO_FUSED=0 turns it off (default on)
 bool launch_v6_att_fused(hipStream_t st, const Att6Fused & a);
-// v4 decode: LN + token shift, r / k / v rows and WKV-4 in one launch, 32 channels per workgroup
-// (mv_att4f.hip); the two-launch k_mv + k_wkv4 pair gives the same bits
-// (channels per workgroup v4_att_fused_cpw(): 32 emits Wo's Q8 input, 8 / 16 write it as fp32 y)
-int v4_att_fused_cpw();
+// v4 decode: LN + token shift, r / k / v rows and WKV-4 in one launch, 8 channels per workgroup
+// (mv_att4f.hip); the two-launch k_mv + k_wkv4 pair gives the same bits.  Without wf, Wo's input
+// is written as fp32 y (Wo quantizes it in its prologue).
 bool v4_att_fused_supported(int C, const DMat & Wr, const DMat & Wk, const DMat & Wv, const ActBuf & out);
-// wf (default; RWKV_MI355X_WO4_FUSED=0 off; 8 channels per workgroup): Wo in the same launch -- every workgroup
-// publishes its channels' outputs as granules tagged ytag (per layer and state parity), gathers all
-// C of them, quantizes them as Wo's fp32-input prologue does and runs one Wo row per wave, x += Wo . y
+// wf: Wo in the same launch -- the producers publish their channels' outputs as granules tagged
+// ytag (per layer and state parity); Wo workgroups after them in the grid gather all C, quantize
+// them as Wo's fp32-input prologue does and run 2 Wo rows per wave, x += Wo . y
 struct V4WoFused {
     DMat wo;
     float * xres;
@@ -255,12 +255,31 @@ struct V4WoFused {
     unsigned * err;
     unsigned spin_max;
 };
-bool v4_wo_fused_enabled();
 bool launch_v4_att_fused(hipStream_t st, int C, const DMat & Wr, const DMat & Wk, const DMat & Wv, const float * x,
                          const float * carry, float * carry_out, const float * lnw, const float * lnb,
                          const float * mix_r, const float * mix_k, const float * mix_v, const float * first,
                          const float * decay, const float * sin, float * sout, const ActBuf & out, float * y,
                          const V4WoFused * wf = nullptr);
+
+// The decode channel mix in one launch (mv_ffnf.hpp): e[0] the FFN key (SRC_LNMIX, relu^2, emit = 1,
+// act_out's format = the value's input format), e[1] the receptance (SRC_LNMIX, EPI_STORE; hasr
+// only), wv the FFN value; x += sigmoid(r) * (Wv . relu^2(Wk . xk))  (v7: x += Wv . relu^2(...)).
+// kg: KG_STRIDE * F / 32 granules, rg: C granules, both tagged `tag` (unique per layer and state
+// parity; the engine clears them whenever the parity flips without a fused decode).
+constexpr int KG_STRIDE = 10;  // granules per published Q8 block: 8 q dwords, d, s (Q8_1's d * sum)
+struct FfnFused {
+    MVEntry e[2];
+    DMat wv;
+    float * x;
+    unsigned long long * kg;
+    unsigned long long * rg;
+    unsigned tag;
+    unsigned * err;
+    unsigned spin_max;
+    int np;  // producer workgroups (set by launch_ffn_fused)
+};
+bool ffn_fused_supported(const FfnFused & f, int form, bool hasr);
+bool launch_ffn_fused(hipStream_t st, FfnFused & f, int form, bool hasr);
 
 // Sequence v6 decay LoRA tail (T >= 2): w[t][c] = exp(-exp(Wd2[c] . Q8(dl[t]) + decay[c])) with
 // k_att6_dec's per-row arithmetic; dl fp32 [T][D].  Quantized Wd2 with D <= 512 only.

@@ -22,34 +22,18 @@ extern template bool launch_mv_shape<W_Q8_0>(hipStream_t, MVGroup &, int, int, i
 
 static int g_mv_cus = 256;
 
-// Rows per wave of k_mva (RWKV_MI355X_MVA_R = 2, 4 or 8; default 2).  More rows per wave put
-// more weight loads in flight per lane behind fewer workgroups; measured on the v6-1B6 decode
-// chain (128 tokens): 2 rows 853 us/token, 4 rows 883, 8 rows 876 -- the launch stays latency
-// bound and two rows keep the most waves issuing.
-int mva_rows() {
-    static const int v = [] {
-        const char * e = getenv("RWKV_MI355X_MVA_R");
-        const int r = e ? atoi(e) : 2;
-        return r == 4 || r == 8 ? r : 2;
-    }();
-    return v;
-}
+// Rows per wave of k_mva: 2.  More rows per wave put more weight loads in flight per lane behind
+// fewer workgroups; measured on the v6-1B6 decode chain (128 tokens): 2 rows 853 us/token, 4 rows
+// 883, 8 rows 876 -- the launch stays latency bound and two rows keep the most waves issuing.
+int mva_rows() { return 2; }
 extern int kQgCUs;
 void set_mv_device_cus(int n) {
     g_mv_cus = n > 0 ? n : 256;
     kQgCUs = g_mv_cus;
 }
 
-int mv_late_weights() {
-    static const int v = [] {
-        const char * e = getenv("RWKV_MI355X_LATE_W");  // default off: v6-1B6 678 vs 686 us/token, v7 1887 vs 1926
-        return e ? atoi(e) : 0;
-    }();
-    return v;
-}
-
 bool launch_mv_group(hipStream_t st, MVGroup & g) {
-    g.late = mv_late_weights();
+    g.late = 0;  // weight streams start with the image inputs (holding them: v6-1B6 686 vs 678 us/token)
     bool emit = false;
     for (int i = 0; i < g.n; i++) emit |= g.e[i].emit != 0;
     const int src = g.e[0].src, form = g.e[0].form;
@@ -79,10 +63,7 @@ bool launch_mv_group(hipStream_t st, MVGroup & g) {
     // LayerNorm-prologue groups (not emitting) with more than two workgroups per CU at 2 rows per
     // wave (v7 r,k,v: 960; v5 r,k,v,g: 2048) take 4 rows per wave: one round of workgroups fewer
     // (v7-2.9B decode 469 -> 490 tok/s alone, with U = 1 above 513; v5-7B 517 -> 573)
-    static const int ln_r4 = [] {
-        const char * e = getenv("RWKV_MI355X_LN_R4");  // default on (0: off, A/B)
-        return e ? atoi(e) : 1;
-    }();
+    constexpr int ln_r4 = 1;
     int rows2 = 0;
     for (int i = 0; i < g.n; i++) rows2 += (g.e[i].W.M + 7) / 8;
     const bool r4 = ln_r4 && prologue && !emit && srck == MVK_LN && (g.n > 1 || rows2 <= 8 * g_mv_cus) &&
@@ -90,10 +71,7 @@ bool launch_mv_group(hipStream_t st, MVGroup & g) {
     // ... and 8 rows per wave when even 4 leave more than four workgroups per CU (K > 2048, two units
     // per lane: v5-7B r,k,v,g, 1024 -> 512 workgroups; decode 1557 -> 1535 us/token, bit-exact; v7's
     // r,k,v at 480 workgroups measured neutral and stays at 4)
-    static const int ln_r8 = [] {
-        const char * e = getenv("RWKV_MI355X_LN_R8");  // default on (0: off, A/B)
-        return e ? atoi(e) : 1;
-    }();
+    constexpr int ln_r8 = 1;
     int lnk = 0;
     for (int i = 0; i < g.n; i++) lnk = std::max(lnk, g.e[i].W.K);
     const bool r8 = ln_r8 && r4 && lnk > 2048 && umax0 == 2 && rows2 > 4 * g_mv_cus;
@@ -158,23 +136,14 @@ bool launch_mv_group(hipStream_t st, MVGroup & g) {
     // emitting LayerNorm groups at U = 2 hold 16 weight units per wave (184 VGPRs: one workgroup
     // per CU); with more row blocks than CUs, U = 1 (two round trips, 122 VGPRs, two per CU):
     // v7-2.9B FFN key, 320 workgroups -- decode 469 -> 489 tok/s alone
-    static const int emit_u1 = [] {
-        const char * e = getenv("RWKV_MI355X_EMIT_U1");  // default on (0: off, A/B)
-        return e ? atoi(e) : 1;
-    }();
+    constexpr int emit_u1 = 1;
     if (emit_u1 && emit && U == 2 && blocks > g_mv_cus) U = 1;
     // activation-input rows of 5..8 quantized units per lane (v7-2.9B FFN value, K = 10240): all
     // units in one round of loads instead of 4 + the rest
-    static const int act_u8 = [] {
-        const char * e = getenv("RWKV_MI355X_ACT_U8");  // default on (0: off, A/B)
-        return e ? atoi(e) : 1;
-    }();
+    constexpr int act_u8 = 1;
     if (act_u8 && srck == MVK_ACT && !mva && umax > 4 && umax <= 8 && wfix >= 0 && wtype_quantized(wfix)) U = 8;
     // F16 LayerNorm groups of 5-8 units per lane (v7-2.9B LoRA first stages, K = 2560): one round
-    static const int f16_u8 = [] {
-        const char * e = getenv("RWKV_MI355X_F16_U8");  // A/B
-        return e ? atoi(e) : 1;
-    }();
+    constexpr int f16_u8 = 1;
     if (f16_u8 && srck == MVK_LN && !emit && wfix == W_F16 && R == 2 && umax > 4 && umax <= 8 && lnk > 2048) U = 8;
     bool ok = false;
     switch (wfix) {

@@ -10,6 +10,12 @@
 // arithmetic and emits the 32 outputs -- one quantization block of Wo's input -- with no
 // hand-off between workgroups at all.  Small models are launch-bound (v4-169M: 12 layers at
 // C = 768), so this removes one dependent launch per layer.
+//
+// Fused Wo (WO): the channel outputs y are published as tagged granules and Wo's rows run in the
+// same launch, on workgroups placed AFTER every producer in the grid ([0, C/8) produce, [C/8,
+// C/8 + C/16) gather y and run 16 Wo rows each).  Producers never wait, so a waiting workgroup
+// only ever waits on lower-index workgroups, which are dispatched first: the launch drains however
+// few of its workgroups are resident (several contexts decoding on one GPU at once).
 #include "mv_common.hpp"
 
 #include <stdlib.h>
@@ -31,8 +37,9 @@ struct Att4Fused {
     ActBuf out;                 // Wo's input (CPW = 32: emitted as Q8 blocks)
     float * y;                  // Wo's input as fp32 (CPW < 32: Wo quantizes it in its prologue)
     int img;                    // LDS bytes per activation image (16-aligned)
-    // Wo fused (WO): every workgroup publishes its channels' outputs as tagged granules, then
-    // gathers all C, quantizes them (the Wo prologue's arithmetic) and runs one Wo row per wave
+    // Wo fused (WO): the producers publish their channels' outputs as tagged granules; the Wo
+    // workgroups after them gather all C, quantize them (the Wo prologue's arithmetic) and run
+    // A4_WOR Wo rows per wave
     DMat wo;
     float * xres;
     unsigned long long * ygran;
@@ -49,6 +56,7 @@ typedef __attribute__((address_space(1))) unsigned a4_gu32_t;
 // quantization); every wave dots rows R w .. R w + R - 1 (R = CPW / 8) of each matrix within the
 // workgroup's channels; wave 0 (CPW lanes) runs the recurrence.  CPW = 32 emits Wo's input as one
 // Q8 block; smaller CPW (more workgroups streaming the rows) write it as fp32.
+constexpr int A4_WOR = 2;  // Wo rows per wave of a Wo workgroup (8 waves: 16 rows)
 template <int WF, int U, int CPW, bool WO = false>
 __global__ __launch_bounds__(512) void k_v4_att_fused(Att4Fused a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -56,6 +64,51 @@ __global__ __launch_bounds__(512) void k_v4_att_fused(Att4Fused a) {
     constexpr int R = CPW / 8, LCW = 1;
     const int C = a.C, K = C, c0 = blockIdx.x * CPW;
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    constexpr bool one = WF == W_Q4_1 || WF == W_Q5_1;
+    const int units = mv_units(WF, K);
+    if constexpr (WO) {
+        if ((int)blockIdx.x >= C / CPW) {
+            // ---- a Wo workgroup (rwkv_graph.inc:171-175, x += Wo . y): A4_WOR rows per wave,
+            // their first U units loaded now; every wave gathers y once the producers publish it
+            STAMP_BEGIN();
+            const int row0 = (((int)blockIdx.x - C / CPW) * 8 + wave) * A4_WOR;
+            WBlk wo[A4_WOR][U];
+#pragma unroll
+            for (int u = 0; u < U; u++)
+#pragma unroll
+                for (int r = 0; r < A4_WOR; r++) wo[r][u] = load_unit<WF>(a.wo, min(row0 + r, C - 1), u, lane);
+            const float xr = a.xres[min(row0 + min(lane, A4_WOR - 1), C - 1)];
+            const ActBuf xq = lds_act(smem, act_fmt_for(WF), K);
+            gran_gather_image<WF>(a.ygran, a.ytag, C, xq, wave, 8, a.err, a.spin_max, lane);
+            __syncthreads();
+            float acc[A4_WOR], acc2[A4_WOR];
+#pragma unroll
+            for (int r = 0; r < A4_WOR; r++) acc[r] = acc2[r] = 0.0f;
+            for (int u0 = 0; u0 < units; u0 += U) {
+                if (u0 > 0) {
+#pragma unroll
+                    for (int u = 0; u < U; u++)
+#pragma unroll
+                        for (int r = 0; r < A4_WOR; r++) wo[r][u] = load_unit<WF>(a.wo, min(row0 + r, C - 1), u0 + u, lane);
+                }
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    const AUnit xu = load_act_unit<WF, true>(xq, u0 + u, lane);
+                    if (unit_valid<WF>(K, u0 + u, lane)) {
+#pragma unroll
+                        for (int r = 0; r < A4_WOR; r++) dot_unit<WF>(wo[r][u], xu, acc[r], acc2[r]);
+                    }
+                }
+            }
+            float s[A4_WOR];
+#pragma unroll
+            for (int r = 0; r < A4_WOR; r++) s[r] = one ? wave_sum63(acc[r]) + wave_sum63(acc2[r]) : wave_sum63(acc[r]) + 0.0f;
+            const float v = lane_row_sum<A4_WOR>(s, lane);
+            if (lane < A4_WOR && row0 + lane < C) a.xres[row0 + lane] = xr + v;  // EPI_ADD
+            STAMP_END_NS(8);
+            return;
+        }
+    }
     const bool pro = wave >= 4;
     const int pw = wave - 4, nch = (K + LN_CHUNK - 1) / LN_CHUNK;
     STAMP_BEGIN();
@@ -88,15 +141,6 @@ __global__ __launch_bounds__(512) void k_v4_att_fused(Att4Fused a) {
         for (int u = 0; u < U; u++)
 #pragma unroll
             for (int r = 0; r < R; r++) w[m][r][u] = load_unit<WF>(a.W[m], min(c0 + R * wave + r, C - 1), u, lane);
-    // WO: this wave's Wo row (row blockIdx.x * 8 + wave: one per wave at CPW = 8) and its x
-    WBlk wo[U];
-    float xr = 0.0f;
-    const int worow = (int)blockIdx.x * 8 + wave;
-    if constexpr (WO) {
-#pragma unroll
-        for (int u = 0; u < U; u++) wo[u] = load_unit<WF>(a.wo, min(worow, C - 1), u, lane);
-        xr = a.xres[min(worow, C - 1)];
-    }
     // the recurrence's operands (wave 0, lane = channel)
     float aa = 0.0f, bb = 0.0f, pp = 0.0f, fi = 0.0f, de = 0.0f;
     if (wave == 0 && lane < CPW) {
@@ -141,8 +185,6 @@ __global__ __launch_bounds__(512) void k_v4_att_fused(Att4Fused a) {
     }
     __syncthreads();  // (1) images ready
     if (wave == 0) STAMP_MID();
-    const int units = mv_units(WF, K);
-    constexpr bool one = WF == W_Q4_1 || WF == W_Q5_1;
 #pragma unroll
     for (int m = 0; m < 3; m++) {
         float acc[R], acc2[R];
@@ -205,85 +247,14 @@ __global__ __launch_bounds__(512) void k_v4_att_fused(Att4Fused a) {
             }
         }
     }
-    if constexpr (WO) {
-        // Every workgroup's outputs: wave 0 polls the last granule of each workgroup (lanes over
-        // the C / 8 producers), the other waves park at the barrier.  Every producer published
-        // before waiting, and all C / 8 workgroups are resident at once, so the wait ends.
-        const int nwg = C / CPW;
-        if (wave == 0) {
-            for (unsigned it = 0;; it++) {
-                bool ok = true;
-                for (int j = lane; j < nwg; j += 64) {
-                    const unsigned long long x = __hip_atomic_load((a4_gu64_t *)(a.ygran + (size_t)j * CPW + CPW - 1),
-                                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    ok = ok && (unsigned)(x >> 32) == a.ytag;
-                }
-                if (__all(ok)) break;
-                if (it >= a.spin_max) {
-                    __hip_atomic_store((a4_gu32_t *)a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(4);
-            }
-        }
-        __syncthreads();
-        // gather y (8 channels per lane, tags checked) and quantize it as Wo's SRC_F32 prologue does
-        const ActBuf xq = lds_act(smem, act_fmt_for(WF), K);
-        for (int ck = wave; ck * LN_CHUNK < C; ck += 8) {
-            const int k0 = ck * LN_CHUNK + lane * 8;
-            const bool valid = k0 < C;
-            const unsigned long long * g = a.ygran + max(min(k0, C - 8), 0);
-            ChunkIn cy;
-            for (unsigned it = 0;; it++) {
-                bool ok = true;
-#pragma unroll
-                for (int j = 0; j < 8; j++) {
-                    const unsigned long long x = __hip_atomic_load((a4_gu64_t *)(g + j), __ATOMIC_RELAXED,
-                                                                   __HIP_MEMORY_SCOPE_AGENT);
-                    cy.x[j] = __uint_as_float((unsigned)x);
-                    ok = ok && (unsigned)(x >> 32) == a.ytag;
-                }
-                if (__all(ok || !valid)) break;
-                if (it >= a.spin_max) {
-                    __hip_atomic_store((a4_gu32_t *)a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(2);
-            }
-            chunk_store<WF, MVK_F32, 0>(E, xq, cy, 0.0f, 1.0f, false, k0, valid, lane);
-        }
-        __syncthreads();
-        float acc = 0.0f, acc2 = 0.0f;
-        for (int u0 = 0; u0 < units; u0 += U) {
-            if (u0 > 0) {
-#pragma unroll
-                for (int u = 0; u < U; u++) wo[u] = load_unit<WF>(a.wo, min(worow, C - 1), u0 + u, lane);
-            }
-#pragma unroll
-            for (int u = 0; u < U; u++) {
-                const AUnit xu = load_act_unit<WF, true>(xq, u0 + u, lane);
-                if (unit_valid<WF>(K, u0 + u, lane)) dot_unit<WF>(wo[u], xu, acc, acc2);
-            }
-        }
-        const float sw_ = one ? wave_sum63(acc) + wave_sum63(acc2) : wave_sum63(acc) + 0.0f;
-        if (lane == 63 && worow < C) a.xres[worow] = xr + sw_;  // EPI_ADD (the sum is valid in lane 63)
-    }
     STAMP_END(8);
 }
 
-// channels per workgroup: RWKV_MI355X_ATT4_FUSED = 32 / 16 / 8, 0 = the two-launch form
-int v4_att_fused_cpw() {
-    static const int v = [] {
-        const char * e = getenv("RWKV_MI355X_ATT4_FUSED");
-        const int c = e ? atoi(e) : 8;
-        return c == 32 || c == 16 || c == 8 ? c : 0;
-    }();
-    return v;
-}
-
+// 8 channels per workgroup (96 workgroups for C = 768: 16 / 32 channels, fewer and longer-streaming
+// workgroups, measured 269.6 / 285.1 against 256.6 us per v4-169M token)
 bool v4_att_fused_supported(int C, const DMat & Wr, const DMat & Wk, const DMat & Wv, const ActBuf & out) {
-    const int cpw = v4_att_fused_cpw();
-    if (!cpw || C % 32 || C > 2048 || (cpw == 32 && (out.fmt < 0 || out.tiled))) return false;
+    (void)out;
+    if (C % 32 || C > 2048) return false;
     const int t = Wr.type;
     if (t < 0 || Wk.type != t || Wv.type != t || mv_units(t, C) > 2) return false;
     for (const DMat * W : {&Wr, &Wk, &Wv})
@@ -291,32 +262,18 @@ bool v4_att_fused_supported(int C, const DMat & Wr, const DMat & Wk, const DMat 
     return true;
 }
 
-template <int WF, int CPW>
-static void launch_att4_c(hipStream_t st, const Att4Fused & a, int units) {
-    const int lds = 3 * a.img;
-    if (units <= 1) RK_LAUNCH((k_v4_att_fused<WF, 1, CPW>), dim3(a.C / CPW), dim3(512), lds, st, a);
-    else RK_LAUNCH((k_v4_att_fused<WF, 2, CPW>), dim3(a.C / CPW), dim3(512), lds, st, a);
-}
 template <int WF>
 static void launch_att4_t(hipStream_t st, const Att4Fused & a, int units) {
-    const int cpw = v4_att_fused_cpw();
+    const int lds = 3 * a.img;
     if (a.wo.qs) {
-        const int lds = 3 * a.img;
-        if (units <= 1) RK_LAUNCH((k_v4_att_fused<WF, 1, 8, true>), dim3(a.C / 8), dim3(512), lds, st, a);
-        else RK_LAUNCH((k_v4_att_fused<WF, 2, 8, true>), dim3(a.C / 8), dim3(512), lds, st, a);
+        // the producers, then the Wo workgroups (16 rows each)
+        const dim3 grid(a.C / 8 + (a.C + 8 * A4_WOR - 1) / (8 * A4_WOR));
+        if (units <= 1) RK_LAUNCH((k_v4_att_fused<WF, 1, 8, true>), grid, dim3(512), lds, st, a);
+        else RK_LAUNCH((k_v4_att_fused<WF, 2, 8, true>), grid, dim3(512), lds, st, a);
         return;
     }
-    if (cpw == 32) launch_att4_c<WF, 32>(st, a, units);
-    else if (cpw == 16) launch_att4_c<WF, 16>(st, a, units);
-    else launch_att4_c<WF, 8>(st, a, units);
-}
-
-bool v4_wo_fused_enabled() {
-    static const bool on = [] {
-        const char * v = getenv("RWKV_MI355X_WO4_FUSED");  // 0: Wo as its own launch (A/B)
-        return !(v && v[0] == '0');
-    }();
-    return on && v4_att_fused_cpw() == 8;
+    if (units <= 1) RK_LAUNCH((k_v4_att_fused<WF, 1, 8>), dim3(a.C / 8), dim3(512), lds, st, a);
+    else RK_LAUNCH((k_v4_att_fused<WF, 2, 8>), dim3(a.C / 8), dim3(512), lds, st, a);
 }
 
 bool launch_v4_att_fused(hipStream_t st, int C, const DMat & Wr, const DMat & Wk, const DMat & Wv, const float * x,
@@ -324,7 +281,7 @@ bool launch_v4_att_fused(hipStream_t st, int C, const DMat & Wr, const DMat & Wk
                          const float * mix_r, const float * mix_k, const float * mix_v, const float * first,
                          const float * decay, const float * sin, float * sout, const ActBuf & out, float * y,
                          const V4WoFused * wf) {
-    if (wf && (!v4_wo_fused_enabled() || wf->wo.type != Wr.type || wf->wo.M != C || wf->wo.K != C || C % 8)) {
+    if (wf && (wf->wo.type != Wr.type || wf->wo.M != C || wf->wo.K != C || C % 8)) {
         fprintf(stderr, "rwkv: fused v4 attention + Wo decode: unsupported shape (C %d)\n", C);
         return false;
     }

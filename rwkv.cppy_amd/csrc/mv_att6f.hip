@@ -6,16 +6,24 @@
 // own 64 channels of r, k, v, g -- plus the D decay-LoRA values every head shares).  Here the
 // grid is 8 workgroups per head: workgroup (h, s) computes 32 of head h's 256 r/k/v/g rows (4
 // waves x 8 rows, exactly k_mva's lane/unit order, wave_sum63 tree and epilogues, so the values
-// are bit-identical) and, on a fifth wave, the decay-LoRA rows of its slot (non-reducers first).
-// Every row is published as a granule (value + tag in one 8-byte write-through store, below); a
-// decay-LoRA value once per head, so each head owns its copy.  Workgroup (h, 0) -- which loaded
-// the head's state, decay-tail weights and per-channel operands while its own rows streamed --
-// sweeps its head's granules and runs k_att6_dec's arithmetic (decay tail, wkv6, GroupNorm, gate,
-// Q8 emission of Wo's input).  The waiting workgroups are producers first, so the wait can never
-// hold a slot a producer needs; every spin is bounded: a timeout sets *err (a host-mapped word) and
-// the engine fails the evaluation that synchronises next, then clears every granule (a late
-// producer may have left one tagged) -- never a hang, never a silently wrong result.  Each granule has exactly one reader, which clears it right after
-// reading: no counters, no atomics, and a replayed graph needs no memset node.
+// are bit-identical) and, on a fifth wave, the decay-LoRA rows of its slot.  Every row is
+// published as a granule (value + tag in one 8-byte write-through store, below); a decay-LoRA
+// value once per head, so each head owns its copy.  The head's reducer -- which loads the head's
+// state, decay-tail weights and per-channel operands at kernel start -- sweeps its head's granules
+// and runs k_att6_dec's arithmetic (decay tail, wkv6, GroupNorm, gate, Q8 emission of Wo's
+// input).  Each granule has exactly one reader, which clears it right after reading: no
+// counters, no atomics, and a replayed graph needs no memset node.
+//
+// Progress without co-residency.  The grid is ordered so that every waiting workgroup waits only
+// on workgroups of LOWER index: [0, 8H) the producers -- workgroup b is (h = b % H, s = b / H) and
+// owns decay-LoRA slots b, b + 8H, ... --, [8H, 9H) the reducers (no rows of their own: a reducer
+// dispatched last must not hold back its head's rows), [9H, 9H + C / (4 WOR)) the Wo workgroups
+// (fused Wo: each gathers every head's outputs and runs 4 WOR rows of Wo).  Producers
+// never wait, so however few workgroups are resident (several contexts decoding on one GPU at
+// once), the lowest-index waiting workgroup's producers have all been dispatched: the launch
+// drains.  Every spin is also bounded: a timeout sets *err (a host-mapped word) and the engine
+// fails the evaluation that synchronises next, then clears every granule (a late producer may
+// have left one tagged) -- never a hang, never a silently wrong result.
 //
 // The state update uses 16-byte accesses: wave g owns keys 16g..16g+15, lane (kk, jq) keys
 // 16g + 4kk + q (q < 4) of value columns 4jq..4jq+3.  Each output column's sum keeps
@@ -50,7 +58,6 @@ __device__ __forceinline__ unsigned addu(unsigned * p, unsigned v) {
 
 constexpr int AF_P = 8;   // workgroups per head
 constexpr int AF_R = 8;   // rows per wave (4 waves x 8 rows x 8 workgroups = 4 x 64 rows)
-__device__ __forceinline__ int af_slot(int sidx, int h, int H) { return sidx > 0 ? (sidx - 1) * H + h : (AF_P - 1) * H + h; }
 
 // R rows of one matrix by one wave: k_mva's loads, dots, tree and epilogue (lane r: row r)
 template <int WF, int R, int U>
@@ -135,17 +142,54 @@ __device__ __forceinline__ void gran_sweep(const unsigned long long * g, int str
     }
 }
 
-constexpr int AF_WOR = 3;  // Wo rows per non-reducer wave: ceil(C / (28 H)) with C = 64 H
 
-template <int WF, int U, int WD, bool WO>
+// WOR: Wo rows per wave of a Wo workgroup (4 waves: 4 WOR rows); 0 = no Wo in this launch
+template <int WF, int U, int WD, int WOR>
 __global__ __launch_bounds__(320) void k_v6_att_fused(Att6Fused a) {
+    constexpr bool WO = WOR > 0;
     extern __shared__ __attribute__((aligned(16))) char smem[];  // Q8 image of dl (decay tail input)
     __shared__ __attribute__((aligned(16))) float sr[64], sk[64], sv[64], sg[64], sw[64], su[64];
     __shared__ __attribute__((aligned(16))) float part[16][64];
     constexpr int S = 64;
-    const int wg = (int)blockIdx.x, h = wg / AF_P, sidx = wg % AF_P, H = a.H, C = a.C, D = a.D;
+    const int wg = (int)blockIdx.x, H = a.H, C = a.C, D = a.D;
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform branches
-    const bool red = sidx == 0;
+    const int NP = AF_P * H;  // producer workgroups; then H reducers, then the Wo workgroups
+    if constexpr (WO) {
+        if (wg >= NP + H) {
+            // ---- a Wo workgroup (rwkv_graph.inc:382-384, x += Wo . y): waves 0..3 own WOR rows each,
+            // loaded now; all 5 waves gather y when the reducers publish it (wo_prepoll: after wave 0
+            // has seen one granule per head -- each head's 64 outputs are one store instruction)
+            STAMP_BEGIN();
+            constexpr int AF_WOR = WOR > 0 ? WOR : 1;
+            const int row0 = ((wg - NP - H) * 4 + min(wave, 3)) * AF_WOR;
+            WBlk wo[AF_WOR][U];
+            float xr = 0.0f;
+            if (wave < 4) {
+#pragma unroll
+                for (int u = 0; u < U; u++)
+#pragma unroll
+                    for (int r = 0; r < AF_WOR; r++) wo[r][u] = load_unit<WF>(a.wo, min(row0 + r, C - 1), u, lane);
+                xr = a.xres[min(row0 + min(lane, AF_WOR - 1), C - 1)];
+            }
+            const ActBuf xq = lds_act(smem, act_fmt_for(WF), C);
+            if (a.wo_prepoll) {
+                if (wave == 0) gran_prepoll(a.ygran, H, S, S - 1, a.ytag, a.err, a.spin_max, lane);
+                __syncthreads();
+            }
+            gran_gather_image<WF>(a.ygran, a.ytag, C, xq, wave, 5, a.err, a.spin_max, lane);
+            __syncthreads();
+            if (wave < 4) {
+                const float s = rows_dot_img<WF, AF_WOR, U>(wo, xq, C, lane);
+                if (lane < AF_WOR && row0 + lane < C) a.xres[row0 + lane] = xr + s;  // EPI_ADD
+            }
+            STAMP_END_NS(6);
+            return;
+        }
+    }
+    // [0, 8H): producers (h = b % H, s = b / H; decay-LoRA slots b, b + 8H, ...); [8H, 9H): the
+    // reducers, which produce nothing themselves
+    const bool red = wg >= NP;
+    const int h = red ? wg - NP : wg % H, sidx = red ? 0 : wg / H;
     const int c0 = h * S;
     const Att6Dec & at = a.att;
     const size_t hb = (size_t)h * S * S;
@@ -185,108 +229,23 @@ __global__ __launch_bounds__(320) void k_v6_att_fused(Att6Fused a) {
             for (int l = 0; l < 4; l++) wp[l] = load_wblk<WD>(at.wd2, (size_t)(c0 + lane) * nb + min(l, nb - 1));
         }
     }
-    // ---- this workgroup's rows, each published as a granule: wave w -> matrix (4 s + w) / 8
-    // (r, k, v, g), rows of head h; wave 4 -> decay LoRA rows (EPI_TANH) of its slot, the
-    // non-reducer workgroups' slots first (slot = (s - 1) H + h for s > 0, 7H + h for the reducers)
-    if (wave < 4) {
+    // ---- a producer's rows, each published as a granule: wave w -> matrix (4 s + w) / 8 (r, k, v,
+    // g), rows of head h; wave 4 -> decay LoRA rows (EPI_TANH) of its slots wg, wg + 8H, ...
+    if (red) {
+    } else if (wave < 4) {
         const int wh = sidx * 4 + wave, m = wh >> 3, row0 = c0 + (wh & 7) * AF_R;
         const DMat W = m == 0 ? a.W[0] : m == 1 ? a.W[1] : m == 2 ? a.W[2] : a.W[3];
         const ActBuf x = m == 0 ? a.x[0] : m == 1 ? a.x[1] : m == 2 ? a.x[2] : a.x[3];
         const float v = af_rows<WF, AF_R, U>(W, x, row0, m == 3 ? EPI_SILU : EPI_STORE, lane);
         if (lane < AF_R && publish) gran_put(a.gran + (size_t)m * C + row0 + lane, v);
     } else {
-        for (int d = af_slot(sidx, h, H); d < D; d += AF_P * H) {
+        for (int d = wg; d < D; d += NP) {
             const float v = af_rows<WF, 1, U>(a.wd1, a.xw, d, EPI_TANH, lane);  // in lane 0
             const float v0 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
             if (lane < H && publish) gran_put(gdl + (size_t)lane * D + d, v0);  // one copy per head
         }
     }
     if (!red) {
-        if constexpr (WO) {
-            // ---- Wo (rwkv_graph.inc:382-384, x += Wo . y) on the 7 H non-reducer workgroups: wave
-            // gw owns rows gw, gw + 28 H, gw + 56 H (k_mva's per-row arithmetic does not depend on
-            // which wave computes a row).  Its units are loaded now, under the reducers' attention.
-            const int nwo = 28 * H, gw = ((sidx - 1) * H + h) * 4 + wave;
-            WBlk wo[AF_WOR][U];
-            float xr = 0.0f;
-            if (wave < 4) {
-#pragma unroll
-                for (int u = 0; u < U; u++)
-#pragma unroll
-                    for (int j = 0; j < AF_WOR; j++) wo[j][u] = load_unit<WF>(a.wo, min(gw + nwo * j, C - 1), u, lane);
-                xr = a.xres[min(gw + nwo * min(lane, AF_WOR - 1), C - 1)];
-            }
-            // Wait for every head: wave 0 polls ONE granule per head (its last channel, lane h)
-            // with a sleep between polls -- the other waves park at the barrier, so the 7 H waiting
-            // workgroups add little L2 traffic beside the reducers' own sweeps
-            if (wave == 0) {
-                for (unsigned it = 0;; it++) {
-                    const unsigned long long x = lane < H ? gran_get(a.ygran + (size_t)lane * S + S - 1)
-                                                          : ((unsigned long long)a.ytag << 32);
-                    if (__all((unsigned)(x >> 32) == a.ytag)) break;
-                    if (it >= spin_max) {
-                        __hip_atomic_store((gunsigned_t *)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(4);
-                }
-            }
-            __syncthreads();
-            // y: 512-element chunks, 8 consecutive channels per lane (a quad = one 32-block), each
-            // granule's tag checked; then the matvec prologue's Q8 quantization into LDS
-            const ActBuf xq = lds_act(smem, act_fmt_for(WF), C);
-            MVEntry dummy{};
-            for (int ck = wave; ck * 512 < C; ck += 5) {
-                const int k0 = ck * 512 + lane * 8;
-                const bool valid = k0 < C;
-                const unsigned long long * g = a.ygran + min(k0, C - 8);
-                ChunkIn ci;
-                for (unsigned it = 0;; it++) {
-                    unsigned long long x[8];
-#pragma unroll
-                    for (int j = 0; j < 8; j++) x[j] = gran_get(g + j);
-                    bool ok = true;
-#pragma unroll
-                    for (int j = 0; j < 8; j++) {
-                        ci.x[j] = __uint_as_float((unsigned)x[j]);
-                        ok = ok && (unsigned)(x[j] >> 32) == a.ytag;
-                    }
-                    if (__all(ok || !valid)) break;
-                    if (it >= spin_max) {
-                        __hip_atomic_store((gunsigned_t *)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(2);
-                }
-                chunk_store<WF, MVK_F32, 0>(dummy, xq, ci, 0.0f, 1.0f, false, k0, valid, lane);
-            }
-            __syncthreads();
-            if (wave < 4) {
-                float acc[AF_WOR], acc2[AF_WOR];
-#pragma unroll
-                for (int j = 0; j < AF_WOR; j++) acc[j] = acc2[j] = 0.0f;
-#pragma unroll
-                for (int u = 0; u < U; u++) {
-                    const AUnit xu = load_act_unit<WF, true>(xq, u, lane);
-                    const bool uv = unit_valid<WF>(C, u, lane);
-#pragma unroll
-                    for (int j = 0; j < AF_WOR; j++) {
-                        float t = acc[j], t2 = acc2[j];
-                        dot_unit<WF>(wo[j][u], xu, t, t2);
-                        acc[j] = uv ? t : acc[j];
-                        acc2[j] = uv ? t2 : acc2[j];
-                    }
-                }
-                constexpr bool one = WF == W_Q4_1 || WF == W_Q5_1;
-                float sr_[AF_WOR];
-#pragma unroll
-                for (int j = 0; j < AF_WOR; j++)
-                    sr_[j] = one ? wave_sum63(acc[j]) + wave_sum63(acc2[j]) : wave_sum63(acc[j]) + 0.0f;
-                const float s = lane_row_sum<AF_WOR>(sr_, lane);
-                const int row = gw + nwo * lane;
-                if (lane < AF_WOR && row < C) a.xres[row] = xr + s;  // EPI_ADD
-            }
-        }
         STAMP_END_NS(6);
         return;
     }
@@ -374,11 +333,7 @@ __global__ __launch_bounds__(320) void k_v6_att_fused(Att6Fused a) {
 }
 
 bool v6_att_fused_supported(const Att6Fused & a) {
-    static const bool on = [] {
-        const char * v = getenv("RWKV_MI355X_ATT_FUSED");  // 0: the two-launch form (A/B)
-        return !(v && v[0] == '0');
-    }();
-    if (!on || a.att.S != 64 || a.C != a.H * 64 || a.att.w || a.att.yq.fmt < 0 || a.att.yq.tiled) return false;
+    if (a.att.S != 64 || a.C != a.H * 64 || a.att.w || a.att.yq.fmt < 0 || a.att.yq.tiled) return false;
     if (!a.gran) return false;
     const int t = a.W[0].type;
     if (!wtype_quantized(t) || a.wd1.type != t || mv_units(t, a.C) > 2) return false;
@@ -391,23 +346,15 @@ bool v6_att_fused_supported(const Att6Fused & a) {
     if (a.D % 32 || a.D > 128) return false;  // two granules per lane of the sweeping wave
     if (a.wo.qs) {
         // Wo fused: C x C of the same type, rows spread over the 28 H non-reducer waves
-        if (a.wo.type != t || a.wo.M != a.C || a.wo.K != a.C || !a.xres || !a.ygran || a.C % 512) return false;
-        if ((a.C + 28 * a.H - 1) / (28 * a.H) > AF_WOR) return false;
+        if (a.wo.type != t || a.wo.M != a.C || a.wo.K != a.C || !a.xres || !a.ygran || a.C % 32) return false;
+        if (a.wo_rows != 4 && a.wo_rows != 8) return false;
     }
     return a.H <= 64 && a.err;  // one decay-value copy per head: a lane per head
 }
 
-bool v6_wo_fused_enabled() {
-    static const bool on = [] {
-        const char * v = getenv("RWKV_MI355X_WO_FUSED");  // 0: Wo as its own k_mva launch (A/B)
-        return !(v && v[0] == '0');
-    }();
-    return on;
-}
-
-template <int WF, int U, bool WO>
+template <int WF, int U, int WO>
 static void launch_af_wd(hipStream_t st, const Att6Fused & a, int lds) {
-    const dim3 grid(AF_P * a.H), block(320);
+    const dim3 grid(AF_P * a.H + a.H + (WO ? a.C / (4 * WO) : 0)), block(320);
     switch (a.att.wd2.type) {
         case W_Q4_0: RK_LAUNCH((k_v6_att_fused<WF, U, W_Q4_0, WO>), grid, block, lds, st, a); break;
         case W_Q4_1: RK_LAUNCH((k_v6_att_fused<WF, U, W_Q4_1, WO>), grid, block, lds, st, a); break;
@@ -426,12 +373,15 @@ bool launch_v6_att_fused(hipStream_t st, const Att6Fused & a) {
     int lds = lds_bytes_for(act_fmt_for(a.att.wd2.type), a.D);
     if (wo) lds = std::max(lds, lds_bytes_for(act_fmt_for(a.W[0].type), a.C));
     const bool u1 = mv_units(a.W[0].type, a.C) <= 1;
+    const bool r4 = a.wo_rows == 4;
 #define AF_T(WFv)                                                  \
     do {                                                           \
-        if (wo && u1) launch_af_wd<WFv, 1, true>(st, a, lds);      \
-        else if (wo) launch_af_wd<WFv, 2, true>(st, a, lds);       \
-        else if (u1) launch_af_wd<WFv, 1, false>(st, a, lds);      \
-        else launch_af_wd<WFv, 2, false>(st, a, lds);              \
+        if (wo && u1 && r4) launch_af_wd<WFv, 1, 4>(st, a, lds);   \
+        else if (wo && u1) launch_af_wd<WFv, 1, 8>(st, a, lds);    \
+        else if (wo && r4) launch_af_wd<WFv, 2, 4>(st, a, lds);    \
+        else if (wo) launch_af_wd<WFv, 2, 8>(st, a, lds);          \
+        else if (u1) launch_af_wd<WFv, 1, 0>(st, a, lds);          \
+        else launch_af_wd<WFv, 2, 0>(st, a, lds);                  \
     } while (0)
     switch (a.W[0].type) {
         case W_Q4_0: AF_T(W_Q4_0); break;

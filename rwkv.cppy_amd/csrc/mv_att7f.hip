@@ -194,11 +194,7 @@ __global__ __launch_bounds__(1024) void k_att7_lora(Att7Lora a) {
 }
 
 bool att7_lora_supported(const Att7Lora & a) {
-    static const bool on = [] {
-        const char * v = getenv("RWKV_MI355X_ATT7_LORA");  // 0: LoRA-out launch + k_att7_dec (A/B)
-        return !(v && v[0] == '0');
-    }();
-    if (!on || a.att.S != 64 || a.att.nb > 1 || a.att.yq.fmt < 0) return false;
+    if (a.att.S != 64 || a.att.nb > 1 || a.att.yq.fmt < 0) return false;
     const int t = a.W2[0].type;
     if (t != W_F16 && t != W_F32) return false;
     const int C = a.att.H * 64;

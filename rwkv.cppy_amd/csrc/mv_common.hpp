@@ -312,6 +312,67 @@ __device__ __forceinline__ void chunk_store(const MVEntry & E, const ActBuf & a,
     }
 }
 
+// Hand-off of a C-vector inside a fused decode launch (the head / channel outputs y feeding the
+// Wo rows): every element is a granule {tag (high word), value bits (low word)} written by ONE
+// aligned 8-byte agent-scope store, so the data is its own flag.  The gathering waves of a
+// workgroup (wave, wave + nwaves, ... over 512-element chunks; 8 consecutive granules per lane, so
+// a quad holds one quantization block) re-read their chunk, sleeping between passes, until every
+// tag reads `tag`, then write it into the LDS image in WF's activation format with the matvec
+// prologue's SRC_F32 arithmetic (chunk_store): Wo's input bits equal a separate Wo launch's.  The
+// poll IS the gather -- one round trip after the last value lands, not a flag poll and then a
+// gather.  Bounded: after spin_max passes *err (a host-mapped word) is set at system scope.
+typedef __attribute__((address_space(1))) unsigned long long gran_u64_t;
+typedef __attribute__((address_space(1))) unsigned gran_u32_t;
+template <int WF>
+__device__ __forceinline__ void gran_gather_image(const unsigned long long * yg, unsigned tag, int C, const ActBuf & img,
+                                                  int wave, int nwaves, unsigned * err, unsigned spin_max, int lane) {
+    MVEntry none{};
+    for (int ck = wave; ck * LN_CHUNK < C; ck += nwaves) {
+        const int k0 = ck * LN_CHUNK + lane * 8;
+        const bool valid = k0 < C;
+        const unsigned long long * g = yg + max(min(k0, C - 8), 0);
+        ChunkIn ci;
+        for (unsigned it = 0;; it++) {
+            unsigned long long x[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++)
+                x[j] = __hip_atomic_load((gran_u64_t *)(g + j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            bool ok = true;
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                ci.x[j] = __uint_as_float((unsigned)x[j]);
+                ok = ok && (unsigned)(x[j] >> 32) == tag;
+            }
+            if (__all(ok || !valid)) break;
+            if (it >= spin_max) {
+                __hip_atomic_store((gran_u32_t *)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        chunk_store<WF, MVK_F32, 0>(none, img, ci, 0.0f, 1.0f, false, k0, valid, lane);
+    }
+}
+
+// Wait before a gather: ONE wave polls n granules (lane i: yg[off + i * stride], n <= 64) with a
+// sleep between passes until every tag reads `tag` -- a few hundred bytes per pass instead of the
+// gather's whole vector, so a waiting workgroup adds little traffic beside the producers' weight
+// streams (the gather after it checks every tag again).  Bounded like the gather.
+__device__ __forceinline__ void gran_prepoll(const unsigned long long * yg, int n, int stride, int off, unsigned tag,
+                                             unsigned * err, unsigned spin_max, int lane) {
+    for (unsigned it = 0;; it++) {
+        const unsigned long long x = lane < n ? __hip_atomic_load((gran_u64_t *)(yg + off + (size_t)lane * stride),
+                                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                              : ((unsigned long long)tag << 32);
+        if (__all((unsigned)(x >> 32) == tag)) return;
+        if (it >= spin_max) {
+            __hip_atomic_store((gran_u32_t *)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            return;
+        }
+        __builtin_amdgcn_s_sleep(4);
+    }
+}
+
 // Row sums r = 0..R-1 (valid in lane 63 after wave_sum63) gathered so that lane r holds row r's
 // sum: the rows' epilogues (exp/tanh chains) then run side by side in R lanes instead of one
 // after another in lane 63.  Pure data movement: results are bit-identical.
@@ -324,6 +385,33 @@ __device__ __forceinline__ float lane_row_sum(const float (&s)[R], int lane) {
         mine = lane == r ? v : mine;
     }
     return mine;
+}
+
+// R rows whose U units per lane are already in registers, dotted with an LDS activation image:
+// k_mva's per-row arithmetic (lane/unit order, wave_sum63 tree; the unit count mv_units(WF, K)
+// must be <= U).  Lane r < R returns row r's sum.
+template <int WF, int R, int U>
+__device__ __forceinline__ float rows_dot_img(const WBlk (&w)[R][U], const ActBuf & img, int K, int lane) {
+    float acc[R], acc2[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) acc[r] = acc2[r] = 0.0f;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const AUnit xu = load_act_unit<WF, true>(img, u, lane);
+        const bool uv = unit_valid<WF>(K, u, lane);
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            float t = acc[r], t2 = acc2[r];
+            dot_unit<WF>(w[r][u], xu, t, t2);
+            acc[r] = uv ? t : acc[r];
+            acc2[r] = uv ? t2 : acc2[r];
+        }
+    }
+    constexpr bool one = WF == W_Q4_1 || WF == W_Q5_1;
+    float s[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) s[r] = one ? wave_sum63(acc[r]) + wave_sum63(acc2[r]) : wave_sum63(acc[r]) + 0.0f;
+    return lane_row_sum<R>(s, lane);
 }
 
 // Epilogue operands of one output row, loaded at kernel start (not after the dots).
@@ -449,9 +537,7 @@ __device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, int b0, in
         // the weight pointers reach SGPRs before the issue-order barrier, so the stream starts
         // right after it (a kernarg scalar load behind the barrier is a round trip in the path)
         asm volatile("" ::"s"(W.qs), "s"(W.sc), "s"(W.qh));
-        // issue order: the image inputs go out before any weight stream starts (late: they have
-        // landed before it starts)
-        if (late && pro_wave) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // issue order: the image inputs go out before any weight stream starts
         asm volatile("s_barrier" ::: "memory");
     }
     // ---- this wave's weight units (HBM), all in flight before anything waits
@@ -641,9 +727,36 @@ __device__ __forceinline__ void mv_body(const MVEntry & Ent, int wgi, int b0, in
 // conditions apart), the kernel needs 145-235 VGPRs -- one workgroup per CU -- and the multi-round
 // LayerNorm groups of the 2.9B / 7B models ran 10-14 % slower.  Same arithmetic and association as
 // mv_body (bit-identical); the barrier sequence of both paths matches one for one.
-template <int WF, int R, int U, int SRCK, int FORM, bool EMIT, int NW, int LNP>
+// Outputs of a producer group handed to consumers in the same launch (mv_ffnf.hpp): an emitting
+// entry publishes each 32-row Q8 block as KG_STRIDE granules {tag, dword} -- the block's 32 int8 (4
+// per granule), its fp16-rounded d and Q8_1's fp16-rounded d * sum (the qsum is an exact integer sum
+// the consumer recomputes) -- and a plain entry its rows' values as granules: emit32's bits.
+struct GranPub {
+    unsigned long long * kg;  // KG_STRIDE granules per 32-row block of the emitting entry
+    unsigned long long * rg;  // one granule per row of the other entry
+    unsigned tag;
+};
+// lanes 0..31 (one half-wave, block-uniform): rows 32 b .. 32 b + 31 of the emitting entry
+__device__ __forceinline__ void pub_q8(unsigned long long * kg, int b, float v, unsigned tag, int lane) {
+    const Q32 q = quant32(v);
+    unsigned p = ((unsigned)q.q & 0xffu) << (8 * (lane & 3));
+    p |= (unsigned)__shfl_xor((int)p, 1);
+    p |= (unsigned)__shfl_xor((int)p, 2);
+    const unsigned long long t = (unsigned long long)tag << 32;
+    unsigned long long * const g = kg + (size_t)b * KG_STRIDE;
+    if ((lane & 3) == 0)
+        __hip_atomic_store((gran_u64_t *)(g + ((lane & 31) >> 2)), t | p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((lane & 31) == 0) {
+        __hip_atomic_store((gran_u64_t *)(g + 8), t | __float_as_uint(f16_round(q.d)), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store((gran_u64_t *)(g + 9), t | __float_as_uint(f16_round(q.d * (float)q.sum)), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+template <int WF, int R, int U, int SRCK, int FORM, bool EMIT, int NW, int LNP, bool PUB = false>
 __device__ __forceinline__ void mv_body_split(const MVEntry & Ent, int wgi, int b0, int stride, char * smem,
-                                              float * red, int late) {
+                                              float * red, int late, const GranPub * pub = nullptr) {
     constexpr int LCW = LNP > 32 ? 2 : 1;
     constexpr int RR = 2 * R, RW = NW * RR;
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -664,7 +777,6 @@ __device__ __forceinline__ void mv_body_split(const MVEntry & Ent, int wgi, int 
             kc[q] = (pw + q * NW) * LN_CHUNK + lane * 8;
             chunk_load<SRCK, FORM>(Ent, min(kc[q], K - 8), ci[q]);
         }
-        if (late) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         asm volatile("s_barrier" ::: "memory");  // issue order: the image inputs ahead of the weights
         float mean = 0.0f, scale = 0.0f;
         if constexpr (SRCK == MVK_LN) {
@@ -735,7 +847,7 @@ __device__ __forceinline__ void mv_body_split(const MVEntry & Ent, int wgi, int 
         asm volatile("" ::"s"(epi), "s"(ey));
         if constexpr (EMIT) pin_act(ao);
         asm volatile("" ::"s"(W.qs), "s"(W.sc), "s"(W.qh));
-        asm volatile("s_barrier" ::: "memory");  // issue order (late: the image inputs have landed)
+        asm volatile("s_barrier" ::: "memory");  // issue order
         int row0 = wgi * RW + wave * RR;
         int rows[RR];
 #pragma unroll
@@ -789,9 +901,19 @@ __device__ __forceinline__ void mv_body_split(const MVEntry & Ent, int wgi, int 
                     float vv = 0.0f;
                     if (row < M) {
                         vv = epi_apply(epi, red[tid], ep);
-                        if (ey) ey[row] = vv;
+                        if constexpr (PUB) {
+                            if (!emit_on)
+                                __hip_atomic_store((gran_u64_t *)(pub->rg + row),
+                                                   ((unsigned long long)pub->tag << 32) | __float_as_uint(vv),
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        } else if (ey) {
+                            ey[row] = vv;
+                        }
                     }
-                    if (emit_on) emit32(ao, 0, row, vv);
+                    if (emit_on) {
+                        if constexpr (PUB) pub_q8(pub->kg, wgi, vv, pub->tag, tid);
+                        else emit32(ao, 0, row, vv);
+                    }
                 }
             }
             wgi += stride;

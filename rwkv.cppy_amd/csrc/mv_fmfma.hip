@@ -289,13 +289,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 // input in the weight type's activation format, row-major (not tiled); emitting entries need M % 32
 // == 0.  Returns false with *launched = false when the group is outside that (caller keeps k_mm).
 bool launch_fmm_group(hipStream_t st, MMGroup & g, int wtype, bool * launched) {
-    static const bool on = [] {
-        const char * v = getenv("RWKV_MI355X_FMM");  // 0: float matmuls stay on k_mm / k_mvb
-        return !(v && v[0] == '0');
-    }();
     *launched = false;
     // below 32 tokens (contexts) the 64-token tile is mostly padding: k_mvb / k_mm_small stay
-    if (!on || (wtype != W_F16 && wtype != W_F32) || g.T < 16 || (g.T < 32 && !g.fmm)) return true;
+    if ((wtype != W_F16 && wtype != W_F32) || g.T < 16 || (g.T < 32 && !g.fmm)) return true;
     // short rows over few tokens (the v7 LoRA second stages, K <= 320, in a batched decode step: a
     // few steps against the stage and epilogue overhead) stay on k_mvb (22 us vs 51 us at B = 32);
     // over a sequence k_fmm wins (135 us vs k_mm_small's 177 us at T = 1024)

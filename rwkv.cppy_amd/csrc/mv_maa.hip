@@ -327,14 +327,7 @@ __global__ __launch_bounds__(512) void k_v6_maa_dec4(MaaDec a) {
 // Channels mixed per workgroup (CPW): the workgroups of one mix each recompute its D rows of W1
 // (37 KB of L2 reads for v6-1B6) and stream CPW columns of W2 from HBM; 64 gives 32 x 5 = 160
 // workgroups for C = 2048 (256: 40), so the W2 stream is spread over more CUs.
-static int maa_cpw() {
-    static const int v = [] {
-        const char * e = getenv("RWKV_MI355X_MAA_CPW");
-        const int c = e ? atoi(e) : 64;
-        return c == 128 || c == 256 ? c : 64;
-    }();
-    return v;
-}
+static int maa_cpw() { return 64; }
 
 template <int WF>
 static bool launch_maa_t(hipStream_t st, const MaaDec & a, int lds, int units) {

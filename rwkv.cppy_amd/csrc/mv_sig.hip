@@ -23,12 +23,8 @@ static void fill_hot(const MVEntry & e, MVHot & h) {
 }
 
 bool mv_sigmul_supported(const MVEntry & ev, const MVEntry & er) {
-    static const bool on = [] {
-        const char * v = getenv("RWKV_MI355X_FFN_SIGMUL");  // 0: receptance in the key launch (A/B)
-        return !(v && v[0] == '0');
-    }();
     const int t = ev.W.type;
-    if (!on || !wtype_quantized(t) || er.W.type != t || ev.W.M != er.W.M) return false;
+    if (!wtype_quantized(t) || er.W.type != t || ev.W.M != er.W.M) return false;
     if (ev.src != SRC_ACT || er.src != SRC_ACT || !ev.y || ev.W.K % 32 || er.W.K % 32) return false;
     if (ev.act.fmt != act_fmt_for(t) || er.act.fmt != act_fmt_for(t) || ev.act.K != ev.W.K || er.act.K != er.W.K)
         return false;

@@ -76,21 +76,6 @@ __device__ __forceinline__ void qg_chunk_done() {
 }
 
 constexpr int QG_STEPS = 8;  // blocks per chunk
-#ifndef QG32_PK
-#define QG32_PK 0  // k_qg32 epilogue in packed f32 (1) or scalar f32 (0)
-#endif
-#ifndef QG32_PROBE
-#define QG32_PROBE 0  // tools: 1 = copies only, 2 = compute only (stale LDS after the first chunks)
-#endif
-#ifndef QG32_PMUL
-#define QG32_PMUL 0  // 1: p = d_w * d_x on the VALU instead of the f32 outer-product MFMA
-#endif
-#ifndef QG32_PIPE
-#define QG32_PIPE 0  // 1: MFMAs of step k + 1 issued before step k's epilogue
-#endif
-#ifndef QG32_RT
-#define QG32_RT 1  // k_qg32 workgroup rows in 64-row tiles (2: 128 x 64 tiles, 8 waves)
-#endif
 
 template <int WF>
 struct QGLayout {
@@ -618,408 +603,6 @@ __global__ __launch_bounds__(256) void k_qgemm(MMGroup g) {
     }
 }
 
-// ------------------------------------------------------------------------------------------------
-// k_qg32 (round 5): the same arithmetic as k_qgemm on the 32 x 32 MFMA shapes.
-//
-// A wave owns a 32-row x 32-token tile of the workgroup's 64 x 64 (as before); per step (block):
-//   * ONE v_mfma_i32_32x32x32_i8 gives the 32 x 32 integer block dots (k_qgemm issued four
-//     16x16x32, each holding the SIMD's vector issue as long as this one does);
-//   * ONE v_mfma_f32_32x32x2_f32 gives p = d_w * d_x for the 32 x 32 outputs as an outer product
-//     (k = 0: d_w of row i times d_x of token j onto C = 0; k = 1: 0 x 0).  d_w and d_x are fp16
-//     values, so d_w * d_x is exact in f32 and the MFMA's fma reproduces the VALU product bit for
-//     bit (a product of -0 becomes +0, which no chain can see: every class chain starts with
-//     fma(p, s, +0)).  The VALU epilogue is then s = sumi (bias trick) and acc = fma(p, s, acc):
-//     two ops per output and block instead of three, and the operands of a step are three LDS
-//     reads (row fragment, token fragment, one d each) instead of k_qgemm's eight;
-//   * lane l holds token (l & 31) and rows 8g + 4 (l >> 5) + q (g, q < 4) -- the 32x32 D layout.
-// The class walk, the binary-counter folds, the LDS-DMA ring of CH-step chunks, the epilogue
-// stores / fused Q8 emission / split-K partials are k_qgemm's, so y is bit-identical.
-typedef int qg_v16i_t __attribute__((ext_vector_type(16)));
-typedef float qg_v16f_t __attribute__((ext_vector_type(16)));
-
-struct Q32Ops {
-    v4i_t a, b;  // row fragment (16 int8 of row l & 31, half l >> 5), token fragment (same half)
-    float dw, dx;  // lanes < 32: d of row l / token l (k = 0 of the outer product); lanes >= 32: 0 (k = 1)
-};
-
-// sp: the step's LDS base ([RT weight records][activation record]); wr: the wave's first row in the
-// workgroup's RT x 64 rows (its 32 rows sit in weight record wr / 64)
-template <int WF, int RT = 1>
-__device__ __forceinline__ void q32_read(const char * sp0, Q32Ops & o, int wr, int wt, int lane) {
-    using Lt = QGLayout<WF>;
-    const char * sp = sp0 + (wr >> 6) * Lt::WB;
-    const int r = (wr & 63) + (lane & 31), hh = lane >> 5, t = wt + (lane & 31);
-    o.a = *(const v4i_t *)(sp + qg_w_off(r, hh * 16));
-    const char * ap = sp0 + RT * Lt::WB;
-    o.b = *(const v4i_t *)(ap + hh * QG_TOK * 16 + t * 16);
-    const float dw = *(const float *)(sp + qg_w_d(WF) + r * 4);
-    const float dx = *(const float *)(ap + QG_A_D + t * 4);
-    o.dw = hh ? 0.0f : dw;
-    o.dx = hh ? 0.0f : dx;
-}
-
-// y[t][m] for the lane's 16 outputs (token tok0 + wt + (l & 31), rows row0 + wr + 8g + 4(l >> 5) + q)
-__device__ __forceinline__ void q32_store(const MMEntry & E, const float * m2, int T, int M, int tok0, int row0, int wt,
-                                          int wr, int lane, const float (&tot)[16]) {
-    const int t = tok0 + wt + (lane & 31), hh = lane >> 5;
-    if (E.fuse_emit) {
-        // the wave's 32 rows of token t are one quantization block of the next matmul's input: 16 in
-        // this lane, 16 in lane l ^ 32.  quant32 / store32's values: amax over the block (order-free),
-        // d = amax / 127 (fp16-rounded), q = rint(v * 127 / amax).
-        const int tc = min(t, T - 1);
-        float v[16];
-        float am = 0.0f;
-#pragma unroll
-        for (int g = 0; g < 4; g++)
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const int m = row0 + wr + 8 * g + 4 * hh + q;
-                const float t2 = m2 ? m2[(size_t)m * T + tc] : 0.0f;
-                v[4 * g + q] = apply_epi_v(E, m, tot[4 * g + q] + t2, 0.0f, 0.0f);
-                am = fmaxf(am, fabsf(v[4 * g + q]));
-            }
-        am = fmaxf(am, __shfl_xor(am, 32));
-        const float d = am / 127.f;
-        const float id = (am != 0.0f) ? 127.f / am : 0.0f;
-        if (t < T) {
-            uint8_t * rec = E.out.tq + ((size_t)(t / QG_TOK) * (M >> 5) + ((row0 + wr) >> 5)) * qg_a_bytes(false);
-            const int tl = t % QG_TOK;
-#pragma unroll
-            for (int g = 0; g < 4; g++) {
-                uint32_t packed = 0;
-#pragma unroll
-                for (int q = 0; q < 4; q++) packed |= ((uint32_t)(int)rintf(v[4 * g + q] * id) & 0xffu) << (8 * q);
-                // block element e = 8g + 4hh + q: half e >> 4 = g >> 1, byte (8 (g & 1) + 4 hh + q)
-                *(uint32_t *)(rec + (g >> 1) * QG_TOK * 16 + tl * 16 + 8 * (g & 1) + 4 * hh) = packed;
-            }
-            if (hh == 0) ((float *)(rec + QG_A_D))[tl] = f16_round(d);
-        }
-        return;
-    }
-    if (t >= T) return;
-    const bool vec = ((E.ldy | M) & 3) == 0 && (((uintptr_t)E.y | (uintptr_t)E.aux) & 15) == 0;
-#pragma unroll
-    for (int g = 0; g < 4; g++) {
-        const int m0 = row0 + wr + 8 * g + 4 * hh;
-        if (m0 >= M) continue;
-        float acc[4];
-#pragma unroll
-        for (int q = 0; q < 4; q++) acc[q] = tot[4 * g + q] + (m2 && m0 + q < M ? m2[(size_t)(m0 + q) * T + t] : 0.0f);
-        float * yp = E.y + (size_t)t * E.ldy + m0;
-        if (vec) {
-            float4 yv = make_float4(0.f, 0.f, 0.f, 0.f), av = yv;
-            if (epi_reads_y(E.epi)) yv = *(const float4 *)yp;
-            if (epi_reads_aux(E.epi)) av = *(const float4 *)(E.aux + (size_t)t * E.ldy + m0);
-            float4 o;
-            o.x = apply_epi_v(E, m0, acc[0], yv.x, av.x);
-            o.y = apply_epi_v(E, m0 + 1, acc[1], yv.y, av.y);
-            o.z = apply_epi_v(E, m0 + 2, acc[2], yv.z, av.z);
-            o.w = apply_epi_v(E, m0 + 3, acc[3], yv.w, av.w);
-            *(float4 *)yp = o;
-        } else {
-#pragma unroll
-            for (int q = 0; q < 4; q++)
-                if (m0 + q < M) yp[q] = apply_epi(E, t, m0 + q, acc[q]);
-        }
-    }
-}
-
-__device__ __forceinline__ void q32_store_part(float * part, int sidx, int T, int M, int tok0, int row0, int wt, int wr,
-                                               int lane, const float (&sub)[16]) {
-    const int t = tok0 + wt + (lane & 31), hh = lane >> 5;
-    if (t >= T) return;
-#pragma unroll
-    for (int g = 0; g < 4; g++) {
-        const int m0 = row0 + wr + 8 * g + 4 * hh;
-        float * pp = part + ((size_t)sidx * T + t) * M + m0;
-#pragma unroll
-        for (int q = 0; q < 4; q++)
-            if (m0 + q < M) pp[q] = sub[4 * g + q];
-    }
-}
-
-// This wave's share of chunk c of CH steps: steps CH c + wave + 4 h2 (the walk is at the first of
-// them and is left at CH (c + 1) + wave).
-// RT weight records per step (row tiles of the workgroup; rw2 = the second one's descriptor, used
-// when it exists) and one activation record; NW = 4 RT waves, wave w copies steps w, w + NW, ...
-template <int WF, int CH, int RT = 1>
-__device__ __forceinline__ void q32_load_chunk(v4i_t rw, v4i_t rw2, bool two, v4i_t ra, unsigned lds_buf, int c,
-                                               QGWalk & wk, int nsteps, int wave, int lane) {
-    using Lt = QGLayout<WF>;
-    constexpr int NW = 4 * RT, STEP = RT * Lt::WB + Lt::AC;
-#pragma unroll
-    for (int h2 = 0; h2 < (CH + NW - 1) / NW; h2++) {
-        const int k = wave + NW * h2;
-        if (k < CH && c * CH + k < nsteps) {
-            const int b = wk.block();
-            const unsigned m = lds_buf + k * STEP;
-            qg_record<Lt::WB>(rw, (unsigned)(b * Lt::WB), m, lane);
-            if (RT == 2 && two) qg_record<Lt::WB>(rw2, (unsigned)(b * Lt::WB), m + Lt::WB, lane);
-            qg_record<Lt::AC>(ra, (unsigned)(b * Lt::AB), m + RT * Lt::WB, lane);
-        }
-#pragma unroll
-        for (int i = 0; i < NW; i++) wk.next();
-    }
-}
-
-// SPILL (SPLIT == 1): tree level 5 (the sum of classes 0..31, written once and read once per tile)
-// lives in LDS instead of 16 VGPRs per lane
-#ifndef QG32_LB
-#define QG32_LB 1  // __launch_bounds__ minimum waves per SIMD (3: <= 168 VGPRs)
-#endif
-// RT = 2: 128-row x 64-token workgroup tiles (8 waves, 4 x 2 wave tiles of 32 x 32): every token
-// record feeds twice the rows, so the operand bytes per output and block drop from 1.125 to 0.84.
-template <int WF, int SPLIT, int CH, bool K64 = false, bool SPILL = false, int RT = 1>
-__global__ __launch_bounds__(256 * RT, QG32_LB) void k_qg32(MMGroup g) {
-    using Lt = QGLayout<WF>;
-    constexpr bool ONE = Lt::ONE;
-    constexpr int CPS = 64 / SPLIT;  // classes per split
-    constexpr int STEP = RT * Lt::WB + Lt::AC;
-    constexpr int BUF = STEP * CH;
-    constexpr int NW = 4 * RT;
-    static_assert(!SPILL || SPLIT == 1, "k_qg32 spill: unsplit tiles only");
-    __shared__ __attribute__((aligned(16))) char smem[2][BUF];
-    __shared__ __attribute__((aligned(16))) float sp5[SPILL ? NW : 1][16][64];
-    int e = 0;
-#pragma unroll 1
-    while (e + 1 < g.n && (int)blockIdx.x >= g.e[e + 1].block0) e++;
-    const MMEntry & E = g.e[e];
-    const int M = E.W.M, K = E.W.K, T = g.T, nb = K >> 5;
-    const int tilesT = (T + QG_TOK - 1) / QG_TOK;
-    const int local0 = (int)blockIdx.x - E.block0;
-    const int sidx = local0 % SPLIT, local = local0 / SPLIT, l0 = sidx * CPS;
-    const int mtile = local / tilesT, ttile = local % tilesT;
-    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int row0 = mtile * Lt::ROWS * RT, tok0 = ttile * QG_TOK;
-    // this wave's tile-local rows / tokens
-    const int wr = (wave & (2 * RT - 1)) * 32, wt = (wave / (2 * RT)) * 32;
-    const v4i_t rw = qg_rsrc(E.W.gt + (size_t)mtile * RT * nb * Lt::WB);
-    const bool two = RT == 2 && (mtile * RT + 1) * Lt::ROWS < M;  // the second row tile exists
-    const v4i_t rw2 = qg_rsrc(E.W.gt + (size_t)(mtile * RT + (two ? 1 : 0)) * nb * Lt::WB);
-    const v4i_t ra = qg_rsrc(E.in.tq + (size_t)ttile * nb * Lt::AB);
-    const unsigned lds0 = __builtin_amdgcn_readfirstlane((unsigned)(unsigned long)(lds_void_t *)&smem[0][0]);
-    const int cq = nb >> 6, crem = nb & 63;
-    const int nsteps = CPS * cq + min(max(crem - l0, 0), CPS);
-    QGWalk ld;
-    ld.init(nb, l0);
-    for (int i = 0; i < wave; i++) ld.next();
-
-    float st[6][16];
-    float tot[16];
-    float c[16];
-    const int nchunks = (nsteps + CH - 1) / CH;
-    int k = 0, cb = 0, cn = 1;
-    Q32Ops cur;
-    // C = 0 (an inline constant: a bias vector in C would be re-materialised into 16 VGPRs before
-    // every MFMA, whose D overwrites it); sumi -> f32 by v_cvt_f32_i32 (exact: |sumi| < 2^24)
-    const qg_v16i_t izero = {};
-    const qg_v16f_t fzero = {};
-#if QG32_PIPE
-    // Software-pipelined: step k's epilogue runs beside the MFMAs of step k + 1 (issued first from
-    // operands read one step earlier) and the LDS reads of step k + 2.  A chunk's buffer is
-    // released two steps before its end (all its operands are in registers by then).
-    Q32Ops nx;                    // operands of step k + 1
-    qg_v16i_t sv_c;               // MFMA results of step k
-    qg_v16f_t p_c;
-    auto mfma = [&](const Q32Ops & o, qg_v16i_t & sv, qg_v16f_t & pp) {
-        sv = __builtin_amdgcn_mfma_i32_32x32x32_i8(o.a, o.b, izero, 0, 0, 0);
-        pp = __builtin_amdgcn_mfma_f32_32x32x2f32(o.dw, o.dx, fzero, 0, 0, 0);
-    };
-    auto step = [&](auto first, float (&acc)[16]) {
-        constexpr bool FIRST = decltype(first)::value;
-        if (k == CH - 2) {
-            qg_chunk_done();  // the next chunk has landed; every wave holds this chunk's operands
-            if (cn < nchunks) q32_load_chunk<WF, CH, RT>(rw, rw2, two, ra, lds0 + cb * BUF, cn, ld, nsteps, wave, lane);
-            cn++;
-        }
-        Q32Ops nn;
-        if (k + 2 < CH) q32_read<WF, RT>(smem[cb] + (k + 2) * STEP, nn, wr, wt, lane);
-        else q32_read<WF, RT>(smem[cb ^ 1] + (k + 2 - CH) * STEP, nn, wr, wt, lane);
-        qg_v16i_t sv_n;
-        qg_v16f_t p_n;
-        mfma(nx, sv_n, p_n);
-        // keep the epilogue below the MFMAs (the scheduler would hoist it above them, and the next
-        // epilogue would then wait on MFMAs issued just before it)
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int r = 0; r < 16; r++) {
-            const float si = (float)sv_c[r];
-            acc[r] = __builtin_fmaf(p_c[r], si, FIRST ? 0.0f : acc[r]);
-        }
-        sv_c = sv_n;
-        p_c = p_n;
-        nx = nn;
-        if (++k == CH) {
-            k = 0;
-            cb ^= 1;
-        }
-        // straight-line (K64) chunks: no MFMA of a later step above this step's epilogue (the
-        // scheduler would hoist all of them and hold every result: 256 VGPRs)
-        if constexpr (K64) __builtin_amdgcn_sched_barrier(0);
-    };
-#else
-    auto step = [&](auto first, float (&acc)[16]) {
-        constexpr bool FIRST = decltype(first)::value;
-        if (k == CH) {
-            k = 0;
-            qg_chunk_done();
-#if QG32_PROBE == 2
-            if (cn < nchunks && cn < 2)  // probe: compute only (stale LDS after the first chunks)
-#else
-            if (cn < nchunks)
-#endif
-                q32_load_chunk<WF, CH, RT>(rw, rw2, two, ra, lds0 + cb * BUF, cn, ld, nsteps, wave, lane);
-            cn++;
-            cb ^= 1;
-            q32_read<WF, RT>(smem[cb], cur, wr, wt, lane);
-        }
-#if QG32_PROBE == 1
-        if (0)  // probe: copies only
-#endif
-        {
-        const qg_v16i_t sv = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.a, cur.b, izero, 0, 0, 0);
-#if QG32_PMUL
-        // p = d_w * d_x on the VALU: d_w of the lane's 16 rows (4 broadcast b128 reads), d_x of its token
-        qg_v16f_t p;
-        {
-            const char * sp = smem[cb] + k * STEP;
-            const float dxv = *(const float *)(sp + RT * Lt::WB + QG_A_D + (wt + (lane & 31)) * 4);
-#pragma unroll
-            for (int g4 = 0; g4 < 4; g4++) {
-                const float4 dw4 = *(const float4 *)(sp + (wr >> 6) * Lt::WB + qg_w_d(WF) + ((wr & 63) + 8 * g4 + 4 * (lane >> 5)) * 4);
-                p[4 * g4 + 0] = dw4.x * dxv;
-                p[4 * g4 + 1] = dw4.y * dxv;
-                p[4 * g4 + 2] = dw4.z * dxv;
-                p[4 * g4 + 3] = dw4.w * dxv;
-            }
-        }
-#else
-        const qg_v16f_t p = __builtin_amdgcn_mfma_f32_32x32x2f32(cur.dw, cur.dx, fzero, 0, 0, 0);
-#endif
-        Q32Ops nxt = cur;
-        if (k + 1 < CH) q32_read<WF, RT>(smem[cb] + (k + 1) * STEP, nxt, wr, wt, lane);
-#if QG32_PK
-#pragma unroll
-        for (int r = 0; r < 16; r += 2) {
-            const qf2_t si = qf2_t{(float)sv[r], (float)sv[r + 1]};
-            const qf2_t a0 = FIRST ? qf2_t{0.0f, 0.0f} : qf2_t{acc[r], acc[r + 1]};
-            const qf2_t a = __builtin_elementwise_fma(qf2_t{p[r], p[r + 1]}, si, a0);
-            acc[r] = a.x;
-            acc[r + 1] = a.y;
-        }
-#else
-        // scalar f32 (packed f32 VALU beside MFMAs costs extra issue cycles: MI355X_MICROARCH.md)
-#pragma unroll
-        for (int r = 0; r < 16; r++) {
-            const float si = (float)sv[r];
-            acc[r] = __builtin_fmaf(p[r], si, FIRST ? 0.0f : acc[r]);
-        }
-#endif
-        cur = nxt;
-        }
-        k++;
-    };
-#endif
-    using T1 = std::integral_constant<bool, true>;
-    using T0 = std::integral_constant<bool, false>;
-    auto run_class = [&](int l, float (&acc)[16]) {
-        const int n = cq + (l < crem ? 1 : 0);
-        if (n == 0) {
-#pragma unroll
-            for (int r = 0; r < 16; r++) acc[r] = 0.0f;
-            return;
-        }
-        step(T1{}, acc);
-        for (int u = 1; u < n; u++) step(T0{}, acc);
-    };
-#define Q32_CASE(N, DST)                                                          \
-    case N: {                                                                     \
-        _Pragma("unroll") for (int r = 0; r < 16; r++) {                          \
-            float v = c[r];                                                       \
-            for (int kk = 0; kk < N; kk++) v = st[kk][r] + v;                     \
-            DST[r] = v;                                                           \
-        }                                                                         \
-        break;                                                                    \
-    }
-    if (nchunks > 0) q32_load_chunk<WF, CH, RT>(rw, rw2, two, ra, lds0, 0, ld, nsteps, wave, lane);
-    qg_chunk_done();
-    if (nchunks > 1) q32_load_chunk<WF, CH, RT>(rw, rw2, two, ra, lds0 + BUF, 1, ld, nsteps, wave, lane);
-    cn = 2;
-#if QG32_PIPE
-    {
-        Q32Ops o0;
-        q32_read<WF, RT>(smem[0], o0, wr, wt, lane);
-        q32_read<WF, RT>(smem[0] + STEP, nx, wr, wt, lane);
-        mfma(o0, sv_c, p_c);
-    }
-#else
-    q32_read<WF, RT>(smem[0], cur, wr, wt, lane);
-#endif
-    if constexpr (K64) {
-        // K = 2048: every class is one block, the walk is block order, chunk ch = classes CH ch ..
-        // CH ch + CH - 1 (of this split): the folds after the odd steps are known at compile time
-        // except the chunk's last, which closes log2(CH) + ctz(~ch) levels
-        static_assert(CH == 8 || CH == 4, "k_qg32 K64 chunk");
-        constexpr int LCH = CH == 8 ? 3 : 2;
-#pragma unroll 1
-        for (int ch = 0; ch < CPS / CH; ch++) {
-#pragma unroll
-            for (int kk = 0; kk < CH; kk++) {
-                if (kk & 1) {
-                    step(T1{}, c);
-                    constexpr int N0 = 0;
-                    (void)N0;
-                    const int nf = kk + 1 < CH ? __builtin_ctz(~kk) : LCH + __builtin_ctz(~ch);
-                    switch (nf) {
-                        Q32_CASE(1, st[1])
-                        Q32_CASE(2, st[2])
-                        Q32_CASE(3, st[3])
-                        Q32_CASE(4, st[4])
-                        Q32_CASE(5, st[5])
-                        default:
-                        Q32_CASE(6, tot)
-                    }
-                } else {
-                    step(T1{}, st[0]);
-                }
-            }
-        }
-    } else
-    for (int pr = 0; pr < CPS / 2; pr++) {
-        run_class(l0 + 2 * pr, st[0]);
-        run_class(l0 + 2 * pr + 1, c);
-        const int nf = __builtin_ctz(~(2 * pr + 1));
-        if (SPILL && nf >= 5) {
-#pragma unroll
-            for (int r = 0; r < 16; r++) {
-                float v = c[r];
-#pragma unroll
-                for (int kk = 0; kk < 5; kk++) v = st[kk][r] + v;
-                if (nf == 5) sp5[SPILL ? wave : 0][r][lane] = v;
-                else tot[r] = sp5[SPILL ? wave : 0][r][lane] + v;
-            }
-            continue;
-        }
-        switch (nf) {
-            Q32_CASE(1, st[1])
-            Q32_CASE(2, st[2])
-            Q32_CASE(3, st[3])
-            Q32_CASE(4, st[4])
-            Q32_CASE(5, st[5])
-            default:
-            Q32_CASE(6, tot)
-        }
-    }
-#undef Q32_CASE
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if constexpr (SPLIT == 1) {
-        q32_store(E, ONE ? g.m2 + E.moff : nullptr, T, M, tok0, row0, wt, wr, lane, tot);
-    } else {
-        constexpr int LEV = SPLIT == 8 ? 3 : SPLIT == 4 ? 4 : 5;
-        q32_store_part(g.part + E.poff, sidx, T, M, tok0, row0, wt, wr, lane, st[LEV]);
-    }
-}
-
 // The _1 formats' m*s chains, in the matvec's association: for class l (= b mod 64) the chain
 // acc = acc + m_w[b] * s_x[b] over b = l + 64 u ascending, from 0; the 64 class sums folded by
 // wave_sum63's tree (the binary counter of the GEMM).  Independent of the int8 dot, so it runs as
@@ -1383,30 +966,10 @@ bool launch_qg_combine(hipStream_t st, MMGroup & g, int split) {
 // next matmul's activation format is a separate launch_act_from_f32 pass by the caller.  The
 // weights need their tile records (upload_mat) and the activations must be token tiles.
 int g_qgemm_generic = 0;  // 1: K = 2048 through the generic kernel too (tools, comparison)
-#ifndef QG32_CH
-#define QG32_CH 8
-#endif
-#ifndef QG32_PK
-#define QG32_PK 0
-#endif
-#ifndef QG32_SPILL
-#define QG32_SPILL 0
-#endif
-// RWKV_MI355X_QG32=1: the 32x32-MFMA GEMM (k_qg32); g_qg32 < 0 = read the environment
-int g_qg32 = -1;
-static bool qg32_on() {
-    if (g_qg32 < 0) {
-        const char * v = getenv("RWKV_MI355X_QG32");
-        g_qg32 = v && v[0] == '1' ? 1 : 0;
-    }
-    return g_qg32 == 1;
-}
-
 int kQgCUs = 256;          // compute units of the device (set_mv_device_cus): the split-K threshold
 
 bool launch_qgemm(hipStream_t st, MMGroup & g, int wtype) {
-    const int RTv = qg32_on() ? QG32_RT : 1;  // k_qg32: RT row tiles of 64 per workgroup
-    const int rows = qg_rows(wtype) * RTv;
+    const int rows = qg_rows(wtype);
     const int tilesT = (g.T + QG_TOK - 1) / QG_TOK;
     int blocks = 0;
     for (int i = 0; i < g.n; i++) {
@@ -1465,22 +1028,14 @@ bool launch_qgemm(hipStream_t st, MMGroup & g, int wtype) {
                       e.W.M % 64 == 0 && e.ldy == e.W.M && e.epi != EPI_ADD && e.epi != EPI_SIGMUL_ADD &&
                       e.epi != EPI_VMIX7 && e.epi != EPI_DECAY6 && e.epi != EPI_DECAY7 && e.epi != EPI_SIGMOID_BIAS;
     }
-    const dim3 grid(blocks), block(256), qblock(256 * RTv);
+    const dim3 grid(blocks), block(256);
     bool k64 = true;
     for (int i = 0; i < g.n; i++) k64 = k64 && g.e[i].W.K == 2048;
     // split-K when the group has few tiles (batched decode's 64-context tiles, small-M entries such
     // as the v6 maa LoRA W1): every tile's class tree in 4 or 8 subtrees on as many workgroups,
     // combined (epilogue, emission) by k_qg_combine -- the same bits as the unsplit kernel
     int split = g.split;
-    // (RWKV_MI355X_QG_SPLIT2=1: two subtrees for groups of 1-2 tiles per CU -- A/B)
-    static const bool split2 = [] {
-        const char * v = getenv("RWKV_MI355X_QG_SPLIT2");
-        return v && v[0] == '1';
-    }();
-    if (split == 0) {
-        const int wb = blocks * RTv;  // in 4-wave units
-        split = wb >= 2 * kQgCUs ? 1 : (split2 && wb >= kQgCUs) ? 2 : wb * 4 >= 2 * kQgCUs ? 4 : 8;
-    }
+    if (split == 0) split = blocks >= 2 * kQgCUs ? 1 : blocks * 4 >= 2 * kQgCUs ? 4 : 8;
     if (split != 1 && split != 2 && split != 4 && split != 8) split = 1;
     size_t pfl = 0;
     if (split > 1) {
@@ -1498,8 +1053,7 @@ bool launch_qgemm(hipStream_t st, MMGroup & g, int wtype) {
         const dim3 sgrid(blocks * split);
 #define QG_SPLIT_L(WFv, SP)                                                                    \
     do {                                                                                       \
-        if (qg32_on()) RK_LAUNCH((k_qg32<WFv, SP, QG32_CH, false, false, QG32_RT>), sgrid, qblock, 0, st, g);  \
-        else if (k64) RK_LAUNCH((k_qgemm_k64<WFv, SP>), sgrid, block, 0, st, g);      \
+        if (k64) RK_LAUNCH((k_qgemm_k64<WFv, SP>), sgrid, block, 0, st, g);      \
         else RK_LAUNCH((k_qgemm<WFv, SP>), sgrid, block, 0, st, g);                   \
     } while (0)
 #define QG_SPLIT_T(SP)                                                                         \
@@ -1536,23 +1090,6 @@ bool launch_qgemm(hipStream_t st, MMGroup & g, int wtype) {
             if (one) RK_LAUNCH((k_qg_combine<8, true>), dim3(cblocks), block, 0, st, g);
             else RK_LAUNCH((k_qg_combine<8, false>), dim3(cblocks), block, 0, st, g);
         }
-        HIP_OK(hipGetLastError());
-        return true;
-    }
-    if (qg32_on()) {
-#define QG32_T(WFv)                                                                                      \
-    case WFv:                                                                                            \
-        RK_LAUNCH((k_qg32<WFv, 1, QG32_CH, false, QG32_SPILL, QG32_RT>), grid, qblock, 0, st, g);                \
-        break;
-        switch (wtype) {
-            QG32_T(W_Q4_0)
-            QG32_T(W_Q4_1)
-            QG32_T(W_Q5_0)
-            QG32_T(W_Q5_1)
-            QG32_T(W_Q8_0)
-            default: fprintf(stderr, "rwkv: qgemm type %d unsupported\n", wtype); return false;
-        }
-#undef QG32_T
         HIP_OK(hipGetLastError());
         return true;
     }

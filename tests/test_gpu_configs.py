@@ -145,6 +145,59 @@ def test_v7_2b9_width_four_stages(cfg_dir):
     assert_bits_equal(lg, ref_lg, 'four-stage logits')
 
 
+FUSION_MASKS = [0, 127 ^ 2, 127 ^ 8, 127 ^ 16, 127 ^ 32, 127 ^ 1, 127 ^ 64, 127 ^ 96]
+
+
+@pytest.mark.parametrize('name', sorted(CONFIGS))
+def test_decode_fusion_arms_bit_exact(cfg_dir, name):
+    """Every decode fusion has an unfused arm (Engine::FUSE_*: 1 v6 attention launch, 2 its Wo, 4 v4
+    attention launch, 8 its Wo, 16 v7 LoRA + attention, 32 FFN value + receptance, 64 the whole channel
+    mix in one launch).  Each mask,
+    switched per context (rwkv_mi355x_debug_set "decode_fusion") and at creation
+    (RWKV_MI355X_DECODE_FUSION), decodes bit-exactly against the oracle; switching back and forth on
+    one context (the fused Wo's granules cleared at each switch) too."""
+    path = cfg_model(cfg_dir, name)
+    toks = [int(t) for t in np.random.default_rng(7).integers(0, VOCAB, 6)]
+    glg, gst = gpu_variant(path, toks)
+    L = library()
+    m = RWKVModel(L, path)
+    for mask in FUSION_MASKS + [127]:
+        assert L.library.rwkv_mi355x_debug_set(m._ctx.ptr, b'decode_fusion', mask)
+        lg, st = gpu_serial(m, toks)
+        assert_bits_equal(lg, glg, f'{name} decode logits, fusion mask {mask}')
+        assert_bits_equal(st, gst, f'{name} decode state, fusion mask {mask}')
+    m.free()
+    os.environ['RWKV_MI355X_DECODE_FUSION'] = '0'
+    try:
+        m = RWKVModel(L, path)
+    finally:
+        os.environ.pop('RWKV_MI355X_DECODE_FUSION', None)
+    lg, st = gpu_serial(m, toks)
+    assert_bits_equal(lg, glg, f'{name} decode logits, RWKV_MI355X_DECODE_FUSION=0')
+    assert_bits_equal(st, gst, f'{name} decode state, RWKV_MI355X_DECODE_FUSION=0')
+    m.free()
+
+
+@pytest.mark.parametrize('arch,fmt', [(4, 'Q8_0'), (6, 'Q4_0')])
+def test_width_above_4096_generic_path(cfg_dir, arch, fmt):
+    """n_embed 4608 (> the 4096 that the register LayerNorm prologues hold; RWKV-4 14B is 5120): the
+    engine routes decode through the sequence kernels and the embedding LayerNorm through its wide
+    form.  Serial decode, sequence evaluation and the oracle agree bit for bit."""
+    p = os.path.join(str(cfg_dir), f'wide-v{arch}.bin')
+    if not os.path.isfile(p):
+        assert library().library.rwkv_mi355x_write_synthetic_model(p.encode(), arch, 1024, 4608, 1, 0, fmt.encode(), 23)
+    toks = [int(t) for t in np.random.default_rng(14).integers(0, 1024, 5)]
+    m = RWKVModel(library(), p)
+    lg, st = gpu_serial(m, toks)
+    slg, sst = m.eval_sequence(toks, None, use_numpy=True)
+    m.free()
+    assert_bits_equal(lg, slg, 'wide decode vs sequence logits')
+    assert_bits_equal(st, sst, 'wide decode vs sequence state')
+    glg, gst = gpu_variant(p, toks)
+    assert_bits_equal(lg, glg, 'wide decode logits vs oracle')
+    assert_bits_equal(st, gst, 'wide decode state vs oracle')
+
+
 def test_v6_1b6_width_1024_tokens(cfg_dir):
     """The headline sequence length: 1024 tokens in one rwkv_eval_sequence at the v6-1B6 width."""
     path = cfg_model(cfg_dir, 'v6-1b6-q4_0')
@@ -183,8 +236,8 @@ def test_v6_decode_handoff_many_tokens(cfg_dir):
 def test_v6_decode_handoff_timeout_fails_the_call(cfg_dir, skip_wg):
     """A hand-off that times out must fail the evaluation, never return garbage with success
     (reference error convention: false + RWKV_ERROR_CTX, rwkv_error_handling.inc:1-54).  The test hook
-    makes one producer workgroup of k_v6_att_fused publish nothing (9: head 1's slot 1 -- r, k, v, g
-    rows; 255: the last head's slot 7 -- decay-LoRA rows) with a short sweep bound.  rwkv_eval (host
+    makes one producer workgroup of k_v6_att_fused publish nothing (9: head 9's first 32 rows and
+    decay-LoRA row 9; 255: head 31's last 32 rows) with a short sweep bound.  rwkv_eval (host
     state, the chunked graphs) and rwkv_mi355x_eval_device + rwkv_mi355x_sync both fail with
     RWKV_ERROR_CTX; with the hook off the same context then decodes bit-exactly again (the granules
     were cleared and the flag re-armed)."""

@@ -14,9 +14,8 @@ Beside it, bounds against the reference semantics (written here, see DESIGN.md "
     ggml-order oracle (variant 0) is therefore bounded by max(1e-3, 1.5 * noise), noise = the
     largest deviation among the oracle's own 7 re-associated restatements; it documents that
     the GPU association is one more valid restatement -- the bit-exact gate above is the check.
-  * the reference's signed-sum rule |sum(logits - expected)| <= 1.05*|bound|
-    (logit_difference_validator.inc:68,83), widened by 1.5x the spread of that sum across the
-    oracle's re-associated variants (the rule was written for one summation order).
+  * the reference's signed-sum rule |sum(logits - expected)| <= 1.05*|bound| exactly as written
+    (logit_difference_validator.inc:68,83: fp32 sum in index order), no widening.
   * Layout/bookkeeping properties are bit-exact: serial == sequence == chunked state,
     NULL-logits state, cloned contexts (reference tests/test_eval_sequence_in_chunks.c,
     test_logit_calculation_skipping.c, test_context_cloning.c).
@@ -43,13 +42,20 @@ def expected(v):
     return np.fromfile(os.path.join(GOLD, f'expected-logits-{v}.bin'), np.float32)
 
 
-def assert_signed_sum(lg, v, bound, variants):
-    """Reference rule |sum(logits - expected)| <= 1.05*|bound|, plus the oracle's own spread."""
-    ref = expected(v)
-    sums = [float((o - ref).sum()) for o in variants]
-    spread = max(abs(x - sums[0]) for x in sums[1:])
-    s = float((lg - ref).sum())
-    assert abs(s) <= abs(bound) * 1.05 + 1.5 * spread, (s, bound, spread)
+def diff_sum_f32(lg, ref):
+    """The reference's difference sum: one float accumulator over the vocabulary in index order
+    (logit_difference_validator.inc:60-66)."""
+    d = np.asarray(lg, np.float32) - np.asarray(ref, np.float32)
+    return float(np.cumsum(d, dtype=np.float32)[-1])
+
+
+def assert_signed_sum(lg, v, bound, variants=None):
+    """The reference rule as written: |sum(logits - expected)| <= 1.05 * |bound|
+    (logit_difference_validator.inc:68,83).  Every case of this file meets it without any widening
+    (round 6: each of the 48 tiny-model cases computed on the oracle's GPU-association variant, which
+    the GPU equals bit for bit); `variants` is unused and kept for the callers' signature."""
+    s = diff_sum_f32(lg, expected(v))
+    assert abs(s) <= abs(bound) * 1.05, (s, bound)
 
 
 def gpu_serial(model, tokens, state=None):
@@ -375,3 +381,28 @@ def test_v6_fused_maa_decode_equals_split(tmp_path, fmt):
         outs.append(gpu_serial(m, toks))
         m.free()
     assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+
+
+def test_v6_1b6_width_token1_vs_ggml_order(tmp_path):
+    """At the headline width (v6-1B6: C 2048, H 32, FFN 7168, Q4_0; 2 layers, 4096-token vocabulary),
+    the FIRST token -- before any Q8 re-quantization flip can be amplified by the recurrence -- must
+    sit within 1e-4 of the ggml-order oracle (variant 0): max|dlogit| <= 1e-4 and max|dstate| <= 1e-4
+    relative to max|state|.  This is where a systematic error of the GPU association would show;
+    later tokens are bounded by the oracle's noise band (bench.py's parity reports the growth).
+    Measured on the oracle's GPU-association variant (which the GPU equals bit for bit): 1.7e-5 and
+    3.6e-7 relative."""
+    L = library()
+    p = str(tmp_path / 'v6-1b6-width.bin')
+    assert L.library.rwkv_mi355x_write_synthetic_model(p.encode(), 6, 4096, 2048, 2, 0, b'Q4_0', 21)
+    tok = [int(np.random.default_rng(31).integers(0, 4096))]
+    m = RWKVModel(L, p)
+    lg, st = gpu_serial(m, tok)
+    m.free()
+    glg, gst = gpu_variant(p, tok)
+    assert_bits_equal(lg, glg, 'token-1 logits vs GPU-association oracle')
+    assert_bits_equal(st, gst, 'token-1 state vs GPU-association oracle')
+    o = OracleModel(p)
+    olg, ost = o.eval_serial(tok)
+    o.close()
+    assert np.abs(lg - olg).max() <= 1e-4, np.abs(lg - olg).max()
+    assert np.abs(st - ost).max() <= 1e-4 * np.abs(ost).max(), (np.abs(st - ost).max(), np.abs(ost).max())

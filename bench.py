@@ -35,7 +35,8 @@ METRIC = 'tokens/sec RWKV-v6-World-1B6 Q4_0 decode + seq-eval @1/2/4/8 GPU; HBM 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 INT8_MFMA_PEAK_TOPS = 5000.0  # dense int8 MFMA: 2x the ~2.5 PF dense bf16 rate (MI355X_MICROARCH.md, Matrix cores)
 # decode kernels that stream layer / head weights (the roofline's pooled kernel class)
-STREAM_KERNELS = ('k_mv', 'k_mva', 'k_v6_maa_dec', 'k_v6_maa_dec4', 'k_v6_att_fused', 'k_mvsig', 'k_v4_att_fused')
+STREAM_KERNELS = ('k_mv', 'k_mva', 'k_v6_maa_dec', 'k_v6_maa_dec4', 'k_v6_att_fused', 'k_mvsig', 'k_v4_att_fused',
+                  'k_ffn_fused', 'k_att7_lora')
 
 CONFIGS = {
     # name: arch, n_vocab, n_embed, n_layer, ffn (0 = arch default), format, label
@@ -490,8 +491,11 @@ def main():
         assert L.rwkv_mi355x_state_upload(ctx.ptr, None)
         L.rwkv_mi355x_set_kernel_timing(ctx.ptr, True)
         for i in range(timing_steps):
+            # a lead kernel per step: the step's launches queue up behind it and then run back to
+            # back -- the same conditions with and without a profiler attached (profiles/)
+            assert L.rwkv_mi355x_debug_set(ctx.ptr, b'delay_us', 4000)
             step(i % len(arrs))
-        L.rwkv_mi355x_sync(ctx.ptr)
+            L.rwkv_mi355x_sync(ctx.ptr)
         kstats = read_stats()
         L.rwkv_mi355x_set_kernel_timing(ctx.ptr, False)
         for k in kstats:
@@ -527,7 +531,8 @@ def main():
             'launches_per_token': round(p_launches / timing_steps, 1),
             'method': 'per-dispatch HIP events (hipExtLaunchKernelGGL start/stop: the dispatch timestamps '
                       'rocprofv3 reports) on the engine stream over '
-                      f'{timing_steps} eager decode steps; profiles/ holds the rocprofv3 kernel trace of this pass '
+                      f'{timing_steps} eager decode steps, each queued behind a 4 ms lead kernel so its launches '
+                      'run back to back; profiles/ holds the rocprofv3 kernel trace of this pass '
                       '(bench.py --roofline-only, reproduces these averages) and of the graph-replayed decode '
                       '(bench.py --decode-only, which the profiler itself slows down)',
             'per_kernel': {k['name']: {'launches_per_token': round(k['launches'] / timing_steps, 1),

@@ -1590,6 +1590,8 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits, uint32
                 ff.tag = (unsigned)(l + 1) | ((unsigned)(cur_ + 1) << 16);
                 ff.err = herr_d_;
                 ff.spin_max = spin_max_;
+                ff.wdelay = ffn_wdelay_ >= 0 ? ffn_wdelay_ : (int)std::min(2000.0, wbytes(L.ffn_k) / 4e4);
+                ff.prepoll = ffn_prepoll_;
                 if (ffn_fused_supported(ff, 1, false)) {
                     if (timing_) {
                         kt_bytes_ = wbytes(L.ffn_k) + wbytes(L.ffn_v) + 5.0 * C * 4 + 2.0 * C * 4 +
@@ -1657,6 +1659,8 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits, uint32
                 ff.tag = (unsigned)(l + 1) | ((unsigned)(cur_ + 1) << 16);
                 ff.err = herr_d_;
                 ff.spin_max = spin_max_;
+                ff.wdelay = ffn_wdelay_ >= 0 ? ffn_wdelay_ : (int)std::min(2000.0, (wbytes(L.ffn_k) + wbytes(L.ffn_r)) / 4e4);
+                ff.prepoll = ffn_prepoll_;
                 if (ffn_fused_supported(ff, form, true)) {
                     if (timing_) {
                         kt_bytes_ = wbytes(L.ffn_k) + wbytes(L.ffn_r) + wbytes(L.ffn_v) + 5.0 * C * 4 + 2.0 * C * 4 +
@@ -1834,6 +1838,11 @@ bool Engine::handoff_check() {
 bool Engine::debug_set(const char * name, long long value) {
     if (!name) return false;
     const std::string n(name);
+    // "delay_us": a kernel that holds the context's stream for value us, enqueued now (no sync) --
+    // the timing pass puts one ahead of each eager decode step, so the host queues the step's
+    // launches before the GPU reaches them and they run back to back, as in a graph replay (and as
+    // under a profiler, whose slower launches would otherwise leave the GPU idle between kernels)
+    if (n == "delay_us") return value > 0 && value <= 100000 && launch_delay(stream_, (int)value);
     if (n == "skip_granule") dbg_skip_gran_ = (int)value;
     else if (n == "spin_max") spin_max_ = value > 0 ? (unsigned)std::min<long long>(value, 0xffffffffLL) : (1u << 20);
     else if (n == "wkv_chunk") wkv_chunk_ = value != 0;
@@ -1842,6 +1851,8 @@ bool Engine::debug_set(const char * name, long long value) {
     else if (n == "decode_fusion") fuse_ = (unsigned)value & FUSE_ALL;
     else if (n == "wo_rows" && (value == 4 || value == 8)) wo_rows_ = (int)value;
     else if (n == "wo_prepoll") wo_prepoll_ = value != 0;
+    else if (n == "ffn_wdelay" && value >= -1 && value <= 10000) ffn_wdelay_ = (int)value;
+    else if (n == "ffn_prepoll") ffn_prepoll_ = value != 0;
     else return false;
     // the decode graphs captured the old values; a decode program without the fused Wo flips the
     // state parity without writing the Wo granules (see run_tokens_impl): clear them

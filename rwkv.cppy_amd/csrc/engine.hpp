@@ -185,12 +185,13 @@ class Engine : public KLaunchTimer {
         FUSE_SIG = 32,   // k_mvsig (FFN value + receptance rows)
         FUSE_FFN = 64,   // k_ffn_fused (the whole channel mix: key, receptance and value rows)
         FUSE_ALL = 127,
-        // default: everything but the one-launch channel mix (measured slower: v6-1B6 708.9 vs
-        // 697.5 us/token, its 21 MB of weights streaming at once delay the key rows)
-        FUSE_DEFAULT = FUSE_ALL & ~FUSE_FFN,
+        FUSE_DEFAULT = FUSE_ALL,
     };
     unsigned fuse_ = FUSE_DEFAULT;
     int wo_rows_ = 8;      // k_v6_att_fused: Wo rows per wave of a Wo workgroup (debug knob "wo_rows": 4 / 8)
+    int ffn_wdelay_ = -1;  // k_ffn_fused: consumer weight-issue delay in 100 MHz ticks ("ffn_wdelay"; -1:
+                           // the producers' weight bytes at 4 TB/s, so the two streams do not overlap)
+    int ffn_prepoll_ = 1;  // k_ffn_fused: poll the key blocks' d granules before the gather ("ffn_prepoll")
     int wo_prepoll_ = 1;   // k_v6_att_fused: one wave polls a granule per head before the gather ("wo_prepoll"; 0: 707.5 -> 708.9 us/token)
     bool generic_decode_ = false;  // RWKV_MI355X_GENERIC_DECODE=1: decode through the T>1 kernels
     hipEvent_t tok_event_ = nullptr;

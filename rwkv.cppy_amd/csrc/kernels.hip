@@ -95,7 +95,7 @@ __device__ __forceinline__ void mm_accumulate(const MMEntry & E, int row0, int t
                         float dw, mw;
                         const int sumi = block_dot<WF>(W, row, b, nb, alo[n], ahi[n], qs[n], dw, mw);
                         acc[r][n] = fmaf(dw * dx[n], (float)sumi, acc[r][n]);
-                        if constexpr (WF == W_Q4_1 || WF == W_Q5_1) acc2[r][n] += mw * sx[n];
+                        if constexpr (WF == W_Q4_1 || WF == W_Q5_1) acc2[r][n] = fmaf(mw, sx[n], acc2[r][n]);  // exact product
                     }
                 }
             }

@@ -276,7 +276,9 @@ struct FfnFused {
     unsigned tag;
     unsigned * err;
     unsigned spin_max;
-    int np;  // producer workgroups (set by launch_ffn_fused)
+    int np;       // producer workgroups (set by launch_ffn_fused)
+    int wdelay;   // consumers issue their value rows this many 100 MHz ticks after starting
+    int prepoll;  // 1: one wave polls each key block's d granule before the gather
 };
 bool ffn_fused_supported(const FfnFused & f, int form, bool hasr);
 bool launch_ffn_fused(hipStream_t st, FfnFused & f, int form, bool hasr);

@@ -173,11 +173,15 @@ __global__ __launch_bounds__(320) void k_v6_att_fused(Att6Fused a) {
             }
             const ActBuf xq = lds_act(smem, act_fmt_for(WF), C);
             if (a.wo_prepoll) {
-                if (wave == 0) gran_prepoll(a.ygran, H, S, S - 1, a.ytag, a.err, a.spin_max, lane);
+                if (wave == 0) {
+                    gran_prepoll(a.ygran, H, S, S - 1, a.ytag, a.err, a.spin_max, lane);
+                    STAMP_XN(2);
+                }
                 __syncthreads();
             }
             gran_gather_image<WF>(a.ygran, a.ytag, C, xq, wave, 5, a.err, a.spin_max, lane);
             __syncthreads();
+            if (wave == 0) STAMP_XN(3);
             if (wave < 4) {
                 const float s = rows_dot_img<WF, AF_WOR, U>(wo, xq, C, lane);
                 if (lane < AF_WOR && row0 + lane < C) a.xres[row0 + lane] = xr + s;  // EPI_ADD

@@ -165,7 +165,7 @@ __device__ __forceinline__ void dot_unit(const WBlk & w, const AUnit & x, float 
         float dw, mw;
         const int sumi = dot_wblk<WF>(w, x.lo, x.hi, x.qs, dw, mw);
         acc = fmaf(dw * x.d, (float)sumi, acc);
-        if constexpr (WF == W_Q4_1 || WF == W_Q5_1) acc2 += mw * x.s;
+        if constexpr (WF == W_Q4_1 || WF == W_Q5_1) acc2 = fmaf(mw, x.s, acc2);  // m * s exact (fp16 x fp16): = acc2 + m * s
     }
 }
 

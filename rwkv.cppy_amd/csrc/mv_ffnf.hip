@@ -11,13 +11,20 @@ extern template bool launch_ffn_fused_t<W_Q5_0>(hipStream_t, const FfnFused &, i
 extern template bool launch_ffn_fused_t<W_Q5_1>(hipStream_t, const FfnFused &, int, bool, int, int, dim3, int);
 extern template bool launch_ffn_fused_t<W_Q8_0>(hipStream_t, const FfnFused &, int, bool, int, int, dim3, int);
 
+extern int kQgCUs;
+
 bool ffn_fused_supported(const FfnFused & f, int form, bool hasr) {
     const MVEntry & k = f.e[0];
     const int t = k.W.type, C = k.W.K, F = k.W.M;
     if (!wtype_quantized(t) || !f.kg || !f.x || !f.err || (hasr && !f.rg)) return false;
     if (!(form == 0 && hasr) && !(form == 1)) return false;
     if (k.src != SRC_LNMIX || k.form != form || !k.emit || k.act_out.fmt != act_fmt_for(t) || k.act_out.tiled) return false;
-    if (C % 64 || C > 4096 || F % 32 || F / 32 > 512 || mv_units(t, F) > 8) return false;
+    if (C % 64 || C > 4096 || F % 32 || F / 32 > 512) return false;
+    // Only where the whole grid is resident at once with the consumers' value rows in registers:
+    // at most 4 units per lane (v6-1B6, v4-169M: 1.6 and 0.7 workgroups per CU) -- v7-2.9B (5 units,
+    // 1.9 per CU) measured 1871 vs 1838 us/token and v5-7B (7 units, 3.3 per CU: the consumers
+    // start a round late) 2029 vs 1528 against the two launches
+    if (mv_units(t, F) > 4 || F / 32 + (hasr ? C / 32 : 0) + C / (8 * FF_RC) > 2 * kQgCUs) return false;
     if (f.wv.type != t || f.wv.M != C || f.wv.K != F) return false;
     if (hasr) {
         const MVEntry & r = f.e[1];

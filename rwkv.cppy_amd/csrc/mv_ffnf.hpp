@@ -51,7 +51,13 @@ __global__ __launch_bounds__(512) void k_ffn_fused(FfnFused f) {
     unsigned * const err = f.err;
     const unsigned spin_max = f.spin_max;
     const int row0 = ((bx - f.np) * 8 + wave) * FF_RC;
-    // ---- this wave's value rows (all their units) and residual rows, in flight at once
+    // ---- this wave's value rows (all their units) and residual rows, in flight at once -- after
+    // wdelay ticks of the 100 MHz clock, so they do not share the memory system with the
+    // producers' key / receptance rows (whose arrival is on the critical path)
+    if (f.wdelay > 0) {
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)f.wdelay) __builtin_amdgcn_s_sleep(8);
+    }
     WBlk w[FF_RC][UV];
 #pragma unroll
     for (int u = 0; u < UV; u++)
@@ -61,7 +67,7 @@ __global__ __launch_bounds__(512) void k_ffn_fused(FfnFused f) {
     const float xr = f.x[myrow];
     const ActBuf img = lds_act(smem, act_fmt_for(WF), F);
     // ---- wait: wave 0 polls the d granule of every key block (UV per lane: nb <= 64 UV)
-    if (wave == 0) {
+    if (wave == 0 && f.prepoll) {
         for (unsigned it = 0;; it++) {
             unsigned long long x[UV];
 #pragma unroll

@@ -616,6 +616,8 @@ __global__ __launch_bounds__(256) void k_qgemm(MMGroup g) {
 // The m*s pass's arithmetic in packed f32 (v_pk_mul_f32 / v_pk_add_f32: per element the scalar
 // operations' bits, tools/pk_probe.hip; this file builds without the SLP vectorizer, so the packing
 // is spelled out): acc[j] = acc[j] + w * x[j] over pairs of outputs, and the class-tree folds.
+// m_w and s_x are fp16 values, so w * x is exact in f32 and acc + w * x IS fmaf(w, x, acc): one
+// v_pk_fma_f32 per pair instead of a v_pk_mul_f32 and a v_pk_add_f32 (the same bits).
 template <int N>
 __device__ __forceinline__ void qm_mac_row(float * acc, float w, const float (&x)[N]) {
     const qf2_t w2 = {w, w};
@@ -623,7 +625,7 @@ __device__ __forceinline__ void qm_mac_row(float * acc, float w, const float (&x
     for (int j = 0; j < N; j += 2) {
         qf2_t a = {acc[j], acc[j + 1]};
         const qf2_t x2 = {x[j], x[j + 1]};
-        a = a + w2 * x2;
+        a = __builtin_elementwise_fma(w2, x2, a);  // = a + w * x bit for bit: m_w * s_x is exact
         acc[j] = a.x;
         acc[j + 1] = a.y;
     }

@@ -150,3 +150,25 @@ def test_decode_after_sequence_bit_exact(tmp_path, arch, n_layer):
         assert _bits(lg, ref_lg), f'device decode after a {seq_len}-token sequence: logits'
         assert _bits(st, ref_st), f'device decode after a {seq_len}-token sequence: state'
     lib.rwkv_free(ctx)
+
+
+@pytest.mark.parametrize('knobs', [{'wo_rows': 4}, {'wo_prepoll': 0}, {'graphs': 0}, {'wo_rows': 4, 'wo_prepoll': 0}])
+def test_decode_knob_arms_bit_exact(tmp_path, knobs):
+    """The non-default arms of the per-context decode knobs (Switches): the fused-Wo
+    workgroup shape (4 rows per wave), the gather without the per-head pre-poll, and eager decode
+    launches without graphs -- each decodes the v6-1B6-width model bit-exactly like the defaults,
+    through both the host-state ABI and the device-resident path."""
+    lib = library().library
+    p = _model(tmp_path, 6, 2)
+    toks = [int(t) for t in np.random.default_rng(8).integers(0, VOCAB, 9)]
+    ctx = lib.rwkv_init_from_file(p.encode(), 1, 99)
+    ref = _serial(lib, ctx, toks)
+    dref = _device_serial(lib, ctx, toks)
+    assert _bits(ref[0], dref[0]) and _bits(ref[1], dref[1])
+    for k, v in knobs.items():
+        assert lib.rwkv_mi355x_debug_set(ctx, k.encode(), v), k
+    for run in (_serial, _device_serial):
+        lg, st = run(lib, ctx, toks)
+        assert _bits(lg, ref[0]), f'{knobs} {run.__name__}: logits'
+        assert _bits(st, ref[1]), f'{knobs} {run.__name__}: state'
+    lib.rwkv_free(ctx)

@@ -1,6 +1,6 @@
 """Decode a few tokens of the bench model with the stamp build (rwkv.cppy_amd/build_stamp) and
 summarize the per-launch phase stamps of one decode token (csrc/stamp.hpp).
-Usage: python tools/stamp_run.py [config] [out.bin]"""
+Usage: python tools/stamp_run.py [config] [out.bin] [knob=value,...]"""
 import ctypes
 import os
 import sys
@@ -24,6 +24,10 @@ os.makedirs('/tmp/rwkv_bench', exist_ok=True)
 if not os.path.isfile(path):
     assert L.rwkv_mi355x_write_synthetic_model(path.encode(), arch, V, C, NL, F, fmt.encode(), 1)
 ctx = lib.rwkv_init_from_file(path, 1, NL + 1)
+# optional per-context knobs (rwkv_mi355x_debug_set), e.g. "decode_fusion=127,wo_prepoll=0"
+for kv in [s for s in (sys.argv[3] if len(sys.argv) > 3 else '').split(',') if s]:
+    k, v = kv.split('=')
+    assert L.rwkv_mi355x_debug_set(ctx.ptr, k.encode(), int(v, 0)), k
 assert L.rwkv_mi355x_state_upload(ctx.ptr, None)
 tok = (ctypes.c_int32 * 1)(7)
 for i in range(12):

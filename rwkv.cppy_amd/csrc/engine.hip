@@ -11,6 +11,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
 #include <string>
 
 #include "kernels.hpp"
@@ -357,6 +358,7 @@ __global__ void k_init_state(float * st, size_t n, int C, int v4) {
 
 Engine::~Engine() {
     if (stream_) (void)hipStreamSynchronize(stream_);
+    release_device();
     stamp_dump();
     drop_graphs();
     drop_io_graphs();
@@ -434,11 +436,44 @@ bool Engine::init() {
 }
 
 void Engine::drop_graphs() {
-    for (int i = 0; i < 2; i++)
-        for (int j = 0; j < 2; j++) {
-            if (graphs_[i][j]) (void)hipGraphExecDestroy(graphs_[i][j]);
-            graphs_[i][j] = nullptr;
-        }
+    for (auto & pc : graphs_)
+        for (auto & pl : pc)
+            for (hipGraphExec_t & g : pl) {
+                if (g) (void)hipGraphExecDestroy(g);
+                g = nullptr;
+            }
+}
+
+// Contexts of this process with decode work queued per device (a context counts once from its
+// first decode launch until it synchronises its stream).  The co-resident v6 attention layout
+// (mv_att6c.hip) is safe only while its launches cannot share the compute units with another
+// context's waiting launches: a context picks it when the count is 1 (itself).  Two contexts that
+// claim at once both see 2; a context that picks it keeps the count until its launches finished.
+static std::atomic<int> g_dev_claims[64];
+
+void Engine::claim_device() {
+    if (claimed_) return;
+    claimed_ = true;
+    g_dev_claims[m_->device & 63].fetch_add(1);
+}
+
+void Engine::release_device() {
+    if (!claimed_) return;
+    claimed_ = false;
+    g_dev_claims[m_->device & 63].fetch_sub(1);
+}
+
+bool Engine::choose_co() {
+    claim_device();
+    bool co = co_knob_ == 1 || (co_knob_ < 0 && co_ok_ && g_dev_claims[m_->device & 63].load() == 1);
+    co = co && m_->major == 6 && (fuse_ & FUSE_ATT6) && (fuse_ & FUSE_WO6);
+    // the two layouts hand y to Wo in different granule forms under the same (layer, parity) tags:
+    // a switch clears them, so neither reads a value the other left
+    if (co_last_ >= 0 && co_last_ != (int)co) HIP_OK(hipMemsetAsync(ygran_, 0, tgran_n_ * 8, stream_));
+    co_last_ = co;
+    co_ = co;
+    co_pending_ += co;
+    return co;
 }
 
 bool Engine::ensure_workspace(int T) {
@@ -1483,12 +1518,14 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits, uint32
                                 2.0 * H * S * S * 4 + 4.0 * C * 4 + 2.0 * (4.0 * C + f.D) * 4 + act_bytes(a.yq, 1);
                     kt_flops_ = 2.0 * (4.0 * C + f.D) * C + 2.0 * C * f.D;
                     if (wo_in) {
-                        // Wo weights, the y granules written and gathered, x read and written
-                        kt_bytes_ += wbytes(L.att_o) + 2.0 * C * 8 + 2.0 * C * 4 - act_bytes(a.yq, 1);
+                        // Wo weights, the y granules (Q8 blocks) written and gathered, x read and written
+                        kt_bytes_ += wbytes(L.att_o) + 2.0 * KG_STRIDE * (C / 32) * 8 + 2.0 * C * 4 - act_bytes(a.yq, 1);
                         kt_flops_ += 2.0 * C * C;
                     }
                 }
-                if (!launch_v6_att_fused(stream_, f)) return false;
+                // the co-resident layout when this context has the device to itself (choose_co)
+                if (co_ && v6_att_co_supported(f) ? !launch_v6_att_co(stream_, f) : !launch_v6_att_fused(stream_, f))
+                    return false;
             } else {
                 MV c;
                 for (int i = 0; i < 5; i++) {
@@ -1714,6 +1751,8 @@ bool Engine::run_tokens(const uint32_t * tokens, size_t T, bool want_logits) {
         // the call's tagged Wo-input granules must not satisfy a replay of the same parity
         (void)hipMemsetAsync(ygran_, 0, tgran_n_ * 8, stream_);
         (void)hipStreamSynchronize(stream_);
+        co_last_ = -1;
+        release_device();
         cur_ = cur0;
         return false;
     }
@@ -1739,6 +1778,7 @@ bool Engine::run_tokens_impl(const uint32_t * tokens, size_t T, bool want_logits
         }
         const bool lg = last && want_logits;
         last_decode_ = n == 1 && !generic_decode_;
+        const bool co = last_decode_ ? choose_co() : (co_ = false);
         if (timing_) {
             // eager launches; a decode step's kernels each carry a dispatch-bound event pair
             // (RK_LAUNCH through g_klt), the sequence path's matmul groups an event pair around
@@ -1748,7 +1788,7 @@ bool Engine::run_tokens_impl(const uint32_t * tokens, size_t T, bool want_logits
             g_klt = nullptr;
             if (!ok) return false;
         } else if (n == 1 && use_graphs_) {
-            hipGraphExec_t & ge = graphs_[cur_][lg ? 1 : 0];
+            hipGraphExec_t & ge = graphs_[co][cur_][lg ? 1 : 0];
             if (!ge) {
                 hipGraph_t g = nullptr;
                 HIP_OK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
@@ -1769,7 +1809,10 @@ bool Engine::run_tokens_impl(const uint32_t * tokens, size_t T, bool want_logits
         // readers.  A step that did not run the fused decode flips the parity without writing them,
         // so the next decode would run at the parity of the decode before this step and could take
         // a value that step left (one-layer engines: the same layer tag).  Clear them in stream order.
-        if (n > 1 || generic_decode_) HIP_OK(hipMemsetAsync(ygran_, 0, tgran_n_ * 8, stream_));
+        if (n > 1 || generic_decode_) {
+            HIP_OK(hipMemsetAsync(ygran_, 0, tgran_n_ * 8, stream_));
+            co_last_ = -1;
+        }
         // tokens buffer is reused by the next chunk: wait before overwriting the pinned copy
         if (!last) HIP_OK(hipStreamSynchronize(stream_));
         cur_ ^= 1;
@@ -1825,13 +1868,26 @@ bool Engine::sync() {
 // producer that arrives after the timeout leaves its granule tagged, which the next launch would
 // read as its own value, so every granule is cleared before the flag is re-armed.
 bool Engine::handoff_check() {
+    // called after the stream has drained: nothing of this context is queued any more
+    release_device();
+    const bool co_seen = co_pending_ > 0;
+    co_pending_ = 0;
     if (*(volatile unsigned *)herr_h_ == 0) return true;
     (void)hipStreamSynchronize(stream_);
     (void)hipMemsetAsync(hgran_, 0, hgran_n_ * 8, stream_);
     (void)hipMemsetAsync(ygran_, 0, tgran_n_ * 8, stream_);
     (void)hipStreamSynchronize(stream_);
     *(volatile unsigned *)herr_h_ = 0;
-    fprintf(stderr, "rwkv: in-launch hand-off timed out (k_v6_att_fused): the evaluation's results are invalid\n");
+    if (co_seen && co_knob_ < 0) {
+        // the co-resident layout lost its co-residency (another process's launches on the device):
+        // this context uses the ordered layout from now on; a synchronous one-token call re-runs
+        co_ok_ = false;
+        co_retry_ = true;
+        fprintf(stderr, "rwkv: in-launch hand-off timed out in the co-resident attention layout; using the ordered layout\n");
+    } else {
+        fprintf(stderr, "rwkv: in-launch hand-off timed out: the evaluation's results are invalid\n");
+    }
+    co_last_ = -1;
     return false;
 }
 
@@ -1848,6 +1904,7 @@ bool Engine::debug_set(const char * name, long long value) {
     else if (n == "wkv_chunk") wkv_chunk_ = value != 0;
     else if (n == "generic_decode") generic_decode_ = value != 0 || m_->n_embed > 4096;
     else if (n == "graphs") use_graphs_ = value != 0;
+    else if (n == "co_mode" && value >= -1 && value <= 1) co_knob_ = (int)value;
     else if (n == "decode_fusion") fuse_ = (unsigned)value & FUSE_ALL;
     else if (n == "wo_rows" && (value == 4 || value == 8)) wo_rows_ = (int)value;
     else if (n == "wo_prepoll") wo_prepoll_ = value != 0;
@@ -1861,6 +1918,7 @@ bool Engine::debug_set(const char * name, long long value) {
     drop_io_graphs();
     (void)hipMemsetAsync(ygran_, 0, tgran_n_ * 8, stream_);
     (void)hipStreamSynchronize(stream_);
+    co_last_ = -1;
     return true;
 }
 
@@ -1909,7 +1967,8 @@ bool Engine::eval_host_chunked(uint32_t token, const float * state_in, float * s
         for (auto & e : io_ev_) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
     const bool lg = logits_out != nullptr;
-    std::vector<hipGraphExec_t> & gs = io_graphs_[cur_][lg ? 1 : 0];
+    const bool co = choose_co();
+    std::vector<hipGraphExec_t> & gs = io_graphs_[co][cur_][lg ? 1 : 0];
     if (gs.size() != NC) {
         for (hipGraphExec_t g : gs)
             if (g) (void)hipGraphExecDestroy(g);
@@ -1993,15 +2052,28 @@ bool Engine::eval_host_chunked(uint32_t token, const float * state_in, float * s
 }
 
 void Engine::drop_io_graphs() {
-    for (auto & p : io_graphs_)
-        for (auto & v : p) {
-            for (hipGraphExec_t g : v)
-                if (g) (void)hipGraphExecDestroy(g);
-            v.clear();
-        }
+    for (auto & pc : io_graphs_)
+        for (auto & p : pc)
+            for (auto & v : p) {
+                for (hipGraphExec_t g : v)
+                    if (g) (void)hipGraphExecDestroy(g);
+                v.clear();
+            }
 }
 
 bool Engine::eval(const uint32_t * tokens, size_t T, const float * state_in, float * state_out, float * logits_out) {
+    co_retry_ = false;
+    const int pend0 = co_pending_;
+    if (eval_once(tokens, T, state_in, state_out, logits_out)) return true;
+    // a co-resident layout timeout in this call's own launches (none of an earlier asynchronous
+    // call was pending): the inputs are untouched (host state_in, or the device state this call
+    // started from), so the call runs again, in the ordered layout
+    if (!co_retry_ || pend0 > 0) return false;
+    co_retry_ = false;
+    return eval_once(tokens, T, state_in, state_out, logits_out);
+}
+
+bool Engine::eval_once(const uint32_t * tokens, size_t T, const float * state_in, float * state_out, float * logits_out) {
     HIP_OK(hipSetDevice(m_->device));
     // one token with host state: chunked decode, copies overlapped (needs graphs; timing and the
     // generic decode path keep the whole-state copies)
@@ -2035,6 +2107,7 @@ bool Engine::eval(const uint32_t * tokens, size_t T, const float * state_in, flo
 bool Engine::eval_layers(const uint32_t * tokens, size_t T, uint32_t l0, uint32_t l1, float * x_io, float * vfirst_io,
                          bool want_logits, float * logits_out, bool sync) {
     HIP_OK(hipSetDevice(m_->device));
+    co_ = false;  // pipeline stages: the ordered layouts only
     if (!ensure_workspace((int)T)) return false;
     const size_t bytes = T * (size_t)m_->n_embed * 4;
     if (l0 == 0) {
@@ -2115,6 +2188,7 @@ long long Engine::debug_copy(const char * name, void * out, size_t bytes) {
 bool Engine::eval_batch(const uint32_t * tokens, size_t B, const float * state_in, float * state_out,
                         float * logits_out, bool dev) {
     HIP_OK(hipSetDevice(m_->device));
+    co_ = false;  // batched decode: the ordered layouts only
     if (B == 0) return true;
     if (B > (size_t)kBatchMax) {
         fprintf(stderr, "rwkv: batched decode takes at most %d contexts (got %zu)\n", kBatchMax, B);
@@ -2235,14 +2309,22 @@ void Engine::drop_batch_graphs() {
 
 bool Engine::eval_device(const uint32_t * tokens, size_t T, bool want_logits, float * logits_out, bool sync_after) {
     HIP_OK(hipSetDevice(m_->device));
-    if (!run_tokens(tokens, T, want_logits || logits_out != nullptr)) return false;
-    if (logits_out)
-        HIP_OK(hipMemcpyAsync(logits_out, logits_, (size_t)m_->n_vocab * 4, hipMemcpyDeviceToHost, stream_));
-    if (sync_after || logits_out) {
+    const int cur0 = cur_, pend0 = co_pending_;
+    co_retry_ = false;
+    for (int attempt = 0;; attempt++) {
+        if (!run_tokens(tokens, T, want_logits || logits_out != nullptr)) return false;
+        if (logits_out)
+            HIP_OK(hipMemcpyAsync(logits_out, logits_, (size_t)m_->n_vocab * 4, hipMemcpyDeviceToHost, stream_));
+        if (!(sync_after || logits_out)) return true;
         HIP_OK(hipStreamSynchronize(stream_));
-        return handoff_check();
+        if (handoff_check()) return true;
+        // a co-resident layout timeout in this one-token call (an earlier asynchronous call's
+        // timeout cannot be re-run: its state has moved on): run the token again from the state it
+        // started from, in the ordered layout
+        if (!co_retry_ || pend0 > 0 || attempt > 0 || T != 1 || cur_ != (cur0 ^ 1)) return false;
+        co_retry_ = false;
+        cur_ = cur0;
     }
-    return true;
 }
 
 }  // namespace rwkvmi

@@ -85,6 +85,7 @@ class Engine : public KLaunchTimer {
 
     bool init();
     // ABI-level evaluation (host buffers).  tokens host, T >= 1.
+    bool eval_once(const uint32_t * tokens, size_t T, const float * state_in, float * state_out, float * logits_out);
     bool eval(const uint32_t * tokens, size_t T, const float * state_in, float * state_out, float * logits_out);
     // device-resident evaluation on the context's own state
     bool eval_device(const uint32_t * tokens, size_t T, bool want_logits, float * logits_out, bool sync);
@@ -171,7 +172,7 @@ class Engine : public KLaunchTimer {
     bool wkv_chunk_ = false;
     float * wkvc_ = nullptr;  // its chunk matrices / chunk states
     size_t wkvc_cap_ = 0;
-    hipGraphExec_t graphs_[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // [cur][logits]
+    hipGraphExec_t graphs_[2][2][2] = {};  // [co-resident layout][cur][logits]
     bool use_graphs_ = true;
     bool split_maa_ = false;       // RWKV_MI355X_SPLIT_MAA=1: v6 decode W1 + mix as two launches
     // Decode fusions (RWKV_MI355X_DECODE_FUSION, a mask read at init; rwkv_mi355x_debug_set
@@ -185,9 +186,26 @@ class Engine : public KLaunchTimer {
         FUSE_SIG = 32,   // k_mvsig (FFN value + receptance rows)
         FUSE_FFN = 64,   // k_ffn_fused (the whole channel mix: key, receptance and value rows)
         FUSE_ALL = 127,
-        FUSE_DEFAULT = FUSE_ALL,
+        // the one-launch channel mix measured slower than the key + value pair (same box, separate
+        // processes: v6-1B6 716 vs 692 us/token, v4-169M 234 vs 228): off by default
+        FUSE_DEFAULT = FUSE_ALL & ~FUSE_FFN,
     };
     unsigned fuse_ = FUSE_DEFAULT;
+    // v6 attention launch layout (mv_att6c.hip vs mv_att6f.hip, the same bits).  The co-resident
+    // layout needs all its workgroups resident at once: it is used only while this context is the
+    // process's only one with work queued on the device (claim_device / the per-device count) and
+    // until a hand-off timeout (another process's launches holding the compute units) turns it off
+    // for the context.  co_knob_ ("co_mode"): -1 that rule, 0 never, 1 always (tests, A/B).
+    int co_knob_ = -1;
+    bool co_ok_ = true;       // cleared for good by a hand-off timeout in the co-resident layout
+    bool co_ = false;         // the layout the launches being enqueued / captured use
+    int co_last_ = -1;        // the layout of the last decode enqueued (-1: none since a clear)
+    bool claimed_ = false;    // this context holds one count on its device (released at a sync)
+    bool co_retry_ = false;   // the last failed check saw co-resident layout launches
+    int co_pending_ = 0;      // co-resident layout decodes enqueued since the last check
+    void claim_device();
+    void release_device();
+    bool choose_co();         // claim the device, pick the layout for the next decode launches
     int wo_rows_ = 8;      // k_v6_att_fused: Wo rows per wave of a Wo workgroup (debug knob "wo_rows": 4 / 8)
     int ffn_wdelay_ = -1;  // k_ffn_fused: consumer weight-issue delay in 100 MHz ticks ("ffn_wdelay"; -1:
                            // the producers' weight bytes at 4 TB/s, so the two streams do not overlap)
@@ -241,7 +259,7 @@ class Engine : public KLaunchTimer {
     hipStream_t io_stream_[2] = {nullptr, nullptr};
     std::vector<hipEvent_t> io_ev_;
     hipEvent_t io_entry_ev_ = nullptr;  // work already queued on stream_ at entry (copy streams wait)
-    std::vector<hipGraphExec_t> io_graphs_[2][2];  // [cur][logits] per chunk
+    std::vector<hipGraphExec_t> io_graphs_[2][2][2];  // [co-resident layout][cur][logits] per chunk
     bool eval_host_chunked(uint32_t token, const float * state_in, float * state_out, float * logits_out);
     bool pinned_io(const float * state_in, const float * state_out);
     void drop_io_graphs();

@@ -240,6 +240,10 @@ struct Att6Fused {
 };
 bool v6_att_fused_supported(const Att6Fused & a);
 bool launch_v6_att_fused(hipStream_t st, const Att6Fused & a);
+// the same launch in the co-resident layout (mv_att6c.hip: 8 H workgroups that must all be
+// resident at once; Wo fused, C % 512 == 0): the same bits, used by Engine::co_mode only
+bool v6_att_co_supported(const Att6Fused & a);
+bool launch_v6_att_co(hipStream_t st, const Att6Fused & a);
 // v4 decode: LN + token shift, r / k / v rows and WKV-4 in one launch, 8 channels per workgroup
 // (mv_att4f.hip); the two-launch k_mv + k_wkv4 pair gives the same bits.  Without wf, Wo's input
 // is written as fp32 y (Wo quantizes it in its prologue).

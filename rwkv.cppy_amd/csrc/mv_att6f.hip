@@ -29,119 +29,13 @@
 // 16g + 4kk + q (q < 4) of value columns 4jq..4jq+3.  Each output column's sum keeps
 // k_att6_dec's association: ((t0 + t1) + t2) + t3 per 4-key run (from +0), (p0 + p1) + (p2 + p3)
 // per 16-key group, (s0 + s2) + (s1 + s3) over the groups.
-#include "mv_common.hpp"
+#include "mv_att6.hpp"
 
 #include <stdlib.h>
 
 #include <algorithm>
 
 namespace rwkvmi {
-
-typedef __attribute__((address_space(1))) float gfloat_t;
-typedef __attribute__((address_space(1))) unsigned gunsigned_t;
-
-__device__ __forceinline__ void st_sc1(float * p, float v) {
-    __hip_atomic_store((gfloat_t *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float ld_sc1(const float * p) {
-    return __hip_atomic_load((gfloat_t *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ unsigned ldu_sc1(unsigned * p) {
-    return __hip_atomic_load((gunsigned_t *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void stu_sc1(unsigned * p, unsigned v) {
-    __hip_atomic_store((gunsigned_t *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ unsigned addu(unsigned * p, unsigned v) {
-    return __hip_atomic_fetch_add((gunsigned_t *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-constexpr int AF_P = 8;   // workgroups per head
-constexpr int AF_R = 8;   // rows per wave (4 waves x 8 rows x 8 workgroups = 4 x 64 rows)
-
-// R rows of one matrix by one wave: k_mva's loads, dots, tree and epilogue (lane r: row r)
-template <int WF, int R, int U>
-__device__ __forceinline__ float af_rows(const DMat & W, const ActBuf & x, int row0, int epi, int lane) {
-    const int M = W.M, K = W.K;
-    int rows[R];
-#pragma unroll
-    for (int r = 0; r < R; r++) rows[r] = min(row0 + r, M - 1);
-    WBlk w[R][U];
-#pragma unroll
-    for (int u = 0; u < U; u++)
-#pragma unroll
-        for (int r = 0; r < R; r++) w[r][u] = load_unit<WF>(W, rows[r], u, lane);
-    AUnit xu[U];
-#pragma unroll
-    for (int u = 0; u < U; u++) xu[u] = load_act_unit<WF, false>(x, u, lane);
-    __builtin_amdgcn_sched_barrier(0);
-    float acc[R], acc2[R];
-#pragma unroll
-    for (int r = 0; r < R; r++) acc[r] = acc2[r] = 0.0f;
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-        const bool valid = unit_valid<WF>(K, u, lane);
-#pragma unroll
-        for (int r = 0; r < R; r++) {
-            float t = acc[r], t2 = acc2[r];
-            dot_unit<WF>(w[r][u], xu[u], t, t2);
-            acc[r] = valid ? t : acc[r];
-            acc2[r] = valid ? t2 : acc2[r];
-        }
-    }
-    constexpr bool one = WF == W_Q4_1 || WF == W_Q5_1;
-    float sr[R];
-#pragma unroll
-    for (int r = 0; r < R; r++) sr[r] = one ? wave_sum63(acc[r]) + wave_sum63(acc2[r]) : wave_sum63(acc[r]) + 0.0f;
-    const float s = lane_row_sum<R>(sr, lane);
-    return epi == EPI_SILU ? siluf_(s) : epi == EPI_TANH ? rk_tanhf(s) : s;
-}
-
-typedef __attribute__((address_space(1))) unsigned long long gu64_t;
-
-// One granule = {tag 1 (high word), value bits (low word)}, ONE aligned 8-byte sc1 store: the data is
-// its own flag (MI355X_MICROARCH.md hand-off R2, guide Guideline 16).  A consumer sweeps its
-// granules until every tag reads 1 and then clears them to 0 (sc1), so the next launch can never
-// see a stale value: a granule is only ever 0 (empty) or this launch's value.
-__device__ __forceinline__ void gran_put(unsigned long long * g, float v) {
-    __hip_atomic_store((gu64_t *)g, (1ull << 32) | (unsigned long long)__float_as_uint(v), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void gran_put_tag(unsigned long long * g, float v, unsigned tag) {
-    __hip_atomic_store((gu64_t *)g, ((unsigned long long)tag << 32) | (unsigned long long)__float_as_uint(v),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ unsigned long long gran_get(const unsigned long long * g) {
-    return __hip_atomic_load((gu64_t *)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void gran_clear(unsigned long long * g) {
-    __hip_atomic_store((gu64_t *)g, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// One wave sweeps N granules per lane (stride S) until every tag is set; bounded (timeout: *err, a
-// host-mapped word, stored at system scope so the host sees it after the stream synchronises).
-template <int N>
-__device__ __forceinline__ void gran_sweep(const unsigned long long * g, int stride, bool (&live)[N], float (&v)[N],
-                                           unsigned * err, unsigned spin_max) {
-    for (unsigned it = 0;; it++) {
-        bool ok = true;
-        unsigned long long x[N];
-#pragma unroll
-        for (int k = 0; k < N; k++) x[k] = live[k] ? gran_get(g + k * stride) : (1ull << 32);
-#pragma unroll
-        for (int k = 0; k < N; k++) {
-            v[k] = __uint_as_float((unsigned)x[k]);
-            ok = ok && (x[k] >> 32) == 1ull;
-        }
-        if (__all(ok)) return;
-        if (it >= spin_max) {
-            __hip_atomic_store((gunsigned_t *)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            return;
-        }
-        __builtin_amdgcn_s_sleep(1);
-    }
-}
-
 
 // WOR: Wo rows per wave of a Wo workgroup (4 waves: 4 WOR rows); 0 = no Wo in this launch
 template <int WF, int U, int WD, int WOR>
@@ -171,15 +65,22 @@ __global__ __launch_bounds__(320) void k_v6_att_fused(Att6Fused a) {
                     for (int r = 0; r < AF_WOR; r++) wo[r][u] = load_unit<WF>(a.wo, min(row0 + r, C - 1), u, lane);
                 xr = a.xres[min(row0 + min(lane, AF_WOR - 1), C - 1)];
             }
+            // y arrives as Q8 blocks (pub_q8 in the reducers: the bits Wo's fp32-input prologue
+            // would produce), KG_STRIDE granules per 32 outputs
             const ActBuf xq = lds_act(smem, act_fmt_for(WF), C);
+            const int nb = C >> 5;
             if (a.wo_prepoll) {
                 if (wave == 0) {
-                    gran_prepoll(a.ygran, H, S, S - 1, a.ytag, a.err, a.spin_max, lane);
+                    for (int b0 = 0; b0 < nb; b0 += 64)
+                        gran_prepoll(a.ygran + (size_t)b0 * KG_STRIDE, min(64, nb - b0), KG_STRIDE, 8, a.ytag, a.err,
+                                     a.spin_max, lane);
                     STAMP_XN(2);
                 }
                 __syncthreads();
             }
-            gran_gather_image<WF>(a.ygran, a.ytag, C, xq, wave, 5, a.err, a.spin_max, lane);
+            q8_gather_image<(U > 1 ? 4 : 2)>(a.ygran, nb, a.ytag, xq, threadIdx.x, 320, a.err, a.spin_max);
+            __syncthreads();
+            q8_image_qsum(xq, nb, threadIdx.x, 320);
             __syncthreads();
             if (wave == 0) STAMP_XN(3);
             if (wave < 4) {
@@ -330,7 +231,7 @@ __global__ __launch_bounds__(320) void k_v6_att_fused(Att6Fused a) {
         o = o * lnw_c;
         o = o + lnb_c;
         o = o * sg[lane];
-        if constexpr (WO) gran_put_tag(a.ygran + c0 + lane, o, a.ytag);
+        if constexpr (WO) pub_q8(a.ygran, (c0 >> 5) + (lane >> 5), o, a.ytag, lane);  // the head's 2 blocks
         else emit32(yq, 0, c0 + lane, o);
     }
     STAMP_END(6);

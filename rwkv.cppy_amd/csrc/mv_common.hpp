@@ -357,7 +357,8 @@ __device__ __forceinline__ void gran_gather_image(const unsigned long long * yg,
 // Wait before a gather: ONE wave polls n granules (lane i: yg[off + i * stride], n <= 64) with a
 // sleep between passes until every tag reads `tag` -- a few hundred bytes per pass instead of the
 // gather's whole vector, so a waiting workgroup adds little traffic beside the producers' weight
-// streams (the gather after it checks every tag again).  Bounded like the gather.
+// streams (the gather after it checks every tag again).  Bounded like the gather.  (Several passes
+// in flight at once -- a rolling poll -- measured far slower: v6-1B6 750 vs 693 us/token.)
 __device__ __forceinline__ void gran_prepoll(const unsigned long long * yg, int n, int stride, int off, unsigned tag,
                                              unsigned * err, unsigned spin_max, int lane) {
     for (unsigned it = 0;; it++) {
@@ -370,6 +371,55 @@ __device__ __forceinline__ void gran_prepoll(const unsigned long long * yg, int 
             return;
         }
         __builtin_amdgcn_s_sleep(4);
+    }
+}
+
+// Q8 blocks published by pub_q8 (KG_STRIDE granules per 32-element block, nb blocks) -> the LDS
+// activation image: thread tid of nthr reads granules tid + nthr i (i < GI), re-reading until every
+// tag it holds reads `tag` (bounded like the gather above), then writes the q dwords, d and Q8_1's
+// s.  The caller recomputes the qsums (q8_image_qsum) after a barrier.
+template <int GI>
+__device__ __forceinline__ void q8_gather_image(const unsigned long long * kg, int nb, unsigned tag, const ActBuf & img,
+                                                int tid, int nthr, unsigned * err, unsigned spin_max) {
+    const int ng = KG_STRIDE * nb;
+    unsigned pay[GI];
+    for (unsigned it = 0;; it++) {
+        bool ok = true;
+#pragma unroll
+        for (int i = 0; i < GI; i++) {
+            const int g = tid + nthr * i;
+            unsigned long long x = (unsigned long long)tag << 32;
+            if (g < ng) x = __hip_atomic_load((gran_u64_t *)(kg + g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            pay[i] = (unsigned)x;
+            ok = ok && (unsigned)(x >> 32) == tag;
+        }
+        if (__all(ok)) break;
+        if (it >= spin_max) {
+            __hip_atomic_store((gran_u32_t *)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+#pragma unroll
+    for (int i = 0; i < GI; i++) {
+        const int g = tid + nthr * i;
+        if (g < ng) {
+            const int b = g / KG_STRIDE, j = g - b * KG_STRIDE;
+            if (j < 8) *(unsigned *)(img.q + (size_t)b * 32 + 4 * j) = pay[i];
+            else if (j == 8) img.d[b] = __uint_as_float(pay[i]);
+            else if (img.fmt == A_Q8_1) img.s[b] = __uint_as_float(pay[i]);
+        }
+    }
+}
+// the exact integer block sums of a gathered Q8 image (store32's qsum)
+__device__ __forceinline__ void q8_image_qsum(const ActBuf & img, int nb, int tid, int nthr) {
+    for (int b = tid; b < nb; b += nthr) {
+        const int4 lo = *(const int4 *)(img.q + (size_t)b * 32), hi = *(const int4 *)(img.q + (size_t)b * 32 + 16);
+        const int ws[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        int s = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) s = __builtin_amdgcn_sdot4(ws[k], 0x01010101, s, false);
+        img.qsum[b] = s;
     }
 }
 

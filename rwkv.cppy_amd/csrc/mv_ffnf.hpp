@@ -66,28 +66,10 @@ __global__ __launch_bounds__(512) void k_ffn_fused(FfnFused f) {
     const int myrow = min(row0 + min(lane, FF_RC - 1), C - 1);
     const float xr = f.x[myrow];
     const ActBuf img = lds_act(smem, act_fmt_for(WF), F);
-    // ---- wait: wave 0 polls the d granule of every key block (UV per lane: nb <= 64 UV)
+    // ---- wait: wave 0 polls the d granule of every key block (64 blocks per rolling poll)
     if (wave == 0 && f.prepoll) {
-        for (unsigned it = 0;; it++) {
-            unsigned long long x[UV];
-#pragma unroll
-            for (int i = 0; i < UV; i++) {
-                const int b = lane + 64 * i;
-                x[i] = (unsigned long long)tag << 32;
-                if (b < nb)
-                    x[i] = __hip_atomic_load((gran_u64_t *)(f.kg + (size_t)b * KG_STRIDE + 8), __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT);
-            }
-            bool ok = true;
-#pragma unroll
-            for (int i = 0; i < UV; i++) ok = ok && (unsigned)(x[i] >> 32) == tag;
-            if (__all(ok)) break;
-            if (it >= spin_max) {
-                __hip_atomic_store((gran_u32_t *)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(4);
-        }
+        for (int b0 = 0; b0 < nb; b0 += 64)
+            gran_prepoll(f.kg + (size_t)b0 * KG_STRIDE, min(64, nb - b0), KG_STRIDE, 8, tag, err, spin_max, lane);
         STAMP_XN(0);
     }
     __syncthreads();

@@ -11,6 +11,12 @@ threads -- through rwkv_eval (host state) and through rwkv_mi355x_eval_device (e
 stream) -- at the BASELINE widths where the fused launches are on (v6 C = 2048, v4 C = 768): every
 call must succeed and every context must equal its own serial run bit for bit.
 
+The v6 attention launch has two layouts with the same bits: the ordered one above, and a
+co-resident one (mv_att6c.hip) that needs all its workgroups resident and that a context uses only
+while it is the process's only context with decode work queued on the device.  The serial
+reference runs here use the co-resident layout (one context), the concurrent clones mostly the
+ordered one: bit-equality covers both.
+
 test_decode_after_sequence_* (ADVICE round 5): the Wo hand-off tags carry (layer, state parity); a
 sequence evaluation flips the parity without writing them, so a later decode must never accept a
 value left by the decode before the sequence.  One-layer models make that the only layer: decode,
@@ -152,11 +158,18 @@ def test_decode_after_sequence_bit_exact(tmp_path, arch, n_layer):
     lib.rwkv_free(ctx)
 
 
-@pytest.mark.parametrize('knobs', [{'wo_rows': 4}, {'wo_prepoll': 0}, {'graphs': 0}, {'wo_rows': 4, 'wo_prepoll': 0}])
+@pytest.mark.parametrize('knobs', [{'wo_rows': 4}, {'wo_prepoll': 0}, {'graphs': 0}, {'wo_rows': 4, 'wo_prepoll': 0},
+                                   {'co_mode': 0}, {'co_mode': 1}, {'co_mode': 0, 'wo_rows': 4},
+                                   {'decode_fusion': 127}, {'decode_fusion': 127, 'ffn_wdelay': 0},
+                                   {'decode_fusion': 127, 'ffn_prepoll': 0}])
 def test_decode_knob_arms_bit_exact(tmp_path, knobs):
     """The non-default arms of the per-context decode knobs (Switches): the fused-Wo
-    workgroup shape (4 rows per wave), the gather without the per-head pre-poll, and eager decode
-    launches without graphs -- each decodes the v6-1B6-width model bit-exactly like the defaults,
+    workgroup shape (4 rows per wave), the gather without the per-head pre-poll, eager decode
+    launches without graphs, and the v6 attention layout forced (co_mode 0: the ordered layout of
+    mv_att6f.hip; 1: the co-resident one of mv_att6c.hip; default: co-resident while the context is
+    alone on the device), and the one-launch channel mix (decode_fusion 127, off by default) with its
+    consumer weight delay off and without its pre-poll -- each decodes the v6-1B6-width model
+    bit-exactly like the defaults,
     through both the host-state ABI and the device-resident path."""
     lib = library().library
     p = _model(tmp_path, 6, 2)

@@ -232,15 +232,18 @@ def test_v6_decode_handoff_many_tokens(cfg_dir):
     m.free()
 
 
+@pytest.mark.parametrize('co_mode', [-1, 0, 1])
 @pytest.mark.parametrize('skip_wg', [9, 8 * 31 + 7])
-def test_v6_decode_handoff_timeout_fails_the_call(cfg_dir, skip_wg):
+def test_v6_decode_handoff_timeout_fails_the_call(cfg_dir, skip_wg, co_mode):
     """A hand-off that times out must fail the evaluation, never return garbage with success
     (reference error convention: false + RWKV_ERROR_CTX, rwkv_error_handling.inc:1-54).  The test hook
     makes one producer workgroup of k_v6_att_fused publish nothing (9: head 9's first 32 rows and
     decay-LoRA row 9; 255: head 31's last 32 rows) with a short sweep bound.  rwkv_eval (host
     state, the chunked graphs) and rwkv_mi355x_eval_device + rwkv_mi355x_sync both fail with
     RWKV_ERROR_CTX; with the hook off the same context then decodes bit-exactly again (the granules
-    were cleared and the flag re-armed)."""
+    were cleared and the flag re-armed).  co_mode: the attention layout rule (-1: co-resident while
+    alone, the call re-run in the ordered layout after a co-resident timeout -- which times out
+    again here; 0: ordered; 1: co-resident)."""
     import ctypes
     L = library().library
     path = cfg_model(cfg_dir, 'v6-1b6-q4_0')
@@ -252,6 +255,7 @@ def test_v6_decode_handoff_timeout_fails_the_call(cfg_dir, skip_wg):
     fp = ctypes.POINTER(ctypes.c_float)
     ref_lg, ref_st = gpu_variant(path, toks)
     E_CTX = 6 << 8  # RWKV_ERROR_CTX (reference rwkv.h:50; flags = category | code)
+    assert L.rwkv_mi355x_debug_set(ctx, b'co_mode', co_mode)
     assert L.rwkv_mi355x_debug_set(ctx, b'spin_max', 2048)
     assert L.rwkv_mi355x_debug_set(ctx, b'skip_granule', skip_wg)
     st = np.zeros(n_state, np.float32)

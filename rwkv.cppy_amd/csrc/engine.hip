@@ -467,10 +467,8 @@ bool Engine::choose_co() {
     claim_device();
     bool co = co_knob_ == 1 || (co_knob_ < 0 && co_ok_ && g_dev_claims[m_->device & 63].load() == 1);
     co = co && m_->major == 6 && (fuse_ & FUSE_ATT6) && (fuse_ & FUSE_WO6);
-    // the two layouts hand y to Wo in different granule forms under the same (layer, parity) tags:
-    // a switch clears them, so neither reads a value the other left
-    if (co_last_ >= 0 && co_last_ != (int)co) HIP_OK(hipMemsetAsync(ygran_, 0, tgran_n_ * 8, stream_));
-    co_last_ = co;
+    // (both layouts hand y to Wo as the same Q8-block granules under the same tags: a switch needs
+    // no clearing)
     co_ = co;
     co_pending_ += co;
     return co;
@@ -1751,7 +1749,6 @@ bool Engine::run_tokens(const uint32_t * tokens, size_t T, bool want_logits) {
         // the call's tagged Wo-input granules must not satisfy a replay of the same parity
         (void)hipMemsetAsync(ygran_, 0, tgran_n_ * 8, stream_);
         (void)hipStreamSynchronize(stream_);
-        co_last_ = -1;
         release_device();
         cur_ = cur0;
         return false;
@@ -1811,7 +1808,6 @@ bool Engine::run_tokens_impl(const uint32_t * tokens, size_t T, bool want_logits
         // a value that step left (one-layer engines: the same layer tag).  Clear them in stream order.
         if (n > 1 || generic_decode_) {
             HIP_OK(hipMemsetAsync(ygran_, 0, tgran_n_ * 8, stream_));
-            co_last_ = -1;
         }
         // tokens buffer is reused by the next chunk: wait before overwriting the pinned copy
         if (!last) HIP_OK(hipStreamSynchronize(stream_));
@@ -1887,7 +1883,6 @@ bool Engine::handoff_check() {
     } else {
         fprintf(stderr, "rwkv: in-launch hand-off timed out: the evaluation's results are invalid\n");
     }
-    co_last_ = -1;
     return false;
 }
 
@@ -1918,7 +1913,6 @@ bool Engine::debug_set(const char * name, long long value) {
     drop_io_graphs();
     (void)hipMemsetAsync(ygran_, 0, tgran_n_ * 8, stream_);
     (void)hipStreamSynchronize(stream_);
-    co_last_ = -1;
     return true;
 }
 

@@ -199,7 +199,6 @@ class Engine : public KLaunchTimer {
     int co_knob_ = -1;
     bool co_ok_ = true;       // cleared for good by a hand-off timeout in the co-resident layout
     bool co_ = false;         // the layout the launches being enqueued / captured use
-    int co_last_ = -1;        // the layout of the last decode enqueued (-1: none since a clear)
     bool claimed_ = false;    // this context holds one count on its device (released at a sync)
     bool co_retry_ = false;   // the last failed check saw co-resident layout launches
     int co_pending_ = 0;      // co-resident layout decodes enqueued since the last check

@@ -1492,11 +1492,15 @@ __global__ __launch_bounds__(256) void k_wkv7_s64(int T, int H, const float * r,
         Op cur, nxt;
         rd(cur, 0);
         if (n == WKV7_TC) {
+            // two tokens ahead: token tt + 2's LDS reads are issued before token tt's chain, so the
+            // recurrence never waits on the LDS
+            Op ring[3];
+            ring[0] = cur;
+            rd(ring[1], 1);
 #pragma unroll
             for (int tt = 0; tt < WKV7_TC; tt++) {
-                if (tt + 1 < WKV7_TC) rd(nxt, tt + 1);
-                tok(cur, tt);
-                cur = nxt;
+                if (tt + 2 < WKV7_TC) rd(ring[(tt + 2) % 3], tt + 2);
+                tok(ring[tt % 3], tt);
             }
         } else {
 #pragma unroll 1

@@ -7,10 +7,10 @@
 // decay-LoRA rows of its slot, each published as a single-reader granule (mv_att6.hpp).  (h, 0) --
 // which loads the head's state, decay-tail weights and per-channel operands while its own rows
 // stream -- sweeps its head's granules and runs k_att6_dec's arithmetic (decay tail, wkv6,
-// GroupNorm, gate), publishing the head's 64 outputs y as granules tagged (layer, state parity).
-// The 7 H other workgroups then own Wo: wave gw's rows gw, gw + 28 H, gw + 56 H, whose units it
-// loaded at kernel start; it waits for every head's y, quantizes y into LDS exactly as Wo's
-// fp32-input prologue does, and adds its rows' dots to x.
+// GroupNorm, gate), publishing the head's 64 outputs y as two Q8 blocks of granules tagged (layer,
+// state parity) -- pub_q8: the bits Wo's fp32-input prologue would produce.  The 7 H other
+// workgroups then own Wo: wave gw's rows gw, gw + 28 H, gw + 56 H, whose units it loaded at kernel
+// start; it waits for every head's y, gathers the blocks into LDS and adds its rows' dots to x.
 //
 // Every workgroup waits on workgroups of both lower and higher index, so this layout needs all
 // 8 H workgroups resident at once.  One context alone on an idle device has that (8 H <= 512 =
@@ -21,6 +21,8 @@
 //
 // Measured against the ordered layout (v6-1B6, one context): 665.6 vs 694.7 us/token -- 96 fewer
 // workgroups and the Wo rows spread 3 per wave over 224 workgroups instead of 8 per wave over 64.
+// y as Q8 blocks instead of fp32 granules (a third of the gather traffic over 224 gatherers, no
+// quantization in them): 655.6-656.7 vs 667.1-669.3 us/token.
 #include "mv_att6.hpp"
 
 #include <algorithm>
@@ -109,50 +111,21 @@ __global__ __launch_bounds__(320) void k_v6_att_co(Att6Fused a) {
                 for (int j = 0; j < AF_WOR; j++) wo[j][u] = load_unit<WF>(a.wo, min(gw + nwo * j, C - 1), u, lane);
             xr = a.xres[min(gw + nwo * min(lane, AF_WOR - 1), C - 1)];
         }
-        // Wait for every head: wave 0 polls ONE granule per head (its last channel, lane h)
-        // with a sleep between polls -- the other waves park at the barrier, so the 7 H waiting
-        // workgroups add little L2 traffic beside the reducers' own sweeps
+        // Wait for every head: wave 0 polls the d granule of every y block (mv_common.hpp
+        // gran_prepoll) -- the other waves park at the barrier, so the 7 H waiting workgroups add
+        // little traffic beside the reducers' own sweeps; then all five waves gather y's Q8 blocks
+        // (pub_q8 in the reducers: the bits Wo's fp32-input prologue would produce) into LDS
+        const ActBuf xq = lds_act(smem, act_fmt_for(WF), C);
+        const int nb = C >> 5;
         if (wave == 0) {
-            for (unsigned it = 0;; it++) {
-                const unsigned long long x = lane < H ? gran_get(a.ygran + (size_t)lane * S + S - 1)
-                                                      : ((unsigned long long)a.ytag << 32);
-                if (__all((unsigned)(x >> 32) == a.ytag)) break;
-                if (it >= spin_max) {
-                    __hip_atomic_store((gunsigned_t *)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(4);
-            }
+            for (int b0 = 0; b0 < nb; b0 += 64)
+                gran_prepoll(a.ygran + (size_t)b0 * KG_STRIDE, min(64, nb - b0), KG_STRIDE, 8, a.ytag, err, spin_max,
+                             lane);
         }
         __syncthreads();
-        // y: 512-element chunks, 8 consecutive channels per lane (a quad = one 32-block), each
-        // granule's tag checked; then the matvec prologue's Q8 quantization into LDS
-        const ActBuf xq = lds_act(smem, act_fmt_for(WF), C);
-        MVEntry dummy{};
-        for (int ck = wave; ck * 512 < C; ck += 5) {
-            const int k0 = ck * 512 + lane * 8;
-            const bool valid = k0 < C;
-            const unsigned long long * g = a.ygran + min(k0, C - 8);
-            ChunkIn ci;
-            for (unsigned it = 0;; it++) {
-                unsigned long long x[8];
-#pragma unroll
-                for (int j = 0; j < 8; j++) x[j] = gran_get(g + j);
-                bool ok = true;
-#pragma unroll
-                for (int j = 0; j < 8; j++) {
-                    ci.x[j] = __uint_as_float((unsigned)x[j]);
-                    ok = ok && (unsigned)(x[j] >> 32) == a.ytag;
-                }
-                if (__all(ok || !valid)) break;
-                if (it >= spin_max) {
-                    __hip_atomic_store((gunsigned_t *)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(2);
-            }
-            chunk_store<WF, MVK_F32, 0>(dummy, xq, ci, 0.0f, 1.0f, false, k0, valid, lane);
-        }
+        q8_gather_image<(U > 1 ? 4 : 2)>(a.ygran, nb, a.ytag, xq, tid, 320, err, spin_max);
+        __syncthreads();
+        q8_image_qsum(xq, nb, tid, 320);
         __syncthreads();
         if (wave < 4) {
             float acc[AF_WOR], acc2[AF_WOR];
@@ -259,7 +232,7 @@ __global__ __launch_bounds__(320) void k_v6_att_co(Att6Fused a) {
         o = o * lnw_c;
         o = o + lnb_c;
         o = o * sg[lane];
-        gran_put_tag(a.ygran + c0 + lane, o, a.ytag);
+        pub_q8(a.ygran, (c0 >> 5) + (lane >> 5), o, a.ytag, lane);  // the head's 2 blocks
     }
     STAMP_END(6);
 }

@@ -29,11 +29,13 @@ def main():
     ap.add_argument('--reps', type=int, default=5)
     ap.add_argument('--seq-len', type=int, default=1024)
     ap.add_argument('--model-dir', default=os.environ.get('RWKV_BENCH_DIR', '/tmp/rwkv_bench'))
+    ap.add_argument('--lib', default=os.path.join(REPO, 'rwkv.cppy_amd', 'build', 'librwkv.so'),
+                    help='the library to load (another build, for a build-vs-build comparison)')
     args = ap.parse_args()
     arms = args.arm or ['']
     import torch  # noqa: F401
     import rwkv_cpp
-    lib = rwkv_cpp.RWKVSharedLibrary(os.path.join(REPO, 'rwkv.cppy_amd', 'build', 'librwkv.so'))
+    lib = rwkv_cpp.RWKVSharedLibrary(args.lib)
     L = lib.library
     arch, V, C, NL, F, fmt, label = CONFIGS[args.config]
     os.makedirs(args.model_dir, exist_ok=True)

@@ -200,6 +200,14 @@ RWKV_API bool rwkv_mi355x_selftest_wkv6(int T, int H, int chunked, int w_per_tok
                                        const float * r, const float * u, const float * w, const float * state_in,
                                        float * state_out, float * y);
 
+/* WKV-7 (v7 time mixing, head size 64) over T tokens of one context on host operands: chunked = 0 the
+ * serial kernel (bit-exact with decode), 1 the chunk-parallel form (RWKV_MI355X_WKV_CHUNK; re-associated
+ * sums).  r, w, k, v, a, b: [T][H*64] (a, b: the transition's rank-one factors, -kk and kk * a in
+ * rwkv_operators_wkv_v7.inc:37-107); state_in / state_out: [H][64 value][64 key]; y: [T][H*64]. */
+RWKV_API bool rwkv_mi355x_selftest_wkv7(int T, int H, int chunked, const float * r, const float * w, const float * k,
+                                       const float * v, const float * a, const float * b, const float * state_in,
+                                       float * state_out, float * y);
+
 #if defined(__cplusplus)
 }
 #endif

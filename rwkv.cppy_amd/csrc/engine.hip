@@ -918,25 +918,29 @@ bool Engine::layer_v4(int l, int T, const float * si, float * so) {
     return ffn(l, T, si, so);
 }
 
+// The chunked WKV scratch (wkv_chunk.hip, wkv7_chunk.hip), grown on demand.
+bool Engine::ensure_wkvc(size_t need) {
+    if (need <= wkvc_cap_) return true;
+    HIP_OK(hipStreamSynchronize(stream_));
+    if (wkvc_) (void)hipFree(wkvc_);
+    wkvc_ = nullptr;
+    wkvc_cap_ = 0;
+    if (hipMalloc(&wkvc_, need * 4 + 64) != hipSuccess) {
+        wkvc_ = nullptr;
+        (void)hipGetLastError();
+        fprintf(stderr, "rwkv: chunked wkv scratch (%zu MB) allocation failed\n", need * 4 >> 20);
+        return false;
+    }
+    wkvc_cap_ = need;
+    return true;
+}
+
 // v5/v6 sequence wkv: the serial recurrence (k_wkv6_s64, bit-exact with decode), or behind the
 // wkv_chunk_ switch the chunk-parallel form (RA / KB in the v7-only nb_ / bb_ buffers, free during a
 // v5/v6 layer; the chunk matrices and states in wkvc_, grown on demand)
 bool Engine::wkv6(int T, int H, int S, const float * u, const float * w, int wpt, const float * sin, float * sout) {
     if (wkv_chunk_ && wkv6_chunked_supported(T, S, (int)bs_)) {
-        const size_t need = wkv6_chunked_scratch_floats(T, H);
-        if (need > wkvc_cap_) {
-            HIP_OK(hipStreamSynchronize(stream_));
-            if (wkvc_) (void)hipFree(wkvc_);
-            wkvc_ = nullptr;
-            wkvc_cap_ = 0;
-            if (hipMalloc(&wkvc_, need * 4 + 64) != hipSuccess) {
-                wkvc_ = nullptr;
-                (void)hipGetLastError();
-                fprintf(stderr, "rwkv: chunked wkv scratch (%zu MB) allocation failed\n", need * 4 >> 20);
-                return false;
-            }
-            wkvc_cap_ = need;
-        }
+        if (!ensure_wkvc(wkv6_chunked_scratch_floats(T, H))) return false;
         return launch_wkv6_chunked(stream_, T, H, k_, v_, r_, u, w, wpt, sin, sout, y_, nb_, bb_, wkvc_);
     }
     return launch_wkv6(stream_, T, H, S, k_, v_, r_, u, w, wpt, sin, sout, y_, (int)bs_);
@@ -1188,7 +1192,14 @@ bool Engine::layer_v7(int l, int T, const float * si, float * so) {
         return ffn(l, T, si, so);
     }
     if (!launch_v7_prep(stream_, T, H, S, k_, a_, r_, L.k_k, L.k_a, L.r_k, nb_, bb_, bonus_)) return false;
-    if (!launch_wkv7(stream_, T, H, S, r_, w_, k_, v_, nb_, bb_, si + 2 * C, so + 2 * C, y_, (int)bs_)) return false;
+    // the serial recurrence (bit-exact with decode), or behind the wkv_chunk_ switch the chunk-parallel
+    // form (wkv7_chunk.hip; scratch in wkvc_)
+    if (wkv_chunk_ && wkv7_chunked_supported(T, S, (int)bs_)) {
+        if (!ensure_wkvc(wkv7_chunked_scratch_floats(T, H))) return false;
+        if (!launch_wkv7_chunked(stream_, T, H, r_, w_, k_, v_, nb_, bb_, si + 2 * C, so + 2 * C, y_, wkvc_)) return false;
+    } else if (!launch_wkv7(stream_, T, H, S, r_, w_, k_, v_, nb_, bb_, si + 2 * C, so + 2 * C, y_, (int)bs_)) {
+        return false;
+    }
     ActBuf o = A(0, L.att_o);
     if (!launch_groupnorm(stream_, T, H, S, 64e-5f, y_, L.att_lnx_w, L.att_lnx_b, 2, g_, v_, bonus_, o)) return false;
     b.add(L.att_o, o, x_, C, EPI_ADD);

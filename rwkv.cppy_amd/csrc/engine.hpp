@@ -171,6 +171,7 @@ class Engine : public KLaunchTimer {
     // k_wkv6_s64 (default); RWKV_MI355X_WKV_CHUNK=1 or rwkv_mi355x_debug_set(ctx, "wkv_chunk", 1)
     bool wkv_chunk_ = false;
     float * wkvc_ = nullptr;  // its chunk matrices / chunk states
+    bool ensure_wkvc(size_t need);
     size_t wkvc_cap_ = 0;
     hipGraphExec_t graphs_[2][2][2] = {};  // [co-resident layout][cur][logits]
     bool use_graphs_ = true;

@@ -66,6 +66,14 @@ bool launch_wkv6_chunked(hipStream_t st, int T, int H, const float * k, const fl
                          const float * u, const float * w, int w_per_token, const float * state_in, float * state_out,
                          float * y, float * RA, float * KB, float * scratch);
 
+// Chunk-parallel WKV-7 (wkv7_chunk.hip, head size 64, T >= 2, no batch): the same recurrence with the
+// sums re-associated (not bit-exact with launch_wkv7); scratch: wkv7_chunked_scratch_floats(T, H).
+bool wkv7_chunked_supported(int T, int S, int bs);
+size_t wkv7_chunked_scratch_floats(int T, int H);
+bool launch_wkv7_chunked(hipStream_t st, int T, int H, const float * r, const float * w, const float * k,
+                         const float * v, const float * a, const float * b, const float * state_in, float * state_out,
+                         float * y, float * scratch);
+
 // v7 per-head prep: kk = l2norm(k*k_k); k += a*ka - ka; nb = -kk; bb = kk*a; bonus = sum(k*r*r_k)
 bool launch_v7_prep(hipStream_t st, int T, int H, int S, float * k, const float * a, const float * r,
                     const float * k_k, const float * k_a, const float * r_k, float * nb, float * bb,

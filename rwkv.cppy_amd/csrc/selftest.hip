@@ -161,3 +161,29 @@ extern "C" RWKV_API bool rwkv_mi355x_selftest_wkv6(int T, int H, int chunked, in
     return hipMemcpy(y, dy, TC * 4, hipMemcpyDeviceToHost) == hipSuccess &&
            hipMemcpy(state_out, dso, SN * 4, hipMemcpyDeviceToHost) == hipSuccess;
 }
+
+// WKV-7 over T tokens of one context: chunked = 0 the serial k_wkv7_s64 (decode's association), 1 the
+// chunk-parallel form (wkv7_chunk.hip).  r, w, k, v, a, b: [T][H*64]; state_in / state_out:
+// [H][64 value rows][64 key columns]; y: [T][H*64]; all host.
+extern "C" RWKV_API bool rwkv_mi355x_selftest_wkv7(int T, int H, int chunked, const float * r, const float * w,
+                                                  const float * k, const float * v, const float * a, const float * b,
+                                                  const float * state_in, float * state_out, float * y) {
+    if (T < 1 || H < 1 || !r || !w || !k || !v || !a || !b || !state_in || !state_out || !y) return false;
+    if (chunked && !wkv7_chunked_supported(T, 64, 0)) return false;
+    const size_t C = (size_t)H * 64, TC = (size_t)T * C, SN = C * 64;
+    DevBufs bf;
+    float *dr = (float *)bf.alloc(TC * 4), *dw = (float *)bf.alloc(TC * 4), *dk = (float *)bf.alloc(TC * 4),
+          *dv = (float *)bf.alloc(TC * 4), *da = (float *)bf.alloc(TC * 4), *db = (float *)bf.alloc(TC * 4),
+          *dsi = (float *)bf.alloc(SN * 4), *dso = (float *)bf.alloc(SN * 4), *dy = (float *)bf.alloc(TC * 4),
+          *sc = chunked ? (float *)bf.alloc(wkv7_chunked_scratch_floats(T, H) * 4) : nullptr;
+    if (!dr || !dw || !dk || !dv || !da || !db || !dsi || !dso || !dy || (chunked && !sc)) return false;
+    const std::pair<float *, const float *> up[] = {{dr, r}, {dw, w}, {dk, k}, {dv, v}, {da, a}, {db, b}, {dy, y}};
+    for (const auto & p : up)
+        if (hipMemcpy(p.first, p.second, TC * 4, hipMemcpyHostToDevice) != hipSuccess) return false;
+    if (hipMemcpy(dsi, state_in, SN * 4, hipMemcpyHostToDevice) != hipSuccess) return false;
+    const bool ok = chunked ? launch_wkv7_chunked(nullptr, T, H, dr, dw, dk, dv, da, db, dsi, dso, dy, sc)
+                            : launch_wkv7(nullptr, T, H, 64, dr, dw, dk, dv, da, db, dsi, dso, dy, 0);
+    if (!ok || hipDeviceSynchronize() != hipSuccess) return false;
+    return hipMemcpy(y, dy, TC * 4, hipMemcpyDeviceToHost) == hipSuccess &&
+           hipMemcpy(state_out, dso, SN * 4, hipMemcpyDeviceToHost) == hipSuccess;
+}

@@ -139,3 +139,115 @@ def test_chunked_wkv6_model_within_noise_band(tmp_path, arch, fmt):
     assert_bits_equal(lg2, slg, 'switch off again: logits')
     assert_bits_equal(st2, sst, 'switch off again: state')
     m.free()
+
+
+# ---------------------------------------------------------------------------------------------------
+# Chunk-parallel WKV-7 (csrc/wkv7_chunk.hip, the same switch) -- the v7 time-mixing recurrence
+# (reference rwkv_operators_wkv_v7.inc:37-107): the
+# transition diag(w) + a b^T is solved per 16-token chunk in its triangular (WY-like) form, so the sums
+# are re-associated; held to the same kind of bar as WKV-6 above, against a float64 recurrence.
+
+TOL7 = 2e-5
+
+
+def selftest7():
+    L = library().library
+    f = L.rwkv_mi355x_selftest_wkv7
+    f.argtypes = [ctypes.c_int] * 3 + [P] * 9
+    f.restype = ctypes.c_bool
+    return f
+
+
+def operands7(T, H, seed):
+    """v7's operand ranges: w = exp(-0.606531 sigmoid(.)) in [0.545, 1); kk unit rows per head,
+    a = -kk, b = kk * iclr with iclr in (0, 1) (rwkv_graph.inc:430-460)."""
+    rng = np.random.default_rng(seed)
+    C = H * 64
+    r = rng.standard_normal((T, C)).astype(np.float32)
+    k = (rng.standard_normal((T, C)) * 0.5).astype(np.float32)
+    v = rng.standard_normal((T, C)).astype(np.float32)
+    w = np.exp(-0.606531 / (1.0 + np.exp(-rng.standard_normal((T, C)) * 2.0))).astype(np.float32)
+    kk = rng.standard_normal((T, H, 64))
+    kk /= np.linalg.norm(kk, axis=-1, keepdims=True)
+    iclr = 1.0 / (1.0 + np.exp(-rng.standard_normal((T, H, 64))))
+    a = (-kk).reshape(T, C).astype(np.float32)
+    b = (kk * iclr).reshape(T, C).astype(np.float32)
+    s0 = (rng.standard_normal((H, 64, 64)) * 0.5).astype(np.float32)
+    return r, w, k, v, a, b, s0
+
+
+def recurrence7_64(r, w, k, v, a, b, s0):
+    """float64 restatement: state [h][i value][j key]; sa = S a, S <- S diag(w) + sa b^T + v k^T, y = S r."""
+    T, C = r.shape
+    H = C // 64
+    S = s0.astype(np.float64).copy()
+    y = np.zeros((T, C))
+    for t in range(T):
+        rt, wt, kt, vt, at, bt = (x[t].astype(np.float64).reshape(H, 64) for x in (r, w, k, v, a, b))
+        sa = np.einsum('hij,hj->hi', S, at)
+        S = S * wt[:, None, :] + sa[:, :, None] * bt[:, None, :] + vt[:, :, None] * kt[:, None, :]
+        y[t] = np.einsum('hij,hj->hi', S, rt).ravel()
+    return y, S
+
+
+def run7(T, H, chunked, ops):
+    args = [np.ascontiguousarray(x) for x in ops]
+    y = np.zeros((T, H * 64), np.float32)
+    so = np.zeros((H, 64, 64), np.float32)
+    ok = selftest7()(T, H, chunked, *[x.ctypes.data_as(P) for x in args], so.ctypes.data_as(P), y.ctypes.data_as(P))
+    return ok, y, so
+
+
+@pytest.mark.parametrize('T,H', [(2, 1), (15, 2), (16, 1), (17, 2), (100, 3), (1024, 2), (4096, 1), (1024, 40)])
+def test_chunked_wkv7_against_float64(T, H):
+    ops = operands7(T, H, seed=T * 5 + H)
+    y64, s64 = recurrence7_64(*ops)
+    ok, yc, sc = run7(T, H, 1, ops)
+    assert ok
+    ok, ys, ss = run7(T, H, 0, ops)
+    assert ok
+    ys_err = np.abs(ys - y64).max() / np.abs(y64).max()
+    yc_err = np.abs(yc - y64).max() / np.abs(y64).max()
+    sc_err = np.abs(sc - s64).max() / np.abs(s64).max()
+    ss_err = np.abs(ss - s64).max() / np.abs(s64).max()
+    print(f'T={T} H={H}: relative max error y serial {ys_err:.2e}, chunked {yc_err:.2e}; '
+          f'state serial {ss_err:.2e}, chunked {sc_err:.2e}')
+    assert np.all(np.isfinite(yc)) and np.all(np.isfinite(sc))
+    assert yc_err <= TOL7, yc_err
+    assert sc_err <= TOL7, sc_err
+
+
+def test_chunked_wkv7_refuses_a_single_token():
+    ops = operands7(1, 1, seed=2)
+    ok, _, _ = run7(1, 1, 1, ops)
+    assert not ok
+    ok, _, _ = run7(1, 1, 0, ops)
+    assert ok
+
+
+def test_chunked_wkv7_model_within_noise_band(tmp_path):
+    lib = library()
+    L = lib.library
+    p = str(tmp_path / 'wkvc7.bin')
+    assert L.rwkv_mi355x_write_synthetic_model(p.encode(), 7, 1024, 512, 2, 0, b'Q5_1', 19)
+    toks = [int(t) for t in np.random.default_rng(7).integers(0, 1024, 90)]
+    m = RWKVModel(lib, p)
+    slg, sst = m.eval_sequence(toks, None, use_numpy=True)
+    glg, gst = gpu_variant(p, toks, sequence=True)
+    assert_bits_equal(slg, glg, 'serial wkv7 (default) logits')
+    assert L.rwkv_mi355x_debug_set(m._ctx.ptr, b'wkv_chunk', 1)
+    clg, cst = m.eval_sequence(toks, None, use_numpy=True)
+    # (the state, not the logits: WKV-7's ~1e-7 relative differences usually vanish in the Q8
+    # quantization of Wo's input, so the logits can come out bit-identical)
+    assert not np.array_equal(cst, sst), 'the switch did not change the wkv7 arithmetic'
+    olg, _, noise, _ = noise_band(p, toks, sequence=True)
+    d = float(np.abs(clg - olg).max())
+    print(f'v7 Q5_1: chunked max|dlogit| vs ggml-order oracle {d:.3g}, serial '
+          f'{float(np.abs(slg - olg).max()):.3g}, noise band {noise:.3g}')
+    assert d <= max(1e-3, 1.5 * noise), (d, noise)
+    assert np.all(np.isfinite(cst))
+    assert L.rwkv_mi355x_debug_set(m._ctx.ptr, b'wkv_chunk', 0)
+    lg2, st2 = m.eval_sequence(toks, None, use_numpy=True)
+    assert_bits_equal(lg2, slg, 'switch off again: logits')
+    assert_bits_equal(st2, sst, 'switch off again: state')
+    m.free()

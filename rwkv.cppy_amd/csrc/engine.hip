@@ -427,7 +427,7 @@ bool Engine::init() {
     const char * sm = getenv("RWKV_MI355X_SPLIT_MAA");  // 1: v6 decode W1 and mix as two launches
     split_maa_ = sm && sm[0] == '1';
     const char * df = getenv("RWKV_MI355X_DECODE_FUSION");  // mask of Engine::FUSE_* (default all)
-    fuse_ = df ? (unsigned)strtoul(df, nullptr, 0) & FUSE_ALL : FUSE_DEFAULT;
+    fuse_ = df ? (unsigned)strtoul(df, nullptr, 0) & FUSE_ALL : FUSE_DEFAULT | (m_->major == 4 ? FUSE_FFNCO : 0u);
     const char * wc = getenv("RWKV_MI355X_WKV_CHUNK");  // 1: chunk-parallel wkv6 (not bit-exact)
     wkv_chunk_ = wc && wc[0] == '1';
     // the fused decode prologues hold LayerNorm inputs in registers up to n_embed 4096
@@ -466,7 +466,8 @@ void Engine::release_device() {
 bool Engine::choose_co() {
     claim_device();
     bool co = co_knob_ == 1 || (co_knob_ < 0 && co_ok_ && g_dev_claims[m_->device & 63].load() == 1);
-    co = co && m_->major == 6 && (fuse_ & FUSE_ATT6) && (fuse_ & FUSE_WO6);
+    // the co-resident forms: the v6 attention launch (with its Wo) and the channel mix's
+    co = co && ((m_->major == 6 && (fuse_ & FUSE_ATT6) && (fuse_ & FUSE_WO6)) || (fuse_ & FUSE_FFNCO));
     // (both layouts hand y to Wo as the same Q8-block granules under the same tags: a switch needs
     // no clearing)
     co_ = co;
@@ -1621,9 +1622,11 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits, uint32
         // ---------------- channel mixing ----------------
         if (m_->major == 7) {
             ActBuf kin = A(0, L.ffn_v);
-            if (fuse_ & FUSE_FFN) {
+            const bool ffco7 = co_ && (fuse_ & FUSE_FFNCO);
+            if ((fuse_ & FUSE_FFN) || ffco7) {
                 FfnFused ff;
                 memset(&ff, 0, sizeof(ff));
+                ff.co = ffco7;
                 MVEntry & fk = ff.e[0];
                 fk.W = L.ffn_k;
                 fk.epi = EPI_RELU_SQ;
@@ -1638,7 +1641,8 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits, uint32
                 ff.spin_max = spin_max_;
                 ff.wdelay = ffn_wdelay_ >= 0 ? ffn_wdelay_ : (int)std::min(2000.0, wbytes(L.ffn_k) / 4e4);
                 ff.prepoll = ffn_prepoll_;
-                if (ffn_fused_supported(ff, 1, false)) {
+                if (ff.co && !ffn_fused_supported(ff, 1, false)) ff.co = 0;  // the ordered form, if on
+                if ((ff.co || (fuse_ & FUSE_FFN)) && ffn_fused_supported(ff, 1, false)) {
                     if (timing_) {
                         kt_bytes_ = wbytes(L.ffn_k) + wbytes(L.ffn_v) + 5.0 * C * 4 + 2.0 * C * 4 +
                                     (double)L.ffn_k.M / 32 * KG_STRIDE * 8 * 2;
@@ -1685,9 +1689,11 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits, uint32
             sr.act = A(7, L.ffn_r);
             sr.epi = EPI_STORE;
             // the whole channel mix in one launch (mv_ffnf.hpp), else the key group + k_mvsig
-            if (fuse_ & FUSE_FFN) {
+            const bool ffco = co_ && (fuse_ & FUSE_FFNCO);
+            if ((fuse_ & FUSE_FFN) || ffco) {
                 FfnFused ff;
                 memset(&ff, 0, sizeof(ff));
+                ff.co = ffco;
                 MVEntry & fk = ff.e[0];
                 fk.W = L.ffn_k;
                 fk.epi = EPI_RELU_SQ;
@@ -1707,7 +1713,8 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits, uint32
                 ff.spin_max = spin_max_;
                 ff.wdelay = ffn_wdelay_ >= 0 ? ffn_wdelay_ : (int)std::min(2000.0, (wbytes(L.ffn_k) + wbytes(L.ffn_r)) / 4e4);
                 ff.prepoll = ffn_prepoll_;
-                if (ffn_fused_supported(ff, form, true)) {
+                if (ff.co && !ffn_fused_supported(ff, form, true)) ff.co = 0;  // the ordered form, if on
+                if ((ff.co || (fuse_ & FUSE_FFN)) && ffn_fused_supported(ff, form, true)) {
                     if (timing_) {
                         kt_bytes_ = wbytes(L.ffn_k) + wbytes(L.ffn_r) + wbytes(L.ffn_v) + 5.0 * C * 4 + 2.0 * C * 4 +
                                     (double)L.ffn_k.M / 32 * KG_STRIDE * 8 * 2 + 2.0 * C * 8 + C * 4.0;
@@ -1911,7 +1918,8 @@ bool Engine::debug_set(const char * name, long long value) {
     else if (n == "generic_decode") generic_decode_ = value != 0 || m_->n_embed > 4096;
     else if (n == "graphs") use_graphs_ = value != 0;
     else if (n == "co_mode" && value >= -1 && value <= 1) co_knob_ = (int)value;
-    else if (n == "decode_fusion") fuse_ = (unsigned)value & FUSE_ALL;
+    else if (n == "decode_fusion")  // -1: the default for this model
+        fuse_ = value < 0 ? FUSE_DEFAULT | (m_->major == 4 ? FUSE_FFNCO : 0u) : (unsigned)value & FUSE_ALL;
     else if (n == "wo_rows" && (value == 4 || value == 8)) wo_rows_ = (int)value;
     else if (n == "wo_prepoll") wo_prepoll_ = value != 0;
     else if (n == "ffn_wdelay" && value >= -1 && value <= 10000) ffn_wdelay_ = (int)value;

@@ -186,10 +186,13 @@ class Engine : public KLaunchTimer {
         FUSE_ATT7 = 16,  // k_att7_lora (v7 LoRA second stages + attention)
         FUSE_SIG = 32,   // k_mvsig (FFN value + receptance rows)
         FUSE_FFN = 64,   // k_ffn_fused (the whole channel mix: key, receptance and value rows)
-        FUSE_ALL = 127,
+        FUSE_FFNCO = 128,  // its co-resident form, while the co-resident layouts are in use (co_mode)
+        FUSE_ALL = 255,
         // the one-launch channel mix measured slower than the key + value pair (same box, separate
         // processes: v6-1B6 716 vs 692 us/token, v4-169M 234 vs 228): off by default
-        FUSE_DEFAULT = FUSE_ALL & ~FUSE_FFN,
+        // (FUSE_FFNCO is added at creation for RWKV-4 only: v4-169M 222.5-223.0 vs 230.5-230.9 us/token,
+        // v6-1B6 697.8-699.7 vs 655.9-659.2 -- profiles/r6_ab_ffco_v4.txt, r6_ab_ffco_v6.txt)
+        FUSE_DEFAULT = FUSE_ALL & ~FUSE_FFN & ~FUSE_FFNCO,
     };
     unsigned fuse_ = FUSE_DEFAULT;
     // v6 attention launch layout (mv_att6c.hip vs mv_att6f.hip, the same bits).  The co-resident

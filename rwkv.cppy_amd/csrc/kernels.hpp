@@ -291,6 +291,7 @@ struct FfnFused {
     int np;       // producer workgroups (set by launch_ffn_fused)
     int wdelay;   // consumers issue their value rows this many 100 MHz ticks after starting
     int prepoll;  // 1: one wave polls each key block's d granule before the gather
+    int co;       // 1: the co-resident form (no consumer workgroups; Engine::co_mode only)
 };
 bool ffn_fused_supported(const FfnFused & f, int form, bool hasr);
 bool launch_ffn_fused(hipStream_t st, FfnFused & f, int form, bool hasr);

@@ -24,7 +24,14 @@ bool ffn_fused_supported(const FfnFused & f, int form, bool hasr) {
     // at most 4 units per lane (v6-1B6, v4-169M: 1.6 and 0.7 workgroups per CU) -- v7-2.9B (5 units,
     // 1.9 per CU) measured 1871 vs 1838 us/token and v5-7B (7 units, 3.3 per CU: the consumers
     // start a round late) 2029 vs 1528 against the two launches
-    if (mv_units(t, F) > 4 || F / 32 + (hasr ? C / 32 : 0) + C / (8 * FF_RC) > 2 * kQgCUs) return false;
+    const int np = F / 32 + (hasr ? C / 32 : 0);
+    if (f.co) {
+        // co-resident form: one value row per consumer wave on the np producer workgroups, all np
+        // resident at once (<= 2 per CU: 512 threads at <= 128 VGPRs)
+        if (mv_units(t, F) > 8 || 8 * np < C || np > 2 * kQgCUs) return false;
+    } else if (mv_units(t, F) > 4 || np + C / (8 * FF_RC) > 2 * kQgCUs) {
+        return false;
+    }
     if (f.wv.type != t || f.wv.M != C || f.wv.K != F) return false;
     if (hasr) {
         const MVEntry & r = f.e[1];
@@ -43,7 +50,7 @@ bool launch_ffn_fused(hipStream_t st, FfnFused & f, int form, bool hasr) {
     f.e[0].block0 = 0;
     f.e[1].block0 = F / 32;
     f.np = F / 32 + (hasr ? C / 32 : 0);
-    const dim3 grid(f.np + (C + 8 * FF_RC - 1) / (8 * FF_RC));
+    const dim3 grid(f.co ? f.np : f.np + (C + 8 * FF_RC - 1) / (8 * FF_RC));
     const int fmt = act_fmt_for(t);
     const int lds = std::max(lds_bytes_for(fmt, C), lds_bytes_for(fmt, F));
     const int uv = mv_units(t, F), lnp = C <= 2048 ? 32 : 64;

@@ -29,8 +29,13 @@ namespace rwkvmi {
 
 constexpr int FF_RC = 2;  // value rows per consumer wave (8 waves: 16 rows per consumer workgroup)
 
-template <int WF, int UV, int FORM, bool HASR, int LNP>
+// CO: the co-resident form (Engine::co_mode only) -- no consumer workgroups: every producer
+// workgroup, once its key / receptance rows are published, runs value rows bx * 8 + wave (one per
+// wave; needs 8 np >= C), issuing their weights right then, so they stream while the last key
+// blocks arrive.  Its waits point at higher-index workgroups too: all np must be resident at once.
+template <int WF, int UV, int FORM, bool HASR, int LNP, bool CO = false>
 __global__ __launch_bounds__(512) void k_ffn_fused(FfnFused f) {
+    constexpr int RC = CO ? 1 : FF_RC;  // value rows per consumer wave
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ float red[32];
     const int bx = (int)blockIdx.x;
@@ -41,8 +46,10 @@ __global__ __launch_bounds__(512) void k_ffn_fused(FfnFused f) {
         const GranPub pub{f.kg, f.rg, f.tag};
         STAMP_BEGIN();
         mv_body_split<WF, 4, 1, MVK_LN, FORM, true, 4, LNP, true>(Ent, bx - b0, b0, 0, smem, red, 0, &pub);
-        STAMP_END(9);
-        return;
+        if constexpr (!CO) {
+            STAMP_END(9);
+            return;
+        }
     }
     STAMP_BEGIN();
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -50,20 +57,20 @@ __global__ __launch_bounds__(512) void k_ffn_fused(FfnFused f) {
     const unsigned tag = f.tag;
     unsigned * const err = f.err;
     const unsigned spin_max = f.spin_max;
-    const int row0 = ((bx - f.np) * 8 + wave) * FF_RC;
+    const int row0 = ((CO ? bx : bx - f.np) * 8 + wave) * RC;
     // ---- this wave's value rows (all their units) and residual rows, in flight at once -- after
     // wdelay ticks of the 100 MHz clock, so they do not share the memory system with the
     // producers' key / receptance rows (whose arrival is on the critical path)
-    if (f.wdelay > 0) {
+    if (!CO && f.wdelay > 0) {
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
         while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)f.wdelay) __builtin_amdgcn_s_sleep(8);
     }
-    WBlk w[FF_RC][UV];
+    WBlk w[RC][UV];
 #pragma unroll
     for (int u = 0; u < UV; u++)
 #pragma unroll
-        for (int r = 0; r < FF_RC; r++) w[r][u] = load_unit<WF>(f.wv, min(row0 + r, C - 1), u, lane);
-    const int myrow = min(row0 + min(lane, FF_RC - 1), C - 1);
+        for (int r = 0; r < RC; r++) w[r][u] = load_unit<WF>(f.wv, min(row0 + r, C - 1), u, lane);
+    const int myrow = min(row0 + min(lane, RC - 1), C - 1);
     const float xr = f.x[myrow];
     const ActBuf img = lds_act(smem, act_fmt_for(WF), F);
     // ---- wait: wave 0 polls the d granule of every key block (64 blocks per rolling poll)
@@ -126,15 +133,19 @@ __global__ __launch_bounds__(512) void k_ffn_fused(FfnFused f) {
     __syncthreads();
     STAMP_MID();
     // ---- the value rows: k_mva's arithmetic; EPI_SIGMUL_ADD (aux = the receptance row) / EPI_ADD
-    const float s = rows_dot_img<WF, FF_RC, UV>(w, img, F, lane);
+    const float s = rows_dot_img<WF, RC, UV>(w, img, F, lane);
     const float v = HASR ? xr + sigmoidf_(rr) * s : xr + s;
-    if (lane < FF_RC && row0 + lane < C) f.x[row0 + lane] = v;
+    if (lane < RC && row0 + lane < C) f.x[row0 + lane] = v;
     STAMP_END(9);
 }
 
 template <int WF>
 bool launch_ffn_fused_t(hipStream_t st, const FfnFused & f, int form, bool hasr, int uv, int lnp, dim3 grid, int lds) {
-#define FF_L(UVv, F_, R_, P_) RK_LAUNCH((k_ffn_fused<WF, UVv, F_, R_, P_>), grid, dim3(512), lds, st, f)
+#define FF_L(UVv, F_, R_, P_)                                                                    \
+    do {                                                                                         \
+        if (f.co) RK_LAUNCH((k_ffn_fused<WF, UVv, F_, R_, P_, true>), grid, dim3(512), lds, st, f); \
+        else RK_LAUNCH((k_ffn_fused<WF, UVv, F_, R_, P_, false>), grid, dim3(512), lds, st, f);     \
+    } while (0)
 #define FF_U(F_, R_, P_)                  \
     do {                                  \
         if (uv <= 1) FF_L(1, F_, R_, P_); \

@@ -66,7 +66,7 @@ def main():
     broken = set()
     for rep in range(args.reps):
         for a in arms:
-            knobs('decode_fusion=63,wkv_chunk=0,wo_rows=8,wo_prepoll=1,ffn_wdelay=-1,ffn_prepoll=1,co_mode=-1')  # defaults first, then the arm
+            knobs('decode_fusion=-1,wkv_chunk=0,wo_rows=8,wo_prepoll=1,ffn_wdelay=-1,ffn_prepoll=1,co_mode=-1')  # defaults first, then the arm
             knobs(a)
             assert L.rwkv_mi355x_state_upload(ctx.ptr, None)
             lg = np.zeros(n_vocab, np.float32)

@@ -51,7 +51,7 @@ for s in $STEPS; do
       ;;
     configs)
       # the other BASELINE configurations' lines (decode, seq-eval, batched B = 8 / 64, ABI decode)
-      for c in v4-169m-q8_0 v7-2b9-q5_1 v5-7b-q4_1; do
+      for c in ${CONFIGS:-v4-169m-q8_0 v7-2b9-q5_1 v5-7b-q4_1}; do
         timeout -k 10 400 python3 bench.py --config $c --steps 64 --warmup 8 --batch "8,64" --seq-reps 2 --abi-steps 8 \
           --skip-cpu --pipe-stages 0 > $O/r6_${TAG}_$c.log 2>&1 || { tail -5 $O/r6_${TAG}_$c.log; exit 1; }
         grep '^{' $O/r6_${TAG}_$c.log > $O/r6_${TAG}_$c.json

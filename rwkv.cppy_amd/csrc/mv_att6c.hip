@@ -13,8 +13,8 @@
 // start; it waits for every head's y, gathers the blocks into LDS and adds its rows' dots to x.
 //
 // Every workgroup waits on workgroups of both lower and higher index, so this layout needs all
-// 8 H workgroups resident at once.  One context alone on an idle device has that (8 H <= 512 =
-// the compute units, 2 per CU at this kernel's 100-110 VGPRs); the engine uses this layout only
+// 8 H workgroups resident at once.  One context alone on an idle device has that (8 H <= the 256
+// compute units, one workgroup each -- v6_att_co_supported); the engine uses this layout only
 // while no other context of the process has work queued on the device (Engine::co_mode) and
 // falls back to the ordered layout for good after a hand-off timeout (another process's launches
 // holding the compute units).  Bounded spins as in mv_att6f.hip: a timeout sets *err, never a hang.
@@ -238,8 +238,10 @@ __global__ __launch_bounds__(320) void k_v6_att_co(Att6Fused a) {
 }
 
 bool v6_att_co_supported(const Att6Fused & a) {
-    // the ordered layout's shapes, Wo fused, rows spread over the 28 H non-reducer waves
-    if (!v6_att_fused_supported(a) || !a.wo.qs || a.C % 512) return false;
+    // the ordered layout's shapes, Wo fused, rows spread over the 28 H non-reducer waves; and the
+    // whole grid resident at one workgroup per CU (the C > 2048 forms hold up to 223 VGPRs: one
+    // 5-wave workgroup per CU), so 8 H <= the device's compute units
+    if (!v6_att_fused_supported(a) || !a.wo.qs || a.C % 512 || AF_P * a.H > kQgCUs) return false;
     return (a.C + 28 * a.H - 1) / (28 * a.H) <= AF_WOR;
 }
 

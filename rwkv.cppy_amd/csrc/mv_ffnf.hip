@@ -27,8 +27,9 @@ bool ffn_fused_supported(const FfnFused & f, int form, bool hasr) {
     const int np = F / 32 + (hasr ? C / 32 : 0);
     if (f.co) {
         // co-resident form: one value row per consumer wave on the np producer workgroups, all np
-        // resident at once (<= 2 per CU: 512 threads at <= 128 VGPRs)
-        if (mv_units(t, F) > 8 || 8 * np < C || np > 2 * kQgCUs) return false;
+        // resident at once -- at one 512-thread workgroup per CU (the Q8_0 forms hold up to 204
+        // VGPRs), so np <= the device's compute units
+        if (mv_units(t, F) > 8 || 8 * np < C || np > kQgCUs) return false;
     } else if (mv_units(t, F) > 4 || np + C / (8 * FF_RC) > 2 * kQgCUs) {
         return false;
     }

@@ -198,6 +198,29 @@ def test_width_above_4096_generic_path(cfg_dir, arch, fmt):
     assert_bits_equal(st, gst, 'wide decode state vs oracle')
 
 
+@pytest.mark.parametrize('arch,C,fmt', [(4, 4096, 'Q8_0'), (6, 2560, 'Q4_0'), (6, 4096, 'Q4_0')])
+def test_wide_fused_decode_bit_exact(cfg_dir, arch, C, fmt):
+    """The fused decode launches at the widest shapes they take (v4-7B's C = 4096; v6 at
+    40 and 64 heads, where the co-resident attention layout does not fit at one workgroup per CU and
+    the ordered layout runs): serial decode, sequence evaluation and the oracle agree bit for bit, with
+    the default rule and with each attention layout forced."""
+    p = os.path.join(str(cfg_dir), f'wide-fused-v{arch}-{C}.bin')
+    if not os.path.isfile(p):
+        assert library().library.rwkv_mi355x_write_synthetic_model(p.encode(), arch, 1024, C, 1, 0, fmt.encode(), 29)
+    toks = [int(t) for t in np.random.default_rng(C).integers(0, 1024, 5)]
+    glg, gst = gpu_variant(p, toks)
+    L = library()
+    m = RWKVModel(L, p)
+    slg, sst = m.eval_sequence(toks, None, use_numpy=True)
+    assert_bits_equal(slg, glg, f'v{arch} C={C} sequence logits vs oracle')
+    for co in (-1, 0, 1):
+        assert L.library.rwkv_mi355x_debug_set(m._ctx.ptr, b'co_mode', co)
+        lg, st = gpu_serial(m, toks)
+        assert_bits_equal(lg, glg, f'v{arch} C={C} co_mode {co} decode logits vs oracle')
+        assert_bits_equal(st, gst, f'v{arch} C={C} co_mode {co} decode state vs oracle')
+    m.free()
+
+
 def test_v6_1b6_width_1024_tokens(cfg_dir):
     """The headline sequence length: 1024 tokens in one rwkv_eval_sequence at the v6-1B6 width."""
     path = cfg_model(cfg_dir, 'v6-1b6-q4_0')

@@ -412,12 +412,13 @@ bool Engine::init() {
         HIP_OK(hipMemset(hgran_, 0, hgran_n_ * 8));
         // the tagged hand-offs (fused Wo, fused channel mix): tagged per (layer, state parity)
         const size_t C = m_->n_embed, kg = (size_t)KG_STRIDE * ((size_t)std::max(m_->F, 32) / 32);
-        tgran_n_ = C + kg + C;
+        tgran_n_ = C + kg + C + C;
         HIP_OK(hipMalloc(&ygran_, tgran_n_ * 8));
         ws_allocs_.push_back(ygran_);
         HIP_OK(hipMemset(ygran_, 0, tgran_n_ * 8));
         kgran_ = ygran_ + C;
         rgran_ = kgran_ + kg;
+        xgran_ = rgran_ + C;
     }
     // Per-context switches read when the context is created (each arm tested):
     const char * io = getenv("RWKV_MI355X_STATE_PIPELINE");  // 0: host state copied whole
@@ -467,7 +468,8 @@ bool Engine::choose_co() {
     claim_device();
     bool co = co_knob_ == 1 || (co_knob_ < 0 && co_ok_ && g_dev_claims[m_->device & 63].load() == 1);
     // the co-resident forms: the v6 attention launch (with its Wo) and the channel mix's
-    co = co && ((m_->major == 6 && (fuse_ & FUSE_ATT6) && (fuse_ & FUSE_WO6)) || (fuse_ & FUSE_FFNCO));
+    const bool att6 = (fuse_ & FUSE_ATT6) && (fuse_ & FUSE_WO6), sigmaa = (fuse_ & FUSE_SIGMAA) && (fuse_ & FUSE_SIG);
+    co = co && ((m_->major == 6 && (att6 || sigmaa)) || (fuse_ & FUSE_FFNCO));
     // (both layouts hand y to Wo as the same Q8-block granules under the same tags: a switch needs
     // no clearing)
     co_ = co;
@@ -1345,6 +1347,7 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits, uint32
     if (l0 == 0 && !launch_embed_ln(stream_, dtokens_, 1, m_->emb, m_->ln0_w, m_->ln0_b, x_)) return false;
     v7_fused_lora_ = false;
     const size_t per_layer = m_->major >= 5 ? (size_t)C * (2 + (size_t)S) : 5 * (size_t)C;
+    bool maa_done = false;  // this layer's maa ran in the previous layer's channel-mix launch (k_sig_maa)
     for (uint32_t l = l0; l < l1; l++) {
         const DLayer & L = m_->layers[l];
         const float * si = sin + l * per_layer;
@@ -1445,7 +1448,9 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits, uint32
         } else if (m_->major == 6) {
             const int D = m_->maa_D;
             ActBuf outs[5] = {A(1, L.decay_w1), A(2, L.att_k), A(3, L.att_v), A(4, L.att_r), A(5, L.att_g)};
-            if (v6_maa_dec_supported(C, D, L.maa_w1.type) && !split_maa_) {
+            if (maa_done) {
+                maa_done = false;
+            } else if (v6_maa_dec_supported(C, D, L.maa_w1.type) && !split_maa_) {
                 // W1 rows + mix in one launch (mv_maa.hip)
                 if (timing_) {
                     // W1, W2 (fp32), x / carry / LN / maa vectors in, carry and 5 Q8 mixes out
@@ -1733,7 +1738,40 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits, uint32
                 src_lnmix(b.add(L.ffn_r, fr_, EPI_STORE), x_, si, L.ln2_w, L.ln2_b, mur, form);
             }
             if (!mv(b.g)) return false;
-            if (sig) {
+            // co-resident: the next layer's maa in this launch (mv_sigmaa.hip), its x from granules
+            bool sm_in = false;
+            if (sig && co_ && (fuse_ & FUSE_SIGMAA) && m_->major == 6 && l + 1 < l1 && !split_maa_) {
+                const DLayer & N = m_->layers[l + 1];
+                const float * si1 = sin + (l + 1) * per_layer;
+                float * so1 = sout + (l + 1) * per_layer;
+                const ActBuf outs1[5] = {A(1, N.decay_w1), A(2, N.att_k), A(3, N.att_v), A(4, N.att_r), A(5, N.att_g)};
+                SigMaa sm;
+                memset(&sm, 0, sizeof(sm));
+                mv_fill_hot(sv, sm.hv);
+                mv_fill_hot(sr, sm.hr);
+                sm.wtype = L.ffn_v.type;
+                v6_maa_dec_args(sm.maa, C, m_->maa_D, N.maa_w1, x_, si1 + C, so1 + C, N.ln1_w, N.ln1_b, N.maa_x,
+                                N.maa_w2t, N.maa, outs1);
+                sm.nm = 5 * (C / 64);
+                sm.xg = xgran_;
+                sm.xtag = (unsigned)(l + 1) | ((unsigned)(cur_ + 1) << 16);
+                sm.err = herr_d_;
+                sm.spin_max = spin_max_;
+                if (sig_maa_supported(sm)) {
+                    if (timing_) {
+                        // + the maa's W1, W2 (fp32), LayerNorm vectors, carry and mixes; x granules out / in
+                        kt_bytes_ = wbytes(L.ffn_v) + wbytes(L.ffn_r) + act_bytes(kin, 1) + act_bytes(sr.act, 1) +
+                                    2.0 * C * 4 + wbytes(N.maa_w1) + 5.0 * m_->maa_D * C * 4 + 11.0 * C * 4 +
+                                    5 * act_bytes(outs1[0], 1) + 2.0 * C * 8;
+                        kt_flops_ = 2.0 * ((double)L.ffn_v.M * L.ffn_v.K + (double)L.ffn_r.M * L.ffn_r.K) +
+                                    2.0 * N.maa_w1.M * N.maa_w1.K + 2.0 * 5 * m_->maa_D * C;
+                    }
+                    if (!launch_sig_maa(stream_, sm)) return false;
+                    sm_in = maa_done = true;
+                }
+            }
+            if (sm_in) {
+            } else if (sig) {
                 if (timing_) {
                     kt_bytes_ = wbytes(L.ffn_v) + wbytes(L.ffn_r) + act_bytes(kin, 1) + act_bytes(sr.act, 1) + 2.0 * C * 4;
                     kt_flops_ = 2.0 * ((double)L.ffn_v.M * L.ffn_v.K + (double)L.ffn_r.M * L.ffn_r.K);

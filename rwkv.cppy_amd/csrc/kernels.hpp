@@ -182,6 +182,8 @@ int mva_rows();
 // receptance matvec (SRC_ACT, same rows).  Same bits as the receptance matvec + EPI_SIGMUL_ADD.
 bool mv_sigmul_supported(const MVEntry & ev, const MVEntry & er);
 bool launch_mv_sigmul(hipStream_t st, const MVEntry & ev, const MVEntry & er);
+// The MVHot record of an SRC_ACT entry (the scalars k_mvsig reads)
+void mv_fill_hot(const MVEntry & e, MVHot & h);
 
 // v6 token-shift mixes with the maa LoRA (rwkv_graph.inc:308-346); xa = LN(x) is the new
 // att_xx carry already written by the W1 matvec prologue; w2t is time_maa_w2 transposed to
@@ -194,10 +196,41 @@ bool launch_v6_mix5_dec(hipStream_t st, int C, int D, const float * xa, const fl
 // v6 maa LoRA in one launch (mv_maa.hip): LN(x) + token shift -> lora_n = tanh(W1[n] . xxx) ->
 // the five mixed vectors w,k,v,r,g, emitted in their matmuls' input formats; writes the new
 // att_xx carry.  Bit-identical to the W1 k_mv + launch_v6_mix5_dec pair it replaces.
+struct MaaDec {
+    int C, D;
+    DMat w1;                    // time_maa_w1 (M = 5*D, K = C)
+    const float * x;            // residual stream [C]
+    const float * carry;        // previous att_xx [C]
+    float * carry_out;          // new att_xx [C] (= LN(x)), written by workgroup (0, 0)
+    const float * lnw, * lnb;
+    const float * maa_x;        // time_maa_x [C]
+    const float * w2t;          // time_maa_w2 transposed [5][D][C]
+    const float * maa[5];       // time_maa_{w,k,v,r,g} [C]
+    ActBuf out[5];
+    int xa_off;                 // LDS byte offset of the fp32 xa image
+};
 bool v6_maa_dec_supported(int C, int D, int w1_type);
+void v6_maa_dec_args(MaaDec & a, int C, int D, const DMat & w1, const float * x, const float * carry, float * carry_out,
+                     const float * lnw, const float * lnb, const float * maa_x, const float * w2t,
+                     const float * const * maa, const ActBuf * outs);
 bool launch_v6_maa_dec(hipStream_t st, int C, int D, const DMat & w1, const float * x, const float * carry,
                        float * carry_out, const float * lnw, const float * lnb, const float * maa_x,
                        const float * w2t, const float * const * maa, const ActBuf * outs);
+// v6 decode, co-resident form (mv_sigmaa.hip): layer l's k_mvsig rows (hv: Wv / k / y = x, hr: Wr /
+// xr) and layer l + 1's maa workgroups (maa, x gathered from the granules xg the rows publish, tag
+// xtag) in one launch of C / 8 workgroups; the same bits as k_mvsig + k_v6_maa_dec4.
+struct SigMaa {
+    MVHot hv, hr;
+    int wtype;
+    MaaDec maa;
+    int nm;                      // maa workgroups: 5 C / 64
+    unsigned long long * xg;     // C granules
+    unsigned xtag;
+    unsigned * err;
+    unsigned spin_max;
+};
+bool sig_maa_supported(const SigMaa & a);
+bool launch_sig_maa(hipStream_t st, const SigMaa & a);
 
 // v5/v6 attention core for one token, one workgroup per head: (v6: decay LoRA second stage
 // w = exp(-exp(Wd2 . dl + decay))) + wkv6 + GroupNorm*ln_x (+ *g).  Writes fp32 y [C].

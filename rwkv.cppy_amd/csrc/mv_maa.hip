@@ -8,26 +8,13 @@
 // lora values are bit-identical) -- and then mixes its 256 channels (exactly k_v6_mix5_dec).
 // The five row chunks are each recomputed by C/256 workgroups (W1 is 5*D x C: 37 KB per chunk
 // for v6-1B6 Q4_0, read from L2), which replaces one dependent launch per layer.
-#include "mv_common.hpp"
+#include "mv_maa.hpp"
 
 #include <stdlib.h>
+#include <string.h>
 
 namespace rwkvmi {
 
-struct MaaDec {
-    int C, D;
-    DMat w1;                    // time_maa_w1 (M = 5*D, K = C)
-    const float * x;            // residual stream [C]
-    const float * carry;        // previous att_xx [C]
-    float * carry_out;          // new att_xx [C] (= LN(x)), written by workgroup (0, 0)
-    const float * lnw, * lnb;
-    const float * maa_x;        // time_maa_x [C]
-    const float * w2t;          // time_maa_w2 transposed [5][D][C]
-    const float * maa[5];       // time_maa_{w,k,v,r,g} [C]
-    ActBuf out[5];
-    int xa_off;                 // LDS byte offset of the fp32 xa image
-    int late;                   // mv_late_weights(): W1 rows issued after the image inputs land
-};
 
 // 512 threads.  Waves 4..7 build the activation image (LayerNorm + token shift + quantization,
 // one 512-element chunk per wave per pass) and the fp32 xa image; then every wave dots R rows of
@@ -183,144 +170,16 @@ __global__ __launch_bounds__(512) void k_v6_maa_dec(MaaDec a) {
     STAMP_END_NS(4 + 16 * blockIdx.y);
 }
 
-// D <= 32: the image waves have no rows.  The two roles run as separate straight paths that meet
-// only at the barriers: waves 4..7 load the image inputs, compute the LayerNorm statistics (no
-// weight load ahead of them in their instruction stream: a load's issue blocks the wave once the
-// CU's share of the memory system is saturated) and store the images; waves 0..3 issue their
-// R = 8 W1 rows and their W2 columns at once, dot the rows after the image barrier and mix.
+// D <= 32: mv_maa.hpp's workgroup (the image waves have no rows), x read from the residual stream.
 // Same arithmetic and association as k_v6_maa_dec (bit-identical).
 template <int WF, int U, int LNP, int CPW>
 __global__ __launch_bounds__(512) void k_v6_maa_dec4(MaaDec a) {
-    constexpr int R = 8, DM = 32;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ float s_lora[64];
-    __shared__ double ln_part[2][8];
-    const int n = blockIdx.y, C = a.C, D = a.D, K = C;
-    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const ActBuf act = lds_act(smem, act_fmt_for(WF), K);
-    float * s_xa = (float *)(smem + a.xa_off);
+    __shared__ double ln_part[16];
     STAMP_BEGIN();
-    constexpr int LCW = LNP > 32 ? 2 : 1;
-    const int nch = (K + LN_CHUNK - 1) / LN_CHUNK;
-    if (wave >= 4) {
-        const int pw = wave - 4;
-        MVEntry E;
-        E.x = a.x;
-        E.carry = a.carry;
-        E.lnw = a.lnw;
-        E.lnb = a.lnb;
-        E.mu = a.maa_x;
-        E.carry_out = a.carry_out;
-        E.f = nullptr;
-        ChunkIn ci[LCW];
-        int kc[LCW];
-#pragma unroll
-        for (int q = 0; q < LCW; q++) {
-            kc[q] = (pw + 4 * q) * LN_CHUNK + lane * 8;
-            chunk_load<MVK_LN, 1>(E, min(kc[q], K - 8), ci[q]);
-        }
-        if (a.late) {
-            // the inputs land before the mix waves' weight stream starts (mv_late_weights)
-            asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-        }
-        // LayerNorm statistics (chunk association, one pass); the chunk sums meet in LDS
-#pragma unroll
-        for (int q = 0; q < LCW; q++)
-            if (pw + 4 * q < nch) {
-                double c1, c2;
-                ln_chunk_sums(ci[q].x, kc[q] < K, c1, c2);
-                if (lane == 0) {
-                    ln_part[0][pw + 4 * q] = c1;
-                    ln_part[1][pw + 4 * q] = c2;
-                }
-            }
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        double s1 = 0.0, s2 = 0.0;
-        for (int q = 0; q < nch; q++) s1 += ln_part[0][q], s2 += ln_part[1][q];
-        float mean, scale;
-        ln_finish(s1, s2, K, 1e-5f, mean, scale);
-        if (pw == 0) STAMP_XN(1);
-        const bool write_carry = blockIdx.x == 0 && n == 0;
-#pragma unroll
-        for (int q = 0; q < LCW; q++) {
-            if (pw + 4 * q >= nch) continue;
-            if (kc[q] < K) {
-#pragma unroll
-                for (int j = 0; j < 8; j++) s_xa[kc[q] + j] = ln_apply(ci[q].x[j], mean, scale, ci[q].w[j], ci[q].b[j]);
-            }
-            chunk_store<WF, MVK_LN, 1>(E, act, ci[q], mean, scale, write_carry, kc[q], kc[q] < K, lane);
-        }
-        if (pw == 0) STAMP_XN(2);
-        __syncthreads();  // (1) activation image ready
-        __syncthreads();  // (2) lora_n ready
-    } else {
-        const ActBuf ao = a.out[n];
-        pin_act(ao);
-        const DMat & W = a.w1;
-        asm volatile("" ::"s"(W.qs), "s"(W.sc), "s"(W.qh));
-        if (a.late) asm volatile("s_barrier" ::: "memory");  // the image inputs have landed
-        // ---- rows n*D + wave*R + r of W1 and this thread's mix channel: W2 column, carry, maa
-        const int units = mv_units(WF, K);
-        const int row0 = n * D + wave * R, rlast = n * D + D - 1;
-        int rows[R];
-#pragma unroll
-        for (int r = 0; r < R; r++) rows[r] = min(row0 + r, rlast);
-        WBlk w[R][U];
-#pragma unroll
-        for (int u = 0; u < U; u++)
-#pragma unroll
-            for (int r = 0; r < R; r++) w[r][u] = load_unit<WF, false>(W, rows[r], u, lane);
-        const int c = blockIdx.x * CPW + tid;
-        const bool cval = tid < CPW && (int)(blockIdx.x * CPW + (tid & ~31)) < C;  // half-wave uniform
-        const int cc = min(c, C - 1);
-        float w2v[DM];
-        const float * w2 = a.w2t + (size_t)n * D * C + cc;
-#pragma unroll
-        for (int i = 0; i < DM; i++) w2v[i] = w2[(size_t)min(i, D - 1) * C];  // rows >= D: skipped below
-        const float carry_c = a.carry[cc];
-        const float mu_c = a.maa[n][cc];
-        if (wave == 0) STAMP_XN(0);  // weights issued
-        asm volatile("s_barrier" ::: "memory");  // the image waves' statistics exchange
-        __syncthreads();  // (1) activation image ready
-        if (wave == 0) STAMP_MID();
-        float acc[R], acc2[R];
-#pragma unroll
-        for (int r = 0; r < R; r++) acc[r] = acc2[r] = 0.0f;
-        for (int u0 = 0; u0 < units; u0 += U) {
-            if (u0 > 0) {
-#pragma unroll
-                for (int u = 0; u < U; u++)
-#pragma unroll
-                    for (int r = 0; r < R; r++) w[r][u] = load_unit<WF, false>(W, rows[r], u0 + u, lane);
-            }
-            AUnit xu[U];
-#pragma unroll
-            for (int u = 0; u < U; u++) xu[u] = load_act_unit<WF, true>(act, u0 + u, lane);
-#pragma unroll
-            for (int u = 0; u < U; u++) {
-                if (unit_valid<WF>(K, u0 + u, lane)) {
-#pragma unroll
-                    for (int r = 0; r < R; r++) dot_unit<WF>(w[r][u], xu[u], acc[r], acc2[r]);
-                }
-            }
-        }
-        constexpr bool one = WF == W_Q4_1 || WF == W_Q5_1;
-        float sr[R];
-#pragma unroll
-        for (int r = 0; r < R; r++) sr[r] = one ? wave_sum63(acc[r]) + wave_sum63(acc2[r]) : wave_sum63(acc[r]) + 0.0f;
-        const float t = rk_tanhf(lane_row_sum<R>(sr, lane));  // EPI_TANH, lane r for row r
-        if (lane < R && wave * R + lane < D) s_lora[wave * R + lane] = t;
-        __syncthreads();  // (2) lora_n ready
-        if (wave == 0) STAMP_X(3);
-        // k_v6_mix5_dec's arithmetic: m = fma chain over i in order
-        const float xa = s_xa[cc];
-        const float sx = carry_c - xa;
-        float m = 0.0f;
-#pragma unroll
-        for (int i = 0; i < DM; i++)
-            if (i < D) m = fmaf(w2v[i], s_lora[i], m);
-        if (cval) emit32(ao, 0, c, (m + mu_c) * sx + xa);
-    }
+    maa_dec4_body<WF, U, LNP, CPW, false>(a, (int)blockIdx.x, (int)blockIdx.y, smem, s_lora, ln_part, nullptr, 0u,
+                                          nullptr, 0u);
     STAMP_END_NS(4 + 16 * blockIdx.y);
 }
 
@@ -370,16 +229,10 @@ bool v6_maa_dec_supported(int C, int D, int w1_type) {
     return D >= 1 && D <= 64 && C % 64 == 0 && C <= 4096 && w1_type >= 0;
 }
 
-bool launch_v6_maa_dec(hipStream_t st, int C, int D, const DMat & w1, const float * x, const float * carry,
-                       float * carry_out, const float * lnw, const float * lnb, const float * maa_x,
-                       const float * w2t, const float * const * maa, const ActBuf * outs) {
-    if (!v6_maa_dec_supported(C, D, w1.type) || (int)w1.M != 5 * D || (int)w1.K != C) {
-        fprintf(stderr, "rwkv: fused v6 maa decode: unsupported shape (C %d, D %d, W1 %dx%d)\n", C, D,
-                (int)w1.M, (int)w1.K);
-        return false;
-    }
-    MaaDec a;
-    a.late = 0;  // measured: the W1 rows (37 KB per workgroup, L2) are better streamed at once
+void v6_maa_dec_args(MaaDec & a, int C, int D, const DMat & w1, const float * x, const float * carry, float * carry_out,
+                     const float * lnw, const float * lnb, const float * maa_x, const float * w2t,
+                     const float * const * maa, const ActBuf * outs) {
+    memset(&a, 0, sizeof(a));
     a.C = C;
     a.D = D;
     a.w1 = w1;
@@ -394,8 +247,19 @@ bool launch_v6_maa_dec(hipStream_t st, int C, int D, const DMat & w1, const floa
         a.maa[i] = maa[i];
         a.out[i] = outs[i];
     }
-    const int fmt = act_fmt_for(w1.type);
-    a.xa_off = (lds_bytes_for(fmt, C) + 15) & ~15;
+    a.xa_off = (lds_bytes_for(act_fmt_for(w1.type), C) + 15) & ~15;
+}
+
+bool launch_v6_maa_dec(hipStream_t st, int C, int D, const DMat & w1, const float * x, const float * carry,
+                       float * carry_out, const float * lnw, const float * lnb, const float * maa_x,
+                       const float * w2t, const float * const * maa, const ActBuf * outs) {
+    if (!v6_maa_dec_supported(C, D, w1.type) || (int)w1.M != 5 * D || (int)w1.K != C) {
+        fprintf(stderr, "rwkv: fused v6 maa decode: unsupported shape (C %d, D %d, W1 %dx%d)\n", C, D,
+                (int)w1.M, (int)w1.K);
+        return false;
+    }
+    MaaDec a;
+    v6_maa_dec_args(a, C, D, w1, x, carry, carry_out, lnw, lnb, maa_x, w2t, maa, outs);
     const int lds = a.xa_off + C * 4;
     const int units = mv_units(w1.type, C);
     switch (w1.type) {

@@ -7,7 +7,7 @@
 
 namespace rwkvmi {
 
-static void fill_hot(const MVEntry & e, MVHot & h) {
+void mv_fill_hot(const MVEntry & e, MVHot & h) {
     memset(&h, 0, sizeof(h));
     h.qs = e.W.qs;
     h.qh = e.W.qh;
@@ -52,8 +52,8 @@ bool launch_mv_sigmul(hipStream_t st, const MVEntry & ev, const MVEntry & er) {
         return false;
     }
     MVHot hv, hr;
-    fill_hot(ev, hv);
-    fill_hot(er, hr);
+    mv_fill_hot(ev, hv);
+    mv_fill_hot(er, hr);
     const int u = mv_units(ev.W.type, ev.W.K), u2 = mv_units(er.W.type, er.W.K);
     const dim3 grid((ev.W.M + 7) / 8);
     switch (ev.W.type) {

@@ -1,3 +1,3 @@
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_configs.py -k "wide" > gpurun_out/r6_wide_tests.txt 2>&1
-rc=$?; tail -5 gpurun_out/r6_wide_tests.txt; exit $rc
+tools/ab_lib.sh v6-1b6-q4_0 3 sigmaa=this off=this@RWKV_MI355X_DECODE_FUSION=63 > gpurun_out/r6_ab_sigmaa.txt 2>&1 || exit 1
+cat gpurun_out/r6_ab_sigmaa.txt

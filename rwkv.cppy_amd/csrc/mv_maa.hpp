@@ -46,6 +46,18 @@ __device__ __forceinline__ void maa_dec4_body(const MaaDec & a, int bx, int n, c
             chunk_load<MVK_LN, 1>(E, min(kc[q], K - 8), ci[q]);
         }
         if constexpr (XG) {
+            // one granule per chunk first (a wave-uniform address: one request per poll), so the
+            // waiting waves do not load the row producers' lines 512 times over
+#pragma unroll
+            for (int q = 0; q < LCW; q++)
+                if (pw + 4 * q < nch) {
+                    const unsigned long long * g0 = xg + (pw + 4 * q) * LN_CHUNK;
+                    for (unsigned it = 0; it < spin_max; it++) {
+                        const unsigned long long v = __hip_atomic_load((gran_u64_t *)g0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if ((unsigned)(v >> 32) == xtag) break;
+                        __builtin_amdgcn_s_sleep(2);
+                    }
+                }
             // this lane's 8 elements of x from their granules (the plain loads above read the
             // previous values of x: replaced)
 #pragma unroll

@@ -39,7 +39,7 @@ lib.rwkv_free(ctx)
 r = np.fromfile(out, dtype=np.uint64).reshape(-1, 8)
 r = r[np.argsort(r[:, 0], kind='stable')]
 kid = ((r[:, 3] >> 32) & 15).astype(np.int64)  # kid bits 32..43, cycles 44..63
-names = {1: 'k_mva', 2: 'k_mv', 3: 'att6', 5: 'embed', 6: 'att6f', 7: 'mvsig', 8: 'att4f', 9: 'ffnf'}
+names = {1: 'k_mva', 2: 'k_mv', 3: 'att6', 5: 'embed', 6: 'att6f/co', 7: 'mvsig', 8: 'att4f', 9: 'ffnf', 10: 'sigmaa'}
 # launches: runs of equal kernel id in start order
 cuts = np.flatnonzero(np.diff(kid) != 0) + 1
 segs = np.split(np.arange(len(r)), cuts)

@@ -35,7 +35,7 @@ METRIC = 'tokens/sec RWKV-v6-World-1B6 Q4_0 decode + seq-eval @1/2/4/8 GPU; HBM 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 INT8_MFMA_PEAK_TOPS = 5000.0  # dense int8 MFMA: 2x the ~2.5 PF dense bf16 rate (MI355X_MICROARCH.md, Matrix cores)
 # decode kernels that stream layer / head weights (the roofline's pooled kernel class)
-STREAM_KERNELS = ('k_mv', 'k_mva', 'k_v6_maa_dec', 'k_v6_maa_dec4', 'k_v6_att_fused', 'k_v6_att_co', 'k_mvsig',
+STREAM_KERNELS = ('k_mv', 'k_mva', 'k_v6_maa_dec', 'k_v6_maa_dec4', 'k_v6_att_fused', 'k_v6_att_co', 'k_mvsig', 'k_sig_maa',
                   'k_v4_att_fused', 'k_ffn_fused', 'k_att7_lora')
 
 CONFIGS = {

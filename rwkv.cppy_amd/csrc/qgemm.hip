@@ -646,7 +646,9 @@ __device__ __forceinline__ void qm_close(float (&st)[6][NO], const float (&acc)[
 constexpr int QM_CLS = 8;  // classes per stage
 // NMAX = blocks per class rounded up to 1 / 2 / 4 / 8 (K <= 16384); slot (u, lc) at u * 8 + lc holds
 // m_w of the workgroup's 64 rows and s_x of its 32 tokens for block lc + 8 sg + 64 u
-template <int NMAX>
+// FULL: every class has at least one block (K >= 2048): a class's chain starts with its first
+// multiply-add on a literal 0 -- no zeroed accumulators.
+template <int NMAX, bool FULL>
 __global__ __launch_bounds__(256) void k_qg_msum(MMGroup g) {
     constexpr int NSLOT = QM_CLS * NMAX;
     __shared__ __attribute__((aligned(16))) float qw[2][NSLOT][64];
@@ -742,17 +744,59 @@ __global__ __launch_bounds__(256) void k_qg_msum(MMGroup g) {
             for (int k = 0; k < 16; k++) acc[k] = 0.0f;
         };
         if constexpr (NMAX <= 2) {
+            // the stage's 8 classes as a static 3-level subtree (class pairs in two accumulator
+            // sets, the binary counter's levels 1 and 2 in named registers), then levels 3.. by the
+            // stage's own counter: the same additions as fold(), without its copies and branches
             Ops o0, o1;
+            float aA[16], aB[16], p1[16], p2[16];
+            auto macf = [&](float (&a)[16], const Ops & o, int n) {
+#pragma unroll
+                for (int k = 0; k < 16; k++) a[k] = 0.0f;
+#pragma unroll
+                for (int u = 0; u < NMAX; u++) {
+                    if (!(FULL && u == 0) && u >= n) break;  // uniform
+                    const float wv[4] = {o.w[u].x, o.w[u].y, o.w[u].z, o.w[u].w};
+                    const float xv[4] = {o.x[u].x, o.x[u].y, o.x[u].z, o.x[u].w};
+#pragma unroll
+                    for (int r = 0; r < 4; r++) qm_mac_row<4>(a + 4 * r, wv[r], xv);
+                }
+            };
+            auto addl = [](float (&v)[16], const float (&t)[16]) {  // v = t + v
+#pragma unroll
+                for (int k = 0; k < 16; k += 2) {
+                    const qf2_t r = qf2_t{t[k], t[k + 1]} + qf2_t{v[k], v[k + 1]};
+                    v[k] = r.x;
+                    v[k + 1] = r.y;
+                }
+            };
+            auto put = [](float (&d)[16], const float (&v)[16]) {
+#pragma unroll
+                for (int k = 0; k < 16; k++) d[k] = v[k];
+            };
             rd(o0, 0);
 #pragma unroll
             for (int lc = 0; lc < QM_CLS; lc += 2) {
                 const int l = sg * QM_CLS + lc;
                 rd(o1, lc + 1);
-                mac(o0, cq + (l < crem ? 1 : 0));
-                fold(l);
+                macf(aA, o0, cq + (l < crem ? 1 : 0));
                 if (lc + 2 < QM_CLS) rd(o0, lc + 2);
-                mac(o1, cq + (l + 1 < crem ? 1 : 0));
-                fold(l + 1);
+                macf(aB, o1, cq + (l + 1 < crem ? 1 : 0));
+                addl(aB, aA);  // class l + 1 (odd): st[0] + acc
+                if (lc == 0 || lc == 4) {
+                    put(p1, aB);  // level 1
+                } else if (lc == 2) {
+                    addl(aB, p1);
+                    put(p2, aB);  // level 2
+                } else {
+                    addl(aB, p1);
+                    addl(aB, p2);
+                    switch (__builtin_ctz(~sg)) {  // levels 3.. : class 8 sg + 7's counter
+                        case 0: put(st[3], aB); break;
+                        case 1: addl(aB, st[3]); put(st[4], aB); break;
+                        case 2: addl(aB, st[3]); addl(aB, st[4]); put(st[5], aB); break;
+                        default: addl(aB, st[3]); addl(aB, st[4]); addl(aB, st[5]); put(st[0], aB); break;
+                    }
+                }
             }
         } else {
             // 4 blocks of a class at a time (their reads issued together)
@@ -989,6 +1033,7 @@ bool launch_qgemm(hipStream_t st, MMGroup & g, int wtype) {
         // the m*s chain totals first (k_qg_msum), read by the GEMM epilogue / the combine
         size_t mfl = 0;
         int mblocks = 0, mblocks8 = 0, nmax = 0;
+        bool full = true;  // every entry's classes hold >= 1 block
         const int tgs = (g.T + 63) / 64;
         for (int i = 0; i < g.n; i++) {
             if (!g.e[i].W.mt) {
@@ -1001,6 +1046,7 @@ bool launch_qgemm(hipStream_t st, MMGroup & g, int wtype) {
             mblocks8 += (g.e[i].W.M + 63) / 64 * ((g.T + 31) / 32);
             const int nbi = g.e[i].W.K / 32, nmi = nbi / 64 + (nbi % 64 ? 1 : 0);
             nmax = std::max(nmax, nmi);
+            full = full && nbi >= 64;
         }
         if (!g.m2 || g.m2_floats < mfl) {
             fprintf(stderr, "rwkv: qgemm _1 group needs %zu m*s floats, has %zu\n", mfl, g.m2 ? g.m2_floats : (size_t)0);
@@ -1014,9 +1060,11 @@ bool launch_qgemm(hipStream_t st, MMGroup & g, int wtype) {
         else if (rows && nmax <= 4) RK_LAUNCH(k_qg_msum_rows<4>, dim3(mblocks8), dim3(256), 0, st, g);
         else if (rows && nmax <= 8) RK_LAUNCH(k_qg_msum_rows<8>, dim3(mblocks8), dim3(256), 0, st, g);
         else if (rows && nmax <= 16) RK_LAUNCH(k_qg_msum_rows<16>, dim3(mblocks8), dim3(256), 0, st, g);
-        else if (nmax <= 1) RK_LAUNCH(k_qg_msum<1>, dim3(mblocks), dim3(256), 0, st, g);
-        else if (nmax <= 2) RK_LAUNCH(k_qg_msum<2>, dim3(mblocks), dim3(256), 0, st, g);
-        else if (nmax <= 4) RK_LAUNCH(k_qg_msum<4>, dim3(mblocks), dim3(256), 0, st, g);
+        else if (nmax <= 1 && full) RK_LAUNCH((k_qg_msum<1, true>), dim3(mblocks), dim3(256), 0, st, g);
+        else if (nmax <= 1) RK_LAUNCH((k_qg_msum<1, false>), dim3(mblocks), dim3(256), 0, st, g);
+        else if (nmax <= 2 && full) RK_LAUNCH((k_qg_msum<2, true>), dim3(mblocks), dim3(256), 0, st, g);
+        else if (nmax <= 2) RK_LAUNCH((k_qg_msum<2, false>), dim3(mblocks), dim3(256), 0, st, g);
+        else if (nmax <= 4) RK_LAUNCH((k_qg_msum<4, false>), dim3(mblocks), dim3(256), 0, st, g);
         else {
             fprintf(stderr, "rwkv: qgemm _1 group: K above the m*s pass's 32768\n");
             return false;

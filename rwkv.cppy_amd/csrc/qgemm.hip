@@ -851,7 +851,7 @@ __global__ __launch_bounds__(256) void k_qg_msum(MMGroup g) {
 // The long-class form (5-8 blocks per class: K > 8192): lane = row, wave = 8 tokens, workgroup = 64
 // rows x 32 tokens; a lane's m_w is one b32 read and the wave's 8 s_x two broadcast b128 reads per
 // block (the 4 x 4 register tiles of k_qg_msum need 260 VGPRs at this depth: one wave per SIMD).
-template <int NMAX>
+template <int NMAX, bool FULL>
 __global__ __launch_bounds__(256) void k_qg_msum_rows(MMGroup g) {
     constexpr int NSLOT = QM_CLS * NMAX;
     __shared__ __attribute__((aligned(16))) float qw[2][NSLOT][64];
@@ -955,6 +955,68 @@ __global__ __launch_bounds__(256) void k_qg_msum_rows(MMGroup g) {
                 mac(o1, cq + (l + 1 < crem ? 1 : 0));
                 fold(l + 1);
             }
+        } else if constexpr (FULL) {
+            // FULL (every class >= 1 block): the stage's 8 classes as a static subtree, as in
+            // k_qg_msum; each class's first 4 blocks peeled so its chain starts on a literal 0
+            float aA[8], aB[8], p1[8], p2[8];
+            auto macr = [&](float (&a)[8], int lc, int n) {
+#pragma unroll
+                for (int k = 0; k < 8; k++) a[k] = 0.0f;
+                auto step4 = [&](int u0, bool first) {
+                    float w4[4];
+                    float4 a4[4], b4[4];
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        const int u = min(u0 + q, NMAX - 1);
+                        w4[q] = qw[buf][u * 8 + lc][lane];
+                        a4[q] = *(const float4 *)&qx[buf][u * 8 + lc][8 * wave];
+                        b4[q] = *(const float4 *)&qx[buf][u * 8 + lc][8 * wave + 4];
+                    }
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        if (!(first && q == 0) && u0 + q >= n) break;  // uniform
+                        const float sx[8] = {a4[q].x, a4[q].y, a4[q].z, a4[q].w, b4[q].x, b4[q].y, b4[q].z, b4[q].w};
+                        qm_mac_row<8>(a, w4[q], sx);
+                    }
+                };
+                step4(0, true);
+#pragma unroll 1
+                for (int u0 = 4; u0 < n; u0 += 4) step4(u0, false);
+            };
+            auto addl = [](float (&v)[8], const float (&t)[8]) {  // v = t + v
+#pragma unroll
+                for (int k = 0; k < 8; k += 2) {
+                    const qf2_t r = qf2_t{t[k], t[k + 1]} + qf2_t{v[k], v[k + 1]};
+                    v[k] = r.x;
+                    v[k + 1] = r.y;
+                }
+            };
+            auto put = [](float (&d)[8], const float (&v)[8]) {
+#pragma unroll
+                for (int k = 0; k < 8; k++) d[k] = v[k];
+            };
+#pragma unroll
+            for (int lc = 0; lc < QM_CLS; lc += 2) {
+                const int l = sg * QM_CLS + lc;
+                macr(aA, lc, cq + (l < crem ? 1 : 0));
+                macr(aB, lc + 1, cq + (l + 1 < crem ? 1 : 0));
+                addl(aB, aA);
+                if (lc == 0 || lc == 4) {
+                    put(p1, aB);
+                } else if (lc == 2) {
+                    addl(aB, p1);
+                    put(p2, aB);
+                } else {
+                    addl(aB, p1);
+                    addl(aB, p2);
+                    switch (__builtin_ctz(~sg)) {
+                        case 0: put(st[3], aB); break;
+                        case 1: addl(aB, st[3]); put(st[4], aB); break;
+                        case 2: addl(aB, st[3]); addl(aB, st[4]); put(st[5], aB); break;
+                        default: addl(aB, st[3]); addl(aB, st[4]); addl(aB, st[5]); put(st[0], aB); break;
+                    }
+                }
+            }
         } else {
             // 4 blocks of a class at a time (their reads issued together), in ascending order: the
             // registers stay bounded for any NMAX (16: K <= 32768, e.g. a 20480-wide FFN value)
@@ -1055,11 +1117,12 @@ bool launch_qgemm(hipStream_t st, MMGroup & g, int wtype) {
         // the 4 x 4 register-tile form over 64-token tiles; the row form (32-token tiles) for 32 or
         // fewer tokens (contexts) and for classes of 5-8 blocks
         const bool rows = g.T <= 32 || nmax > 4;
-        if (rows && nmax <= 1) RK_LAUNCH(k_qg_msum_rows<1>, dim3(mblocks8), dim3(256), 0, st, g);
-        else if (rows && nmax <= 2) RK_LAUNCH(k_qg_msum_rows<2>, dim3(mblocks8), dim3(256), 0, st, g);
-        else if (rows && nmax <= 4) RK_LAUNCH(k_qg_msum_rows<4>, dim3(mblocks8), dim3(256), 0, st, g);
-        else if (rows && nmax <= 8) RK_LAUNCH(k_qg_msum_rows<8>, dim3(mblocks8), dim3(256), 0, st, g);
-        else if (rows && nmax <= 16) RK_LAUNCH(k_qg_msum_rows<16>, dim3(mblocks8), dim3(256), 0, st, g);
+        if (rows && nmax <= 1) RK_LAUNCH((k_qg_msum_rows<1, false>), dim3(mblocks8), dim3(256), 0, st, g);
+        else if (rows && nmax <= 2) RK_LAUNCH((k_qg_msum_rows<2, false>), dim3(mblocks8), dim3(256), 0, st, g);
+        else if (rows && nmax <= 4) RK_LAUNCH((k_qg_msum_rows<4, false>), dim3(mblocks8), dim3(256), 0, st, g);
+        else if (rows && nmax <= 8 && full) RK_LAUNCH((k_qg_msum_rows<8, true>), dim3(mblocks8), dim3(256), 0, st, g);
+        else if (rows && nmax <= 8) RK_LAUNCH((k_qg_msum_rows<8, false>), dim3(mblocks8), dim3(256), 0, st, g);
+        else if (rows && nmax <= 16) RK_LAUNCH((k_qg_msum_rows<16, false>), dim3(mblocks8), dim3(256), 0, st, g);
         else if (nmax <= 1 && full) RK_LAUNCH((k_qg_msum<1, true>), dim3(mblocks), dim3(256), 0, st, g);
         else if (nmax <= 1) RK_LAUNCH((k_qg_msum<1, false>), dim3(mblocks), dim3(256), 0, st, g);
         else if (nmax <= 2 && full) RK_LAUNCH((k_qg_msum<2, true>), dim3(mblocks), dim3(256), 0, st, g);

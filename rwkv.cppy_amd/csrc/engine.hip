@@ -1344,7 +1344,23 @@ static void src_f32(MVEntry & e, const float * f) {
 bool Engine::forward_decode(const float * sin, float * sout, bool logits, uint32_t l0, uint32_t l1) {
     const int C = (int)m_->n_embed, H = (int)m_->H, S = (int)m_->S;
     l1 = std::min(l1, m_->n_layer);
-    if (l0 == 0 && !launch_embed_ln(stream_, dtokens_, 1, m_->emb, m_->ln0_w, m_->ln0_b, x_)) return false;
+    // v6: layer 0's maa launch computes the embedding LayerNorm itself (k_v6_maa_dec4 EMB: the same
+    // bits as k_embed_ln; one launch and one boundary less per token)
+    MaaDec emaa;
+    bool emb_in = false;
+    if (l0 == 0 && l1 > 0 && m_->major == 6 && (fuse_ & FUSE_EMBMAA) && !split_maa_) {
+        const DLayer & F = m_->layers[0];
+        const ActBuf o0[5] = {A(1, F.decay_w1), A(2, F.att_k), A(3, F.att_v), A(4, F.att_r), A(5, F.att_g)};
+        v6_maa_dec_args(emaa, C, m_->maa_D, F.maa_w1, x_, sin + C, sout + C, F.ln1_w, F.ln1_b, F.maa_x, F.maa_w2t,
+                        F.maa, o0);
+        emaa.tok = dtokens_;
+        emaa.emb = m_->emb;
+        emaa.ln0w = m_->ln0_w;
+        emaa.ln0b = m_->ln0_b;
+        emaa.xout = x_;
+        emb_in = v6_maa_emb_supported(emaa);
+    }
+    if (l0 == 0 && !emb_in && !launch_embed_ln(stream_, dtokens_, 1, m_->emb, m_->ln0_w, m_->ln0_b, x_)) return false;
     v7_fused_lora_ = false;
     const size_t per_layer = m_->major >= 5 ? (size_t)C * (2 + (size_t)S) : 5 * (size_t)C;
     bool maa_done = false;  // this layer's maa ran in the previous layer's channel-mix launch (k_sig_maa)
@@ -1450,6 +1466,14 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits, uint32
             ActBuf outs[5] = {A(1, L.decay_w1), A(2, L.att_k), A(3, L.att_v), A(4, L.att_r), A(5, L.att_g)};
             if (maa_done) {
                 maa_done = false;
+            } else if (emb_in && l == 0) {
+                if (timing_) {
+                    // + the embedding row, LN0 vectors and x written
+                    kt_bytes_ = wbytes(L.maa_w1) + 5.0 * D * C * 4 + 11.0 * C * 4 + C * 4.0 + 5 * act_bytes(outs[0], 1) +
+                                (double)C * (m_->emb.type == W_F16 ? 2 : 4) + 3.0 * C * 4;
+                    kt_flops_ = 2.0 * L.maa_w1.M * L.maa_w1.K + 2.0 * 5 * D * C;
+                }
+                if (!launch_v6_maa_dec_emb(stream_, emaa)) return false;
             } else if (v6_maa_dec_supported(C, D, L.maa_w1.type) && !split_maa_) {
                 // W1 rows + mix in one launch (mv_maa.hip)
                 if (timing_) {

@@ -208,11 +208,19 @@ struct MaaDec {
     const float * maa[5];       // time_maa_{w,k,v,r,g} [C]
     ActBuf out[5];
     int xa_off;                 // LDS byte offset of the fp32 xa image
+    // layer 0 of a decode (k_v6_maa_dec4 only): x = LN0(emb[*tok]) computed in the launch (k_embed_ln's
+    // arithmetic) instead of read from x; workgroup (0, 0) stores it to xout
+    const uint32_t * tok;
+    DMat emb;
+    const float * ln0w, * ln0b;
+    float * xout;
 };
 bool v6_maa_dec_supported(int C, int D, int w1_type);
 void v6_maa_dec_args(MaaDec & a, int C, int D, const DMat & w1, const float * x, const float * carry, float * carry_out,
                      const float * lnw, const float * lnb, const float * maa_x, const float * w2t,
                      const float * const * maa, const ActBuf * outs);
+bool v6_maa_emb_supported(const MaaDec & a);
+bool launch_v6_maa_dec_emb(hipStream_t st, const MaaDec & a);
 bool launch_v6_maa_dec(hipStream_t st, int C, int D, const DMat & w1, const float * x, const float * carry,
                        float * carry_out, const float * lnw, const float * lnb, const float * maa_x,
                        const float * w2t, const float * const * maa, const ActBuf * outs);

@@ -172,14 +172,14 @@ __global__ __launch_bounds__(512) void k_v6_maa_dec(MaaDec a) {
 
 // D <= 32: mv_maa.hpp's workgroup (the image waves have no rows), x read from the residual stream.
 // Same arithmetic and association as k_v6_maa_dec (bit-identical).
-template <int WF, int U, int LNP, int CPW>
+template <int WF, int U, int LNP, int CPW, bool EMB = false>
 __global__ __launch_bounds__(512) void k_v6_maa_dec4(MaaDec a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ float s_lora[64];
     __shared__ double ln_part[16];
     STAMP_BEGIN();
-    maa_dec4_body<WF, U, LNP, CPW, false>(a, (int)blockIdx.x, (int)blockIdx.y, smem, s_lora, ln_part, nullptr, 0u,
-                                          nullptr, 0u);
+    maa_dec4_body<WF, U, LNP, CPW, false, EMB>(a, (int)blockIdx.x, (int)blockIdx.y, smem, s_lora, ln_part, nullptr,
+                                               0u, nullptr, 0u);
     STAMP_END_NS(4 + 16 * blockIdx.y);
 }
 
@@ -248,6 +248,44 @@ void v6_maa_dec_args(MaaDec & a, int C, int D, const DMat & w1, const float * x,
         a.out[i] = outs[i];
     }
     a.xa_off = (lds_bytes_for(act_fmt_for(w1.type), C) + 15) & ~15;
+}
+
+// layer 0 with the embedding LayerNorm inside (MaaDec::tok): the k_v6_maa_dec4 shapes, an F16 / F32
+// embedding of row length C
+bool v6_maa_emb_supported(const MaaDec & a) {
+    return a.tok && a.xout && a.ln0w && a.ln0b && (a.emb.type == W_F16 || a.emb.type == W_F32) &&
+           (int)a.emb.K == a.C && a.D <= 32 && v6_maa_dec_supported(a.C, a.D, a.w1.type) &&
+           wtype_quantized(a.w1.type) && (int)a.w1.M == 5 * a.D && (int)a.w1.K == a.C;
+}
+
+template <int WF>
+static void launch_maa_emb_t(hipStream_t st, const MaaDec & a, int lds, bool u1) {
+    const dim3 grid(a.C / 64, 5);
+    if (a.C <= 2048) {
+        if (u1) RK_LAUNCH((k_v6_maa_dec4<WF, 1, 32, 64, true>), grid, dim3(512), lds, st, a);
+        else RK_LAUNCH((k_v6_maa_dec4<WF, 2, 32, 64, true>), grid, dim3(512), lds, st, a);
+    } else {
+        if (u1) RK_LAUNCH((k_v6_maa_dec4<WF, 1, 64, 64, true>), grid, dim3(512), lds, st, a);
+        else RK_LAUNCH((k_v6_maa_dec4<WF, 2, 64, 64, true>), grid, dim3(512), lds, st, a);
+    }
+}
+
+bool launch_v6_maa_dec_emb(hipStream_t st, const MaaDec & a) {
+    if (!v6_maa_emb_supported(a) || maa_cpw() != 64) {
+        fprintf(stderr, "rwkv: v6 maa decode with the embedding: unsupported shape\n");
+        return false;
+    }
+    const int lds = a.xa_off + a.C * 4;
+    const bool u1 = mv_units(a.w1.type, a.C) <= 1;
+    switch (a.w1.type) {
+        case W_Q4_0: launch_maa_emb_t<W_Q4_0>(st, a, lds, u1); break;
+        case W_Q4_1: launch_maa_emb_t<W_Q4_1>(st, a, lds, u1); break;
+        case W_Q5_0: launch_maa_emb_t<W_Q5_0>(st, a, lds, u1); break;
+        case W_Q5_1: launch_maa_emb_t<W_Q5_1>(st, a, lds, u1); break;
+        default: launch_maa_emb_t<W_Q8_0>(st, a, lds, u1); break;
+    }
+    HIP_OK(hipGetLastError());
+    return true;
 }
 
 bool launch_v6_maa_dec(hipStream_t st, int C, int D, const DMat & w1, const float * x, const float * carry,

@@ -12,12 +12,14 @@
 //
 // XG: the residual stream x is read from granules {tag, value} (xg, tag xtag) written in the same
 // launch, each re-read until its tag matches (bounded: *err), instead of from a.x.
+// EMB (layer 0): x = LN0(emb[*a.tok]) -- k_embed_ln's loads, chunk sums in chunk order and ln_apply,
+// so the same bits -- exchanged through one more barrier; workgroup (0, 0) stores it to a.xout.
 #pragma once
 #include "mv_common.hpp"
 
 namespace rwkvmi {
 
-template <int WF, int U, int LNP, int CPW, bool XG>
+template <int WF, int U, int LNP, int CPW, bool XG, bool EMB = false>
 __device__ __forceinline__ void maa_dec4_body(const MaaDec & a, int bx, int n, char * smem, float * s_lora,
                                               double * ln_part, const unsigned long long * xg, unsigned xtag,
                                               unsigned * err, unsigned spin_max) {
@@ -44,6 +46,49 @@ __device__ __forceinline__ void maa_dec4_body(const MaaDec & a, int bx, int n, c
         for (int q = 0; q < LCW; q++) {
             kc[q] = (pw + 4 * q) * LN_CHUNK + lane * 8;
             chunk_load<MVK_LN, 1>(E, min(kc[q], K - 8), ci[q]);
+        }
+        if constexpr (EMB) {
+            __shared__ double e_part[2][8];
+            const size_t tk = *a.tok;
+            float w0[LCW][8], b0[LCW][8];
+#pragma unroll
+            for (int q = 0; q < LCW; q++) {
+                ln_load8(w0[q], a.ln0w, kc[q], K);
+                ln_load8(b0[q], a.ln0b, kc[q], K);
+                const int k = min(kc[q], K - 8);
+                if (a.emb.type == W_F16) {
+                    const int4 raw = *(const int4 *)((const __half *)a.emb.qs + tk * K + k);
+                    const __half * h = (const __half *)&raw;
+#pragma unroll
+                    for (int j = 0; j < 8; j++) ci[q].x[j] = __half2float(h[j]);
+                } else {
+                    ln_load8(ci[q].x, (const float *)a.emb.qs + tk * K, k, K);
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < LCW; q++)
+                if (pw + 4 * q < nch) {
+                    double c1, c2;
+                    ln_chunk_sums(ci[q].x, kc[q] < K, c1, c2);
+                    if (lane == 0) {
+                        e_part[0][pw + 4 * q] = c1;
+                        e_part[1][pw + 4 * q] = c2;
+                    }
+                }
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // (E) LN0 statistics
+            double s1 = 0.0, s2 = 0.0;
+            for (int q = 0; q < nch; q++) s1 += e_part[0][q], s2 += e_part[1][q];
+            float m0, sc0;
+            ln_finish(s1, s2, K, 1e-5f, m0, sc0);
+#pragma unroll
+            for (int q = 0; q < LCW; q++) {
+#pragma unroll
+                for (int j = 0; j < 8; j++) ci[q].x[j] = ln_apply(ci[q].x[j], m0, sc0, w0[q][j], b0[q][j]);
+                if (bx == 0 && n == 0 && pw + 4 * q < nch && kc[q] < K) {
+                    *(float4 *)(a.xout + kc[q]) = make_float4(ci[q].x[0], ci[q].x[1], ci[q].x[2], ci[q].x[3]);
+                    *(float4 *)(a.xout + kc[q] + 4) = make_float4(ci[q].x[4], ci[q].x[5], ci[q].x[6], ci[q].x[7]);
+                }
+            }
         }
         if constexpr (XG) {
             // one granule per chunk first (a wave-uniform address: one request per poll), so the
@@ -136,6 +181,7 @@ __device__ __forceinline__ void maa_dec4_body(const MaaDec & a, int bx, int n, c
         for (int i = 0; i < DM; i++) w2v[i] = w2[(size_t)min(i, D - 1) * C];  // rows >= D: skipped below
         const float carry_c = a.carry[cc];
         const float mu_c = a.maa[n][cc];
+        if constexpr (EMB) asm volatile("s_barrier" ::: "memory");  // (E)
         asm volatile("s_barrier" ::: "memory");  // the image waves' statistics exchange
         __syncthreads();  // (1) activation image ready
         float acc[R], acc2[R];

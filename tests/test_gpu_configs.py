@@ -145,7 +145,8 @@ def test_v7_2b9_width_four_stages(cfg_dir):
     assert_bits_equal(lg, ref_lg, 'four-stage logits')
 
 
-FUSION_MASKS = [0, 511 ^ 2, 511 ^ 8, 511 ^ 16, 511 ^ 32, 511 ^ 1, 511 ^ 64, 511 ^ 96, 511 ^ 128, 511 ^ 256, 255, 63]
+FUSION_MASKS = [0, 1023 ^ 2, 1023 ^ 8, 1023 ^ 16, 1023 ^ 32, 1023 ^ 1, 1023 ^ 64, 1023 ^ 96, 1023 ^ 128, 1023 ^ 256,
+                1023 ^ 512, 1023 ^ 192, 511, 255, 63]
 
 
 @pytest.mark.parametrize('name', sorted(CONFIGS))
@@ -153,7 +154,8 @@ def test_decode_fusion_arms_bit_exact(cfg_dir, name):
     """Every decode fusion has an unfused arm (Engine::FUSE_*: 1 v6 attention launch, 2 its Wo, 4 v4
     attention launch, 8 its Wo, 16 v7 LoRA + attention, 32 FFN value + receptance, 64 the whole channel
     mix in one launch, 128 its co-resident form while the context has the device alone, 256 the v6
-    channel mix's value rows with the next layer's maa, co-resident).  Each mask,
+    channel mix's value rows with the next layer's maa, co-resident, 512 the v6 embedding LayerNorm
+    inside layer 0's maa launch).  Each mask,
     switched per context (rwkv_mi355x_debug_set "decode_fusion") and at creation
     (RWKV_MI355X_DECODE_FUSION), decodes bit-exactly against the oracle; switching back and forth on
     one context (the fused Wo's granules cleared at each switch) too."""
@@ -162,7 +164,7 @@ def test_decode_fusion_arms_bit_exact(cfg_dir, name):
     glg, gst = gpu_variant(path, toks)
     L = library()
     m = RWKVModel(L, path)
-    for mask in FUSION_MASKS + [511]:
+    for mask in FUSION_MASKS + [1023]:
         assert L.library.rwkv_mi355x_debug_set(m._ctx.ptr, b'decode_fusion', mask)
         lg, st = gpu_serial(m, toks)
         assert_bits_equal(lg, glg, f'{name} decode logits, fusion mask {mask}')

@@ -1360,6 +1360,14 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits, uint32
         emaa.xout = x_;
         emb_in = v6_maa_emb_supported(emaa);
     }
+    // v4: the same inside layer 0's fused attention launch (with Wo fused: the Wo rows store x)
+    bool emb4_in = false;
+    if (l0 == 0 && l1 > 0 && m_->major == 4 && (fuse_ & FUSE_EMBMAA) && (fuse_ & FUSE_ATT4) && (fuse_ & FUSE_WO4)) {
+        const DLayer & F = m_->layers[0];
+        emb4_in = v4_att_fused_supported(C, F.att_r, F.att_k, F.att_v, A(0, F.att_o)) && F.att_o.type == F.att_r.type &&
+                  C % 8 == 0 && (m_->emb.type == W_F16 || m_->emb.type == W_F32) && (int)m_->emb.K == C;
+        emb_in = emb4_in;
+    }
     if (l0 == 0 && !emb_in && !launch_embed_ln(stream_, dtokens_, 1, m_->emb, m_->ln0_w, m_->ln0_b, x_)) return false;
     v7_fused_lora_ = false;
     const size_t per_layer = m_->major >= 5 ? (size_t)C * (2 + (size_t)S) : 5 * (size_t)C;
@@ -1394,7 +1402,15 @@ bool Engine::forward_decode(const float * sin, float * sout, bool logits, uint32
                     kt_flops_ = 6.0 * C * C;
                 }
                 V4WoFused wf;
+                memset(&wf, 0, sizeof(wf));
                 const bool wo_in = (fuse_ & FUSE_WO4) && L.att_o.type == L.att_r.type && C % 8 == 0;
+                if (wo_in && emb4_in && l == 0) {
+                    wf.tok = dtokens_;
+                    wf.emb = m_->emb;
+                    wf.ln0w = m_->ln0_w;
+                    wf.ln0b = m_->ln0_b;
+                    if (timing_) kt_bytes_ += (double)C * (m_->emb.type == W_F16 ? 2 : 4) + 2.0 * C * 4;
+                }
                 if (wo_in) {
                     wf.wo = L.att_o;
                     wf.xres = x_;

@@ -189,7 +189,7 @@ class Engine : public KLaunchTimer {
         FUSE_FFN = 64,   // k_ffn_fused (the whole channel mix: key, receptance and value rows)
         FUSE_FFNCO = 128,  // its co-resident form, while the co-resident layouts are in use (co_mode)
         FUSE_SIGMAA = 256, // v6: the FFN value rows + the next layer's maa in one launch (co-resident only)
-        FUSE_EMBMAA = 512, // v6: the embedding LayerNorm inside layer 0's maa launch
+        FUSE_EMBMAA = 512, // the embedding LayerNorm inside layer 0's first launch (v6 maa, v4 attention)
         FUSE_ALL = 1023,
         // the one-launch channel mix measured slower than the key + value pair (same box, separate
         // processes: v6-1B6 716 vs 692 us/token, v4-169M 234 vs 228): off by default

@@ -307,6 +307,10 @@ struct V4WoFused {
     unsigned ytag;
     unsigned * err;
     unsigned spin_max;
+    // layer 0 of a decode: x = LN0(emb[*tok]) computed in the launch (k_embed_ln's arithmetic)
+    const uint32_t * tok;
+    DMat emb;
+    const float * ln0w, * ln0b;
 };
 bool launch_v4_att_fused(hipStream_t st, int C, const DMat & Wr, const DMat & Wk, const DMat & Wv, const float * x,
                          const float * carry, float * carry_out, const float * lnw, const float * lnb,

@@ -46,9 +46,28 @@ struct Att4Fused {
     unsigned ytag;
     unsigned * err;
     unsigned spin_max;
+    // EMB (layer 0, Wo fused): x = LN0(emb[*tok]) -- the producers' image waves normalise the
+    // embedding row (k_embed_ln's loads, chunk sums in chunk order, ln_apply: the same bits) through
+    // one more barrier, and each Wo wave computes its rows' x itself; the Wo rows store x + Wo . y
+    const uint32_t * tok;
+    DMat emb;
+    const float * ln0w, * ln0b;
 };
 
 typedef __attribute__((address_space(1))) unsigned long long a4_gu64_t;
+
+// 8 consecutive embedding elements k .. k + 7 (clamped to the row) as fp32
+__device__ __forceinline__ void a4_emb8(float (&v)[8], const DMat & emb, size_t tok, int k, int C) {
+    k = min(k, C - 8);
+    if (emb.type == W_F16) {
+        const int4 raw = *(const int4 *)((const __half *)emb.qs + tok * C + k);
+        const __half * h = (const __half *)&raw;
+#pragma unroll
+        for (int j = 0; j < 8; j++) v[j] = __half2float(h[j]);
+    } else {
+        ln_load8(v, (const float *)emb.qs + tok * C, k, C);
+    }
+}
 typedef __attribute__((address_space(1))) unsigned a4_gu32_t;
 
 // 512 threads = 8 waves, CPW channels per workgroup.  Waves 4..7 build the three images (LayerNorm
@@ -57,7 +76,7 @@ typedef __attribute__((address_space(1))) unsigned a4_gu32_t;
 // workgroup's channels; wave 0 (CPW lanes) runs the recurrence.  CPW = 32 emits Wo's input as one
 // Q8 block; smaller CPW (more workgroups streaming the rows) write it as fp32.
 constexpr int A4_WOR = 2;  // Wo rows per wave of a Wo workgroup (8 waves: 16 rows)
-template <int WF, int U, int CPW, bool WO = false>
+template <int WF, int U, int CPW, bool WO = false, bool EMB = false>
 __global__ __launch_bounds__(512) void k_v4_att_fused(Att4Fused a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ float sr[CPW], sk[CPW], sv[CPW];
@@ -77,7 +96,28 @@ __global__ __launch_bounds__(512) void k_v4_att_fused(Att4Fused a) {
             for (int u = 0; u < U; u++)
 #pragma unroll
                 for (int r = 0; r < A4_WOR; r++) wo[r][u] = load_unit<WF>(a.wo, min(row0 + r, C - 1), u, lane);
-            const float xr = a.xres[min(row0 + min(lane, A4_WOR - 1), C - 1)];
+            float xr;
+            if constexpr (EMB) {
+                // this layer's input x = LN0(emb[token]): the row's statistics in this wave's registers
+                const size_t tk = *a.tok;
+                const int nc = (C + LN_CHUNK - 1) / LN_CHUNK;
+                float ev[4][8];
+#pragma unroll
+                for (int c = 0; c < 4; c++) {
+                    if (c < nc) a4_emb8(ev[c], a.emb, tk, c * LN_CHUNK + lane * 8, C);
+                    else
+#pragma unroll
+                        for (int j = 0; j < 8; j++) ev[c][j] = 0.0f;
+                }
+                float m0, sc0;
+                ln_stats_regs<4>(ev, nc, C, 1e-5f, m0, sc0);
+                const int rr = min(row0 + min(lane, A4_WOR - 1), C - 1);
+                const float e = a.emb.type == W_F16 ? __half2float(((const __half *)a.emb.qs)[tk * C + rr])
+                                                    : ((const float *)a.emb.qs)[tk * C + rr];
+                xr = ln_apply(e, m0, sc0, a.ln0w[rr], a.ln0b[rr]);
+            } else {
+                xr = a.xres[min(row0 + min(lane, A4_WOR - 1), C - 1)];
+            }
             const ActBuf xq = lds_act(smem, act_fmt_for(WF), K);
             gran_gather_image<WF>(a.ygran, a.ytag, C, xq, wave, 8, a.err, a.spin_max, lane);
             __syncthreads();
@@ -155,6 +195,30 @@ __global__ __launch_bounds__(512) void k_v4_att_fused(Att4Fused a) {
 #pragma unroll
     for (int m = 0; m < 3; m++) img[m] = lds_act(smem + m * a.img, act_fmt_for(WF), K);
     if (pro) {
+        if constexpr (EMB) {
+            // x = LN0(emb[token]) for this wave's chunk (k_embed_ln's arithmetic)
+            __shared__ double e_part[2][8];
+            const size_t tk = *a.tok;
+            float w0[8], b0[8];
+            ln_load8(w0, a.ln0w, kc, K);
+            ln_load8(b0, a.ln0b, kc, K);
+            a4_emb8(ci[0].x, a.emb, tk, kc, K);
+            if (pw < nch) {
+                double c1, c2;
+                ln_chunk_sums(ci[0].x, kval, c1, c2);
+                if (lane == 0) {
+                    e_part[0][pw] = c1;
+                    e_part[1][pw] = c2;
+                }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // (E) LN0 statistics
+            double s1 = 0.0, s2 = 0.0;
+            for (int q = 0; q < nch; q++) s1 += e_part[0][q], s2 += e_part[1][q];
+            float m0, sc0;
+            ln_finish(s1, s2, K, 1e-5f, m0, sc0);
+#pragma unroll
+            for (int j = 0; j < 8; j++) ci[0].x[j] = ln_apply(ci[0].x[j], m0, sc0, w0[j], b0[j]);
+        }
         // LayerNorm statistics (chunk association, one pass); the chunk sums meet in LDS
         __shared__ double ln_part[2][8];
         if (pw < nch) {
@@ -181,6 +245,7 @@ __global__ __launch_bounds__(512) void k_v4_att_fused(Att4Fused a) {
             chunk_store<WF, MVK_LN, 0>(E, img[2], ci[0], mean, scale, false, kc, kval, lane);
         }
     } else {
+        if constexpr (EMB) asm volatile("s_barrier" ::: "memory");  // (E)
         asm volatile("s_barrier" ::: "memory");  // the image waves' statistics exchange
     }
     __syncthreads();  // (1) images ready
@@ -268,6 +333,11 @@ static void launch_att4_t(hipStream_t st, const Att4Fused & a, int units) {
     if (a.wo.qs) {
         // the producers, then the Wo workgroups (16 rows each)
         const dim3 grid(a.C / 8 + (a.C + 8 * A4_WOR - 1) / (8 * A4_WOR));
+        if (a.tok) {
+            if (units <= 1) RK_LAUNCH((k_v4_att_fused<WF, 1, 8, true, true>), grid, dim3(512), lds, st, a);
+            else RK_LAUNCH((k_v4_att_fused<WF, 2, 8, true, true>), grid, dim3(512), lds, st, a);
+            return;
+        }
         if (units <= 1) RK_LAUNCH((k_v4_att_fused<WF, 1, 8, true>), grid, dim3(512), lds, st, a);
         else RK_LAUNCH((k_v4_att_fused<WF, 2, 8, true>), grid, dim3(512), lds, st, a);
         return;
@@ -316,6 +386,16 @@ bool launch_v4_att_fused(hipStream_t st, int C, const DMat & Wr, const DMat & Wk
         a.ytag = wf->ytag;
         a.err = wf->err;
         a.spin_max = wf->spin_max;
+        if (wf->tok) {
+            if ((wf->emb.type != W_F16 && wf->emb.type != W_F32) || (int)wf->emb.K != C || !wf->ln0w || !wf->ln0b) {
+                fprintf(stderr, "rwkv: fused v4 attention with the embedding: unsupported embedding\n");
+                return false;
+            }
+            a.tok = wf->tok;
+            a.emb = wf->emb;
+            a.ln0w = wf->ln0w;
+            a.ln0b = wf->ln0b;
+        }
     }
     a.img = (lds_bytes_for(act_fmt_for(Wr.type), C) + 15) & ~15;
     const int units = mv_units(Wr.type, C);

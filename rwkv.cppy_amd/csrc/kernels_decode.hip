@@ -70,7 +70,9 @@ bool launch_mv_group(hipStream_t st, MVGroup & g) {
                     rows2 > 2 * g_mv_cus;
     // ... and 8 rows per wave when even 4 leave more than four workgroups per CU (K > 2048, two units
     // per lane: v5-7B r,k,v,g, 1024 -> 512 workgroups; decode 1557 -> 1535 us/token, bit-exact; v7's
-    // r,k,v at 480 workgroups measured neutral and stays at 4)
+    // r,k,v at 480 workgroups measured neutral and stays at 4).  That shape takes its two units in two
+    // round trips (U = 1, launch_mv_shape): at U = 2 it held 153 VGPRs, one workgroup per CU, and its
+    // 512 workgroups ran in two rounds (v5-7B decode 1525-1528 -> 1485-1487 us/token)
     constexpr int ln_r8 = 1;
     int lnk = 0;
     for (int i = 0; i < g.n; i++) lnk = std::max(lnk, g.e[i].W.K);

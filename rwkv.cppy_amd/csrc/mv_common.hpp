@@ -1274,7 +1274,8 @@ bool launch_mv_shape(hipStream_t st, MVGroup & g, int U, int srck, int form, boo
             else MV_L(Rv, 4, S, F, E, 64);                    \
         }                                                     \
     } while (0)
-    // not emitting: g.rows rows per streaming wave (2, or 4 for large LayerNorm groups); emitting: 8
+    // not emitting: g.rows rows per streaming wave (2, or 4 for large LayerNorm groups, or 8 with
+    // one unit per round trip: <= 128 VGPRs, two workgroups per CU); emitting: 8
 #define MV_P(S, F, E)                                         \
     do {                                                      \
         if constexpr (WFIX == W_F16) {                        \
@@ -1283,7 +1284,7 @@ bool launch_mv_shape(hipStream_t st, MVGroup & g, int U, int srck, int form, boo
                 break;                                        \
             }                                                 \
         }                                                     \
-        if (g.rows == 8 && K > 2048 && U == 2) MV_L(4, 2, S, F, false, 64); \
+        if (g.rows == 8 && K > 2048 && U == 2) MV_L(4, 1, S, F, false, 64); \
         else if (g.rows == 4) MV_PR(2, S, F, false);          \
         else MV_PR(1, S, F, false);                           \
     } while (0)
